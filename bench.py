@@ -1,0 +1,252 @@
+"""Headline benchmark: batched suffix-array pattern lookups on MI355X.
+
+BASELINE.json metric: "pattern lookups/s + achieved HBM GB/s, 2^30-byte text,
+10^7 len-32 queries".  One step = one batched lookup of all queries of this
+GPU (inputs already resident in HBM), through the C ABI (sas_search_fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--algo stree|plain|lcp]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+
+Multi-GPU: the index is replicated (the text is generated and indexed on every
+GPU), each rank searches its own 10^7 queries -> weak scaling, no collective on
+the data path; only the timing barrier and a MAX all-reduce of elapsed times.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(REPO, "suffix-array-searching_amd")
+for _p in (REPO, PKG):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+METRIC = "pattern lookups/s + achieved HBM GB/s, 2^30-byte text, 10^7 len-32 queries"
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+SEED = 31415  # sas/main.rs:38
+
+
+def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes: float) -> float:
+    """Bytes a lookup must move: 4 B SA word + m text bytes per
+    probe, the query, the 8 B position.  PLAIN/LCP: P = ilog2(n)+1 probes.
+    STREE: H 64-B nodes + measured tail probes."""
+    if algo == "stree":
+        return stree_layers * 64 + tail_probes * (4 + m) + m + 8
+    P = int(np.log2(n)) + 1
+    return P * (4 + m) + m + 8
+
+
+def timed_loop(step, steps: int, warmup: int, sync, barrier, reduce_max):
+    """W untimed steps, then K steps bracketed by barrier + device sync on both
+    sides; returns the MAX over ranks of the elapsed seconds."""
+    for _ in range(warmup):
+        step()
+    sync()
+    barrier()
+    sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    sync()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    return reduce_max(elapsed)
+
+
+def dist_env():
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return ws, rank, local
+
+
+def load_traffic(algo: str, n: int, nq: int, m: int):
+    """HBM bytes per launch from a committed rocprofv3 --pmc pass of this exact
+    workload (profiles/pmc_<algo>_n<n>_q<nq>_m<m>.json, written by
+    tools/pmc_to_json.py), or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_{algo}_n{n}_q{nq}_m{m}.json")
+    if not os.path.exists(path):
+        return None, None
+    d = json.load(open(path))
+    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+
+
+def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
+    """The oracle's restatement of the reference CPU search, timed on this host's
+    cores on a bounded sample of the same queries (rank 0, N=1 only)."""
+    from oracle import pyoracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    n = idx.n
+    t = O.padded(text_dev.cpu().numpy())
+    sa = idx.suffix_array()
+    best = None
+    for algo in ("binary_search", "batch_c16"):
+        sample = min(nq, 50_000)
+        while True:
+            qb = np.concatenate([qbytes_dev[: sample * m].cpu().numpy(), np.zeros(64, np.uint8)])
+            off = np.arange(sample, dtype=np.uint64) * m
+            ln = np.full(sample, m, np.uint32)
+            t0 = time.perf_counter()
+            O.search_many(t, n, sa, qb, off, ln, algo, threads)
+            dt = time.perf_counter() - t0
+            if dt * 2 > seconds / 2 or sample >= nq:
+                break
+            sample = min(nq, int(sample * max(2.0, (seconds / 2) / max(dt, 1e-3))))
+        rate = sample / dt
+        if best is None or rate > best[0]:
+            best = (rate, algo, sample, dt)
+    rate, algo, sample, dt = best
+    return {"value": rate, "unit": "lookups/s", "cores": threads, "kind": "port",
+            "sample": f"oracle/{algo} (restates sas/sa_search.rs "
+                      f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
+                      f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA, {dt:.1f} s, "
+                      f"{threads} threads, contiguous chunks (sst/bin/bench.rs:558-573)"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
+    ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
+    ap.add_argument("--m", type=int, default=32, help="query length")
+    ap.add_argument("--algo", default="stree", choices=["stree", "plain", "lcp"])
+    ap.add_argument("--variants", default="plain,lcp", help="other algos timed beside the headline one")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import sas_amd
+
+    ws, rank, local = dist_env()
+    dist = None
+    if ws > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    n, nq, m = args.n, args.nq, args.m
+
+    t_build0 = time.perf_counter()
+    text = sas_amd.random_string(n, seed=SEED, device=dev)  # sas/util.rs:9-15, identical on every rank
+    idx = sas_amd.SaNaive.build(text, lcp=True, stree=True)
+    stats = idx.stats()
+    # this rank's queries: positive len-m substrings (sas/util.rs:18-26), stream continued after the text
+    off, _, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 4 * nq, margin=200,
+                                       len_lo=m, len_hi=m + 1)
+    off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
+    qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
+    ar = torch.arange(m, device=dev, dtype=torch.int64)
+    chunk = 1 << 20
+    for s in range(0, nq, chunk):
+        e = min(nq, s + chunk)
+        qbytes[s * m:e * m] = text[(off_t[s:e, None] + ar[None, :]).reshape(-1)]
+    out = torch.empty(nq, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    build_s = time.perf_counter() - t_build0
+
+    def reduce_max(x):
+        if dist is None:
+            return x
+        tt = torch.tensor([x], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    barrier = (lambda: dist.barrier()) if dist is not None else (lambda: None)
+    stream = torch.cuda.current_stream(dev)
+
+    def run_algo(algo, steps, warmup):
+        def step():
+            idx.search_fixed(qbytes, m, algo=algo, out=out)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        holder = {}
+
+        def timed_step_factory():
+            # events bracket exactly the K timed launches on the launch stream
+            state = {"i": 0}
+
+            def s():
+                if state["i"] == warmup:
+                    ev0.record(stream)
+                step()
+                state["i"] += 1
+                if state["i"] == warmup + steps:
+                    ev1.record(stream)
+            return s
+        el = timed_loop(timed_step_factory(), steps, warmup, torch.cuda.synchronize, barrier, reduce_max)
+        holder["kernel_ms"] = ev0.elapsed_time(ev1) / steps
+        # correctness guard (untimed): every answer must be an occurrence of its query
+        occ = text[(out[:, None] + ar[None, :]).reshape(-1).clamp_(max=n - 1)]
+        ok = bool(torch.equal(occ, qbytes))
+        return el, holder["kernel_ms"], ok
+
+    el, kernel_ms, ok = run_algo(args.algo, args.steps, args.warmup)
+    if not ok:
+        raise SystemExit(f"bench: {args.algo} returned a non-occurrence position")
+    # probes -> tail probes for the algorithmic byte count (untimed pass)
+    _, probes = idx.search_fixed(qbytes, m, algo=args.algo, probes=True)
+    mean_probes = float(probes.double().mean().item())
+    tail = max(0.0, mean_probes - stats["stree_layers"]) if args.algo == "stree" else mean_probes
+    algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail)
+    achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
+
+    variants = {}
+    for v in [x for x in args.variants.split(",") if x and x != args.algo]:
+        vel, vk, vok = run_algo(v, max(3, args.steps // 4), 1)
+        _, vp = idx.search_fixed(qbytes, m, algo=v, probes=True)
+        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], float(vp.double().mean().item()))
+        variants[v] = {"lookups_per_s": ws * nq * max(3, args.steps // 4) / vel, "kernel_ms": vk,
+                       "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
+                       "mean_probes": float(vp.double().mean().item()), "verified": vok}
+
+    traffic, traffic_src = load_traffic(args.algo, n, nq, m)
+    cpu = None
+    if rank == 0 and ws == 1 and not args.no_cpu:
+        cpu = cpu_baseline(text, idx, qbytes, m, nq, args.cpu_seconds)
+
+    if rank == 0:
+        ms = el / args.steps * 1e3
+        value = ws * nq * args.steps / el
+        workload = {"stree": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, LCP-skipping search over an "
+                             "S-tree of 16-char SA keys (top layers LDS-staged)",
+                    "plain": "configs[1]: 2^30 text in HBM, 10^7 len-32 queries, plain binary search over SA",
+                    "lcp": "configs[1] + mlr LCP skipping"}[args.algo]
+        line = {
+            "metric": METRIC, "value": value, "unit": "lookups/s", "n_gpus": ws, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic: random_string(ChaCha8Rng::seed_from_u64({SEED})) text + positive len-{m} "
+                    f"substrings (sas/util.rs:9-26), per-rank query stream",
+            "config": {"workload": workload, "algo": args.algo, "n": n, "queries_per_gpu": nq, "m": m,
+                       "parallelism": f"replicated index x{ws}, query shards (no data-path collective)"},
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBPS,
+                         "traffic": traffic, "traffic_source": traffic_src,
+                         "kernel": "k_sa_stree" if args.algo == "stree" else "k_sa_binary",
+                         "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
+                         "mean_probes": mean_probes},
+            "cpu_baseline": cpu,
+            "variants": variants,
+            "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "top_levels", "iterations",
+                                            "sa_rounds", "build_sa_ns", "build_total_ns")},
+            "setup_s": build_s, "verified": ok,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,128 @@
+/*
+ * sas.h -- C ABI of the MI355X suffix-array search engine (libsas_amd.so).
+ *
+ * Drop-in boundary for the reference's Rust SA query API
+ * (RagnarGrootKoerkamp/suffix-array-searching, sas/ = suffix-array-searching/src):
+ *
+ *   sas_build          replaces SaNaive::build(t: &Seq) -> SaNaive      sas/sa_search.rs:30-57
+ *                      and Search::build                                  sas/util.rs:31
+ *   sas_search_batch   replaces the batch type F<B>                       sas/sa_search.rs:454
+ *                        fn(&SaNaive, [&[u8]; B], &mut usize) -> [usize; B]
+ *                      and the single-query type F1                       sas/sa_search.rs:453
+ *                        fn(&SaNaive, &[u8], &mut usize) -> usize   (nq = 1)
+ *                      Semantics of every algo = binary_search            sas/sa_search.rs:98-112
+ *                        position SA[lower_bound(q)] under Rust slice order.
+ *   sas_search_fixed   the same for a contiguous block of fixed-length queries
+ *   sas_gen_text       random_string(n, ChaCha8Rng::seed_from_u64(seed))  sas/util.rs:9-15, sas/main.rs:38
+ *   sas_gen_queries    random_queries(t, q, rng)                          sas/util.rs:18-26
+ *
+ * Conventions (no C++ exceptions cross this ABI; sas/Cargo.toml panics instead):
+ *   - every function returns 0 on success or a positive errno value
+ *     (EINVAL bad argument, ENOMEM device memory, ENOTSUP unsupported size,
+ *     EIO HIP runtime failure); sas_last_error() gives a thread-local message.
+ *   - text and query bytes are DNA codes 0..3 (the reference's random_string
+ *     and FASTA loader only produce these, sas/util.rs:9-15,144-169).
+ *   - a query above every suffix gets the sentinel position n (the reference
+ *     reads sa[n] out of bounds there).
+ *   - pointers are host pointers unless SAS_DEVICE_PTRS is set, in which case
+ *     every input/output array of the call is device (HBM) memory.
+ *   - a built index is immutable and thread-safe; concurrent searches on
+ *     different streams are allowed.
+ */
+#ifndef SAS_H
+#define SAS_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct sas_index sas_index;
+
+/* flags */
+#define SAS_DEVICE_PTRS   (1u << 0)  /* all array arguments are device pointers          */
+#define SAS_BUILD_LCP     (1u << 1)  /* also build the LCP array (Kasai semantics)       */
+#define SAS_BUILD_STREE   (1u << 2)  /* also build the S-tree over 16-char SA keys       */
+#define SAS_BUILD_VERIFY  (1u << 3)  /* run the adjacency + permutation check on the SA  */
+#define SAS_NO_LDS_TOP    (1u << 4)  /* search: do not serve the top levels from LDS     */
+#define SAS_VALIDATE      (1u << 5)  /* search: reject query bytes > 3 (synchronises)    */
+
+/* search algorithms; all return bit-identical positions */
+enum sas_algo {
+    SAS_ALGO_PLAIN = 0, /* lockstep lower-bound binary search over SA (A6/A9)              */
+    SAS_ALGO_LCP   = 1, /* same probes, Manber-Myers mlr LCP skipping of known chars (A21) */
+    SAS_ALGO_STREE = 2  /* S-tree over 16-char SA keys + exact tail search (K2+K3)         */
+};
+
+typedef struct sas_stats {
+    uint64_t n;              /* text length (chars)                               */
+    uint64_t text_bytes;     /* packed 2-bit text in HBM                          */
+    uint64_t sa_bytes;       /* suffix array (u32)                                */
+    uint64_t lcp_bytes;      /* LCP array (u32), 0 if not built                   */
+    uint64_t stree_bytes;    /* S-tree incl. 16-char key leaves, 0 if not built   */
+    uint32_t stree_layers;   /* S-tree height (layers incl. leaves)               */
+    uint32_t stree_lds_layers; /* layers served from LDS                          */
+    uint32_t top_levels;     /* binary-search levels served from LDS (PLAIN/LCP)  */
+    uint32_t iterations;     /* ilog2(n)+1 lockstep iterations (sa_search.rs:171) */
+    uint64_t build_sa_ns;    /* wall time of the SA construction (0 if supplied)  */
+    uint64_t build_total_ns; /* wall time of sas_build                            */
+    uint32_t sa_rounds;      /* prefix-doubling rounds after the 32-char sort     */
+    uint32_t reserved;
+} sas_stats;
+
+const char* sas_last_error(void);
+
+/* Build an index over text[0..n).  sa_or_null: caller's suffix array (u32,
+ * sa_width must be 4) or NULL to construct it on the GPU (prefix doubling on
+ * 32-char packed keys, n < 2^31).  The library copies everything into HBM. */
+int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
+              uint32_t flags, sas_index** out);
+int sas_free(sas_index* index);
+int sas_get_stats(const sas_index* index, sas_stats* out);
+
+/* Copy the suffix array / LCP array out (dst host or device per flags). */
+int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags);
+int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags);
+
+/* GPU check of the SA: strictly increasing adjacent suffixes (the
+ * reference's build assertion, sas/sa_search.rs:36-38) + permutation.
+ * Returns 0 if valid, EINVAL (with message) if not. */
+int sas_verify(const sas_index* index);
+
+/* Ragged batch: query k = qbytes[qoff[k] .. qoff[k] + qlen[k]).
+ * out_pos[k] = SA[lower_bound(q_k)] (or n).  out_probes (optional) = number
+ * of suffix comparisons / S-tree nodes touched for query k, the reference's
+ * `cnt` counter (sas/sa_search.rs:104,178).  stream: hipStream_t or NULL.
+ * With host pointers the call is synchronous; with SAS_DEVICE_PTRS it is
+ * asynchronous on `stream`. */
+int sas_search_batch(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,
+                     const uint32_t* qlen, uint64_t nq, int algo, uint64_t* out_pos,
+                     uint32_t* out_probes, void* stream, uint32_t flags);
+
+/* Fixed-length batch: query k = qbytes[k*m .. (k+1)*m). */
+int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, uint64_t nq,
+                     int algo, uint64_t* out_pos, uint32_t* out_probes, void* stream,
+                     uint32_t flags);
+
+/* Timing helper for benches: run `reps` back-to-back fixed-length searches on
+ * device buffers and report the average duration of the search kernel itself
+ * (HIP events on `stream`) in *kernel_ns and of the whole call in *call_ns. */
+int sas_time_fixed(const sas_index* index, const uint8_t* d_qbytes, uint32_t m, uint64_t nq,
+                   int algo, uint64_t* d_out_pos, int reps, void* stream, uint32_t flags,
+                   double* kernel_ns, double* call_ns);
+
+/* Generators (bit-exact restatements of the reference's seeded inputs). */
+int sas_gen_text(uint64_t seed, uint64_t n, uint8_t* out, uint32_t flags);
+/* Offsets i = gen_range(0..n - margin) and lengths gen_range(len_lo..len_hi)
+ * (fixed when len_hi == len_lo + 1), continuing the ChaCha8 stream at
+ * keystream word `word_pos` (= n after sas_gen_text).  Host arrays only.
+ * Returns the next free keystream word through *next_word (may be NULL). */
+int sas_gen_queries(uint64_t seed, uint64_t word_pos, uint64_t n, uint64_t nq, uint64_t margin,
+                    uint32_t len_lo, uint32_t len_hi, uint64_t* off, uint32_t* len,
+                    uint64_t* next_word);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SAS_H */

@@ -1,0 +1,210 @@
+// common.hpp -- shared host/device pieces of libsas_amd.so.
+//
+// Data layout in HBM:
+//   text   : 2-bit packed DNA, u64 words, MSB-first (char p lives in word p/32,
+//            bits 63-2*(p%32) .. 62-2*(p%32)), followed by SAS_TEXT_PAD_WORDS
+//            zero words.  Unsigned compare of packed words == lexicographic
+//            compare of the chars (codes 0..3, sas/util.rs:9-15).
+//   sa     : u32[n] suffix array.
+//   lcp    : u32[n], lcp[0] = 0, lcp[r] = lcp(SA[r-1], SA[r]).
+//   stree  : STree<16,16>-shaped B+ tree over key16[r] = first 16 chars of
+//            suffix SA[r] (zero padded), internal layers first, the leaf layer
+//            IS the key16 array (padded with 0xFFFFFFFF to a node multiple).
+//   top    : Eytzinger array of the first TOP_LEVELS levels of the lockstep
+//            binary search: pivot SA value + 32-char key, staged into LDS.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <errno.h>
+#include <string>
+
+#include "../../include/sas.h"
+#include "../../include/sst.h"
+
+#define SAS_TEXT_PAD_WORDS 4
+#define SAS_TOP_LEVELS 12             // 4095 pivots: 32 KiB keys + 16 KiB SA in LDS
+#define SAS_TOP_NODES (1u << SAS_TOP_LEVELS)
+#define SAS_STREE_B 16                // keys per node / branching factor - 1
+#define SAS_STREE_MAX_LAYERS 16
+#define SAS_STREE_LDS_NODES 1024      // <= 64 KiB of top S-tree layers in LDS
+#define SAS_KEY_MAX 0xFFFFFFFFu       // padding key of the SA S-tree (unsigned)
+
+// ---------------------------------------------------------------- errors
+void sas_set_error(int code, const std::string& msg);
+int sas_errno_of(hipError_t e);
+
+#define SAS_FAIL(code, msg)                  \
+    do {                                     \
+        sas_set_error((code), (msg));        \
+        return (code);                       \
+    } while (0)
+
+#define HIP_TRY(expr)                                                              \
+    do {                                                                           \
+        hipError_t e_ = (expr);                                                    \
+        if (e_ != hipSuccess) {                                                    \
+            int c_ = sas_errno_of(e_);                                             \
+            sas_set_error(c_, std::string(#expr) + ": " + hipGetErrorString(e_));  \
+            return c_;                                                             \
+        }                                                                          \
+    } while (0)
+
+// ---------------------------------------------------------------- index structs
+struct sas_index {
+    uint64_t n = 0;
+    int device = 0;
+    int num_cus = 256;
+    uint64_t* text_w = nullptr;  // packed text
+    uint64_t text_words = 0;
+    uint32_t* sa = nullptr;
+    uint32_t* lcp = nullptr;
+    uint32_t* stree = nullptr;   // all nodes, 16 u32 each
+    uint64_t stree_nodes = 0;
+    uint32_t stree_height = 0;
+    uint64_t stree_off[SAS_STREE_MAX_LAYERS] = {};
+    uint32_t stree_lds_layers = 0;
+    uint32_t stree_lds_nodes = 0;
+    uint64_t* top_key = nullptr;  // [SAS_TOP_NODES], index 0 unused
+    uint32_t* top_sa = nullptr;   // [SAS_TOP_NODES]
+    uint32_t top_levels = 0;
+    uint32_t iters = 0;           // ilog2(n) + 1
+    sas_stats stats = {};
+};
+
+struct sst_index {
+    int layout = 0;
+    uint32_t flags = 0;
+    uint64_t n = 0;
+    uint32_t B = 16, N = 16;
+    uint32_t* nodes = nullptr;  // device: STree nodes / Eytzinger vals / sorted vals
+    uint64_t words = 0;         // u32 words in `nodes`
+    uint32_t height = 0;
+    uint64_t off[SAS_STREE_MAX_LAYERS] = {};
+    uint64_t layer_nodes[SAS_STREE_MAX_LAYERS] = {};
+    uint32_t lds_layers = 0;
+    uint32_t lds_nodes = 0;
+    int num_cus = 256;
+};
+
+// ---------------------------------------------------------------- device helpers
+__device__ __forceinline__ uint64_t chars_mask(uint32_t c) {
+    // top 2c bits set, c in [0, 32]
+    return c == 0 ? 0ull : (~0ull << (64 - 2 * c));
+}
+
+// 32 chars of the packed text starting at char p (zero beyond n: padding).
+__device__ __forceinline__ uint64_t text_chars32(const uint64_t* __restrict__ tw, uint64_t p) {
+    uint64_t w = p >> 5;
+    uint32_t s = (uint32_t)(p & 31) << 1;
+    uint64_t a = tw[w];
+    uint64_t b = tw[w + 1];
+    return s ? ((a << s) | (b >> (64 - s))) : a;
+}
+
+// Pack 4 byte-codes (little-endian u32, each byte 0..3) into 8 bits, first char high.
+__device__ __forceinline__ uint32_t pack4(uint32_t x) {
+    return ((x & 3u) << 6) | (((x >> 8) & 3u) << 4) | (((x >> 16) & 3u) << 2) | ((x >> 24) & 3u);
+}
+
+// Word j (chars 32j .. 32j+31, zero padded) of a byte-coded query of length m.
+__device__ __forceinline__ uint64_t pack_query_word(const uint8_t* __restrict__ q, uint32_t m, uint32_t j,
+                                                    uint32_t* bad) {
+    uint32_t base = j * 32;
+    uint64_t w = 0;
+    if (base >= m) return 0;
+    if (base + 32 <= m && ((((uintptr_t)(q + base)) & 15) == 0)) {
+        const uint4* p = reinterpret_cast<const uint4*>(q + base);
+        uint4 a = p[0], b = p[1];
+        uint32_t v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+        for (int i = 0; i < 8; i++) {
+            *bad |= v[i] & 0xFCFCFCFCu;
+            w = (w << 8) | pack4(v[i]);
+        }
+        return w;
+    }
+    uint32_t c = m - base < 32 ? m - base : 32;
+    for (uint32_t i = 0; i < c; i++) {
+        uint32_t b = q[base + i];
+        *bad |= b & 0xFCu;
+        w |= (uint64_t)(b & 3u) << (62 - 2 * i);
+    }
+    return w;
+}
+
+template <int QW>
+struct QueryRegs {
+    uint64_t w[QW];
+    const uint8_t* bytes;
+    uint32_t m;
+
+    __device__ __forceinline__ void load(const uint8_t* q, uint32_t len, uint32_t* bad) {
+        bytes = q;
+        m = len;
+#pragma unroll
+        for (int j = 0; j < QW; j++) w[j] = pack_query_word(q, len, j, bad);
+    }
+    // aligned word j (static select over the register copy; beyond QW, repack from bytes)
+    __device__ __forceinline__ uint64_t word(uint32_t j) const {
+        if (j < (uint32_t)QW) {
+            uint64_t r = w[0];
+#pragma unroll
+            for (int k = 1; k < QW; k++) r = (j == (uint32_t)k) ? w[k] : r;
+            return r;
+        }
+        uint32_t dummy = 0;
+        return pack_query_word(bytes, m, j, &dummy);
+    }
+    // 32 chars starting at char offset off (unaligned)
+    __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
+        uint32_t j = off >> 5, s = (off & 31) << 1;
+        uint64_t a = word(j);
+        if (s == 0) return a;
+        return (a << s) | (word(j + 1) >> (64 - s));
+    }
+};
+
+// Rust slice order `t[p..n] < q`, with the first h chars known equal.
+// Returns lt; *lcp = lcp(t[p..n], q) (capped at min(n-p, m)).
+template <int QW>
+__device__ __forceinline__ bool suffix_less_from(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
+                                                 const QueryRegs<QW>& q, uint32_t h, uint32_t* lcp) {
+    uint64_t lenS = n - p;
+    uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
+    for (uint32_t off = h; off < L; off += 32) {
+        uint32_t c = L - off < 32 ? L - off : 32;
+        uint64_t mk = chars_mask(c);
+        uint64_t a = text_chars32(tw, p + off) & mk;
+        uint64_t b = q.chars32(off) & mk;
+        if (a != b) {
+            *lcp = off + (uint32_t)(__clzll(a ^ b) >> 1);
+            return a < b;
+        }
+    }
+    *lcp = L;
+    return lenS < (uint64_t)q.m;
+}
+
+// Same decision when the first 32 chars of the suffix are already known (key).
+template <int QW>
+__device__ __forceinline__ bool suffix_less_key(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
+                                                uint64_t key, const QueryRegs<QW>& q, uint32_t h,
+                                                uint32_t* lcp) {
+    uint64_t lenS = n - p;
+    uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
+    if (h < 32) {
+        uint32_t c = L < 32 ? L : 32;
+        uint64_t mk = chars_mask(c);
+        uint64_t a = key & mk, b = q.w[0] & mk;
+        if (a != b) {
+            *lcp = (uint32_t)(__clzll(a ^ b) >> 1);
+            return a < b;
+        }
+        if (L <= 32) {
+            *lcp = L;
+            return lenS < (uint64_t)q.m;
+        }
+        h = 32;
+    }
+    return suffix_less_from<QW>(tw, n, p, q, h, lcp);
+}

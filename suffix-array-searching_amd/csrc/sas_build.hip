@@ -1,0 +1,669 @@
+// sas_build.hip -- index construction for the MI355X suffix-array engine.
+//
+// Replaces SaNaive::build (sas/sa_search.rs:30-57): the reference calls
+// libsais (sais64::parallel::sais, :33), casts to u32 (:35), asserts adjacent
+// suffixes increase (:36-38) and fills a (dead, p = 0) prefix table (:59-74).
+// Here everything is built on the GPU into HBM:
+//   1. pack the byte-coded text to 2 bits/char (rejects codes > 3),
+//   2. suffix array by prefix doubling: one rocPRIM radix sort of
+//      (32-char packed key, position) pairs, then doubling rounds over the
+//      still-tied groups only (h = 32, 64, ...),
+//   3. optional LCP array (direct parallel word compares),
+//   4. optional S-tree over 16-char keys (STree<16,16> layout of
+//      sst/s_tree.rs:72-176, unsigned keys, MAX padding),
+//   5. the LDS "top" of the lockstep binary search (Eytzinger order).
+#include "common.hpp"
+
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
+
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+// ------------------------------------------------------------------ error state
+static thread_local std::string g_err = "ok";
+
+void sas_set_error(int code, const std::string& msg) {
+    g_err = "[" + std::to_string(code) + "] " + msg;
+}
+int sas_errno_of(hipError_t e) {
+    if (e == hipErrorOutOfMemory || e == hipErrorMemoryAllocation) return ENOMEM;
+    if (e == hipErrorInvalidValue) return EINVAL;
+    return EIO;
+}
+extern "C" const char* sas_last_error(void) { return g_err.c_str(); }
+
+static unsigned grid_for(uint64_t count, unsigned block = 256) {
+    uint64_t g = (count + block - 1) / block;
+    if (g < 1) g = 1;
+    if (g > 262144) g = 262144;  // grid-stride beyond
+    return (unsigned)g;
+}
+
+#define GRID_STRIDE(i, count) \
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (count); i += (uint64_t)gridDim.x * blockDim.x)
+
+// ------------------------------------------------------------------ text packing
+__global__ void k_pack_text(const uint8_t* __restrict__ text, uint64_t n, uint64_t* __restrict__ tw,
+                            uint64_t words, uint32_t* __restrict__ bad) {
+    uint32_t b = 0;
+    GRID_STRIDE(w, words) {
+        uint64_t base = w * 32;
+        uint64_t v = 0;
+        if (base < n) {
+            uint32_t m = n - base < 32 ? (uint32_t)(n - base) : 32;
+            v = pack_query_word(text + base, m, 0, &b);
+        }
+        tw[w] = v;
+    }
+    if (b) atomicOr(bad, 1u);
+}
+
+// ------------------------------------------------------------------ ChaCha8 text generator
+// random_string (sas/util.rs:9-15) with ChaCha8Rng::seed_from_u64 (sas/main.rs:38):
+// char i = keystream word i >> 30 (rand 0.8.5 UniformInt<u8>, range 4, no rejection).
+__device__ __forceinline__ uint32_t rotl32d(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+#define DQR(a, b, c, d)                    \
+    a += b; d ^= a; d = rotl32d(d, 16);   \
+    c += d; b ^= c; b = rotl32d(b, 12);   \
+    a += b; d ^= a; d = rotl32d(d, 8);    \
+    c += d; b ^= c; b = rotl32d(b, 7);
+
+struct ChaKey { uint32_t k[8]; };
+
+__global__ void k_gen_text(ChaKey key, uint64_t n, uint8_t* __restrict__ out) {
+    uint64_t blocks = (n + 15) / 16;
+    GRID_STRIDE(blk, blocks) {
+        uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                          key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
+                          (uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
+        uint32_t x[16];
+#pragma unroll
+        for (int i = 0; i < 16; i++) x[i] = s[i];
+#pragma unroll
+        for (int r = 0; r < 8; r += 2) {
+            DQR(x[0], x[4], x[8], x[12]) DQR(x[1], x[5], x[9], x[13])
+            DQR(x[2], x[6], x[10], x[14]) DQR(x[3], x[7], x[11], x[15])
+            DQR(x[0], x[5], x[10], x[15]) DQR(x[1], x[6], x[11], x[12])
+            DQR(x[2], x[7], x[8], x[13]) DQR(x[3], x[4], x[9], x[14])
+        }
+        uint64_t base = blk * 16;
+        if (base + 16 <= n && (((uintptr_t)(out + base)) & 15) == 0) {
+            uint32_t wv[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int i = 0; i < 4; i++) v |= ((x[4 * q + i] + s[4 * q + i]) >> 30) << (8 * i);
+                wv[q] = v;
+            }
+            *reinterpret_cast<uint4*>(out + base) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+        } else {
+            for (int i = 0; i < 16 && base + i < n; i++) out[base + i] = (uint8_t)((x[i] + s[i]) >> 30);
+        }
+    }
+}
+
+// Host ChaCha8Rng (rand_chacha 0.3.1) + rand_core 0.6 seed_from_u64 (PCG32 expansion).
+static void h_seed_from_u64(uint64_t state, uint32_t key[8]) {
+    const uint64_t MUL = 6364136223846793005ull, INC = 11634580027462260723ull;
+    for (int i = 0; i < 8; i++) {
+        state = state * MUL + INC;
+        uint32_t xs = (uint32_t)(((state >> 18) ^ state) >> 27);
+        uint32_t rot = (uint32_t)(state >> 59);
+        key[i] = (xs >> rot) | (xs << ((32 - rot) & 31));
+    }
+}
+static inline uint32_t h_rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+#define HQR(a, b, c, d)                  \
+    a += b; d ^= a; d = h_rotl(d, 16);  \
+    c += d; b ^= c; b = h_rotl(b, 12);  \
+    a += b; d ^= a; d = h_rotl(d, 8);   \
+    c += d; b ^= c; b = h_rotl(b, 7);
+
+struct HostRng {
+    uint32_t key[8];
+    uint64_t blk = UINT64_MAX, pos = 0;
+    uint32_t buf[16];
+    uint32_t word(uint64_t w) {
+        uint64_t b = w >> 4;
+        if (b != blk) {
+            uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u, key[0], key[1], key[2], key[3],
+                              key[4], key[5], key[6], key[7], (uint32_t)b, (uint32_t)(b >> 32), 0, 0};
+            uint32_t x[16];
+            memcpy(x, s, sizeof x);
+            for (int r = 0; r < 8; r += 2) {
+                HQR(x[0], x[4], x[8], x[12]) HQR(x[1], x[5], x[9], x[13])
+                HQR(x[2], x[6], x[10], x[14]) HQR(x[3], x[7], x[11], x[15])
+                HQR(x[0], x[5], x[10], x[15]) HQR(x[1], x[6], x[11], x[12])
+                HQR(x[2], x[7], x[8], x[13]) HQR(x[3], x[4], x[9], x[14])
+            }
+            for (int i = 0; i < 16; i++) buf[i] = x[i] + s[i];
+            blk = b;
+        }
+        return buf[w & 15];
+    }
+    uint64_t next_u64() {  // BlockRng::next_u64: two consecutive words, low first
+        uint64_t lo = word(pos), hi = word(pos + 1);
+        pos += 2;
+        return lo | (hi << 32);
+    }
+    uint64_t range(uint64_t low, uint64_t high) {  // rand 0.8.5 UniformInt<usize>::sample_single
+        uint64_t r = high - low;
+        uint64_t zone = (r << __builtin_clzll(r)) - 1;
+        for (;;) {
+            unsigned __int128 p = (unsigned __int128)next_u64() * r;
+            if ((uint64_t)p <= zone) return low + (uint64_t)(p >> 64);
+        }
+    }
+};
+
+extern "C" int sas_gen_text(uint64_t seed, uint64_t n, uint8_t* out, uint32_t flags) {
+    if (!out && n) SAS_FAIL(EINVAL, "sas_gen_text: null output");
+    if (n == 0) return 0;
+    ChaKey key;
+    h_seed_from_u64(seed, key.k);
+    uint8_t* d = out;
+    if (!(flags & SAS_DEVICE_PTRS)) HIP_TRY(hipMalloc(&d, n));
+    hipLaunchKernelGGL(k_gen_text, dim3(grid_for((n + 15) / 16)), dim3(256), 0, 0, key, n, d);
+    HIP_TRY(hipGetLastError());
+    if (!(flags & SAS_DEVICE_PTRS)) {
+        HIP_TRY(hipMemcpy(out, d, n, hipMemcpyDeviceToHost));
+        HIP_TRY(hipFree(d));
+    } else {
+        HIP_TRY(hipDeviceSynchronize());
+    }
+    return 0;
+}
+
+extern "C" int sas_gen_queries(uint64_t seed, uint64_t word_pos, uint64_t n, uint64_t nq, uint64_t margin,
+                               uint32_t len_lo, uint32_t len_hi, uint64_t* off, uint32_t* len,
+                               uint64_t* next_word) {
+    if (margin >= n) SAS_FAIL(EINVAL, "sas_gen_queries: margin >= n (gen_range(0..n-margin) is empty)");
+    if (len_hi <= len_lo) SAS_FAIL(EINVAL, "sas_gen_queries: empty length range");
+    if (nq && (!off || !len)) SAS_FAIL(EINVAL, "sas_gen_queries: null output");
+    HostRng r;
+    h_seed_from_u64(seed, r.key);
+    r.pos = word_pos;
+    for (uint64_t k = 0; k < nq; k++) {  // sas/util.rs:20-24
+        off[k] = r.range(0, n - margin);
+        len[k] = (len_hi == len_lo + 1) ? len_lo : (uint32_t)r.range(len_lo, len_hi);
+    }
+    if (next_word) *next_word = r.pos;
+    return 0;
+}
+
+// ------------------------------------------------------------------ SA construction
+__global__ void k_init_pairs(const uint64_t* __restrict__ tw, uint64_t n, uint64_t* __restrict__ keys,
+                             uint32_t* __restrict__ vals) {
+    GRID_STRIDE(i, n) {
+        keys[i] = text_chars32(tw, i);
+        vals[i] = (uint32_t)i;
+    }
+}
+
+// headpos[k] = k if element k starts a new key group (else 0); group id = max-scan.
+__global__ void k_heads(const uint64_t* __restrict__ keys, uint64_t cnt, const uint32_t* __restrict__ pos_of,
+                        uint32_t* __restrict__ headpos) {
+    GRID_STRIDE(k, cnt) {
+        bool h = (k == 0) || keys[k] != keys[k - 1];
+        headpos[k] = h ? (pos_of ? pos_of[k] : (uint32_t)k) : 0u;
+    }
+}
+
+// rank[p] = group id; unresolved flag = element's group has size > 1.
+__global__ void k_assign(const uint64_t* __restrict__ keys, uint64_t cnt, const uint32_t* __restrict__ list,
+                         const uint32_t* __restrict__ sa, const uint32_t* __restrict__ group,
+                         uint32_t* __restrict__ rank, uint8_t* __restrict__ unresolved) {
+    GRID_STRIDE(k, cnt) {
+        uint32_t r = list ? list[k] : (uint32_t)k;
+        rank[sa[r]] = group[k];
+        bool h0 = (k == 0) || keys[k] != keys[k - 1];
+        bool h1 = (k + 1 == cnt) || keys[k + 1] != keys[k];
+        unresolved[k] = !(h0 && h1);
+    }
+}
+
+// Doubling key for the tied element at rank list[k]: (group of p, order of p + h).
+// p + h >= n -> the suffix is shorter than h: value n - p (< 2^31) sorts it
+// before every longer one and by length among the short ones (Rust slice order:
+// a proper prefix sorts first); otherwise 2^31 | rank[p + h].
+__global__ void k_round_keys(const uint32_t* __restrict__ list, uint64_t cnt, const uint32_t* __restrict__ sa,
+                             const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
+                             uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    GRID_STRIDE(k, cnt) {
+        uint32_t p = sa[list[k]];
+        uint32_t second = (p + h < n) ? (0x80000000u | rank[p + h]) : (uint32_t)(n - p);
+        keys[k] = ((uint64_t)rank[p] << 32) | second;
+        vals[k] = p;
+    }
+}
+
+__global__ void k_scatter_sa(const uint32_t* __restrict__ list, uint64_t cnt, const uint32_t* __restrict__ vals,
+                             uint32_t* __restrict__ sa) {
+    GRID_STRIDE(k, cnt) sa[list[k]] = vals[k];
+}
+
+struct MaxOp {
+    __device__ __host__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
+};
+
+struct DevBuf {
+    void* p = nullptr;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    template <class T> T* as() { return static_cast<T*>(p); }
+    int alloc(size_t bytes, const char* what) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
+        if (e != hipSuccess) {
+            p = nullptr;
+            sas_set_error(ENOMEM, std::string("hipMalloc(") + what + ", " + std::to_string(bytes) + " B): " +
+                                      hipGetErrorString(e));
+            return ENOMEM;
+        }
+        return 0;
+    }
+    void* release() { void* q = p; p = nullptr; return q; }
+};
+
+#define TRY(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
+
+// Prefix doubling on the GPU.  sa_out: device u32[n].
+static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32_t* rounds_out) {
+    hipStream_t st = 0;
+    DevBuf keys_a, keys_b, vals_b, rank, aux, list_a, list_b, flags, tmp, counter;
+    TRY(keys_a.alloc(n * 8, "sa keys"));
+    TRY(keys_b.alloc(n * 8, "sa keys alt"));
+    TRY(vals_b.alloc(n * 4, "sa vals alt"));
+    hipLaunchKernelGGL(k_init_pairs, dim3(grid_for(n)), dim3(256), 0, st, tw, n, keys_a.as<uint64_t>(), sa_out);
+    HIP_TRY(hipGetLastError());
+
+    // 1) sort all suffixes by their 32-char packed prefix
+    rocprim::double_buffer<uint64_t> kdb(keys_a.as<uint64_t>(), keys_b.as<uint64_t>());
+    rocprim::double_buffer<uint32_t> vdb(sa_out, vals_b.as<uint32_t>());
+    size_t tbytes = 0;
+    HIP_TRY(rocprim::radix_sort_pairs(nullptr, tbytes, kdb, vdb, (size_t)n, 0, 64, st));
+    TRY(tmp.alloc(tbytes, "radix sort temp"));
+    HIP_TRY(rocprim::radix_sort_pairs(tmp.p, tbytes, kdb, vdb, (size_t)n, 0, 64, st));
+    if (vdb.current() != sa_out)
+        HIP_TRY(hipMemcpyAsync(sa_out, vdb.current(), n * 4, hipMemcpyDeviceToDevice, st));
+    const uint64_t* skeys = kdb.current();
+    tmp.alloc(0, "free");
+
+    // 2) group ids + first unresolved list
+    TRY(rank.alloc(n * 4, "rank"));
+    TRY(aux.alloc(n * 4, "group"));
+    TRY(flags.alloc(n, "flags"));
+    TRY(list_a.alloc(n * 4, "tied list"));
+    TRY(list_b.alloc(n * 4, "tied list alt"));
+    TRY(counter.alloc(16, "counter"));
+    hipLaunchKernelGGL(k_heads, dim3(grid_for(n)), dim3(256), 0, st, skeys, n, (const uint32_t*)nullptr,
+                       aux.as<uint32_t>());
+    size_t sbytes = 0;
+    HIP_TRY(rocprim::inclusive_scan(nullptr, sbytes, aux.as<uint32_t>(), aux.as<uint32_t>(), (size_t)n, MaxOp(), st));
+    TRY(tmp.alloc(sbytes, "scan temp"));
+    HIP_TRY(rocprim::inclusive_scan(tmp.p, sbytes, aux.as<uint32_t>(), aux.as<uint32_t>(), (size_t)n, MaxOp(), st));
+    hipLaunchKernelGGL(k_assign, dim3(grid_for(n)), dim3(256), 0, st, skeys, n, (const uint32_t*)nullptr, sa_out,
+                       aux.as<uint32_t>(), rank.as<uint32_t>(), flags.as<uint8_t>());
+    HIP_TRY(hipGetLastError());
+    rocprim::counting_iterator<uint32_t> cit(0);
+    size_t selbytes = 0;
+    HIP_TRY(rocprim::select(nullptr, selbytes, cit, flags.as<uint8_t>(), list_a.as<uint32_t>(),
+                            counter.as<uint64_t>(), (size_t)n, st));
+    TRY(tmp.alloc(selbytes, "select temp"));
+    HIP_TRY(rocprim::select(tmp.p, selbytes, cit, flags.as<uint8_t>(), list_a.as<uint32_t>(), counter.as<uint64_t>(),
+                            (size_t)n, st));
+    uint64_t cnt = 0;
+    HIP_TRY(hipMemcpyAsync(&cnt, counter.p, 8, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+
+    // 3) doubling rounds over the tied elements only (keys_a/keys_b, vals_b reused)
+    uint32_t rounds = 0;
+    uint32_t* list = list_a.as<uint32_t>();
+    uint32_t* list_next = list_b.as<uint32_t>();
+    for (uint64_t h = 32; cnt > 0; h *= 2) {
+        if (h >= 2 * n + 64) SAS_FAIL(EIO, "sa construction did not converge");
+        rounds++;
+        uint64_t* rk = keys_a.as<uint64_t>();
+        uint64_t* rk2 = keys_b.as<uint64_t>();
+        uint32_t* rv = vals_b.as<uint32_t>();
+        uint32_t* rv2 = aux.as<uint32_t>();
+        hipLaunchKernelGGL(k_round_keys, dim3(grid_for(cnt)), dim3(256), 0, st, list, cnt, sa_out,
+                           rank.as<uint32_t>(), n, h, rk, rv);
+        rocprim::double_buffer<uint64_t> k2(rk, rk2);
+        rocprim::double_buffer<uint32_t> v2(rv, rv2);
+        size_t b2 = 0;
+        HIP_TRY(rocprim::radix_sort_pairs(nullptr, b2, k2, v2, (size_t)cnt, 0, 64, st));
+        TRY(tmp.alloc(b2, "round sort temp"));
+        HIP_TRY(rocprim::radix_sort_pairs(tmp.p, b2, k2, v2, (size_t)cnt, 0, 64, st));
+        const uint64_t* sk = k2.current();
+        uint32_t* sv = v2.current();
+        uint32_t* gbuf = (sv == rv) ? rv2 : rv;  // the free value buffer holds group ids
+        hipLaunchKernelGGL(k_scatter_sa, dim3(grid_for(cnt)), dim3(256), 0, st, list, cnt, sv, sa_out);
+        hipLaunchKernelGGL(k_heads, dim3(grid_for(cnt)), dim3(256), 0, st, sk, cnt, list, gbuf);
+        size_t b3 = 0;
+        HIP_TRY(rocprim::inclusive_scan(nullptr, b3, gbuf, gbuf, (size_t)cnt, MaxOp(), st));
+        TRY(tmp.alloc(b3, "round scan temp"));
+        HIP_TRY(rocprim::inclusive_scan(tmp.p, b3, gbuf, gbuf, (size_t)cnt, MaxOp(), st));
+        hipLaunchKernelGGL(k_assign, dim3(grid_for(cnt)), dim3(256), 0, st, sk, cnt, list, sa_out, gbuf,
+                           rank.as<uint32_t>(), flags.as<uint8_t>());
+        HIP_TRY(hipGetLastError());
+        size_t b4 = 0;
+        HIP_TRY(rocprim::select(nullptr, b4, list, flags.as<uint8_t>(), list_next, counter.as<uint64_t>(),
+                                (size_t)cnt, st));
+        TRY(tmp.alloc(b4, "round select temp"));
+        HIP_TRY(rocprim::select(tmp.p, b4, list, flags.as<uint8_t>(), list_next, counter.as<uint64_t>(),
+                                (size_t)cnt, st));
+        HIP_TRY(hipMemcpyAsync(&cnt, counter.p, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        uint32_t* t = list; list = list_next; list_next = t;
+    }
+    *rounds_out = rounds;
+    return 0;
+}
+
+// ------------------------------------------------------------------ LCP, verify
+__global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+                      uint32_t* __restrict__ lcp) {
+    GRID_STRIDE(r, n) {
+        if (r == 0) { lcp[0] = 0; continue; }
+        uint64_t a = sa[r - 1], b = sa[r];
+        uint64_t L = n - (a > b ? a : b);  // min suffix length
+        uint64_t l = 0;
+        while (l < L) {
+            uint64_t x = text_chars32(tw, a + l) ^ text_chars32(tw, b + l);
+            if (x) { l += __clzll(x) >> 1; break; }
+            l += 32;
+        }
+        lcp[r] = (uint32_t)(l < L ? l : L);
+    }
+}
+
+__global__ void k_verify_adj(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+                             uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bad) {
+    GRID_STRIDE(r, n) {
+        uint64_t b = sa[r];
+        if (b >= n) { atomicOr(bad, 1u); continue; }
+        atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+        if (r == 0) continue;
+        uint64_t a = sa[r - 1];
+        if (a >= n) continue;
+        uint64_t la = n - a, lb = n - b, L = la < lb ? la : lb, l = 0;
+        bool lt;
+        for (;;) {
+            if (l >= L) { lt = la < lb; break; }
+            uint64_t c = L - l < 32 ? L - l : 32;
+            uint64_t mk = chars_mask((uint32_t)c);
+            uint64_t x = text_chars32(tw, a + l) & mk, y = text_chars32(tw, b + l) & mk;
+            if (x != y) { lt = x < y; break; }
+            l += 32;
+        }
+        if (!lt) atomicOr(bad, 2u);  // sas/sa_search.rs:36-38 assert!(t[x..] < t[y..])
+    }
+}
+
+__global__ void k_count_bits(const uint32_t* __restrict__ bitmap, uint64_t words, unsigned long long* cnt) {
+    unsigned long long c = 0;
+    GRID_STRIDE(w, words) c += __popc(bitmap[w]);
+    if (c) atomicAdd(cnt, c);
+}
+
+// ------------------------------------------------------------------ S-tree over 16-char keys
+__global__ void k_keys16(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+                         uint32_t* __restrict__ leaves, uint64_t leaf_words) {
+    GRID_STRIDE(r, leaf_words) leaves[r] = r < n ? (uint32_t)(text_chars32(tw, sa[r]) >> 32) : SAS_KEY_MAX;
+}
+
+// One internal layer (sst/s_tree.rs:149-172 with left_max = false):
+// key j of node i = first key of child subtree j+1, MAX if beyond n.
+__global__ void k_stree_layer(uint32_t* __restrict__ tree, uint64_t oh, uint64_t layer_nodes, uint64_t ol,
+                              uint32_t h, uint32_t height, uint64_t n) {
+    const uint64_t B = SAS_STREE_B;
+    GRID_STRIDE(i, B * layer_nodes) {
+        uint64_t k = (i / B) * (B + 1) + (i % B) + 1;
+        for (uint32_t l = h; l + 2 < height; l++) k *= (B + 1);
+        tree[(oh + i / B) * 16 + (i % B)] = (k * B < n) ? tree[(ol + k) * 16] : SAS_KEY_MAX;
+    }
+}
+
+// TreeBase<16> (sst/s_tree.rs:22-45)
+static uint64_t tb_blocks(uint64_t n) { return (n + 15) / 16; }
+static uint64_t tb_prev(uint64_t n) { return (tb_blocks(n) + 16) / 17 * 16; }
+static uint32_t tb_height(uint64_t n) { return n <= 16 ? 1 : tb_height(tb_prev(n)) + 1; }
+static uint64_t tb_layer(uint64_t n, uint32_t h, uint32_t height) {
+    for (uint32_t i = h; i + 1 < height; i++) n = tb_prev(n);
+    return n;
+}
+
+// ------------------------------------------------------------------ LDS top of the binary search
+// Node k (1-based Eytzinger) = state after the path given by k's bits below
+// the leading one (0 = went left: r = mid, 1 = right: l = mid + 1).
+__global__ void k_top(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+                      uint64_t* __restrict__ top_key, uint32_t* __restrict__ top_sa, uint32_t nodes) {
+    GRID_STRIDE(k, nodes) {
+        if (k == 0) { top_key[0] = 0; top_sa[0] = 0xFFFFFFFFu; continue; }
+        uint64_t l = 0, r = n;
+        int depth = 63 - __clzll(k);
+        for (int b = depth - 1; b >= 0; b--) {
+            uint64_t mid = (l + r) >> 1;
+            if (l >= r) break;
+            if ((k >> b) & 1) l = mid + 1; else r = mid;
+        }
+        if (l < r) {
+            uint32_t p = sa[(l + r) >> 1];
+            top_sa[k] = p;
+            top_key[k] = text_chars32(tw, p);
+        } else {
+            top_sa[k] = 0xFFFFFFFFu;
+            top_key[k] = 0;
+        }
+    }
+}
+
+// ------------------------------------------------------------------ C ABI
+static void free_index(sas_index* x) {
+    if (!x) return;
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa};
+    for (void* p : ptrs) if (p) (void)hipFree(p);
+    delete x;
+}
+
+extern "C" int sas_free(sas_index* index) {
+    free_index(index);
+    return 0;
+}
+
+static uint64_t now_ns() {
+    return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+static int verify_impl(const sas_index* x) {
+    DevBuf bitmap, bad;
+    uint64_t words = (x->n + 31) / 32;
+    TRY(bitmap.alloc(words * 4, "verify bitmap"));
+    TRY(bad.alloc(16, "verify flags"));
+    HIP_TRY(hipMemset(bitmap.p, 0, words * 4));
+    HIP_TRY(hipMemset(bad.p, 0, 16));
+    hipLaunchKernelGGL(k_verify_adj, dim3(grid_for(x->n)), dim3(256), 0, 0, x->text_w, x->n, x->sa,
+                       bitmap.as<uint32_t>(), bad.as<uint32_t>());
+    hipLaunchKernelGGL(k_count_bits, dim3(grid_for(words)), dim3(256), 0, 0, bitmap.as<uint32_t>(), words,
+                       reinterpret_cast<unsigned long long*>(bad.as<uint32_t>() + 2));
+    HIP_TRY(hipGetLastError());
+    uint32_t h[4];
+    HIP_TRY(hipMemcpy(h, bad.p, 16, hipMemcpyDeviceToHost));
+    uint64_t seen = (uint64_t)h[2] | ((uint64_t)h[3] << 32);
+    if (h[0] & 1) SAS_FAIL(EINVAL, "suffix array holds an entry >= n");
+    if (h[0] & 2) SAS_FAIL(EINVAL, "suffix array not sorted: adjacent suffixes not strictly increasing");
+    if (seen != x->n) SAS_FAIL(EINVAL, "suffix array is not a permutation of 0..n");
+    return 0;
+}
+
+extern "C" int sas_verify(const sas_index* index) {
+    if (!index) SAS_FAIL(EINVAL, "sas_verify: null index");
+    HIP_TRY(hipSetDevice(index->device));
+    return verify_impl(index);
+}
+
+static int build_stree(sas_index* x) {
+    uint64_t n = x->n;
+    uint32_t height = tb_height(n);
+    if (height > SAS_STREE_MAX_LAYERS) SAS_FAIL(ENOTSUP, "S-tree too high");
+    uint64_t ls[SAS_STREE_MAX_LAYERS], tot = 0;
+    for (uint32_t h = 0; h < height; h++) {
+        ls[h] = (tb_layer(n, h, height) + 15) / 16;
+        x->stree_off[h] = tot;
+        tot += ls[h];
+    }
+    DevBuf t;
+    TRY(t.alloc(tot * 64, "S-tree"));
+    uint32_t* tree = t.as<uint32_t>();
+    uint64_t ol = x->stree_off[height - 1];
+    hipLaunchKernelGGL(k_keys16, dim3(grid_for(ls[height - 1] * 16)), dim3(256), 0, 0, x->text_w, n, x->sa,
+                       tree + ol * 16, ls[height - 1] * 16);
+    for (int h = (int)height - 2; h >= 0; h--) {
+        // internal nodes: slots B..N stay MAX (B == N == 16 here, so none)
+        hipLaunchKernelGGL(k_stree_layer, dim3(grid_for(16 * ls[h])), dim3(256), 0, 0, tree, x->stree_off[h],
+                           ls[h], ol, (uint32_t)h, height, n);
+    }
+    HIP_TRY(hipGetLastError());
+    x->stree = static_cast<uint32_t*>(t.release());
+    x->stree_nodes = tot;
+    x->stree_height = height;
+    uint32_t lds_layers = 0;
+    uint64_t lds_nodes = 0;
+    for (uint32_t h = 0; h + 1 < height; h++) {
+        if (lds_nodes + ls[h] > SAS_STREE_LDS_NODES) break;
+        lds_nodes += ls[h];
+        lds_layers++;
+    }
+    x->stree_lds_layers = lds_layers;
+    x->stree_lds_nodes = (uint32_t)lds_nodes;
+    return 0;
+}
+
+extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
+                         sas_index** out) {
+    if (!out) SAS_FAIL(EINVAL, "sas_build: null out");
+    *out = nullptr;
+    if (n == 0) SAS_FAIL(EINVAL, "sas_build: empty text");
+    if (!text) SAS_FAIL(EINVAL, "sas_build: null text");
+    if (n >= (1ull << 32) - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^32 needs a 40/64-bit SA (not built yet)");
+    if (sa_or_null && sa_width != 4) SAS_FAIL(EINVAL, "sas_build: only sa_width 4 (u32) is supported");
+    if (!sa_or_null && n >= (1ull << 31)) SAS_FAIL(ENOTSUP, "sas_build: GPU SA construction needs n < 2^31");
+    uint64_t t0 = now_ns();
+    sas_index* x = new sas_index();
+    x->n = n;
+    HIP_TRY(hipGetDevice(&x->device));
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, x->device) == hipSuccess) x->num_cus = prop.multiProcessorCount;
+    struct Guard { sas_index*& p; ~Guard() { if (p) free_index(p); } } guard{x};
+    bool dev = flags & SAS_DEVICE_PTRS;
+
+    // text -> packed words
+    DevBuf tbytes, bad, tw;
+    const uint8_t* dtext = text;
+    if (!dev) {
+        TRY(tbytes.alloc(n, "text bytes"));
+        HIP_TRY(hipMemcpy(tbytes.p, text, n, hipMemcpyHostToDevice));
+        dtext = tbytes.as<uint8_t>();
+    }
+    x->text_words = (n + 31) / 32 + SAS_TEXT_PAD_WORDS;
+    TRY(tw.alloc(x->text_words * 8, "packed text"));
+    TRY(bad.alloc(4, "flag"));
+    HIP_TRY(hipMemset(bad.p, 0, 4));
+    hipLaunchKernelGGL(k_pack_text, dim3(grid_for(x->text_words)), dim3(256), 0, 0, dtext, n, tw.as<uint64_t>(),
+                       x->text_words, bad.as<uint32_t>());
+    HIP_TRY(hipGetLastError());
+    uint32_t hbad = 0;
+    HIP_TRY(hipMemcpy(&hbad, bad.p, 4, hipMemcpyDeviceToHost));
+    if (hbad) SAS_FAIL(EINVAL, "sas_build: text bytes must be DNA codes 0..3");
+    tbytes.alloc(0, "free");
+    x->text_w = tw.as<uint64_t>();
+    tw.release();
+
+    // suffix array
+    DevBuf sa;
+    TRY(sa.alloc(n * 4, "suffix array"));
+    x->sa = sa.as<uint32_t>();
+    sa.release();
+    if (sa_or_null) {
+        HIP_TRY(hipMemcpy(x->sa, sa_or_null, n * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+        if (flags & SAS_BUILD_VERIFY) TRY(verify_impl(x));
+    } else {
+        uint64_t s0 = now_ns();
+        TRY(build_sa_gpu(x->text_w, n, x->sa, &x->stats.sa_rounds));
+        HIP_TRY(hipDeviceSynchronize());
+        x->stats.build_sa_ns = now_ns() - s0;
+        if (flags & SAS_BUILD_VERIFY) TRY(verify_impl(x));
+    }
+
+    if (flags & SAS_BUILD_LCP) {
+        DevBuf l;
+        TRY(l.alloc(n * 4, "lcp"));
+        hipLaunchKernelGGL(k_lcp, dim3(grid_for(n)), dim3(256), 0, 0, x->text_w, n, x->sa, l.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+        x->lcp = static_cast<uint32_t*>(l.release());
+    }
+    if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
+
+    // binary-search top in LDS
+    {
+        uint32_t iters = 64 - __builtin_clzll(n);  // ilog2(n) + 1 (sas/sa_search.rs:171)
+        x->iters = iters;
+        x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
+        DevBuf k, s;
+        TRY(k.alloc(SAS_TOP_NODES * 8, "top keys"));
+        TRY(s.alloc(SAS_TOP_NODES * 4, "top sa"));
+        hipLaunchKernelGGL(k_top, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, n, x->sa,
+                           k.as<uint64_t>(), s.as<uint32_t>(), (uint32_t)SAS_TOP_NODES);
+        HIP_TRY(hipGetLastError());
+        x->top_key = static_cast<uint64_t*>(k.release());
+        x->top_sa = static_cast<uint32_t*>(s.release());
+    }
+    HIP_TRY(hipDeviceSynchronize());
+
+    sas_stats& st = x->stats;
+    st.n = n;
+    st.text_bytes = x->text_words * 8;
+    st.sa_bytes = n * 4;
+    st.lcp_bytes = x->lcp ? n * 4 : 0;
+    st.stree_bytes = x->stree_nodes * 64;
+    st.stree_layers = x->stree_height;
+    st.stree_lds_layers = x->stree_lds_layers;
+    st.top_levels = x->top_levels;
+    st.iterations = x->iters;
+    st.build_total_ns = now_ns() - t0;
+    *out = x;
+    x = nullptr;  // disarm guard
+    return 0;
+}
+
+extern "C" int sas_get_stats(const sas_index* index, sas_stats* out) {
+    if (!index || !out) SAS_FAIL(EINVAL, "sas_get_stats: null argument");
+    *out = index->stats;
+    return 0;
+}
+
+static int copy_out(const void* src, void* dst, uint64_t bytes, uint32_t flags) {
+    HIP_TRY(hipMemcpy(dst, src, bytes, (flags & SAS_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost));
+    return 0;
+}
+
+extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
+    if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_sa: null argument");
+    if (count > index->n) SAS_FAIL(EINVAL, "sas_copy_sa: count > n");
+    return copy_out(index->sa, dst, count * 4, flags);
+}
+
+extern "C" int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
+    if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_lcp: null argument");
+    if (!index->lcp) SAS_FAIL(EINVAL, "sas_copy_lcp: index built without SAS_BUILD_LCP");
+    if (count > index->n) SAS_FAIL(EINVAL, "sas_copy_lcp: count > n");
+    return copy_out(index->lcp, dst, count * 4, flags);
+}

@@ -1,0 +1,432 @@
+// sas_search.hip -- batched suffix-array lookup kernels for gfx950 (MI355X).
+//
+// Every algorithm returns SA[lower_bound(q)] under Rust slice order, i.e. the
+// result of binary_search (sas/sa_search.rs:98-112), bit for bit.
+//
+//   PLAIN  one lane per query, the whole wave64 walks 64 queries in lockstep for
+//          ilog2(n)+1 iterations exactly like binary_search_batch<64>
+//          (sas/sa_search.rs:157-196).  The first SAS_TOP_LEVELS probes of every
+//          query hit the same 4095 pivots; they are served from LDS (pivot SA
+//          value + 32-char packed key), so those probes cost no HBM traffic.
+//          The lane remembers SA[r] of the last right move, so the final
+//          `sa[l]` (:195) needs no extra load.
+//   LCP    PLAIN + Manber-Myers mlr skipping: chars [0, min(llcp, rlcp)) are known
+//          equal and are not compared again (sas/sa_search.rs:344-345 TODO).
+//   STREE  descend an STree<16,16> over the 16-char keys of the SA (top layers in
+//          LDS), giving the key range [r0, r1) of suffixes whose padded 16-char
+//          prefix equals the query's; the lower bound lies in [r0, r1] and is
+//          found by an exact binary search there (mlr skipping from char 16).
+//
+// Text compares are 2-bit packed: 32 chars per u64 compare.
+#include "common.hpp"
+
+#include <chrono>
+#include <vector>
+
+#define SEARCH_BLOCK 1024
+#define BLOCKS_PER_CU 2
+
+struct SearchArgs {
+    const uint64_t* tw;
+    uint64_t n;
+    const uint32_t* sa;
+    const uint64_t* top_key;
+    const uint32_t* top_sa;
+    uint32_t top_levels;
+    uint32_t iters;
+    const uint32_t* stree;
+    uint64_t stree_off[SAS_STREE_MAX_LAYERS];
+    uint32_t stree_height;
+    uint32_t stree_lds_layers;
+    uint32_t stree_lds_nodes;
+    const uint8_t* qbytes;
+    const uint64_t* qoff;
+    const uint32_t* qlen;
+    uint32_t m_fixed;
+    uint64_t nq;
+    uint64_t* out_pos;
+    uint32_t* out_probes;
+    uint32_t* bad;
+};
+
+__device__ __forceinline__ void query_ptr(const SearchArgs& a, uint64_t i, const uint8_t** qb, uint32_t* m) {
+    if (a.qoff) {
+        *qb = a.qbytes + a.qoff[i];
+        *m = a.qlen[i];
+    } else {
+        *qb = a.qbytes + i * (uint64_t)a.m_fixed;
+        *m = a.m_fixed;
+    }
+}
+
+// ------------------------------------------------------------------ PLAIN / LCP
+template <int QW, bool LCP, bool TOP>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
+    __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
+    __shared__ uint32_t s_sa[TOP ? SAS_TOP_NODES : 1];
+    uint32_t D = 0;
+    if (TOP) {
+        D = a.top_levels;
+        uint32_t nodes = 1u << D;
+        for (uint32_t k = threadIdx.x; k < nodes; k += blockDim.x) {
+            s_key[k] = a.top_key[k];
+            s_sa[k] = a.top_sa[k];
+        }
+        __syncthreads();
+    }
+    uint32_t bad = 0;
+    const uint64_t n = a.n;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+
+        uint64_t l = 0, r = n;
+        uint32_t k = 1, probes = 0, llcp = 0, rlcp = 0;
+        uint32_t pr = 0;  // SA[r] once r has moved
+        for (uint32_t it = 0; it < a.iters; ++it) {
+            if (l < r) {
+                uint64_t mid = (l + r) >> 1;
+                uint32_t h = LCP ? (llcp < rlcp ? llcp : rlcp) : 0u;
+                uint32_t p, lcp;
+                bool lt;
+                if (TOP && it < D) {
+                    p = s_sa[k];
+                    lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
+                    k = 2 * k + (lt ? 1u : 0u);
+                } else {
+                    p = a.sa[mid];
+                    lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
+                }
+                probes++;
+                if (lt) {
+                    l = mid + 1;
+                    llcp = lcp;
+                } else {
+                    r = mid;
+                    rlcp = lcp;
+                    pr = p;
+                }
+            }
+        }
+        a.out_pos[i] = (r >= n) ? n : (uint64_t)pr;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// ------------------------------------------------------------------ STREE
+__device__ __forceinline__ void cnt_node(const uint4* node, uint32_t K, uint32_t* lt, uint32_t* eq) {
+    uint32_t c = 0, e = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint4 v = node[j];
+        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
+        e += (v.x == K) + (v.y == K) + (v.z == K) + (v.w == K);
+    }
+    *lt = c;
+    *eq = e;
+}
+
+__device__ __forceinline__ uint32_t cnt_lt_node(const uint4* node, uint32_t K) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint4 v = node[j];
+        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
+    }
+    return c;
+}
+
+// Descend the internal layers for key K; returns the leaf node index (within
+// the leaf layer).  sst/s_tree.rs:196-203 with unsigned keys.
+__device__ __forceinline__ uint64_t stree_descend(const SearchArgs& a, const uint4* s_nodes, uint32_t K,
+                                                  uint32_t* probes) {
+    uint64_t k = 0;
+    const uint4* g = reinterpret_cast<const uint4*>(a.stree);
+    for (uint32_t h = 0; h + 1 < a.stree_height; h++) {
+        const uint4* node = (h < a.stree_lds_layers) ? s_nodes + (a.stree_off[h] + k) * 4
+                                                     : g + (a.stree_off[h] + k) * 4;
+        k = k * (SAS_STREE_B + 1) + cnt_lt_node(node, K);
+        (*probes)++;
+    }
+    return k;
+}
+
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
+    __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.stree);
+        for (uint32_t w = threadIdx.x; w < a.stree_lds_nodes * 4; w += blockDim.x) s_nodes[w] = g[w];
+        __syncthreads();
+    }
+    uint32_t bad = 0;
+    const uint64_t n = a.n;
+    const uint4* g = reinterpret_cast<const uint4*>(a.stree);
+    const uint64_t ol = a.stree_off[a.stree_height - 1];
+    const uint64_t leaf_nodes = (n + 15) / 16;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint32_t K = (uint32_t)(q.w[0] >> 32);  // padded 16-char key of q
+        uint32_t probes = 0;
+
+        uint64_t k = stree_descend(a, s_nodes, K, &probes);
+        uint32_t c, e;
+        cnt_node(g + (ol + k) * 4, K, &c, &e);
+        probes++;
+        uint64_t r0 = k * 16 + c;
+        uint64_t r1 = r0 + e;
+        if (c + e == 16) {  // the run of equal keys may continue in the next leaves
+            uint64_t kk = k + 1;
+            int steps = 0;
+            for (; kk < leaf_nodes && steps < 4; kk++, steps++) {
+                uint32_t c2, e2;
+                cnt_node(g + (ol + kk) * 4, K, &c2, &e2);
+                probes++;
+                r1 += e2;
+                if (e2 < 16) break;
+            }
+            if (kk < leaf_nodes && steps == 4) {  // long run: lower_bound(K + 1)
+                if (K == SAS_KEY_MAX) {
+                    r1 = n;
+                } else {
+                    uint64_t k2 = stree_descend(a, s_nodes, K + 1, &probes);
+                    r1 = k2 * 16 + cnt_lt_node(g + (ol + k2) * 4, K + 1);
+                    probes++;
+                }
+            }
+        }
+        if (r0 > n) r0 = n;
+        if (r1 > n) r1 = n;
+
+        // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
+        const uint32_t h16 = m < 16 ? m : 16;
+        uint64_t l = r0, r = r1;
+        uint32_t llcp = h16, rlcp = h16, pr = 0;
+        bool have = false;
+        while (l < r) {
+            uint64_t mid = (l + r) >> 1;
+            uint32_t p = a.sa[mid], lcp;
+            uint32_t h = llcp < rlcp ? llcp : rlcp;
+            bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
+            probes++;
+            if (lt) {
+                l = mid + 1;
+                llcp = lcp;
+            } else {
+                r = mid;
+                rlcp = lcp;
+                pr = p;
+                have = true;
+            }
+        }
+        uint64_t pos;
+        if (l >= n) pos = n;
+        else if (have) pos = pr;
+        else pos = a.sa[l];
+        a.out_pos[i] = pos;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// ------------------------------------------------------------------ host dispatch
+static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
+    uint64_t blocks = (a.nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return 0;
+    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
+    bool top = !(flags & SAS_NO_LDS_TOP);
+#define QW_CASE(KERNEL_T)                                                           \
+    switch (qw) {                                                                   \
+        case 1: hipLaunchKernelGGL(KERNEL_T(1), grid, block, 0, st, a); break;      \
+        case 2: hipLaunchKernelGGL(KERNEL_T(2), grid, block, 0, st, a); break;      \
+        case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
+        default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
+    }
+#define K_PLAIN_TOP(Q) (k_sa_binary<Q, false, true>)
+#define K_PLAIN(Q) (k_sa_binary<Q, false, false>)
+#define K_LCP_TOP(Q) (k_sa_binary<Q, true, true>)
+#define K_LCP(Q) (k_sa_binary<Q, true, false>)
+#define K_STREE(Q) (k_sa_stree<Q>)
+    if (algo == SAS_ALGO_PLAIN) {
+        if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
+    } else if (algo == SAS_ALGO_LCP) {
+        if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
+    } else {
+        QW_CASE(K_STREE)
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+static int qw_for(uint64_t maxlen) {
+    if (maxlen <= 32) return 1;
+    if (maxlen <= 64) return 2;
+    if (maxlen <= 128) return 4;
+    return 8;
+}
+
+static void fill_args(const sas_index* x, SearchArgs& a) {
+    a.tw = x->text_w;
+    a.n = x->n;
+    a.sa = x->sa;
+    a.top_key = x->top_key;
+    a.top_sa = x->top_sa;
+    a.top_levels = x->top_levels;
+    a.iters = x->iters;
+    a.stree = x->stree;
+    for (int h = 0; h < SAS_STREE_MAX_LAYERS; h++) a.stree_off[h] = x->stree_off[h];
+    a.stree_height = x->stree_height;
+    a.stree_lds_layers = x->stree_lds_layers;
+    a.stree_lds_nodes = x->stree_lds_nodes;
+}
+
+struct AsyncBuf {
+    void* p = nullptr;
+    hipStream_t st = 0;
+    ~AsyncBuf() { if (p) (void)hipFreeAsync(p, st); }
+};
+
+static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
+                       uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
+                       void* stream, uint32_t flags) {
+    if (!x) SAS_FAIL(EINVAL, "search: null index");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_STREE) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "search: SAS_ALGO_STREE needs SAS_BUILD_STREE");
+    if (nq == 0) return 0;
+    if (!out_pos) SAS_FAIL(EINVAL, "search: null out_pos");
+    if (!qbytes) SAS_FAIL(EINVAL, "search: null qbytes");
+    bool ragged = qoff != nullptr;
+    if (ragged && !qlen) SAS_FAIL(EINVAL, "search: qoff without qlen");
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    bool dev = flags & SAS_DEVICE_PTRS;
+
+    SearchArgs a{};
+    fill_args(x, a);
+    a.nq = nq;
+    a.m_fixed = m_fixed;
+    AsyncBuf bqb, bqoff, bqlen, bout, bprobes, bbad;
+    bbad.st = st;
+    HIP_TRY(hipMallocAsync(&bbad.p, 4, st));
+    HIP_TRY(hipMemsetAsync(bbad.p, 0, 4, st));
+    a.bad = static_cast<uint32_t*>(bbad.p);
+
+    int qw = 4;
+    if (dev) {
+        a.qbytes = qbytes;
+        a.qoff = qoff;
+        a.qlen = qlen;
+        a.out_pos = out_pos;
+        a.out_probes = out_probes;
+        if (!ragged) qw = qw_for(m_fixed);
+    } else {
+        uint64_t span;
+        uint64_t maxlen = m_fixed;
+        if (ragged) {
+            span = 0;
+            maxlen = 0;
+            for (uint64_t k = 0; k < nq; k++) {
+                uint64_t e = qoff[k] + qlen[k];
+                if (e > span) span = e;
+                if (qlen[k] > maxlen) maxlen = qlen[k];
+            }
+        } else {
+            span = nq * (uint64_t)m_fixed;
+        }
+        qw = qw_for(maxlen);
+        bqb.st = bqoff.st = bqlen.st = bout.st = bprobes.st = st;
+        HIP_TRY(hipMallocAsync(&bqb.p, span + 64, st));
+        HIP_TRY(hipMemcpyAsync(bqb.p, qbytes, span, hipMemcpyHostToDevice, st));
+        a.qbytes = static_cast<const uint8_t*>(bqb.p);
+        if (ragged) {
+            HIP_TRY(hipMallocAsync(&bqoff.p, nq * 8, st));
+            HIP_TRY(hipMallocAsync(&bqlen.p, nq * 4, st));
+            HIP_TRY(hipMemcpyAsync(bqoff.p, qoff, nq * 8, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMemcpyAsync(bqlen.p, qlen, nq * 4, hipMemcpyHostToDevice, st));
+            a.qoff = static_cast<const uint64_t*>(bqoff.p);
+            a.qlen = static_cast<const uint32_t*>(bqlen.p);
+        }
+        HIP_TRY(hipMallocAsync(&bout.p, nq * 8, st));
+        a.out_pos = static_cast<uint64_t*>(bout.p);
+        if (out_probes) {
+            HIP_TRY(hipMallocAsync(&bprobes.p, nq * 4, st));
+            a.out_probes = static_cast<uint32_t*>(bprobes.p);
+        }
+    }
+    int rc = launch_search(x, a, algo, qw, flags, st);
+    if (rc) return rc;
+    if (!dev) {
+        HIP_TRY(hipMemcpyAsync(out_pos, a.out_pos, nq * 8, hipMemcpyDeviceToHost, st));
+        if (out_probes) HIP_TRY(hipMemcpyAsync(out_probes, a.out_probes, nq * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (!dev || (flags & SAS_VALIDATE)) {
+        uint32_t hbad = 0;
+        HIP_TRY(hipMemcpyAsync(&hbad, a.bad, 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (hbad && ((flags & SAS_VALIDATE) || !dev)) SAS_FAIL(EINVAL, "search: query bytes must be DNA codes 0..3");
+    }
+    return 0;
+}
+
+extern "C" int sas_search_batch(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,
+                                const uint32_t* qlen, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
+                                void* stream, uint32_t flags) {
+    if (nq && (!qoff || !qlen)) SAS_FAIL(EINVAL, "sas_search_batch: null qoff/qlen");
+    return search_impl(index, qbytes, qoff, qlen, 0, nq, algo, out_pos, out_probes, stream, flags);
+}
+
+extern "C" int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, uint64_t nq, int algo,
+                                uint64_t* out_pos, uint32_t* out_probes, void* stream, uint32_t flags) {
+    return search_impl(index, qbytes, nullptr, nullptr, m, nq, algo, out_pos, out_probes, stream, flags);
+}
+
+extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint32_t m, uint64_t nq, int algo,
+                              uint64_t* d_out_pos, int reps, void* stream, uint32_t flags, double* kernel_ns,
+                              double* call_ns) {
+    if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
+    if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SearchArgs a{};
+    fill_args(x, a);
+    a.nq = nq;
+    a.m_fixed = m;
+    a.qbytes = d_qbytes;
+    a.out_pos = d_out_pos;
+    void* bad = nullptr;
+    HIP_TRY(hipMalloc(&bad, 4));
+    a.bad = static_cast<uint32_t*>(bad);
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipStreamSynchronize(st));
+    auto t0 = std::chrono::steady_clock::now();
+    HIP_TRY(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; r++) {
+        int rc = launch_search(x, a, algo, qw_for(m), flags | SAS_DEVICE_PTRS, st);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    auto t1 = std::chrono::steady_clock::now();
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    if (kernel_ns) *kernel_ns = ms * 1e6 / reps;
+    if (call_ns) *call_ns = std::chrono::duration<double, std::nano>(t1 - t0).count() / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    (void)hipFree(bad);
+    return 0;
+}

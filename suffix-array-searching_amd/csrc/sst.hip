@@ -1,0 +1,375 @@
+// sst.hip -- GPU static search tree over sorted u32 keys (drop-in for the
+// reference's static-search-tree crate, sst/).
+//
+// Layouts are built on the host exactly as the reference builds them, then
+// moved to HBM; queries run one lane per query with the top tree layers
+// staged in LDS:
+//   SST_SORTED     SortedVec::binary_search          sst/binary_search.rs:37-49
+//   SST_EYTZINGER  Eytzinger::search_branchless      sst/eytzinger.rs:90-102,19-31
+//   SST_STREE16/15 STree::search (find_popcnt)       sst/s_tree.rs:196-206, sst/node.rs:93-109
+#include "common.hpp"
+
+#include <cstring>
+#include <vector>
+
+#define SST_BLOCK 1024
+#define SST_EYT_LDS 8192  // first 13 Eytzinger levels (32 KiB) in LDS
+
+static constexpr uint32_t SST_MAX = 0x7fffffffu;  // sst/node.rs:5
+
+struct SstArgs {
+    const uint32_t* nodes;
+    uint64_t n;
+    uint64_t off[SAS_STREE_MAX_LAYERS];
+    uint32_t lds_off[SAS_STREE_MAX_LAYERS];
+    uint32_t height;
+    uint32_t B;
+    uint32_t lds_layers;
+    uint32_t lds_nodes;
+    uint32_t eyt_iters;
+    const uint32_t* qs;
+    uint64_t nq;
+    uint32_t* out;
+    uint64_t* rank;
+};
+
+// count of keys < q under SIGNED compare (find_popcnt, sst/node.rs:93-109)
+__device__ __forceinline__ uint32_t popcnt_find(const uint4* node, int32_t q) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint4 v = node[j];
+        c += (q > (int32_t)v.x) + (q > (int32_t)v.y) + (q > (int32_t)v.z) + (q > (int32_t)v.w);
+    }
+    return c;
+}
+
+template <bool TOP>
+__global__ __launch_bounds__(SST_BLOCK) void k_sst_stree(SstArgs a) {
+    __shared__ uint4 s_nodes[TOP ? SAS_STREE_LDS_NODES * 4 : 1];
+    const uint4* g = reinterpret_cast<const uint4*>(a.nodes);
+    if (TOP) {
+        for (uint32_t h = 0; h < a.lds_layers; h++) {
+            uint32_t cnt = ((h + 1 < a.lds_layers) ? a.lds_off[h + 1] : a.lds_nodes) - a.lds_off[h];
+            for (uint32_t w = threadIdx.x; w < cnt * 4; w += blockDim.x)
+                s_nodes[a.lds_off[h] * 4 + w] = g[a.off[h] * 4 + w];
+        }
+        __syncthreads();
+    }
+    const uint32_t B = a.B;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t q = a.qs[i];
+        uint64_t k = 0;
+        for (uint32_t h = 0; h + 1 < a.height; h++) {
+            const uint4* node = (TOP && h < a.lds_layers) ? s_nodes + (a.lds_off[h] + k) * 4 : g + (a.off[h] + k) * 4;
+            k = k * (B + 1) + popcnt_find(node, (int32_t)q);
+        }
+        uint64_t o = a.off[a.height - 1];
+        uint32_t idx = popcnt_find(g + (o + k) * 4, (int32_t)q);
+        a.out[i] = a.nodes[(o + k + idx / 16) * 16 + idx % 16];
+        if (a.rank) a.rank[i] = k * B + idx;
+    }
+}
+
+__global__ __launch_bounds__(SST_BLOCK) void k_sst_eytzinger(SstArgs a) {
+    __shared__ uint32_t s_e[SST_EYT_LDS];
+    uint64_t len = a.n + 1;
+    uint32_t lds = len < SST_EYT_LDS ? (uint32_t)len : SST_EYT_LDS;
+    for (uint32_t w = threadIdx.x; w < lds; w += blockDim.x) s_e[w] = a.nodes[w];
+    __syncthreads();
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t q = a.qs[i];
+        uint64_t idx = 1;
+        for (uint32_t it = 0; it < a.eyt_iters; it++) {
+            uint32_t v = idx < lds ? s_e[idx] : a.nodes[idx];
+            idx = 2 * idx + (q > v ? 1 : 0);
+        }
+        bool inb = idx < len;  // get_next_index_branchless (sst/eytzinger.rs:19-31)
+        uint32_t v = a.nodes[inb ? idx : 0];
+        idx = 2 * idx + (((q > v) || !inb) ? 1 : 0);
+        idx >>= (__ffsll((long long)~idx));  // search_result_to_index: >> (trailing_ones + 1)
+        a.out[i] = a.nodes[idx];
+    }
+}
+
+__global__ __launch_bounds__(SST_BLOCK) void k_sst_sorted(SstArgs a) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t q = a.qs[i];
+        uint64_t l = 0, r = a.n;
+        while (l < r) {
+            uint64_t m = (l + r) >> 1;
+            if (a.nodes[m] < q) l = m + 1;
+            else r = m;
+        }
+        a.out[i] = l < a.n ? a.nodes[l] : 0xFFFFFFFFu;
+        if (a.rank) a.rank[i] = l;
+    }
+}
+
+// ------------------------------------------------------------------ host builders
+// TreeBase<B> (sst/s_tree.rs:22-45)
+static uint64_t blocks_of(uint64_t n, uint64_t B) { return (n + B - 1) / B; }
+static uint64_t prev_keys(uint64_t n, uint64_t B) { return (blocks_of(n, B) + B) / (B + 1) * B; }
+static uint32_t height_of(uint64_t n, uint64_t B) { return n <= B ? 1 : height_of(prev_keys(n, B), B) + 1; }
+static uint64_t layer_size(uint64_t n, uint32_t h, uint32_t height, uint64_t B) {
+    for (uint32_t i = h; i + 1 < height; i++) n = prev_keys(n, B);
+    return n;
+}
+
+// STree::new_params (sst/s_tree.rs:72-176).  The node array starts zeroed
+// like the reference's fresh hugepage allocation (:125-129).
+static int build_stree_host(const uint32_t* vals, uint64_t n, uint32_t B, bool left_max, bool reverse, bool full,
+                            std::vector<uint32_t>& tree, sst_index* x) {
+    const uint32_t N = 16;
+    if (full && reverse) SAS_FAIL(EINVAL, "sst_build: full array only makes sense in forward layout");
+    for (uint64_t i = 0; i < n; i++)
+        if (vals[i] > SST_MAX) SAS_FAIL(EINVAL, "sst_build: S-tree keys must be <= i32::MAX (sst/node.rs:5)");
+    uint32_t height = height_of(n, B);
+    if (height > SAS_STREE_MAX_LAYERS) SAS_FAIL(ENOTSUP, "sst_build: tree too high");
+    uint64_t ls[SAS_STREE_MAX_LAYERS], nb = 0;
+    for (uint32_t h = 0; h < height; h++) {
+        if (full) {
+            uint64_t s = 1;
+            for (uint32_t k = 0; k < h; k++) s *= (B + 1);
+            ls[h] = s;
+        } else {
+            ls[h] = (layer_size(n, h, height, B) + B - 1) / B;
+        }
+        nb += ls[h];
+    }
+    uint64_t sum = 0;
+    for (uint32_t h = 0; h < height; h++) {
+        if (!reverse) { x->off[h] = sum; sum += ls[h]; }
+        else { sum += ls[h]; x->off[h] = nb - sum; }
+        x->layer_nodes[h] = ls[h];
+    }
+    tree.assign(nb * N, 0u);
+    auto node = [&](uint64_t b) { return tree.data() + b * N; };
+    uint64_t ol = x->off[height - 1];
+    for (uint64_t i = 0; i < n; i++) {
+        node(ol + i / B)[i % B] = vals[i];
+        if (B < N && i % B == 0 && i > 0) node(ol + i / B - 1)[B] = vals[i];
+    }
+    if (n / B < ls[height - 1])
+        for (uint64_t j = n % B; j < N; j++) node(ol + n / B)[j] = SST_MAX;
+    for (int h = (int)height - 2; h >= 0; h--) {
+        uint64_t oh = x->off[h];
+        std::fill(tree.begin() + oh * N, tree.begin() + (oh + ls[h]) * N, SST_MAX);
+        for (uint64_t i = 0; i < (uint64_t)B * ls[h]; i++) {
+            uint64_t k = i / B, j = i % B;
+            k = k * (B + 1) + j + 1;
+            for (uint32_t l = (uint32_t)h; l + 2 < height; l++) k *= (B + 1);
+            node(oh + i / B)[i % B] =
+                k * B < n ? (!left_max ? node(ol + k)[0] : node(ol + k - 1)[B - 1]) : SST_MAX;
+        }
+    }
+    x->height = height;
+    x->B = B;
+    x->N = N;
+    // LDS-staged top layers
+    uint32_t L = 0, nodes = 0;
+    for (uint32_t h = 0; h + 1 < height; h++) {
+        if (nodes + ls[h] > SAS_STREE_LDS_NODES) break;
+        nodes += (uint32_t)ls[h];
+        L++;
+    }
+    x->lds_layers = L;
+    x->lds_nodes = nodes;
+    return 0;
+}
+
+// Eytzinger::new (sst/eytzinger.rs:37-63), iterative in-order fill.
+static void build_eytzinger_host(const uint32_t* vals, uint64_t n, std::vector<uint32_t>& e) {
+    e.assign(n + 1, 0);
+    e[0] = 0xFFFFFFFFu;
+    uint64_t i = 0, k = 1;
+    std::vector<uint64_t> stack;
+    while (k <= n || !stack.empty()) {
+        while (k <= n) { stack.push_back(k); k *= 2; }
+        k = stack.back();
+        stack.pop_back();
+        e[k] = vals[i++];
+        k = 2 * k + 1;
+    }
+}
+
+// ------------------------------------------------------------------ C ABI
+extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, uint32_t flags, sst_index** out) {
+    if (!out) SAS_FAIL(EINVAL, "sst_build: null out");
+    *out = nullptr;
+    if (n == 0 || !sorted_vals) SAS_FAIL(EINVAL, "sst_build: empty input (the reference asserts n > 0)");
+    for (uint64_t i = 1; i < n; i++)
+        if (sorted_vals[i - 1] > sorted_vals[i]) SAS_FAIL(EINVAL, "sst_build: values are not sorted");
+    sst_index* x = new sst_index();
+    x->layout = layout;
+    x->flags = flags;
+    x->n = n;
+    HIP_TRY(hipGetDevice(&x->num_cus));  // temporarily the device id
+    {
+        hipDeviceProp_t prop;
+        int dev = x->num_cus;
+        x->num_cus = 256;
+        if (hipGetDeviceProperties(&prop, dev) == hipSuccess) x->num_cus = prop.multiProcessorCount;
+    }
+    std::vector<uint32_t> host;
+    int rc = 0;
+    switch (layout) {
+        case SST_SORTED:
+            host.assign(sorted_vals, sorted_vals + n);
+            break;
+        case SST_EYTZINGER:
+            build_eytzinger_host(sorted_vals, n, host);
+            {
+                uint64_t len = n + 1;
+                x->height = 63 - __builtin_clzll(len);  // num_iters = ilog2(len)
+            }
+            break;
+        case SST_STREE16:
+        case SST_STREE15:
+            rc = build_stree_host(sorted_vals, n, layout == SST_STREE16 ? 16 : 15, flags & SST_LEFT_MAX,
+                                  flags & SST_REVERSE, flags & SST_FULL, host, x);
+            break;
+        default:
+            rc = EINVAL;
+            sas_set_error(EINVAL, "sst_build: unknown layout");
+    }
+    if (rc) { delete x; return rc; }
+    x->words = host.size();
+    hipError_t e = hipMalloc(&x->nodes, x->words * 4);
+    if (e != hipSuccess) { delete x; SAS_FAIL(ENOMEM, "sst_build: hipMalloc failed"); }
+    e = hipMemcpy(x->nodes, host.data(), x->words * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) { (void)hipFree(x->nodes); delete x; SAS_FAIL(EIO, "sst_build: upload failed"); }
+    *out = x;
+    return 0;
+}
+
+extern "C" int sst_free(sst_index* x) {
+    if (x) {
+        if (x->nodes) (void)hipFree(x->nodes);
+        delete x;
+    }
+    return 0;
+}
+
+extern "C" uint64_t sst_size(const sst_index* x) {
+    // SearchIndex::size(): bytes of the node / value array (sst/lib.rs:35-36)
+    return x ? x->words * 4 : 0;
+}
+
+extern "C" uint64_t sst_layers(const sst_index* x) {
+    if (!x) return 0;
+    switch (x->layout) {
+        case SST_SORTED: return 64 - __builtin_clzll(x->n);              // ilog2(len)+1 (binary_search.rs:29-31)
+        case SST_EYTZINGER: return 64 - __builtin_clzll(x->n + 1);       // ilog2(len)+1 (eytzinger.rs:72-74)
+        default: return x->height;                                       // offsets.len() (s_tree.rs:52-54)
+    }
+}
+
+extern "C" int sst_copy_nodes(const sst_index* x, uint32_t* dst, uint64_t count) {
+    if (!x || !dst || count > x->words) SAS_FAIL(EINVAL, "sst_copy_nodes: bad argument");
+    HIP_TRY(hipMemcpy(dst, x->nodes, count * 4, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+static int sst_launch(const sst_index* x, SstArgs& a, uint32_t flags, hipStream_t st) {
+    uint64_t blocks = (a.nq + SST_BLOCK - 1) / SST_BLOCK;
+    uint64_t cap = (uint64_t)x->num_cus * 2;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return 0;
+    dim3 grid((unsigned)blocks), block(SST_BLOCK);
+    if (x->layout == SST_SORTED) {
+        hipLaunchKernelGGL(k_sst_sorted, grid, block, 0, st, a);
+    } else if (x->layout == SST_EYTZINGER) {
+        hipLaunchKernelGGL(k_sst_eytzinger, grid, block, 0, st, a);
+    } else if (flags & SST_NO_LDS_TOP) {
+        hipLaunchKernelGGL(k_sst_stree<false>, grid, block, 0, st, a);
+    } else {
+        hipLaunchKernelGGL(k_sst_stree<true>, grid, block, 0, st, a);
+    }
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
+static void sst_fill(const sst_index* x, SstArgs& a) {
+    a.nodes = x->nodes;
+    a.n = x->n;
+    uint32_t lo = 0;
+    for (uint32_t h = 0; h < SAS_STREE_MAX_LAYERS; h++) {
+        a.off[h] = x->off[h];
+        a.lds_off[h] = lo;
+        if (h < x->lds_layers) lo += (uint32_t)x->layer_nodes[h];
+    }
+    a.height = x->height;
+    a.B = x->B;
+    a.lds_layers = x->lds_layers;
+    a.lds_nodes = x->lds_nodes;
+    a.eyt_iters = x->height;
+}
+
+extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, uint32_t* out_val, uint64_t* out_rank,
+                         void* stream, uint32_t flags) {
+    if (!x) SAS_FAIL(EINVAL, "sst_query: null index");
+    if (nq == 0) return 0;
+    if (!qs || !out_val) SAS_FAIL(EINVAL, "sst_query: null qs/out_val");
+    if (out_rank && x->layout == SST_EYTZINGER) SAS_FAIL(EINVAL, "sst_query: Eytzinger layout has no rank output");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SstArgs a{};
+    sst_fill(x, a);
+    a.nq = nq;
+    bool dev = flags & SST_DEVICE_PTRS;
+    void *dq = nullptr, *dout = nullptr, *drank = nullptr;
+    if (dev) {
+        a.qs = qs;
+        a.out = out_val;
+        a.rank = out_rank;
+    } else {
+        HIP_TRY(hipMallocAsync(&dq, nq * 4, st));
+        HIP_TRY(hipMallocAsync(&dout, nq * 4, st));
+        if (out_rank) HIP_TRY(hipMallocAsync(&drank, nq * 8, st));
+        HIP_TRY(hipMemcpyAsync(dq, qs, nq * 4, hipMemcpyHostToDevice, st));
+        a.qs = static_cast<uint32_t*>(dq);
+        a.out = static_cast<uint32_t*>(dout);
+        a.rank = static_cast<uint64_t*>(drank);
+    }
+    int rc = sst_launch(x, a, flags, st);
+    if (rc) return rc;
+    if (!dev) {
+        HIP_TRY(hipMemcpyAsync(out_val, dout, nq * 4, hipMemcpyDeviceToHost, st));
+        if (out_rank) HIP_TRY(hipMemcpyAsync(out_rank, drank, nq * 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipFreeAsync(dq, st));
+        HIP_TRY(hipFreeAsync(dout, st));
+        if (drank) HIP_TRY(hipFreeAsync(drank, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return 0;
+}
+
+extern "C" int sst_time_query(const sst_index* x, const uint32_t* d_qs, uint64_t nq, uint32_t* d_out, int reps,
+                              void* stream, uint32_t flags, double* kernel_ns) {
+    if (!x || !d_qs || !d_out || reps < 1) SAS_FAIL(EINVAL, "sst_time_query: bad argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SstArgs a{};
+    sst_fill(x, a);
+    a.nq = nq;
+    a.qs = d_qs;
+    a.out = d_out;
+    hipEvent_t e0, e1;
+    HIP_TRY(hipEventCreate(&e0));
+    HIP_TRY(hipEventCreate(&e1));
+    HIP_TRY(hipEventRecord(e0, st));
+    for (int r = 0; r < reps; r++) {
+        int rc = sst_launch(x, a, flags, st);
+        if (rc) return rc;
+    }
+    HIP_TRY(hipEventRecord(e1, st));
+    HIP_TRY(hipEventSynchronize(e1));
+    float ms = 0;
+    HIP_TRY(hipEventElapsedTime(&ms, e0, e1));
+    if (kernel_ns) *kernel_ns = ms * 1e6 / reps;
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return 0;
+}

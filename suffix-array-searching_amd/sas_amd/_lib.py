@@ -1,0 +1,110 @@
+"""ctypes binding of libsas_amd.so (the C ABI declared in include/sas.h and include/sst.h).
+
+The product path has no fallback: if the HIP library is missing this module raises,
+so nothing silently runs on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))  # suffix-array-searching_amd/
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, "libsas_amd.so")
+HEADERS = [os.path.join(REPO_DIR, "include", "sas.h"), os.path.join(REPO_DIR, "include", "sst.h")]
+
+# flags / enums mirrored from include/sas.h and include/sst.h
+SAS_DEVICE_PTRS = 1 << 0
+SAS_BUILD_LCP = 1 << 1
+SAS_BUILD_STREE = 1 << 2
+SAS_BUILD_VERIFY = 1 << 3
+SAS_NO_LDS_TOP = 1 << 4
+SAS_VALIDATE = 1 << 5
+ALGOS = {"plain": 0, "lcp": 1, "stree": 2}
+
+SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15 = 0, 1, 2, 3
+SST_LEFT_MAX = 1 << 0
+SST_REVERSE = 1 << 1
+SST_FULL = 1 << 2
+SST_DEVICE_PTRS = 1 << 8
+SST_NO_LDS_TOP = 1 << 9
+
+
+class SasStats(C.Structure):
+    _fields_ = [
+        ("n", C.c_uint64), ("text_bytes", C.c_uint64), ("sa_bytes", C.c_uint64), ("lcp_bytes", C.c_uint64),
+        ("stree_bytes", C.c_uint64), ("stree_layers", C.c_uint32), ("stree_lds_layers", C.c_uint32),
+        ("top_levels", C.c_uint32), ("iterations", C.c_uint32), ("build_sa_ns", C.c_uint64),
+        ("build_total_ns", C.c_uint64), ("sa_rounds", C.c_uint32), ("reserved", C.c_uint32),
+    ]
+
+    def as_dict(self):
+        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+
+
+class SasError(RuntimeError):
+    """A non-zero status from the C ABI (the reference panics in these cases)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"{msg} (errno {code})")
+        self.code = code
+
+
+_LIB = None
+
+
+def build_library() -> str:
+    subprocess.check_call(["make", "-s", "-C", PKG_DIR])
+    return LIB_PATH
+
+
+def declared_symbols() -> list[str]:
+    """Every function the public headers declare."""
+    names = []
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names += re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*\b((?:sas|sst)_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def lib():
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"HIP extension {LIB_PATH} is missing: run __graft_entry__.build() "
+                          f"(there is no CPU fallback)")
+    L = C.CDLL(LIB_PATH)
+    vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
+    L.sas_last_error.restype = C.c_char_p
+    L.sas_build.argtypes = [vp, u64, vp, i32, u32, C.POINTER(vp)]
+    L.sas_free.argtypes = [vp]
+    L.sas_get_stats.argtypes = [vp, C.POINTER(SasStats)]
+    L.sas_copy_sa.argtypes = [vp, vp, u64, u32]
+    L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]
+    L.sas_verify.argtypes = [vp]
+    L.sas_search_batch.argtypes = [vp, vp, vp, vp, u64, i32, vp, vp, vp, u32]
+    L.sas_search_fixed.argtypes = [vp, vp, u32, u64, i32, vp, vp, vp, u32]
+    L.sas_time_fixed.argtypes = [vp, vp, u32, u64, i32, vp, i32, vp, u32, C.POINTER(C.c_double),
+                                 C.POINTER(C.c_double)]
+    L.sas_gen_text.argtypes = [u64, u64, vp, u32]
+    L.sas_gen_queries.argtypes = [u64, u64, u64, u64, u64, u32, u32, vp, vp, C.POINTER(u64)]
+    L.sst_build.argtypes = [vp, u64, i32, u32, C.POINTER(vp)]
+    L.sst_free.argtypes = [vp]
+    L.sst_size.argtypes = [vp]
+    L.sst_size.restype = u64
+    L.sst_layers.argtypes = [vp]
+    L.sst_layers.restype = u64
+    L.sst_query.argtypes = [vp, vp, u64, vp, vp, vp, u32]
+    L.sst_copy_nodes.argtypes = [vp, vp, u64]
+    L.sst_time_query.argtypes = [vp, vp, u64, vp, i32, vp, u32, C.POINTER(C.c_double)]
+    _LIB = L
+    return L
+
+
+def check(rc: int):
+    if rc != 0:
+        raise SasError(rc, lib().sas_last_error().decode())

@@ -1,0 +1,207 @@
+"""Host-side mirror of the reference's suffix-array query API (sas/sa_search.rs).
+
+    SaNaive.build(t)                      <- SaNaive::build            sas/sa_search.rs:30-57
+    binary_search(sa, q, cnt)             <- binary_search (type F1)    sas/sa_search.rs:98-112, :453
+    binary_search_batch(sa, qs, cnt)      <- binary_search_batch<B>     sas/sa_search.rs:157-196, :454
+    SaNaive.search_batch(queries, algo)   <- bench_batch driver         sas/sa_search.rs:437-451
+    random_string / random_queries        <- sas/util.rs:9-26 (ChaCha8Rng::seed_from_u64, sas/main.rs:38)
+
+Every call runs on the GPU through libsas_amd.so.  `cnt` is the reference's
+`&mut usize` probe counter: pass a `Counter` and it is incremented by the number
+of suffix comparisons the query made.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+
+@dataclass
+class Counter:
+    """Stands in for the reference's `cnt: &mut usize` argument."""
+    value: int = 0
+
+
+def _is_cuda(x) -> bool:
+    return hasattr(x, "is_cuda") and bool(x.is_cuda)
+
+
+def _ptr(x):
+    if x is None:
+        return None
+    if _is_cuda(x) or hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return x.ctypes.data
+
+
+def _as_u8(x):
+    if _is_cuda(x):
+        return x
+    return np.ascontiguousarray(np.frombuffer(x, np.uint8) if isinstance(x, (bytes, bytearray)) else x, np.uint8)
+
+
+class SaNaive:
+    """GPU-resident suffix-array index: 2-bit packed text, u32 SA, optional LCP
+    array and S-tree over 16-char SA keys, all in HBM."""
+
+    def __init__(self, handle, n):
+        self._h = handle
+        self.n = n
+
+    @classmethod
+    def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False) -> "SaNaive":
+        t = _as_u8(t)
+        n = int(t.numel() if _is_cuda(t) else len(t))
+        flags = (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
+        flags |= _lib.SAS_BUILD_VERIFY if verify else 0
+        sa_ptr = None
+        if sa is not None:
+            if _is_cuda(t) != _is_cuda(sa):
+                raise ValueError("text and sa must both be host or both be device arrays")
+            if not _is_cuda(sa):
+                sa = np.ascontiguousarray(sa, np.uint32)
+            sa_ptr = _ptr(sa)
+        if _is_cuda(t):
+            flags |= _lib.SAS_DEVICE_PTRS
+        h = C.c_void_p()
+        check(lib().sas_build(_ptr(t), n, sa_ptr, 4, flags, C.byref(h)))
+        return cls(h, n)
+
+    def free(self):
+        if self._h:
+            lib().sas_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    # -- introspection (Index<usize> for SaNaive, sas/sa_search.rs:21-27)
+    def stats(self) -> dict:
+        s = _lib.SasStats()
+        check(lib().sas_get_stats(self._h, C.byref(s)))
+        return s.as_dict()
+
+    def suffix_array(self) -> np.ndarray:
+        out = np.zeros(self.n, np.uint32)
+        check(lib().sas_copy_sa(self._h, out.ctypes.data, self.n, 0))
+        return out
+
+    def lcp_array(self) -> np.ndarray:
+        out = np.zeros(self.n, np.uint32)
+        check(lib().sas_copy_lcp(self._h, out.ctypes.data, self.n, 0))
+        return out
+
+    def verify(self):
+        check(lib().sas_verify(self._h))
+
+    # -- searching
+    def search_fixed(self, qbytes, m: int, algo: str = "plain", probes: bool = False, stream=None,
+                     out=None, flags: int = 0):
+        """Fixed-length queries, query k = qbytes[k*m:(k+1)*m].  Host numpy in ->
+        numpy out (synchronous); torch CUDA in -> CUDA out (async on `stream`)."""
+        dev = _is_cuda(qbytes)
+        nq = (qbytes.numel() if dev else len(qbytes)) // max(m, 1) if m else 0
+        if m == 0:
+            raise ValueError("use search_batch for empty queries")
+        return self._run(qbytes, None, None, m, nq, algo, probes, stream, out, flags, dev)
+
+    def search_batch(self, qbytes, qoff, qlen, algo: str = "plain", probes: bool = False, stream=None,
+                     out=None, flags: int = 0):
+        """Ragged queries, query k = qbytes[qoff[k] : qoff[k] + qlen[k]]."""
+        dev = _is_cuda(qbytes)
+        if not dev:
+            qoff = np.ascontiguousarray(qoff, np.uint64)
+            qlen = np.ascontiguousarray(qlen, np.uint32)
+        nq = int(qoff.numel() if dev else len(qoff))
+        return self._run(qbytes, qoff, qlen, 0, nq, algo, probes, stream, out, flags, dev)
+
+    def _run(self, qbytes, qoff, qlen, m, nq, algo, probes, stream, out, flags, dev):
+        a = _lib.ALGOS[algo]
+        if dev:
+            import torch
+            if out is None:
+                out = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+            pr = torch.empty(nq, dtype=torch.int32, device=qbytes.device) if probes else None
+            st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
+            flags |= _lib.SAS_DEVICE_PTRS
+        else:
+            qbytes = _as_u8(qbytes)
+            if out is None:
+                out = np.zeros(max(nq, 1), np.uint64)
+            pr = np.zeros(max(nq, 1), np.uint32) if probes else None
+            st = stream
+        if qoff is None:
+            rc = lib().sas_search_fixed(self._h, _ptr(qbytes), m, nq, a, _ptr(out), _ptr(pr), st, flags)
+        else:
+            rc = lib().sas_search_batch(self._h, _ptr(qbytes), _ptr(qoff), _ptr(qlen), nq, a, _ptr(out), _ptr(pr),
+                                        st, flags)
+        check(rc)
+        if not dev:
+            out, pr = out[:nq], (pr[:nq] if pr is not None else None)
+        return (out, pr) if probes else out
+
+    def search(self, queries, algo: str = "plain", probes: bool = False):
+        """List of byte strings / arrays -> positions (host)."""
+        qs = [_as_u8(q) for q in queries]
+        lens = np.array([len(q) for q in qs], np.uint32)
+        off = np.zeros(len(qs), np.uint64)
+        if len(qs):
+            off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+        buf = np.concatenate(qs + [np.zeros(64, np.uint8)]) if qs else np.zeros(64, np.uint8)
+        return self.search_batch(buf, off, lens, algo=algo, probes=probes)
+
+    def time_fixed(self, d_qbytes, m: int, nq: int, d_out, algo="plain", reps=1, stream=None, flags=0):
+        """Average (kernel_ns, call_ns) of `reps` back-to-back searches on device buffers."""
+        kn, cn = C.c_double(0), C.c_double(0)
+        check(lib().sas_time_fixed(self._h, _ptr(d_qbytes), m, nq, _lib.ALGOS[algo], _ptr(d_out), reps, stream,
+                                   flags, C.byref(kn), C.byref(cn)))
+        return kn.value, cn.value
+
+
+def binary_search(sa: SaNaive, q, cnt: Counter | None = None) -> int:
+    """sas/sa_search.rs:98-112 -- position of the first suffix >= q (n if none)."""
+    pos, pr = sa.search([q], algo="plain", probes=True)
+    if cnt is not None:
+        cnt.value += int(pr[0])
+    return int(pos[0])
+
+
+def binary_search_batch(sa: SaNaive, qs, cnt: Counter | None = None, algo: str = "plain") -> list[int]:
+    """sas/sa_search.rs:157-196 -- B queries at once (any B; no remainder is dropped)."""
+    pos, pr = sa.search(list(qs), algo=algo, probes=True)
+    if cnt is not None:
+        cnt.value += int(pr.sum())
+    return [int(p) for p in pos]
+
+
+# ---------------------------------------------------------------- generators
+def random_string(n: int, seed: int = 31415, device=None):
+    """sas/util.rs:9-15 with ChaCha8Rng::seed_from_u64(seed): bit-exact stream."""
+    if device is not None:
+        import torch
+        out = torch.empty(n, dtype=torch.uint8, device=device)
+        check(lib().sas_gen_text(seed, n, out.data_ptr(), _lib.SAS_DEVICE_PTRS))
+        return out
+    out = np.zeros(max(n, 1), np.uint8)
+    check(lib().sas_gen_text(seed, n, out.ctypes.data, 0))
+    return out[:n]
+
+
+def random_queries(n: int, nq: int, seed: int = 31415, word_pos: int | None = None, margin: int = 200,
+                   len_lo: int = 30, len_hi: int = 100):
+    """sas/util.rs:18-26 -> (offsets u64, lengths u32, next keystream word).  The
+    stream continues after the text's n words unless word_pos is given."""
+    off = np.zeros(max(nq, 1), np.uint64)
+    ln = np.zeros(max(nq, 1), np.uint32)
+    nxt = C.c_uint64(0)
+    check(lib().sas_gen_queries(seed, n if word_pos is None else word_pos, n, nq, margin, len_lo, len_hi,
+                                off.ctypes.data, ln.ctypes.data, C.byref(nxt)))
+    return off[:nq], ln[:nq], nxt.value

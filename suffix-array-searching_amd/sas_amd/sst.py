@@ -1,0 +1,117 @@
+"""Host-side mirror of the reference's u32 search API (sst/lib.rs SearchIndex / SearchScheme).
+
+    SortedVec.new(vals)                       <- sst/binary_search.rs:19-27
+    Eytzinger.new(vals)                       <- sst/eytzinger.rs:66-70
+    STree16.new(vals) / STree15.new(vals)     <- sst/s_tree.rs:47-50  (new_params(false,false,false))
+    STree16.new_params(vals, left_max, reverse, full)   <- sst/s_tree.rs:72-176
+    index.size(), index.layers()              <- sst/lib.rs:35-39
+    index.query(qs), index.query_one(q)       <- sst/lib.rs:41-47, SearchScheme::query :55-57
+
+Queries run on the GPU (libsas_amd.so); there is no CPU fallback.  Build-time
+assertions of the reference (sorted input, keys <= i32::MAX) raise SasError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib
+
+MAX = 0x7FFFFFFF  # sst/node.rs:5
+
+
+def _is_cuda(x) -> bool:
+    return hasattr(x, "is_cuda") and bool(x.is_cuda)
+
+
+class _Index:
+    LAYOUT = None
+
+    def __init__(self, handle, n):
+        self._h = handle
+        self.n = n
+
+    @classmethod
+    def _build(cls, vals, layout, flags=0):
+        vals = np.ascontiguousarray(vals, np.uint32)
+        h = C.c_void_p()
+        check(lib().sst_build(vals.ctypes.data if len(vals) else None, len(vals), layout, flags, C.byref(h)))
+        return cls(h, len(vals))
+
+    @classmethod
+    def new(cls, vals):
+        return cls._build(vals, cls.LAYOUT)
+
+    def free(self):
+        if self._h:
+            lib().sst_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return int(lib().sst_size(self._h))
+
+    def layers(self) -> int:
+        return int(lib().sst_layers(self._h))
+
+    def nodes(self) -> np.ndarray:
+        words = self.size() // 4
+        out = np.zeros(max(words, 1), np.uint32)
+        check(lib().sst_copy_nodes(self._h, out.ctypes.data, words))
+        return out[:words]
+
+    def query(self, qs, want_rank: bool = False, stream=None, flags: int = 0):
+        if _is_cuda(qs):
+            import torch
+            out = torch.empty(qs.numel(), dtype=torch.int32, device=qs.device)
+            rank = torch.empty(qs.numel(), dtype=torch.int64, device=qs.device) if want_rank else None
+            st = stream if stream is not None else torch.cuda.current_stream(qs.device).cuda_stream
+            check(lib().sst_query(self._h, qs.data_ptr(), qs.numel(), out.data_ptr(),
+                                  rank.data_ptr() if want_rank else None, st, flags | _lib.SST_DEVICE_PTRS))
+            return (out, rank) if want_rank else out
+        qs = np.ascontiguousarray(qs, np.uint32)
+        out = np.zeros(max(len(qs), 1), np.uint32)
+        rank = np.zeros(max(len(qs), 1), np.uint64) if want_rank else None
+        check(lib().sst_query(self._h, qs.ctypes.data, len(qs), out.ctypes.data,
+                              rank.ctypes.data if want_rank else None, stream, flags))
+        return (out[: len(qs)], rank[: len(qs)]) if want_rank else out[: len(qs)]
+
+    def query_one(self, q: int) -> int:
+        return int(self.query(np.array([q], np.uint32))[0])
+
+    def time_query(self, d_qs, d_out, reps=1, stream=None, flags=0) -> float:
+        kn = C.c_double(0)
+        check(lib().sst_time_query(self._h, d_qs.data_ptr(), d_qs.numel(), d_out.data_ptr(), reps, stream, flags,
+                                   C.byref(kn)))
+        return kn.value
+
+
+class SortedVec(_Index):
+    LAYOUT = _lib.SST_SORTED
+
+
+class Eytzinger(_Index):
+    LAYOUT = _lib.SST_EYTZINGER
+
+
+class _STree(_Index):
+    @classmethod
+    def new_params(cls, vals, left_max: bool, reverse_storage: bool, full_array: bool):
+        flags = (_lib.SST_LEFT_MAX if left_max else 0) | (_lib.SST_REVERSE if reverse_storage else 0)
+        flags |= _lib.SST_FULL if full_array else 0
+        return cls._build(vals, cls.LAYOUT, flags)
+
+
+class STree16(_STree):
+    LAYOUT = _lib.SST_STREE16
+
+
+class STree15(_STree):
+    LAYOUT = _lib.SST_STREE15

@@ -1,0 +1,51 @@
+"""CPU checks of the drop-in boundary: libsas_amd.so loads, exports exactly what
+include/*.h declares, and its host-only entry points agree with the oracle.
+(No kernel is launched here: this container has no GPU.)"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import sas_amd
+from sas_amd import _lib
+from oracle import pyoracle as O
+
+
+def test_library_exports_every_declared_symbol():
+    names = _lib.declared_symbols()
+    assert len(names) >= 19
+    L = C.CDLL(_lib.LIB_PATH)
+    missing = [s for s in names if not hasattr(L, s)]
+    assert not missing, missing
+    for must in ("sas_build", "sas_search_batch", "sas_search_fixed", "sst_build", "sst_query", "sst_size",
+                 "sst_layers", "sas_last_error"):
+        assert must in names
+
+
+def test_library_is_gfx950_code_object():
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in blob
+
+
+def test_gen_queries_matches_oracle():
+    n = 1 << 20
+    off, ln, nxt = sas_amd.random_queries(n, 5000)
+    o_off, o_ln, o_nxt = O.random_queries(n, 5000)
+    assert np.array_equal(off, o_off) and np.array_equal(ln, o_ln) and nxt == o_nxt
+    off, ln, nxt = sas_amd.random_queries(n, 777, word_pos=12345, margin=256, len_lo=8, len_hi=257)
+    o_off, o_ln, o_nxt = O.random_queries(n, 777, word_pos=12345, margin=256, len_lo=8, len_hi=257)
+    assert np.array_equal(off, o_off) and np.array_equal(ln, o_ln) and nxt == o_nxt
+
+
+def test_error_paths_set_last_error():
+    L = _lib.lib()
+    off = np.zeros(4, np.uint64)
+    ln = np.zeros(4, np.uint32)
+    rc = L.sas_gen_queries(1, 0, 100, 4, 200, 30, 100, off.ctypes.data, ln.ctypes.data, None)
+    assert rc == 22  # EINVAL: gen_range(0..n-200) empty
+    assert b"margin" in L.sas_last_error()
+    with pytest.raises(sas_amd.SasError):
+        sas_amd.random_queries(100, 4)
+    # null out pointers are rejected before any device call
+    assert L.sas_build(None, 10, None, 4, 0, None) == 22
+    assert L.sst_build(None, 0, 0, 0, None) == 22

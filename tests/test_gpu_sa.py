@@ -1,0 +1,195 @@
+"""GPU parity of the suffix-array path (libsas_amd.so via the C ABI) against the
+oracle.  Bar: bit-exact positions for every algorithm.
+
+* definition fixtures (tests/golden/sa_definition.json): SA, LCP, positions;
+* C0 shape (1 MiB ChaCha8 text, 10^4 len-16 queries) vs the oracle's
+  restated binary_search (sas/sa_search.rs:98-112) on the oracle-built SA;
+* larger texts: GPU-built SA checked by the reference's adjacency assertion
+  (sas/sa_search.rs:36-38) on the CPU, then positions vs the oracle;
+* edge cases: empty / over-long / above-all queries, text-end suffixes,
+  invalid codes, m > 256 (beyond the register-resident query words).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+ALGOS = ("plain", "lcp", "stree")
+
+
+@pytest.fixture(scope="module")
+def sas():
+    import sas_amd
+    return sas_amd
+
+
+@pytest.fixture(scope="module")
+def sadef(golden_dir):
+    return json.load(open(os.path.join(golden_dir, "sa_definition.json")))
+
+
+def oracle_positions(t, sa, qbuf, off, lens, threads=8):
+    tp = O.padded(t)
+    qb = np.concatenate([qbuf, np.zeros(64, np.uint8)])
+    pos, _ = O.search_many(tp, len(t), sa, qb, off, lens, "binary_search", threads)
+    return pos
+
+
+def pack(qs):
+    lens = np.array([len(q) for q in qs], np.uint32)
+    off = np.zeros(len(qs), np.uint64)
+    if len(qs) > 1:
+        off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.concatenate([np.asarray(q, np.uint8) for q in qs] + [np.zeros(64, np.uint8)])
+    return buf, off, lens
+
+
+def test_definition_fixtures(sas, sadef):
+    for c in sadef["cases"]:
+        t = np.array(c["text"], np.uint8)
+        idx = sas.SaNaive.build(t, lcp=True, stree=True, verify=True)
+        assert idx.suffix_array().tolist() == c["sa"], c["name"]
+        lcp = O.kasai_lcp(t, np.array(c["sa"], np.uint32))
+        assert np.array_equal(idx.lcp_array(), lcp), c["name"]
+        buf, off, lens = pack([q["q"] for q in c["queries"]])
+        expect = np.array([q["pos"] for q in c["queries"]], np.uint64)
+        for algo in ALGOS:
+            got, probes = idx.search_batch(buf, off, lens, algo=algo, probes=True)
+            assert np.array_equal(got, expect), (c["name"], algo, np.nonzero(got != expect))
+        # caller-supplied SA path
+        idx2 = sas.SaNaive.build(t, sa=np.array(c["sa"], np.uint32), lcp=False, stree=True, verify=True)
+        got = idx2.search_batch(buf, off, lens, algo="stree")
+        assert np.array_equal(got, expect)
+
+
+def test_no_lds_top_same(sas, sadef):
+    from sas_amd import _lib
+    c = [c for c in sadef["cases"] if c["name"] == "random_4096"][0]
+    t = np.array(c["text"], np.uint8)
+    idx = sas.SaNaive.build(t)
+    buf, off, lens = pack([q["q"] for q in c["queries"]])
+    expect = np.array([q["pos"] for q in c["queries"]], np.uint64)
+    for algo in ("plain", "lcp"):
+        got = idx.search_batch(buf, off, lens, algo=algo, flags=_lib.SAS_NO_LDS_TOP)
+        assert np.array_equal(got, expect)
+
+
+def test_gen_text_bit_exact(sas):
+    for n in (1, 15, 16, 17, 1000, (1 << 20) + 3):
+        assert np.array_equal(sas.random_string(n), O.random_string(n)), n
+
+
+def test_c0_config_parity(sas):
+    """configs[0]: 1 MiB random ACGT text, 10^4 length-16 queries."""
+    n, nq, m = 1 << 20, 10_000, 16
+    t = sas.random_string(n)
+    sa = O.build_sa(t)
+    idx = sas.SaNaive.build(t, lcp=True, stree=True)
+    assert np.array_equal(idx.suffix_array(), sa)
+    off, lens, _ = sas.random_queries(n, nq, len_lo=m, len_hi=m + 1)
+    qbytes = np.concatenate([t[o:o + m] for o in off.astype(np.int64)])
+    expect = oracle_positions(t, sa, qbytes, np.arange(nq, dtype=np.uint64) * m, np.full(nq, m, np.uint32))
+    for algo in ALGOS:
+        got, probes = idx.search_fixed(qbytes, m, algo=algo, probes=True)
+        assert np.array_equal(got, expect), algo
+        if algo == "plain":
+            assert (probes <= 21).all() and (probes >= 20).all()  # ilog2(n)+1 lockstep, l<r probes only
+    # every positive query's answer is an occurrence of it
+    tp = O.padded(t)
+    got = idx.search_fixed(qbytes, m, algo="stree")
+    occ = np.stack([tp[p:p + m] for p in got.astype(np.int64)])
+    assert np.array_equal(occ.reshape(-1), qbytes)
+
+
+@pytest.mark.parametrize("n", [1 << 16, 3_000_017, 1 << 24])
+def test_random_text_mixed_queries(sas, n):
+    rng = np.random.default_rng(n)
+    t = sas.random_string(n, seed=n)
+    idx = sas.SaNaive.build(t, lcp=True, stree=True, verify=True)
+    sa = idx.suffix_array()
+    assert O.check_sa(t, sa) == 0  # sas/sa_search.rs:36-38 + permutation, on the CPU
+    nq = 20_000
+    off, lens, _ = sas.random_queries(n, nq, seed=7, margin=256, len_lo=8, len_hi=257)  # configs[3] shape
+    qs = [t[o:o + l] for o, l in zip(off.astype(np.int64), lens.astype(np.int64))]
+    qs += [rng.integers(0, 4, rng.integers(0, 70), dtype=np.uint8) for _ in range(2000)]  # negatives
+    qs += [np.concatenate([t[n - k:], np.zeros(5, np.uint8)]) for k in (1, 3, 31, 32, 33)]  # A7 edge
+    qs += [t[n - k:] for k in (1, 2, 16, 40)]
+    buf, qo, ql = pack(qs)
+    expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+    for algo in ALGOS:
+        got = idx.search_batch(buf, qo, ql, algo=algo)
+        bad = np.nonzero(got != expect)[0]
+        assert len(bad) == 0, (algo, bad[:10], [qs[i] for i in bad[:3]])
+
+
+def test_repetitive_texts(sas):
+    """Long repeats force doubling rounds, long tie runs in the S-tree leaves and
+    multi-word compares."""
+    rng = np.random.default_rng(3)
+    blk = rng.integers(0, 4, 5000, dtype=np.uint8)
+    texts = {
+        "all_A": np.zeros(100_000, np.uint8),
+        "period_7": np.tile(rng.integers(0, 4, 7, dtype=np.uint8), 30_000),
+        "repeats": np.concatenate([blk, rng.integers(0, 4, 100, dtype=np.uint8), blk, blk[:3000], blk]),
+    }
+    for name, t in texts.items():
+        idx = sas.SaNaive.build(t, lcp=True, stree=True, verify=True)
+        sa = O.build_sa(t)
+        assert np.array_equal(idx.suffix_array(), sa), name
+        assert np.array_equal(idx.lcp_array(), O.kasai_lcp(t, sa)), name
+        n = len(t)
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 600, 3000), rng.integers(1, 600, 3000))]
+        qs += [np.concatenate([t[o:o + 40], [3]]).astype(np.uint8) for o in rng.integers(0, n - 50, 200)]
+        qs += [t[:300], np.zeros(301, np.uint8), np.full(10, 3, np.uint8), np.zeros(0, np.uint8)]
+        buf, qo, ql = pack(qs)
+        expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+        for algo in ALGOS:
+            got = idx.search_batch(buf, qo, ql, algo=algo)
+            assert np.array_equal(got, expect), (name, algo)
+
+
+def test_invalid_codes_rejected(sas):
+    with pytest.raises(sas.SasError):
+        sas.SaNaive.build(np.array([0, 1, 4, 2], np.uint8))
+    idx = sas.SaNaive.build(np.array([0, 1, 2, 3] * 10, np.uint8))
+    with pytest.raises(sas.SasError):
+        idx.search([np.array([0, 1, 7], np.uint8)])
+    with pytest.raises(sas.SasError):
+        sas.SaNaive.build(np.zeros(0, np.uint8))
+
+
+def test_reference_api_shapes(sas):
+    t = sas.random_string(5000)
+    idx = sas.SaNaive.build(t)
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    cnt = sas.Counter()
+    q = t[1000:1040]
+    assert sas.binary_search(idx, q, cnt) == O.search_one(tp, len(t), sa, q)[0]
+    assert cnt.value == O.search_one(tp, len(t), sa, q)[1]
+    qs = [t[i:i + 35] for i in range(0, 4000, 97)]
+    assert sas.binary_search_batch(idx, qs) == [O.search_one(tp, len(t), sa, x)[0] for x in qs]
+
+
+def test_device_pointer_path(sas):
+    import torch
+    n, nq, m = 1 << 18, 4096, 32
+    t = sas.random_string(n, device="cuda")
+    ht = t.cpu().numpy()
+    assert np.array_equal(ht, O.random_string(n))
+    idx = sas.SaNaive.build(t, lcp=False, stree=True)
+    off, _, _ = sas.random_queries(n, nq, len_lo=m, len_hi=m + 1)
+    qb = torch.from_numpy(np.concatenate([ht[o:o + m] for o in off.astype(np.int64)])).cuda()
+    host = idx.search_fixed(qb.cpu().numpy(), m, algo="plain")
+    for algo in ALGOS:
+        dev = idx.search_fixed(qb, m, algo=algo)
+        torch.cuda.synchronize()
+        assert np.array_equal(dev.cpu().numpy().astype(np.uint64), host), algo
+    out = torch.empty(nq, dtype=torch.int64, device="cuda")
+    kns, cns = idx.time_fixed(qb, m, nq, out, algo="stree", reps=3)
+    assert kns > 0 and np.array_equal(out.cpu().numpy().astype(np.uint64), host)

@@ -1,0 +1,90 @@
+"""GPU parity of the u32 static-search-tree path (sst_* C ABI) -- a port of the
+reference's differential test (sst/test.rs:142-260) plus its KATs, with the
+node arrays compared word for word against the oracle's restatement of
+STree::new_params."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import pyoracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sas():
+    import sas_amd
+    return sas_amd
+
+
+def gen_vals(n, rng):
+    v = rng.integers(0, O.MAX, n, dtype=np.uint64).astype(np.uint32)
+    v[0] = O.MAX  # sst/util.rs:37
+    return np.sort(v)
+
+
+def test_kats(sas, golden_dir):
+    k = json.load(open(os.path.join(golden_dir, "reference_kats.json")))
+    for c in k["eytzinger_layout"]:
+        e = sas.Eytzinger.new(c["input"])
+        assert e.nodes().tolist() == c["vals"]
+    for c in k["eytzinger_search"]:
+        assert sas.Eytzinger.new(c["input"]).query_one(c["q"]) == c["expect"]
+    vals = list(range(1, 2000)) + [O.MAX]
+    for cls in (sas.STree16, sas.STree15, sas.SortedVec, sas.Eytzinger):
+        idx = cls.new(vals)
+        for c in k["stree_search"]:
+            assert idx.query_one(c["q"]) == c["expect"], cls.__name__
+
+
+SIZES = [s for p in range(6, 23) for s in ((1 << p), (1 << p) * 5 // 4, (1 << p) * 6 // 4, (1 << p) * 7 // 4)]
+
+
+@pytest.mark.parametrize("size", SIZES[::3] + [SIZES[-1]])
+def test_differential(sas, size):
+    """sst/test.rs:143-196: every index/scheme returns the same Vec<u32>."""
+    rng = np.random.default_rng(size)
+    vals = gen_vals(size // 4, rng)
+    qs = rng.integers(0, O.MAX, 1024, dtype=np.uint64).astype(np.uint32)  # 1000.next_multiple_of(128)
+    ref, ref_rank = O.SortedVec(vals).query(qs, want_rank=True)
+    got, rank = sas.SortedVec.new(vals).query(qs, want_rank=True)
+    assert np.array_equal(got, ref) and np.array_equal(rank, ref_rank)
+    assert np.array_equal(sas.Eytzinger.new(vals).query(qs), ref)
+    for cls, B in ((sas.STree16, 16), (sas.STree15, 15)):
+        for lm, rev, full in ((False, False, False), (True, False, False), (True, False, True), (False, True, False)):
+            idx = cls.new_params(vals, lm, rev, full)
+            o = O.STree(vals, B=B, left_max=lm, reverse=rev, full=full)
+            assert np.array_equal(idx.nodes(), o.tree), (B, lm, rev, full)  # layout bit-exact
+            assert idx.layers() == o.height and idx.size() == o.n_blocks * 64
+            v, r = idx.query(qs, want_rank=True)
+            assert np.array_equal(v, ref), (B, lm, rev, full)
+            _, orank = o.query(qs, want_rank=True)
+            assert np.array_equal(r, orank)
+
+
+def test_no_lds_and_device_path(sas):
+    import torch
+    from sas_amd import _lib
+    rng = np.random.default_rng(1)
+    vals = gen_vals(1 << 20, rng)
+    qs = rng.integers(0, O.MAX, 1 << 16, dtype=np.uint64).astype(np.uint32)
+    ref = O.SortedVec(vals).query(qs)
+    idx = sas.STree16.new_params(vals, True, False, False)
+    assert np.array_equal(idx.query(qs, flags=_lib.SST_NO_LDS_TOP), ref)
+    dq = torch.from_numpy(qs.view(np.int32)).cuda()
+    out = idx.query(dq)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), ref)
+
+
+def test_build_assertions(sas):
+    with pytest.raises(sas.SasError):
+        sas.STree16.new([3, 2, 1])  # unsorted
+    with pytest.raises(sas.SasError):
+        sas.STree16.new([1, 2, 0x80000000])  # > i32::MAX (sst/node.rs:5)
+    with pytest.raises(sas.SasError):
+        sas.STree16.new([])
+    with pytest.raises(sas.SasError):
+        sas.STree16.new_params([1, 2, 3], False, True, True)  # full + reverse
