@@ -68,6 +68,7 @@ struct sas_index {
     uint32_t* top_sa = nullptr;   // [SAS_TOP_NODES]
     uint32_t top_levels = 0;
     uint32_t iters = 0;           // ilog2(n) + 1
+    uint32_t* scratch = nullptr;  // device flag word(s) for kernels (invalid query codes)
     sas_stats stats = {};
 };
 

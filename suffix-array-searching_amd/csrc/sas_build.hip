@@ -468,7 +468,7 @@ __global__ void k_top(const uint64_t* __restrict__ tw, uint64_t n, const uint32_
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
-    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa};
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa, x->scratch};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete x;
 }
@@ -626,6 +626,8 @@ extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null
         x->top_key = static_cast<uint64_t*>(k.release());
         x->top_sa = static_cast<uint32_t*>(s.release());
     }
+    HIP_TRY(hipMalloc(&x->scratch, 64));
+    HIP_TRY(hipMemset(x->scratch, 0, 64));
     HIP_TRY(hipDeviceSynchronize());
 
     sas_stats& st = x->stats;

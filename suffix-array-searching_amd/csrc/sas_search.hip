@@ -292,12 +292,13 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.stree_lds_nodes = x->stree_lds_nodes;
 }
 
-struct AsyncBuf {
+struct DeviceBuf {
     void* p = nullptr;
-    hipStream_t st = 0;
-    ~AsyncBuf() { if (p) (void)hipFreeAsync(p, st); }
+    ~DeviceBuf() { if (p) (void)hipFree(p); }
 };
 
+// Host-pointer calls stage through plain hipMalloc + synchronous copies: the
+// stream-ordered allocator + pageable async copies raced on the null stream.
 static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
@@ -317,13 +318,12 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
     fill_args(x, a);
     a.nq = nq;
     a.m_fixed = m_fixed;
-    AsyncBuf bqb, bqoff, bqlen, bout, bprobes, bbad;
-    bbad.st = st;
-    HIP_TRY(hipMallocAsync(&bbad.p, 4, st));
-    HIP_TRY(hipMemsetAsync(bbad.p, 0, 4, st));
-    a.bad = static_cast<uint32_t*>(bbad.p);
+    a.bad = x->scratch;
+    bool check_bad = !dev || (flags & SAS_VALIDATE);
+    if (check_bad) HIP_TRY(hipMemsetAsync(x->scratch, 0, 4, st));
 
     int qw = 4;
+    DeviceBuf bqb, bqoff, bqlen, bout, bprobes;
     if (dev) {
         a.qbytes = qbytes;
         a.qoff = qoff;
@@ -346,36 +346,36 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
             span = nq * (uint64_t)m_fixed;
         }
         qw = qw_for(maxlen);
-        bqb.st = bqoff.st = bqlen.st = bout.st = bprobes.st = st;
-        HIP_TRY(hipMallocAsync(&bqb.p, span + 64, st));
-        HIP_TRY(hipMemcpyAsync(bqb.p, qbytes, span, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMalloc(&bqb.p, span + 64));
+        if (span) HIP_TRY(hipMemcpy(bqb.p, qbytes, span, hipMemcpyHostToDevice));
         a.qbytes = static_cast<const uint8_t*>(bqb.p);
         if (ragged) {
-            HIP_TRY(hipMallocAsync(&bqoff.p, nq * 8, st));
-            HIP_TRY(hipMallocAsync(&bqlen.p, nq * 4, st));
-            HIP_TRY(hipMemcpyAsync(bqoff.p, qoff, nq * 8, hipMemcpyHostToDevice, st));
-            HIP_TRY(hipMemcpyAsync(bqlen.p, qlen, nq * 4, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipMalloc(&bqoff.p, nq * 8));
+            HIP_TRY(hipMalloc(&bqlen.p, nq * 4));
+            HIP_TRY(hipMemcpy(bqoff.p, qoff, nq * 8, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(bqlen.p, qlen, nq * 4, hipMemcpyHostToDevice));
             a.qoff = static_cast<const uint64_t*>(bqoff.p);
             a.qlen = static_cast<const uint32_t*>(bqlen.p);
         }
-        HIP_TRY(hipMallocAsync(&bout.p, nq * 8, st));
+        HIP_TRY(hipMalloc(&bout.p, nq * 8));
         a.out_pos = static_cast<uint64_t*>(bout.p);
         if (out_probes) {
-            HIP_TRY(hipMallocAsync(&bprobes.p, nq * 4, st));
+            HIP_TRY(hipMalloc(&bprobes.p, nq * 4));
             a.out_probes = static_cast<uint32_t*>(bprobes.p);
         }
     }
     int rc = launch_search(x, a, algo, qw, flags, st);
     if (rc) return rc;
-    if (!dev) {
-        HIP_TRY(hipMemcpyAsync(out_pos, a.out_pos, nq * 8, hipMemcpyDeviceToHost, st));
-        if (out_probes) HIP_TRY(hipMemcpyAsync(out_probes, a.out_probes, nq * 4, hipMemcpyDeviceToHost, st));
-    }
-    if (!dev || (flags & SAS_VALIDATE)) {
-        uint32_t hbad = 0;
-        HIP_TRY(hipMemcpyAsync(&hbad, a.bad, 4, hipMemcpyDeviceToHost, st));
+    if (check_bad || !dev) {
         HIP_TRY(hipStreamSynchronize(st));
-        if (hbad && ((flags & SAS_VALIDATE) || !dev)) SAS_FAIL(EINVAL, "search: query bytes must be DNA codes 0..3");
+        uint32_t hbad = 0;
+        HIP_TRY(hipMemcpy(&hbad, x->scratch, 4, hipMemcpyDeviceToHost));
+        if (!dev) {
+            HIP_TRY(hipMemcpy(out_pos, a.out_pos, nq * 8, hipMemcpyDeviceToHost));
+            if (out_probes) HIP_TRY(hipMemcpy(out_probes, a.out_probes, nq * 4, hipMemcpyDeviceToHost));
+        }
+        if (hbad) SAS_FAIL(EINVAL, "search: query bytes must be DNA codes 0..3");
     }
     return 0;
 }
@@ -405,9 +405,7 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     a.m_fixed = m;
     a.qbytes = d_qbytes;
     a.out_pos = d_out_pos;
-    void* bad = nullptr;
-    HIP_TRY(hipMalloc(&bad, 4));
-    a.bad = static_cast<uint32_t*>(bad);
+    a.bad = x->scratch;
     hipEvent_t e0, e1;
     HIP_TRY(hipEventCreate(&e0));
     HIP_TRY(hipEventCreate(&e1));
@@ -427,6 +425,5 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (call_ns) *call_ns = std::chrono::duration<double, std::nano>(t1 - t0).count() / reps;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
-    (void)hipFree(bad);
     return 0;
 }

@@ -238,9 +238,12 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
     }
     if (rc) { delete x; return rc; }
     x->words = host.size();
-    hipError_t e = hipMalloc(&x->nodes, x->words * 4);
+    // one guard node of MAX keys after the array: a leaf search with idx == 16 on the
+    // last leaf (no sentinel in the input) reads the "next" node (sst/s_tree.rs:205)
+    host.insert(host.end(), 16, SST_MAX);
+    hipError_t e = hipMalloc(&x->nodes, host.size() * 4);
     if (e != hipSuccess) { delete x; SAS_FAIL(ENOMEM, "sst_build: hipMalloc failed"); }
-    e = hipMemcpy(x->nodes, host.data(), x->words * 4, hipMemcpyHostToDevice);
+    e = hipMemcpy(x->nodes, host.data(), host.size() * 4, hipMemcpyHostToDevice);
     if (e != hipSuccess) { (void)hipFree(x->nodes); delete x; SAS_FAIL(EIO, "sst_build: upload failed"); }
     *out = x;
     return 0;
@@ -321,15 +324,18 @@ extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, ui
     a.nq = nq;
     bool dev = flags & SST_DEVICE_PTRS;
     void *dq = nullptr, *dout = nullptr, *drank = nullptr;
+    struct Free { void** p; ~Free() { if (*p) (void)hipFree(*p); } } f1{&dq}, f2{&dout}, f3{&drank};
     if (dev) {
         a.qs = qs;
         a.out = out_val;
         a.rank = out_rank;
     } else {
-        HIP_TRY(hipMallocAsync(&dq, nq * 4, st));
-        HIP_TRY(hipMallocAsync(&dout, nq * 4, st));
-        if (out_rank) HIP_TRY(hipMallocAsync(&drank, nq * 8, st));
-        HIP_TRY(hipMemcpyAsync(dq, qs, nq * 4, hipMemcpyHostToDevice, st));
+        // host pointers: plain hipMalloc + synchronous copies (see sas_search.hip)
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMalloc(&dq, nq * 4));
+        HIP_TRY(hipMalloc(&dout, nq * 4));
+        if (out_rank) HIP_TRY(hipMalloc(&drank, nq * 8));
+        HIP_TRY(hipMemcpy(dq, qs, nq * 4, hipMemcpyHostToDevice));
         a.qs = static_cast<uint32_t*>(dq);
         a.out = static_cast<uint32_t*>(dout);
         a.rank = static_cast<uint64_t*>(drank);
@@ -337,12 +343,9 @@ extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, ui
     int rc = sst_launch(x, a, flags, st);
     if (rc) return rc;
     if (!dev) {
-        HIP_TRY(hipMemcpyAsync(out_val, dout, nq * 4, hipMemcpyDeviceToHost, st));
-        if (out_rank) HIP_TRY(hipMemcpyAsync(out_rank, drank, nq * 8, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipFreeAsync(dq, st));
-        HIP_TRY(hipFreeAsync(dout, st));
-        if (drank) HIP_TRY(hipFreeAsync(drank, st));
         HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpy(out_val, dout, nq * 4, hipMemcpyDeviceToHost));
+        if (out_rank) HIP_TRY(hipMemcpy(out_rank, drank, nq * 8, hipMemcpyDeviceToHost));
     }
     return 0;
 }

@@ -77,6 +77,13 @@ def lib():
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"HIP extension {LIB_PATH} is missing: run __graft_entry__.build() "
                           f"(there is no CPU fallback)")
+    # PyTorch-ROCm bundles its own libamdhip64.so.7 / libhsa-runtime64.so.1.  Load it
+    # first so the dynamic linker resolves our NEEDED entries to the same runtime:
+    # two HIP runtimes in one process cannot share device pointers or streams.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, u64, u32, i32 = C.c_void_p, C.c_uint64, C.c_uint32, C.c_int
     L.sas_last_error.restype = C.c_char_p
