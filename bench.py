@@ -60,6 +60,16 @@ def timed_loop(step, steps: int, warmup: int, sync, barrier, reduce_max):
     return reduce_max(elapsed)
 
 
+def rank_query_offsets(n: int, nq: int, m: int, rank: int) -> np.ndarray:
+    """This rank's queries: positive len-m substrings t[i..i+m] (sas/util.rs:18-26);
+    the ChaCha8 stream continues after the text's n words, rank r starting at word
+    n + r*4*nq (a fixed-length query draws 2 words, rejections are rare)."""
+    import sas_amd
+    off, _, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 4 * nq, margin=200,
+                                       len_lo=m, len_hi=m + 1)
+    return off
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -142,9 +152,7 @@ def main():
     text = sas_amd.random_string(n, seed=SEED, device=dev)  # sas/util.rs:9-15, identical on every rank
     idx = sas_amd.SaNaive.build(text, lcp=True, stree=True)
     stats = idx.stats()
-    # this rank's queries: positive len-m substrings (sas/util.rs:18-26), stream continued after the text
-    off, _, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 4 * nq, margin=200,
-                                       len_lo=m, len_hi=m + 1)
+    off = rank_query_offsets(n, nq, m, rank)
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
     qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
     ar = torch.arange(m, device=dev, dtype=torch.int64)

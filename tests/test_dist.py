@@ -1,0 +1,70 @@
+"""world_size-2 gloo test of the multi-GPU harness (bench.py) on the CPU:
+per-rank query shards, barrier-bracketed timing, MAX-over-ranks reduction, and
+that the shards' answers equal a single process's answers (replicated index,
+no data-path collective)."""
+import os
+import socket
+
+import numpy as np
+import torch.multiprocessing as mp
+
+import bench
+from oracle import pyoracle as O
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def worker(rank, ws, port, res):
+    import time
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(ws))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    n, nq, m = 1 << 14, 512, 24
+    t = O.random_string(n)
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    off = bench.rank_query_offsets(n, nq, m, rank)
+    qb = np.concatenate([t[o:o + m] for o in off.astype(np.int64)] + [np.zeros(64, np.uint8)])
+    out = {}
+
+    def step():
+        out["pos"], _ = O.search_many(tp, n, sa, qb, np.arange(nq, dtype=np.uint64) * m,
+                                      np.full(nq, m, np.uint32), "binary_search", 1)
+        if rank == 1:
+            time.sleep(0.02)  # uneven ranks: the MAX must be the slow one
+
+    def reduce_max(x):
+        tt = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        return float(tt.item())
+
+    el = bench.timed_loop(step, 3, 1, lambda: None, dist.barrier, reduce_max)
+    res[rank] = (el, off.tolist(), out["pos"].tolist())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_harness():
+    ws = 2
+    mgr = mp.Manager()
+    res = mgr.dict()
+    mp.spawn(worker, args=(ws, free_port(), res), nprocs=ws, join=True)
+    (e0, off0, p0), (e1, off1, p1) = res[0], res[1]
+    assert e0 == e1 and e0 >= 3 * 0.02  # both ranks report the same MAX
+    assert off0 != off1  # disjoint query streams per rank
+    # replicated index: each shard's answers equal a single-process search of those queries
+    n, m = 1 << 14, 24
+    t = O.random_string(n)
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    for off, pos in ((off0, p0), (off1, p1)):
+        for o, p in zip(off[:50], pos[:50]):
+            assert O.search_one(tp, n, sa, t[o:o + m])[0] == p
+            assert list(t[p:p + m]) == list(t[o:o + m])
