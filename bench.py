@@ -132,6 +132,9 @@ def main():
     ap.add_argument("--variants", default="plain,lcp", help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
+                    help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
+                         "ranges with RCCL all-to-all query routing (SURVEY §8e)")
     args = ap.parse_args()
 
     import torch
@@ -150,7 +153,17 @@ def main():
 
     t_build0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)  # sas/util.rs:9-15, identical on every rank
-    idx = sas_amd.SaNaive.build(text, lcp=True, stree=True)
+    if args.mode == "shard":
+        from sas_amd.shard import ShardedSearch, shard_range
+        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, rank_range=shard_range(n, ws, rank))
+        if dist is None:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
+            dist.init_process_group("nccl", rank=0, world_size=1)
+        engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo)
+    else:
+        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True)
     stats = idx.stats()
     off = rank_query_offsets(n, nq, m, rank)
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
@@ -176,7 +189,10 @@ def main():
 
     def run_algo(algo, steps, warmup):
         def step():
-            idx.search_fixed(qbytes, m, algo=algo, out=out)
+            if args.mode == "shard":
+                out.copy_(engine.search_fixed(qbytes, m))
+            else:
+                idx.search_fixed(qbytes, m, algo=algo, out=out)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         holder = {}
 
@@ -202,15 +218,20 @@ def main():
     el, kernel_ms, ok = run_algo(args.algo, args.steps, args.warmup)
     if not ok:
         raise SystemExit(f"bench: {args.algo} returned a non-occurrence position")
-    # probes -> tail probes for the algorithmic byte count (untimed pass)
-    _, probes = idx.search_fixed(qbytes, m, algo=args.algo, probes=True)
-    mean_probes = float(probes.double().mean().item())
+    # probes -> tail probes for the algorithmic byte count (untimed pass; a shard of a
+    # multi-GPU sharded run only holds part of the SA, so the pass needs the whole index)
+    whole = args.mode == "replicated" or ws == 1
+    if whole:
+        _, probes = idx.search_fixed(qbytes, m, algo=args.algo, probes=True)
+        mean_probes = float(probes.double().mean().item())
+    else:
+        mean_probes = float("nan")
     tail = max(0.0, mean_probes - stats["stree_layers"]) if args.algo == "stree" else mean_probes
     algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail)
     achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
 
     variants = {}
-    for v in [x for x in args.variants.split(",") if x and x != args.algo]:
+    for v in [x for x in args.variants.split(",") if x and x != args.algo and args.mode == "replicated"]:
         vel, vk, vok = run_algo(v, max(3, args.steps // 4), 1)
         _, vp = idx.search_fixed(qbytes, m, algo=v, probes=True)
         vb = algorithmic_bytes(v, n, m, stats["stree_layers"], float(vp.double().mean().item()))
@@ -220,7 +241,7 @@ def main():
 
     traffic, traffic_src = load_traffic(args.algo, n, nq, m)
     cpu = None
-    if rank == 0 and ws == 1 and not args.no_cpu:
+    if rank == 0 and ws == 1 and not args.no_cpu and args.mode == "replicated":
         cpu = cpu_baseline(text, idx, qbytes, m, nq, args.cpu_seconds)
 
     if rank == 0:
@@ -237,8 +258,12 @@ def main():
             "data": f"synthetic: random_string(ChaCha8Rng::seed_from_u64({SEED})) text + positive len-{m} "
                     f"substrings (sas/util.rs:9-26), per-rank query stream",
             "config": {"workload": workload, "algo": args.algo, "n": n, "queries_per_gpu": nq, "m": m,
-                       "parallelism": f"replicated index x{ws}, query shards (no data-path collective)"},
-            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                       "mode": args.mode,
+                       "parallelism": (f"replicated index x{ws}, query shards (no data-path collective)"
+                                       if args.mode == "replicated" else
+                                       f"SA rank ranges over {ws} GPUs, sas_route + RCCL all_to_all_single "
+                                       f"(queries out, positions back)")},
+            "roofline": None if not whole else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "k_sa_stree" if args.algo == "stree" else "k_sa_binary",

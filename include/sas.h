@@ -69,6 +69,9 @@ typedef struct sas_stats {
     uint64_t build_total_ns; /* wall time of sas_build                            */
     uint32_t sa_rounds;      /* prefix-doubling rounds after the 32-char sort     */
     uint32_t reserved;
+    uint64_t rank_lo;        /* global SA rank of this index's first entry         */
+    uint64_t sa_entries;     /* SA entries held (n, or a shard's rank range)       */
+    uint64_t next_pos;       /* SA[rank_lo + sa_entries] (n if none)               */
 } sas_stats;
 
 const char* sas_last_error(void);
@@ -79,6 +82,23 @@ const char* sas_last_error(void);
 int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
               uint32_t flags, sas_index** out);
 int sas_free(sas_index* index);
+
+/* Sharded-text mode: the index holds only global SA ranks
+ * [rank_lo, rank_hi) (the packed text stays whole: compares need any suffix).
+ * sa_or_null is the FULL suffix array, or NULL to construct it here.  A
+ * search on a shard returns SA[global lower bound] when that rank lies in
+ * (rank_lo, rank_hi], i.e. for every query routed to it by sas_route. */
+int sas_build_shard(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
+                    uint64_t rank_lo, uint64_t rank_hi, uint32_t flags, sas_index** out);
+
+/* Query routing for the sharded mode: out_shard[k] = number of splitter
+ * suffixes (text positions splitter_pos[0..nsplit), in increasing suffix
+ * order: the first suffix of shards 1..W-1) that are < query k.  Fixed-length
+ * queries qbytes[k*m .. (k+1)*m).  Device pointers with SAS_DEVICE_PTRS. */
+int sas_route(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsplit,
+              const uint8_t* qbytes, uint32_t m, uint64_t nq, uint32_t* out_shard,
+              void* stream, uint32_t flags);
+
 int sas_get_stats(const sas_index* index, sas_stats* out);
 
 /* Copy the suffix array / LCP array out (dst host or device per flags). */

@@ -51,7 +51,10 @@ int sas_errno_of(hipError_t e);
 
 // ---------------------------------------------------------------- index structs
 struct sas_index {
-    uint64_t n = 0;
+    uint64_t n = 0;               // text length (chars)
+    uint64_t sa_n = 0;            // SA entries held (= n, or a shard's rank range)
+    uint64_t rank_lo = 0;         // global rank of sa[0]
+    uint64_t next_pos = 0;        // global SA[rank_lo + sa_n] (n if none): answer when q > every held suffix
     int device = 0;
     int num_cus = 256;
     uint64_t* text_w = nullptr;  // packed text

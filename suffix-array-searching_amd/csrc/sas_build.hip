@@ -368,9 +368,11 @@ static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32
 }
 
 // ------------------------------------------------------------------ LCP, verify
-__global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+// Kernels below take the text length n (suffix lengths) and the number of SA
+// entries sa_n separately: a shard index holds a rank range of the global SA.
+__global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa, uint64_t sa_n,
                       uint32_t* __restrict__ lcp) {
-    GRID_STRIDE(r, n) {
+    GRID_STRIDE(r, sa_n) {
         if (r == 0) { lcp[0] = 0; continue; }
         uint64_t a = sa[r - 1], b = sa[r];
         uint64_t L = n - (a > b ? a : b);  // min suffix length
@@ -385,11 +387,11 @@ __global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, const uint32_
 }
 
 __global__ void k_verify_adj(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
-                             uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bad) {
-    GRID_STRIDE(r, n) {
+                             uint64_t sa_n, uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bad) {
+    GRID_STRIDE(r, sa_n) {
         uint64_t b = sa[r];
         if (b >= n) { atomicOr(bad, 1u); continue; }
-        atomicOr(&bitmap[b >> 5], 1u << (b & 31));
+        if (bitmap) atomicOr(&bitmap[b >> 5], 1u << (b & 31));
         if (r == 0) continue;
         uint64_t a = sa[r - 1];
         if (a >= n) continue;
@@ -414,20 +416,20 @@ __global__ void k_count_bits(const uint32_t* __restrict__ bitmap, uint64_t words
 }
 
 // ------------------------------------------------------------------ S-tree over 16-char keys
-__global__ void k_keys16(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+__global__ void k_keys16(const uint64_t* __restrict__ tw, const uint32_t* __restrict__ sa, uint64_t sa_n,
                          uint32_t* __restrict__ leaves, uint64_t leaf_words) {
-    GRID_STRIDE(r, leaf_words) leaves[r] = r < n ? (uint32_t)(text_chars32(tw, sa[r]) >> 32) : SAS_KEY_MAX;
+    GRID_STRIDE(r, leaf_words) leaves[r] = r < sa_n ? (uint32_t)(text_chars32(tw, sa[r]) >> 32) : SAS_KEY_MAX;
 }
 
 // One internal layer (sst/s_tree.rs:149-172 with left_max = false):
-// key j of node i = first key of child subtree j+1, MAX if beyond n.
+// key j of node i = first key of child subtree j+1, MAX if beyond the keys.
 __global__ void k_stree_layer(uint32_t* __restrict__ tree, uint64_t oh, uint64_t layer_nodes, uint64_t ol,
-                              uint32_t h, uint32_t height, uint64_t n) {
+                              uint32_t h, uint32_t height, uint64_t nkeys) {
     const uint64_t B = SAS_STREE_B;
     GRID_STRIDE(i, B * layer_nodes) {
         uint64_t k = (i / B) * (B + 1) + (i % B) + 1;
         for (uint32_t l = h; l + 2 < height; l++) k *= (B + 1);
-        tree[(oh + i / B) * 16 + (i % B)] = (k * B < n) ? tree[(ol + k) * 16] : SAS_KEY_MAX;
+        tree[(oh + i / B) * 16 + (i % B)] = (k * B < nkeys) ? tree[(ol + k) * 16] : SAS_KEY_MAX;
     }
 }
 
@@ -443,11 +445,11 @@ static uint64_t tb_layer(uint64_t n, uint32_t h, uint32_t height) {
 // ------------------------------------------------------------------ LDS top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
 // the leading one (0 = went left: r = mid, 1 = right: l = mid + 1).
-__global__ void k_top(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+__global__ void k_top(const uint64_t* __restrict__ tw, const uint32_t* __restrict__ sa, uint64_t sa_n,
                       uint64_t* __restrict__ top_key, uint32_t* __restrict__ top_sa, uint32_t nodes) {
     GRID_STRIDE(k, nodes) {
         if (k == 0) { top_key[0] = 0; top_sa[0] = 0xFFFFFFFFu; continue; }
-        uint64_t l = 0, r = n;
+        uint64_t l = 0, r = sa_n;
         int depth = 63 - __clzll(k);
         for (int b = depth - 1; b >= 0; b--) {
             uint64_t mid = (l + r) >> 1;
@@ -483,40 +485,44 @@ static uint64_t now_ns() {
                std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
-static int verify_impl(const sas_index* x) {
+// full = the SA must be a permutation of 0..n (false for a shard's rank range)
+static int verify_sa(const uint64_t* tw, uint64_t n, const uint32_t* sa, uint64_t sa_n, bool full) {
     DevBuf bitmap, bad;
-    uint64_t words = (x->n + 31) / 32;
-    TRY(bitmap.alloc(words * 4, "verify bitmap"));
+    uint64_t words = (n + 31) / 32;
+    if (full) {
+        TRY(bitmap.alloc(words * 4, "verify bitmap"));
+        HIP_TRY(hipMemset(bitmap.p, 0, words * 4));
+    }
     TRY(bad.alloc(16, "verify flags"));
-    HIP_TRY(hipMemset(bitmap.p, 0, words * 4));
     HIP_TRY(hipMemset(bad.p, 0, 16));
-    hipLaunchKernelGGL(k_verify_adj, dim3(grid_for(x->n)), dim3(256), 0, 0, x->text_w, x->n, x->sa,
-                       bitmap.as<uint32_t>(), bad.as<uint32_t>());
-    hipLaunchKernelGGL(k_count_bits, dim3(grid_for(words)), dim3(256), 0, 0, bitmap.as<uint32_t>(), words,
-                       reinterpret_cast<unsigned long long*>(bad.as<uint32_t>() + 2));
+    hipLaunchKernelGGL(k_verify_adj, dim3(grid_for(sa_n)), dim3(256), 0, 0, tw, n, sa, sa_n,
+                       full ? bitmap.as<uint32_t>() : nullptr, bad.as<uint32_t>());
+    if (full)
+        hipLaunchKernelGGL(k_count_bits, dim3(grid_for(words)), dim3(256), 0, 0, bitmap.as<uint32_t>(), words,
+                           reinterpret_cast<unsigned long long*>(bad.as<uint32_t>() + 2));
     HIP_TRY(hipGetLastError());
     uint32_t h[4];
     HIP_TRY(hipMemcpy(h, bad.p, 16, hipMemcpyDeviceToHost));
     uint64_t seen = (uint64_t)h[2] | ((uint64_t)h[3] << 32);
     if (h[0] & 1) SAS_FAIL(EINVAL, "suffix array holds an entry >= n");
     if (h[0] & 2) SAS_FAIL(EINVAL, "suffix array not sorted: adjacent suffixes not strictly increasing");
-    if (seen != x->n) SAS_FAIL(EINVAL, "suffix array is not a permutation of 0..n");
+    if (full && seen != n) SAS_FAIL(EINVAL, "suffix array is not a permutation of 0..n");
     return 0;
 }
 
 extern "C" int sas_verify(const sas_index* index) {
     if (!index) SAS_FAIL(EINVAL, "sas_verify: null index");
     HIP_TRY(hipSetDevice(index->device));
-    return verify_impl(index);
+    return verify_sa(index->text_w, index->n, index->sa, index->sa_n, index->sa_n == index->n);
 }
 
 static int build_stree(sas_index* x) {
-    uint64_t n = x->n;
-    uint32_t height = tb_height(n);
+    uint64_t nk = x->sa_n;
+    uint32_t height = tb_height(nk);
     if (height > SAS_STREE_MAX_LAYERS) SAS_FAIL(ENOTSUP, "S-tree too high");
     uint64_t ls[SAS_STREE_MAX_LAYERS], tot = 0;
     for (uint32_t h = 0; h < height; h++) {
-        ls[h] = (tb_layer(n, h, height) + 15) / 16;
+        ls[h] = (tb_layer(nk, h, height) + 15) / 16;
         x->stree_off[h] = tot;
         tot += ls[h];
     }
@@ -524,12 +530,12 @@ static int build_stree(sas_index* x) {
     TRY(t.alloc(tot * 64, "S-tree"));
     uint32_t* tree = t.as<uint32_t>();
     uint64_t ol = x->stree_off[height - 1];
-    hipLaunchKernelGGL(k_keys16, dim3(grid_for(ls[height - 1] * 16)), dim3(256), 0, 0, x->text_w, n, x->sa,
+    hipLaunchKernelGGL(k_keys16, dim3(grid_for(ls[height - 1] * 16)), dim3(256), 0, 0, x->text_w, x->sa, nk,
                        tree + ol * 16, ls[height - 1] * 16);
     for (int h = (int)height - 2; h >= 0; h--) {
         // internal nodes: slots B..N stay MAX (B == N == 16 here, so none)
         hipLaunchKernelGGL(k_stree_layer, dim3(grid_for(16 * ls[h])), dim3(256), 0, 0, tree, x->stree_off[h],
-                           ls[h], ol, (uint32_t)h, height, n);
+                           ls[h], ol, (uint32_t)h, height, nk);
     }
     HIP_TRY(hipGetLastError());
     x->stree = static_cast<uint32_t*>(t.release());
@@ -547,8 +553,10 @@ static int build_stree(sas_index* x) {
     return 0;
 }
 
-extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
-                         sas_index** out) {
+// Common builder.  [rank_lo, rank_hi) = the SA ranks this index holds
+// (the whole SA for sas_build, a shard's range for sas_build_shard).
+static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
+                      uint64_t rank_lo, uint64_t rank_hi, sas_index** out) {
     if (!out) SAS_FAIL(EINVAL, "sas_build: null out");
     *out = nullptr;
     if (n == 0) SAS_FAIL(EINVAL, "sas_build: empty text");
@@ -556,9 +564,12 @@ extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null
     if (n >= (1ull << 32) - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^32 needs a 40/64-bit SA (not built yet)");
     if (sa_or_null && sa_width != 4) SAS_FAIL(EINVAL, "sas_build: only sa_width 4 (u32) is supported");
     if (!sa_or_null && n >= (1ull << 31)) SAS_FAIL(ENOTSUP, "sas_build: GPU SA construction needs n < 2^31");
+    if (rank_lo >= rank_hi || rank_hi > n) SAS_FAIL(EINVAL, "sas_build_shard: empty or out-of-range rank range");
     uint64_t t0 = now_ns();
     sas_index* x = new sas_index();
     x->n = n;
+    x->rank_lo = rank_lo;
+    x->sa_n = rank_hi - rank_lo;
     HIP_TRY(hipGetDevice(&x->device));
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, x->device) == hipSuccess) x->num_cus = prop.multiProcessorCount;
@@ -587,26 +598,40 @@ extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null
     x->text_w = tw.as<uint64_t>();
     tw.release();
 
-    // suffix array
+    // global suffix array (caller's or built here), then this index's rank range
     DevBuf sa;
     TRY(sa.alloc(n * 4, "suffix array"));
-    x->sa = sa.as<uint32_t>();
-    sa.release();
     if (sa_or_null) {
-        HIP_TRY(hipMemcpy(x->sa, sa_or_null, n * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
-        if (flags & SAS_BUILD_VERIFY) TRY(verify_impl(x));
+        HIP_TRY(hipMemcpy(sa.p, sa_or_null, n * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
     } else {
         uint64_t s0 = now_ns();
-        TRY(build_sa_gpu(x->text_w, n, x->sa, &x->stats.sa_rounds));
+        TRY(build_sa_gpu(x->text_w, n, sa.as<uint32_t>(), &x->stats.sa_rounds));
         HIP_TRY(hipDeviceSynchronize());
         x->stats.build_sa_ns = now_ns() - s0;
-        if (flags & SAS_BUILD_VERIFY) TRY(verify_impl(x));
     }
+    if (flags & SAS_BUILD_VERIFY) TRY(verify_sa(x->text_w, n, sa.as<uint32_t>(), n, true));
+    if (rank_hi < n) {
+        uint32_t np = 0;
+        HIP_TRY(hipMemcpy(&np, sa.as<uint32_t>() + rank_hi, 4, hipMemcpyDeviceToHost));
+        x->next_pos = np;
+    } else {
+        x->next_pos = n;
+    }
+    if (x->sa_n == n) {
+        x->sa = static_cast<uint32_t*>(sa.release());
+    } else {
+        DevBuf part;
+        TRY(part.alloc(x->sa_n * 4, "suffix array shard"));
+        HIP_TRY(hipMemcpy(part.p, sa.as<uint32_t>() + rank_lo, x->sa_n * 4, hipMemcpyDeviceToDevice));
+        sa.alloc(0, "free");
+        x->sa = static_cast<uint32_t*>(part.release());
+    }
+    const uint64_t sa_n = x->sa_n;
 
     if (flags & SAS_BUILD_LCP) {
         DevBuf l;
-        TRY(l.alloc(n * 4, "lcp"));
-        hipLaunchKernelGGL(k_lcp, dim3(grid_for(n)), dim3(256), 0, 0, x->text_w, n, x->sa, l.as<uint32_t>());
+        TRY(l.alloc(sa_n * 4, "lcp"));
+        hipLaunchKernelGGL(k_lcp, dim3(grid_for(sa_n)), dim3(256), 0, 0, x->text_w, n, x->sa, sa_n, l.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         x->lcp = static_cast<uint32_t*>(l.release());
     }
@@ -614,13 +639,13 @@ extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null
 
     // binary-search top in LDS
     {
-        uint32_t iters = 64 - __builtin_clzll(n);  // ilog2(n) + 1 (sas/sa_search.rs:171)
+        uint32_t iters = 64 - __builtin_clzll(sa_n);  // ilog2(len) + 1 (sas/sa_search.rs:171)
         x->iters = iters;
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
         DevBuf k, s;
         TRY(k.alloc(SAS_TOP_NODES * 8, "top keys"));
         TRY(s.alloc(SAS_TOP_NODES * 4, "top sa"));
-        hipLaunchKernelGGL(k_top, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, n, x->sa,
+        hipLaunchKernelGGL(k_top, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, x->sa, sa_n,
                            k.as<uint64_t>(), s.as<uint32_t>(), (uint32_t)SAS_TOP_NODES);
         HIP_TRY(hipGetLastError());
         x->top_key = static_cast<uint64_t*>(k.release());
@@ -633,17 +658,30 @@ extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null
     sas_stats& st = x->stats;
     st.n = n;
     st.text_bytes = x->text_words * 8;
-    st.sa_bytes = n * 4;
-    st.lcp_bytes = x->lcp ? n * 4 : 0;
+    st.sa_bytes = sa_n * 4;
+    st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
     st.stree_bytes = x->stree_nodes * 64;
     st.stree_layers = x->stree_height;
     st.stree_lds_layers = x->stree_lds_layers;
     st.top_levels = x->top_levels;
     st.iterations = x->iters;
+    st.rank_lo = rank_lo;
+    st.sa_entries = sa_n;
+    st.next_pos = x->next_pos;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard
     return 0;
+}
+
+extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
+                         sas_index** out) {
+    return build_impl(text, n, sa_or_null, sa_width, flags, 0, n, out);
+}
+
+extern "C" int sas_build_shard(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
+                               uint64_t rank_lo, uint64_t rank_hi, uint32_t flags, sas_index** out) {
+    return build_impl(text, n, sa_or_null, sa_width, flags, rank_lo, rank_hi, out);
 }
 
 extern "C" int sas_get_stats(const sas_index* index, sas_stats* out) {
@@ -659,13 +697,13 @@ static int copy_out(const void* src, void* dst, uint64_t bytes, uint32_t flags) 
 
 extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
     if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_sa: null argument");
-    if (count > index->n) SAS_FAIL(EINVAL, "sas_copy_sa: count > n");
+    if (count > index->sa_n) SAS_FAIL(EINVAL, "sas_copy_sa: count > number of SA entries");
     return copy_out(index->sa, dst, count * 4, flags);
 }
 
 extern "C" int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
     if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_lcp: null argument");
     if (!index->lcp) SAS_FAIL(EINVAL, "sas_copy_lcp: index built without SAS_BUILD_LCP");
-    if (count > index->n) SAS_FAIL(EINVAL, "sas_copy_lcp: count > n");
+    if (count > index->sa_n) SAS_FAIL(EINVAL, "sas_copy_lcp: count > number of SA entries");
     return copy_out(index->lcp, dst, count * 4, flags);
 }

@@ -28,7 +28,9 @@
 
 struct SearchArgs {
     const uint64_t* tw;
-    uint64_t n;
+    uint64_t n;          // text length
+    uint64_t sa_n;       // SA entries held by this index
+    uint64_t next_pos;   // answer when the lower bound is sa_n (n for a whole index)
     const uint32_t* sa;
     const uint64_t* top_key;
     const uint32_t* top_sa;
@@ -84,7 +86,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
 
-        uint64_t l = 0, r = n;
+        uint64_t l = 0, r = a.sa_n;
         uint32_t k = 1, probes = 0, llcp = 0, rlcp = 0;
         uint32_t pr = 0;  // SA[r] once r has moved
         for (uint32_t it = 0; it < a.iters; ++it) {
@@ -112,7 +114,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                 }
             }
         }
-        a.out_pos[i] = (r >= n) ? n : (uint64_t)pr;
+        a.out_pos[i] = (r >= a.sa_n) ? a.next_pos : (uint64_t)pr;
         if (a.out_probes) a.out_probes[i] = probes;
     }
     if (bad) atomicOr(a.bad, 1u);
@@ -168,7 +170,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
     const uint64_t n = a.n;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
     const uint64_t ol = a.stree_off[a.stree_height - 1];
-    const uint64_t leaf_nodes = (n + 15) / 16;
+    const uint64_t sa_n = a.sa_n;
+    const uint64_t leaf_nodes = (sa_n + 15) / 16;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t* qb;
@@ -197,7 +200,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
             }
             if (kk < leaf_nodes && steps == 4) {  // long run: lower_bound(K + 1)
                 if (K == SAS_KEY_MAX) {
-                    r1 = n;
+                    r1 = sa_n;
                 } else {
                     uint64_t k2 = stree_descend(a, s_nodes, K + 1, &probes);
                     r1 = k2 * 16 + cnt_lt_node(g + (ol + k2) * 4, K + 1);
@@ -205,8 +208,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
                 }
             }
         }
-        if (r0 > n) r0 = n;
-        if (r1 > n) r1 = n;
+        if (r0 > sa_n) r0 = sa_n;
+        if (r1 > sa_n) r1 = sa_n;
 
         // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
         const uint32_t h16 = m < 16 ? m : 16;
@@ -230,7 +233,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
             }
         }
         uint64_t pos;
-        if (l >= n) pos = n;
+        if (l >= sa_n) pos = a.next_pos;
         else if (have) pos = pr;
         else pos = a.sa[l];
         a.out_pos[i] = pos;
@@ -280,6 +283,8 @@ static int qw_for(uint64_t maxlen) {
 static void fill_args(const sas_index* x, SearchArgs& a) {
     a.tw = x->text_w;
     a.n = x->n;
+    a.sa_n = x->sa_n;
+    a.next_pos = x->next_pos;
     a.sa = x->sa;
     a.top_key = x->top_key;
     a.top_sa = x->top_sa;
@@ -425,5 +430,61 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (call_ns) *call_ns = std::chrono::duration<double, std::nano>(t1 - t0).count() / reps;
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
+    return 0;
+}
+
+// ------------------------------------------------------------------ sharded-mode routing
+#define SAS_MAX_SPLIT 1024
+__global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ tw, uint64_t n,
+                                               const uint64_t* __restrict__ sp, uint32_t nsplit,
+                                               const uint8_t* __restrict__ qbytes, uint32_t m, uint64_t nq,
+                                               uint32_t* __restrict__ out, uint32_t* bad) {
+    uint32_t b = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
+        QueryRegs<4> q;
+        q.load(qbytes + i * (uint64_t)m, m, &b);
+        uint32_t lo = 0, hi = nsplit, lcp;
+        while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
+            uint32_t mid = (lo + hi) >> 1;
+            if (suffix_less_from<4>(tw, n, sp[mid], q, 0, &lcp)) lo = mid + 1;
+            else hi = mid;
+        }
+        out[i] = lo;
+    }
+    if (b) atomicOr(bad, 1u);
+}
+
+extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit, const uint8_t* qbytes,
+                         uint32_t m, uint64_t nq, uint32_t* out_shard, void* stream, uint32_t flags) {
+    if (!x || (nsplit && !splitter_pos) || (nq && (!qbytes || !out_shard))) SAS_FAIL(EINVAL, "sas_route: null argument");
+    if (nsplit > SAS_MAX_SPLIT) SAS_FAIL(EINVAL, "sas_route: too many splitters");
+    if (nq == 0) return 0;
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    bool dev = flags & SAS_DEVICE_PTRS;
+    DeviceBuf bsp, bq, bout;
+    const uint64_t* dsp = splitter_pos;
+    const uint8_t* dq = qbytes;
+    uint32_t* dout = out_shard;
+    if (!dev) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMalloc(&bsp.p, nsplit * 8 + 8));
+        if (nsplit) HIP_TRY(hipMemcpy(bsp.p, splitter_pos, nsplit * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&bq.p, nq * (uint64_t)m + 64));
+        HIP_TRY(hipMemcpy(bq.p, qbytes, nq * (uint64_t)m, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&bout.p, nq * 4));
+        dsp = static_cast<const uint64_t*>(bsp.p);
+        dq = static_cast<const uint8_t*>(bq.p);
+        dout = static_cast<uint32_t*>(bout.p);
+    }
+    uint64_t blocks = (nq + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_route, dim3((unsigned)blocks), dim3(256), 0, st, x->text_w, x->n, dsp, nsplit, dq, m, nq,
+                       dout, x->scratch);
+    HIP_TRY(hipGetLastError());
+    if (!dev) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpy(out_shard, dout, nq * 4, hipMemcpyDeviceToHost));
+    }
     return 0;
 }

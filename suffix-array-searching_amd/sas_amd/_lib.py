@@ -38,6 +38,7 @@ class SasStats(C.Structure):
         ("stree_bytes", C.c_uint64), ("stree_layers", C.c_uint32), ("stree_lds_layers", C.c_uint32),
         ("top_levels", C.c_uint32), ("iterations", C.c_uint32), ("build_sa_ns", C.c_uint64),
         ("build_total_ns", C.c_uint64), ("sa_rounds", C.c_uint32), ("reserved", C.c_uint32),
+        ("rank_lo", C.c_uint64), ("sa_entries", C.c_uint64), ("next_pos", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -89,6 +90,8 @@ def lib():
     L.sas_last_error.restype = C.c_char_p
     L.sas_build.argtypes = [vp, u64, vp, i32, u32, C.POINTER(vp)]
     L.sas_free.argtypes = [vp]
+    L.sas_build_shard.argtypes = [vp, u64, vp, i32, u64, u64, u32, C.POINTER(vp)]
+    L.sas_route.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, u32]
     L.sas_get_stats.argtypes = [vp, C.POINTER(SasStats)]
     L.sas_copy_sa.argtypes = [vp, vp, u64, u32]
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]

@@ -51,10 +51,15 @@ class SaNaive:
 
     def __init__(self, handle, n):
         self._h = handle
-        self.n = n
+        self.n = n  # text length
+        self.sa_n = self.stats()["sa_entries"]  # SA entries held (n, or a shard's rank range)
+        self.rank_lo = self.stats()["rank_lo"]
 
     @classmethod
-    def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False) -> "SaNaive":
+    def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
+              rank_range: tuple[int, int] | None = None) -> "SaNaive":
+        """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
+        ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags = (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
@@ -69,7 +74,11 @@ class SaNaive:
         if _is_cuda(t):
             flags |= _lib.SAS_DEVICE_PTRS
         h = C.c_void_p()
-        check(lib().sas_build(_ptr(t), n, sa_ptr, 4, flags, C.byref(h)))
+        if rank_range is None:
+            check(lib().sas_build(_ptr(t), n, sa_ptr, 4, flags, C.byref(h)))
+        else:
+            check(lib().sas_build_shard(_ptr(t), n, sa_ptr, 4, int(rank_range[0]), int(rank_range[1]), flags,
+                                        C.byref(h)))
         return cls(h, n)
 
     def free(self):
@@ -89,15 +98,35 @@ class SaNaive:
         check(lib().sas_get_stats(self._h, C.byref(s)))
         return s.as_dict()
 
-    def suffix_array(self) -> np.ndarray:
-        out = np.zeros(self.n, np.uint32)
-        check(lib().sas_copy_sa(self._h, out.ctypes.data, self.n, 0))
-        return out
+    def suffix_array(self, count: int | None = None) -> np.ndarray:
+        count = self.sa_n if count is None else count
+        out = np.zeros(max(count, 1), np.uint32)
+        check(lib().sas_copy_sa(self._h, out.ctypes.data, count, 0))
+        return out[:count]
 
     def lcp_array(self) -> np.ndarray:
-        out = np.zeros(self.n, np.uint32)
-        check(lib().sas_copy_lcp(self._h, out.ctypes.data, self.n, 0))
+        out = np.zeros(self.sa_n, np.uint32)
+        check(lib().sas_copy_lcp(self._h, out.ctypes.data, self.sa_n, 0))
         return out
+
+    def route(self, splitter_pos, qbytes, m: int, stream=None):
+        """Sharded mode: shard id of each fixed-length query = number of splitter
+        suffixes < q (sas_route).  numpy in -> numpy out; CUDA in -> CUDA out."""
+        if _is_cuda(qbytes):
+            import torch
+            nq = qbytes.numel() // m
+            out = torch.empty(nq, dtype=torch.int32, device=qbytes.device)
+            st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
+            check(lib().sas_route(self._h, splitter_pos.data_ptr(), splitter_pos.numel(), qbytes.data_ptr(), m, nq,
+                                  out.data_ptr(), st, _lib.SAS_DEVICE_PTRS))
+            return out
+        qbytes = _as_u8(qbytes)
+        sp = np.ascontiguousarray(splitter_pos, np.uint64)
+        nq = len(qbytes) // m
+        out = np.zeros(max(nq, 1), np.uint32)
+        check(lib().sas_route(self._h, sp.ctypes.data if len(sp) else None, len(sp), qbytes.ctypes.data, m, nq,
+                              out.ctypes.data, stream, 0))
+        return out[:nq]
 
     def verify(self):
         check(lib().sas_verify(self._h))

@@ -68,3 +68,75 @@ def test_two_rank_harness():
         for o, p in zip(off[:50], pos[:50]):
             assert O.search_one(tp, n, sa, t[o:o + m])[0] == p
             assert list(t[p:p + m]) == list(t[o:o + m])
+
+
+# ------------------------------------------------------------------ sharded-text mode
+class OracleShard:
+    """CPU stand-in for a GPU shard index (same interface as sas_amd.SaNaive)
+    so the all-to-all exchange of sas_amd.shard.ShardedSearch runs on gloo."""
+
+    def __init__(self, t, sa_full, lo, hi):
+        self.tb = bytes(t.tolist())
+        self.n = len(t)
+        self.sa = sa_full[lo:hi]
+        self.next = int(sa_full[hi]) if hi < self.n else self.n
+
+    def suffix_array(self, count):
+        return self.sa[:count]
+
+    def route(self, splitters, qbytes, m):
+        import torch
+        sp = [int(s) for s in splitters.tolist()]
+        qs = qbytes.view(-1, m).tolist()
+        return torch.tensor([sum(self.tb[s:] < bytes(q) for s in sp) for q in qs], dtype=torch.int32)
+
+    def search_fixed(self, qbytes, m, algo=None):
+        import torch
+        out = []
+        for q in qbytes.view(-1, m).tolist():
+            q = bytes(q)
+            l, r = 0, len(self.sa)
+            while l < r:
+                mid = (l + r) // 2
+                if self.tb[int(self.sa[mid]):] < q:
+                    l = mid + 1
+                else:
+                    r = mid
+            out.append(int(self.sa[l]) if l < len(self.sa) else self.next)
+        return torch.tensor(out, dtype=torch.int64)
+
+
+def shard_worker(rank, ws, port, res):
+    import torch
+    import torch.distributed as dist
+    from sas_amd.shard import ShardedSearch, shard_range
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    n, nq, m = 3000, 200, 12
+    t = O.random_string(n, seed=5)
+    sa = O.build_sa(t)
+    lo, hi = shard_range(n, ws, rank)
+    eng = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu")
+    rng = np.random.default_rng(rank)
+    offs = rng.integers(0, n - m, nq)
+    qs = np.stack([t[o:o + m] for o in offs])
+    qs[: nq // 4] = rng.integers(0, 4, (nq // 4, m))  # negatives too
+    qs[-1] = 3  # above every suffix -> n
+    pos = eng.search_fixed(torch.from_numpy(qs.reshape(-1).copy()), m)
+    res[rank] = (qs.tolist(), pos.tolist())
+    dist.destroy_process_group()
+
+
+def test_sharded_exchange_three_ranks():
+    ws = 3
+    mgr = mp.Manager()
+    res = mgr.dict()
+    mp.spawn(shard_worker, args=(ws, free_port(), res), nprocs=ws, join=True)
+    n = 3000
+    t = O.random_string(n, seed=5)
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    for r in range(ws):
+        qs, pos = res[r]
+        for q, p in zip(qs, pos):
+            assert O.search_one(tp, n, sa, np.array(q, np.uint8))[0] == p

@@ -193,3 +193,40 @@ def test_device_pointer_path(sas):
     out = torch.empty(nq, dtype=torch.int64, device="cuda")
     kns, cns = idx.time_fixed(qb, m, nq, out, algo="stree", reps=3)
     assert kns > 0 and np.array_equal(out.cpu().numpy().astype(np.uint64), host)
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_sharded_indexes_single_gpu(sas, world):
+    """Sharded-text mode on one GPU: W shard indexes (global SA rank ranges),
+    queries routed by sas_route, answered by their shard == the whole index."""
+    from sas_amd.shard import shard_range
+    n, nq, m = 200_003, 20_000, 24
+    t = sas.random_string(n, seed=11)
+    full = sas.SaNaive.build(t)
+    sa = full.suffix_array()
+    shards = [sas.SaNaive.build(t, sa=sa, rank_range=shard_range(n, world, g)) for g in range(world)]
+    for g, s in enumerate(shards):
+        lo, hi = shard_range(n, world, g)
+        st = s.stats()
+        assert st["rank_lo"] == lo and st["sa_entries"] == hi - lo
+        assert st["next_pos"] == (sa[hi] if hi < n else n)
+        assert np.array_equal(s.suffix_array(), sa[lo:hi])
+    splitters = np.array([sa[shard_range(n, world, g)[0]] for g in range(1, world)], np.uint64)
+    off, _, _ = sas.random_queries(n, nq, seed=3, len_lo=m, len_hi=m + 1)
+    qb = np.concatenate([t[o:o + m] for o in off.astype(np.int64)])
+    rng = np.random.default_rng(0)
+    qb[: (nq // 4) * m] = rng.integers(0, 4, (nq // 4) * m, dtype=np.uint8)
+    expect = full.search_fixed(qb, m, algo="plain")
+    dest = shards[0].route(splitters, qb, m)
+    assert dest.max() < world
+    got = np.zeros(nq, np.uint64)
+    for g in range(world):
+        sel = np.nonzero(dest == g)[0]
+        if len(sel) == 0:
+            continue
+        sub = qb.reshape(nq, m)[sel].reshape(-1)
+        for algo in ALGOS:
+            r = shards[g].search_fixed(sub, m, algo=algo)
+            assert np.array_equal(r, expect[sel]), (world, g, algo)
+        got[sel] = r
+    assert np.array_equal(got, expect)
