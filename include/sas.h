@@ -47,6 +47,8 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_VERIFY  (1u << 3)  /* run the adjacency + permutation check on the SA  */
 #define SAS_NO_LDS_TOP    (1u << 4)  /* search: do not serve the top levels from LDS     */
 #define SAS_VALIDATE      (1u << 5)  /* search: reject query bytes > 3 (synchronises)    */
+#define SAS_BUILD_WIDE    (1u << 6)  /* build: use the n >= 2^31 two-pass doubling rounds
+                                        at any n (test hook for that path)               */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {

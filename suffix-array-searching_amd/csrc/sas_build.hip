@@ -230,17 +230,64 @@ __global__ void k_assign(const uint64_t* __restrict__ keys, uint64_t cnt, const 
 }
 
 // Doubling key for the tied element at rank list[k]: (group of p, order of p + h).
-// p + h >= n -> the suffix is shorter than h: value n - p (< 2^31) sorts it
+// p + h >= n -> the suffix is shorter than h: value n - p (<= h) sorts it
 // before every longer one and by length among the short ones (Rust slice order:
-// a proper prefix sorts first); otherwise 2^31 | rank[p + h].
+// a proper prefix sorts first); otherwise BIG + rank[p + h] with BIG > h.
+__device__ __forceinline__ uint64_t second_key(const uint32_t* __restrict__ rank, uint64_t n, uint64_t p,
+                                               uint64_t h, uint64_t big) {
+    return (p + h < n) ? (big + rank[p + h]) : (n - p);
+}
+
+// n < 2^31: one 64-bit key (group << 32 | second) with BIG = 2^31.
 __global__ void k_round_keys(const uint32_t* __restrict__ list, uint64_t cnt, const uint32_t* __restrict__ sa,
                              const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
                              uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     GRID_STRIDE(k, cnt) {
         uint32_t p = sa[list[k]];
-        uint32_t second = (p + h < n) ? (0x80000000u | rank[p + h]) : (uint32_t)(n - p);
-        keys[k] = ((uint64_t)rank[p] << 32) | second;
+        keys[k] = ((uint64_t)rank[p] << 32) | second_key(rank, n, p, h, 0x80000000ull);
         vals[k] = p;
+    }
+}
+
+// n >= 2^31: LSD two-pass -- sort by the 33-bit second key (BIG = 2^32), then
+// stably by the group id gathered from the positions.
+__global__ void k_round_second(const uint32_t* __restrict__ list, uint64_t cnt, const uint32_t* __restrict__ sa,
+                               const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
+                               uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    GRID_STRIDE(k, cnt) {
+        uint32_t p = sa[list[k]];
+        keys[k] = second_key(rank, n, p, h, 0x100000000ull);
+        vals[k] = p;
+    }
+}
+__global__ void k_round_group(const uint32_t* __restrict__ vals, uint64_t cnt, const uint32_t* __restrict__ rank,
+                              uint64_t* __restrict__ keys) {
+    GRID_STRIDE(k, cnt) keys[k] = rank[vals[k]];
+}
+
+// Group heads of a sorted round, from the (not yet updated) ranks.
+__global__ void k_round_heads(const uint32_t* __restrict__ vals, uint64_t cnt, const uint32_t* __restrict__ rank,
+                              uint64_t n, uint64_t h, const uint32_t* __restrict__ list,
+                              uint32_t* __restrict__ headpos, uint8_t* __restrict__ head) {
+    GRID_STRIDE(k, cnt) {
+        bool hd = true;
+        if (k > 0) {
+            uint32_t p = vals[k], q = vals[k - 1];
+            hd = rank[p] != rank[q] || second_key(rank, n, p, h, 0x100000000ull) !=
+                                           second_key(rank, n, q, h, 0x100000000ull);
+        }
+        head[k] = hd;
+        headpos[k] = hd ? list[k] : 0u;
+    }
+}
+
+__global__ void k_round_assign(uint64_t cnt, const uint32_t* __restrict__ list, const uint32_t* __restrict__ sa,
+                               const uint32_t* __restrict__ group, const uint8_t* __restrict__ head,
+                               uint32_t* __restrict__ rank, uint8_t* __restrict__ unresolved) {
+    GRID_STRIDE(k, cnt) {
+        rank[sa[list[k]]] = group[k];
+        bool h1 = (k + 1 == cnt) || head[k + 1];
+        unresolved[k] = !(head[k] && h1);
     }
 }
 
@@ -274,7 +321,7 @@ struct DevBuf {
 #define TRY(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
 
 // Prefix doubling on the GPU.  sa_out: device u32[n].
-static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32_t* rounds_out) {
+static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32_t* rounds_out, bool force_wide) {
     hipStream_t st = 0;
     DevBuf keys_a, keys_b, vals_b, rank, aux, list_a, list_b, flags, tmp, counter;
     TRY(keys_a.alloc(n * 8, "sa keys"));
@@ -326,6 +373,9 @@ static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32
     uint32_t rounds = 0;
     uint32_t* list = list_a.as<uint32_t>();
     uint32_t* list_next = list_b.as<uint32_t>();
+    const bool wide = force_wide || n >= (1ull << 31);
+    DevBuf heads;
+    if (cnt) TRY(heads.alloc(n, "round heads"));
     for (uint64_t h = 32; cnt > 0; h *= 2) {
         if (h >= 2 * n + 64) SAS_FAIL(EIO, "sa construction did not converge");
         rounds++;
@@ -333,31 +383,49 @@ static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32
         uint64_t* rk2 = keys_b.as<uint64_t>();
         uint32_t* rv = vals_b.as<uint32_t>();
         uint32_t* rv2 = aux.as<uint32_t>();
-        hipLaunchKernelGGL(k_round_keys, dim3(grid_for(cnt)), dim3(256), 0, st, list, cnt, sa_out,
-                           rank.as<uint32_t>(), n, h, rk, rv);
-        rocprim::double_buffer<uint64_t> k2(rk, rk2);
-        rocprim::double_buffer<uint32_t> v2(rv, rv2);
+        const uint32_t* sv;
         size_t b2 = 0;
-        HIP_TRY(rocprim::radix_sort_pairs(nullptr, b2, k2, v2, (size_t)cnt, 0, 64, st));
-        TRY(tmp.alloc(b2, "round sort temp"));
-        HIP_TRY(rocprim::radix_sort_pairs(tmp.p, b2, k2, v2, (size_t)cnt, 0, 64, st));
-        const uint64_t* sk = k2.current();
-        uint32_t* sv = v2.current();
+        if (!wide) {
+            hipLaunchKernelGGL(k_round_keys, dim3(grid_for(cnt)), dim3(256), 0, st, list, cnt, sa_out,
+                               rank.as<uint32_t>(), n, h, rk, rv);
+            rocprim::double_buffer<uint64_t> k2(rk, rk2);
+            rocprim::double_buffer<uint32_t> v2(rv, rv2);
+            HIP_TRY(rocprim::radix_sort_pairs(nullptr, b2, k2, v2, (size_t)cnt, 0, 64, st));
+            TRY(tmp.alloc(b2, "round sort temp"));
+            HIP_TRY(rocprim::radix_sort_pairs(tmp.p, b2, k2, v2, (size_t)cnt, 0, 64, st));
+            sv = v2.current();
+        } else {
+            hipLaunchKernelGGL(k_round_second, dim3(grid_for(cnt)), dim3(256), 0, st, list, cnt, sa_out,
+                               rank.as<uint32_t>(), n, h, rk, rv);
+            rocprim::double_buffer<uint64_t> k2(rk, rk2);
+            rocprim::double_buffer<uint32_t> v2(rv, rv2);
+            HIP_TRY(rocprim::radix_sort_pairs(nullptr, b2, k2, v2, (size_t)cnt, 0, 33, st));
+            TRY(tmp.alloc(b2, "round sort temp"));
+            HIP_TRY(rocprim::radix_sort_pairs(tmp.p, b2, k2, v2, (size_t)cnt, 0, 33, st));
+            hipLaunchKernelGGL(k_round_group, dim3(grid_for(cnt)), dim3(256), 0, st, v2.current(), cnt,
+                               rank.as<uint32_t>(), k2.current());
+            size_t b3 = 0;
+            HIP_TRY(rocprim::radix_sort_pairs(nullptr, b3, k2, v2, (size_t)cnt, 0, 32, st));
+            TRY(tmp.alloc(b3, "round sort temp 2"));
+            HIP_TRY(rocprim::radix_sort_pairs(tmp.p, b3, k2, v2, (size_t)cnt, 0, 32, st));
+            sv = v2.current();
+        }
         uint32_t* gbuf = (sv == rv) ? rv2 : rv;  // the free value buffer holds group ids
+        hipLaunchKernelGGL(k_round_heads, dim3(grid_for(cnt)), dim3(256), 0, st, sv, cnt, rank.as<uint32_t>(), n, h,
+                           list, gbuf, heads.as<uint8_t>());
         hipLaunchKernelGGL(k_scatter_sa, dim3(grid_for(cnt)), dim3(256), 0, st, list, cnt, sv, sa_out);
-        hipLaunchKernelGGL(k_heads, dim3(grid_for(cnt)), dim3(256), 0, st, sk, cnt, list, gbuf);
-        size_t b3 = 0;
-        HIP_TRY(rocprim::inclusive_scan(nullptr, b3, gbuf, gbuf, (size_t)cnt, MaxOp(), st));
-        TRY(tmp.alloc(b3, "round scan temp"));
-        HIP_TRY(rocprim::inclusive_scan(tmp.p, b3, gbuf, gbuf, (size_t)cnt, MaxOp(), st));
-        hipLaunchKernelGGL(k_assign, dim3(grid_for(cnt)), dim3(256), 0, st, sk, cnt, list, sa_out, gbuf,
-                           rank.as<uint32_t>(), flags.as<uint8_t>());
-        HIP_TRY(hipGetLastError());
         size_t b4 = 0;
-        HIP_TRY(rocprim::select(nullptr, b4, list, flags.as<uint8_t>(), list_next, counter.as<uint64_t>(),
+        HIP_TRY(rocprim::inclusive_scan(nullptr, b4, gbuf, gbuf, (size_t)cnt, MaxOp(), st));
+        TRY(tmp.alloc(b4, "round scan temp"));
+        HIP_TRY(rocprim::inclusive_scan(tmp.p, b4, gbuf, gbuf, (size_t)cnt, MaxOp(), st));
+        hipLaunchKernelGGL(k_round_assign, dim3(grid_for(cnt)), dim3(256), 0, st, cnt, list, sa_out, gbuf,
+                           heads.as<uint8_t>(), rank.as<uint32_t>(), flags.as<uint8_t>());
+        HIP_TRY(hipGetLastError());
+        size_t b5 = 0;
+        HIP_TRY(rocprim::select(nullptr, b5, list, flags.as<uint8_t>(), list_next, counter.as<uint64_t>(),
                                 (size_t)cnt, st));
-        TRY(tmp.alloc(b4, "round select temp"));
-        HIP_TRY(rocprim::select(tmp.p, b4, list, flags.as<uint8_t>(), list_next, counter.as<uint64_t>(),
+        TRY(tmp.alloc(b5, "round select temp"));
+        HIP_TRY(rocprim::select(tmp.p, b5, list, flags.as<uint8_t>(), list_next, counter.as<uint64_t>(),
                                 (size_t)cnt, st));
         HIP_TRY(hipMemcpyAsync(&cnt, counter.p, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
@@ -563,7 +631,6 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     if (!text) SAS_FAIL(EINVAL, "sas_build: null text");
     if (n >= (1ull << 32) - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^32 needs a 40/64-bit SA (not built yet)");
     if (sa_or_null && sa_width != 4) SAS_FAIL(EINVAL, "sas_build: only sa_width 4 (u32) is supported");
-    if (!sa_or_null && n >= (1ull << 31)) SAS_FAIL(ENOTSUP, "sas_build: GPU SA construction needs n < 2^31");
     if (rank_lo >= rank_hi || rank_hi > n) SAS_FAIL(EINVAL, "sas_build_shard: empty or out-of-range rank range");
     uint64_t t0 = now_ns();
     sas_index* x = new sas_index();
@@ -605,7 +672,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         HIP_TRY(hipMemcpy(sa.p, sa_or_null, n * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
     } else {
         uint64_t s0 = now_ns();
-        TRY(build_sa_gpu(x->text_w, n, sa.as<uint32_t>(), &x->stats.sa_rounds));
+        TRY(build_sa_gpu(x->text_w, n, sa.as<uint32_t>(), &x->stats.sa_rounds, flags & SAS_BUILD_WIDE));
         HIP_TRY(hipDeviceSynchronize());
         x->stats.build_sa_ns = now_ns() - s0;
     }

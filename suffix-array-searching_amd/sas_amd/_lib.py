@@ -22,6 +22,7 @@ SAS_BUILD_STREE = 1 << 2
 SAS_BUILD_VERIFY = 1 << 3
 SAS_NO_LDS_TOP = 1 << 4
 SAS_VALIDATE = 1 << 5
+SAS_BUILD_WIDE = 1 << 6
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15 = 0, 1, 2, 3

@@ -230,3 +230,40 @@ def test_sharded_indexes_single_gpu(sas, world):
             assert np.array_equal(r, expect[sel]), (world, g, algo)
         got[sel] = r
     assert np.array_equal(got, expect)
+
+
+def test_wide_doubling_rounds(sas, sadef):
+    """The n >= 2^31 builder path (two stable radix passes per doubling round),
+    forced at small n, must give the same SA as the definition oracle."""
+    from sas_amd import _lib
+    for c in sadef["cases"]:
+        t = np.array(c["text"], np.uint8)
+        idx = sas.SaNaive.build(t, verify=True, flags=_lib.SAS_BUILD_WIDE)
+        assert idx.suffix_array().tolist() == c["sa"], c["name"]
+    rng = np.random.default_rng(9)
+    blk = rng.integers(0, 4, 3000, dtype=np.uint8)
+    for t in (np.zeros(70_000, np.uint8), np.concatenate([blk, blk, rng.integers(0, 4, 999, dtype=np.uint8), blk])):
+        idx = sas.SaNaive.build(t, verify=True, flags=_lib.SAS_BUILD_WIDE)
+        assert np.array_equal(idx.suffix_array(), O.build_sa(t))
+        assert idx.stats()["sa_rounds"] > 0
+
+
+def test_large_text_sampled(sas):
+    """n > 2^31 (the wide builder path for real): GPU adjacency + permutation
+    check (sas/sa_search.rs:36-38) and sampled positions vs the oracle."""
+    import torch
+    n = (1 << 31) + 12345
+    t = sas.random_string(n, seed=123, device="cuda")
+    idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True)
+    ht = t.cpu().numpy()
+    del t
+    torch.cuda.empty_cache()
+    sa = idx.suffix_array()
+    nq, m = 4096, 40
+    off, _, _ = sas.random_queries(n, nq, seed=5, len_lo=m, len_hi=m + 1)
+    qb = np.concatenate([ht[o:o + m] for o in off.astype(np.int64)])
+    rng = np.random.default_rng(1)
+    qb[: 512 * m] = rng.integers(0, 4, 512 * m, dtype=np.uint8)
+    expect = oracle_positions(ht, sa, qb, np.arange(nq, dtype=np.uint64) * m, np.full(nq, m, np.uint32))
+    for algo in ALGOS:
+        assert np.array_equal(idx.search_fixed(qb, m, algo=algo), expect), algo
