@@ -120,6 +120,93 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
                       f"{threads} threads, contiguous chunks (sst/bin/bench.rs:558-573)"}
 
 
+def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
+    """configs[3]-shaped run: the largest text this engine indexes with a u32 SA
+    (BASELINE's "64 GiB" needs a 40/64-bit SA: DESIGN.md §8) and 10^8 positive
+    queries of mixed length 8..256 (random_queries with len in [8, 257)), ragged,
+    through sas_search_batch on device buffers."""
+    n = args.n if args.n != 1 << 30 else (1 << 32) - (1 << 20)
+    nq = args.nq if args.nq != 10_000_000 else 100_000_000
+    t0 = time.perf_counter()
+    text = sas_amd.random_string(n, seed=SEED, device=dev)
+    idx = sas_amd.SaNaive.build(text, lcp=False, stree=True)
+    stats = idx.stats()
+    off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
+                                        len_hi=257)
+    lens = torch.from_numpy(ln.astype(np.int64)).to(dev)
+    qoff = torch.zeros(nq, dtype=torch.int64, device=dev)
+    qoff[1:] = torch.cumsum(lens, 0)[:-1]
+    total = int(lens.sum().item())
+    qbytes = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy(off.astype(np.int64)).to(dev)
+    chunk = 1 << 20
+    for s in range(0, nq, chunk):
+        e = min(nq, s + chunk)
+        L = lens[s:e]
+        start = qoff[s:e]
+        rep = torch.repeat_interleave(torch.arange(e - s, device=dev), L)
+        within = torch.arange(rep.numel(), device=dev) - (start - start[0])[rep]
+        qbytes[start[0]:start[0] + rep.numel()] = text[src[s:e][rep] + within]
+    qlen = lens.to(torch.int32)
+    out = torch.empty(nq, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t0
+    results = {}
+    for algo in [a for a in (args.algo, "plain") if a]:
+        if algo in results:
+            continue
+        def step():
+            idx.search_batch(qbytes, qoff, qlen, algo=algo, out=out)
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        ev0.record()
+        tt = time.perf_counter()
+        steps = args.steps if algo == args.algo else max(2, args.steps // 4)
+        for _ in range(steps):
+            step()
+        ev1.record()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - tt
+        kms = ev0.elapsed_time(ev1) / steps
+        # guard: each answer is an occurrence of its query (positive queries)
+        okc = True
+        for s in range(0, nq, chunk):
+            e = min(nq, s + chunk)
+            L = lens[s:e]
+            rep = torch.repeat_interleave(torch.arange(e - s, device=dev), L)
+            within = torch.arange(rep.numel(), device=dev) - (qoff[s:e] - qoff[s])[rep]
+            got = text[(out[s:e][rep] + within).clamp_(max=n - 1)]
+            okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + rep.numel()]))
+        _, pr = idx.search_batch(qbytes, qoff, qlen, algo=algo, probes=True)
+        mp = float(pr.double().mean().item())
+        mean_m = total / nq
+        P = int(np.log2(n)) + 1
+        ab = (stats["stree_layers"] * 64 + max(0.0, mp - stats["stree_layers"]) * (4 + mean_m) + mean_m + 8
+              if algo == "stree" else P * (4 + mean_m) + mean_m + 8)
+        results[algo] = {"lookups_per_s": nq * steps / el, "kernel_ms": kms, "mean_probes": mp,
+                         "algorithmic_bytes_per_lookup": ab, "achieved_GBps": ab * nq / (kms * 1e-3) / 1e9,
+                         "verified": okc}
+    if rank == 0:
+        h = results[args.algo]
+        print(json.dumps({
+            "metric": "pattern lookups/s (configs[3] shape)", "value": h["lookups_per_s"], "unit": "lookups/s",
+            "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": nq / h["lookups_per_s"] * 1e3,
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic: random_string(ChaCha8Rng({SEED})) text, positive queries len in [8,257)",
+            "config": {"workload": f"configs[3]-shaped: n={n} (largest u32-SA text; 64 GiB needs a wider SA), "
+                                   f"{nq} mixed-length 8..256 queries, ragged", "n": n, "queries_per_gpu": nq,
+                       "mean_m": total / nq, "algo": args.algo},
+            "roofline": {"bound": "hbm", "achieved": h["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": None,
+                         "kernel": "k_sa_stree" if args.algo == "stree" else "k_sa_binary",
+                         "kernel_ms": h["kernel_ms"]},
+            "variants": results, "setup_s": setup,
+            "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
+                                            "build_sa_ns", "build_total_ns")}}), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -132,6 +219,9 @@ def main():
     ap.add_argument("--variants", default="plain,lcp", help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--workload", default="c1", choices=["c1", "c3"],
+                    help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric); c3: largest u32-SA text "
+                         "(2^32 - 2^20 chars), 10^8 queries of mixed length 8..256")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
@@ -149,6 +239,8 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if args.workload == "c3":
+        return run_c3(args, torch, sas_amd, dev, ws, rank, dist)
     n, nq, m = args.n, args.nq, args.m
 
     t_build0 = time.perf_counter()

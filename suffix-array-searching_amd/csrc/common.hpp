@@ -110,6 +110,9 @@ __device__ __forceinline__ uint32_t pack4(uint32_t x) {
     return ((x & 3u) << 6) | (((x >> 8) & 3u) << 4) | (((x >> 16) & 3u) << 2) | ((x >> 24) & 3u);
 }
 
+static __device__ __forceinline__ uint64_t pack_query_word_slow(const uint8_t* __restrict__ q, uint32_t m,
+                                                                     uint32_t base, uint32_t* bad);
+
 // Word j (chars 32j .. 32j+31, zero padded) of a byte-coded query of length m.
 __device__ __forceinline__ uint64_t pack_query_word(const uint8_t* __restrict__ q, uint32_t m, uint32_t j,
                                                     uint32_t* bad) {
@@ -127,11 +130,41 @@ __device__ __forceinline__ uint64_t pack_query_word(const uint8_t* __restrict__ 
         }
         return w;
     }
+    return pack_query_word_slow(q, m, base, bad);
+}
+
+// Unaligned / partial word.
+static __device__ __forceinline__ uint64_t pack_query_word_slow(const uint8_t* __restrict__ q, uint32_t m,
+                                                                     uint32_t base, uint32_t* bad) {
+    uint64_t w = 0;
+    // Unaligned / partial word: read the 16-B aligned blocks that intersect the
+    // c valid bytes (each block holds at least one valid byte, so it can never
+    // touch a page outside the buffer) and realign with v_alignbyte_b32.
     uint32_t c = m - base < 32 ? m - base : 32;
-    for (uint32_t i = 0; i < c; i++) {
-        uint32_t b = q[base + i];
-        *bad |= b & 0xFCu;
-        w |= (uint64_t)(b & 3u) << (62 - 2 * i);
+    uintptr_t addr = (uintptr_t)(q + base);
+    const uint4* p = reinterpret_cast<const uint4*>(addr & ~(uintptr_t)15);
+    uint32_t s = (uint32_t)(addr & 15);
+    const uint4 z = make_uint4(0, 0, 0, 0);
+    uint4 b0 = p[0];
+    uint4 b1 = (s + c > 16) ? p[1] : z;
+    uint4 b2 = (s + c > 32) ? p[2] : z;
+    uint32_t d[13] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w, 0u};
+    uint32_t qi = s >> 2, sb = s & 3;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        uint32_t lo = d[k], hi = d[k + 1];
+        lo = (qi == 1) ? d[k + 1] : lo;
+        hi = (qi == 1) ? d[k + 2] : hi;
+        lo = (qi == 2) ? d[k + 2] : lo;
+        hi = (qi == 2) ? d[k + 3] : hi;
+        lo = (qi == 3) ? d[k + 3] : lo;
+        hi = (qi == 3) ? d[k + 4] : hi;
+        uint32_t v = __builtin_amdgcn_alignbyte(hi, lo, sb);
+        int valid = (int)c - 4 * k;  // bytes of this dword inside the query
+        uint32_t bm = valid >= 4 ? 0xFFFFFFFFu : (valid <= 0 ? 0u : (0xFFFFFFFFu >> (32 - 8 * valid)));
+        v &= bm;
+        *bad |= v & 0xFCFCFCFCu;
+        w = (w << 8) | pack4(v);
     }
     return w;
 }

@@ -267,3 +267,29 @@ def test_large_text_sampled(sas):
     expect = oracle_positions(ht, sa, qb, np.arange(nq, dtype=np.uint64) * m, np.full(nq, m, np.uint32))
     for algo in ALGOS:
         assert np.array_equal(idx.search_fixed(qb, m, algo=algo), expect), algo
+
+
+def test_ragged_unaligned_device_queries(sas):
+    """Ragged queries at odd byte offsets in an exactly-sized device buffer (no
+    padding after the last query): the aligned-block realignment must read only
+    blocks that hold query bytes, and answers must match the host path."""
+    import torch
+    n = 300_007
+    t = sas.random_string(n, seed=21)
+    idx = sas.SaNaive.build(t)
+    rng = np.random.default_rng(4)
+    lens = rng.integers(0, 300, 5000).astype(np.uint32)
+    starts = rng.integers(0, n - 300, 5000)
+    qs = [t[s:s + l] for s, l in zip(starts, lens)]
+    buf = np.concatenate([np.array([1, 2, 3], np.uint8)] + qs)  # odd base offset
+    off = (np.concatenate([[0], np.cumsum(lens[:-1])]) + 3).astype(np.uint64)
+    expect = idx.search_batch(np.concatenate([buf, np.zeros(64, np.uint8)]), off, lens, algo="plain")
+    dbuf = torch.from_numpy(buf).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.view(np.int32)).cuda()
+    for algo in ALGOS:
+        got = idx.search_batch(dbuf, doff, dlen, algo=algo)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().astype(np.uint64), expect), algo
+    sa = idx.suffix_array()
+    assert np.array_equal(expect, oracle_positions(t, sa, buf, off, lens))
