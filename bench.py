@@ -33,12 +33,16 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 SEED = 31415  # sas/main.rs:38
 
 
-def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes: float) -> float:
+def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes: float,
+                      sector_layers: int = 0) -> float:
     """Bytes a lookup must move: 4 B SA word + m text bytes per
     probe, the query, the 8 B position.  PLAIN/LCP: P = ilog2(n)+1 probes.
-    STREE: H 64-B nodes + measured tail probes."""
+    STREE: H 64-B nodes + measured tail probes.  SECTOR: H 32-B nodes (the
+    leaf holds the keys and the SA values) + measured extra leaf probes x 12 B."""
     if algo == "stree":
         return stree_layers * 64 + tail_probes * (4 + m) + m + 8
+    if algo == "sector":
+        return sector_layers * 32 + tail_probes * 12 + m + 8
     P = int(np.log2(n)) + 1
     return P * (4 + m) + m + 8
 
@@ -200,7 +204,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
                        "mean_m": total / nq, "algo": args.algo},
             "roofline": {"bound": "hbm", "achieved": h["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": "k_sa_stree" if args.algo == "stree" else "k_sa_binary",
+                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector"}.get(args.algo, "k_sa_binary"),
                          "kernel_ms": h["kernel_ms"]},
             "variants": results, "setup_s": setup,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
@@ -215,8 +219,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default="stree", choices=["stree", "plain", "lcp"])
-    ap.add_argument("--variants", default="plain,lcp", help="other algos timed beside the headline one")
+    ap.add_argument("--algo", default="sector", choices=["stree", "plain", "lcp", "sector"])
+    ap.add_argument("--variants", default="plain,lcp,stree,sector", help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", default="c1", choices=["c1", "c3"],
@@ -318,15 +322,18 @@ def main():
         mean_probes = float(probes.double().mean().item())
     else:
         mean_probes = float("nan")
-    tail = max(0.0, mean_probes - stats["stree_layers"]) if args.algo == "stree" else mean_probes
-    algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail)
+    layers_of = {"stree": stats["stree_layers"], "sector": stats["sector_layers"]}
+    tail = max(0.0, mean_probes - layers_of[args.algo]) if args.algo in layers_of else mean_probes
+    algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail, stats["sector_layers"])
     achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
 
     variants = {}
     for v in [x for x in args.variants.split(",") if x and x != args.algo and args.mode == "replicated"]:
         vel, vk, vok = run_algo(v, max(3, args.steps // 4), 1)
         _, vp = idx.search_fixed(qbytes, m, algo=v, probes=True)
-        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], float(vp.double().mean().item()))
+        vmean = float(vp.double().mean().item())
+        vtail = max(0.0, vmean - layers_of[v]) if v in layers_of else vmean
+        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], vtail, stats["sector_layers"])
         variants[v] = {"lookups_per_s": ws * nq * max(3, args.steps // 4) / vel, "kernel_ms": vk,
                        "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
                        "mean_probes": float(vp.double().mean().item()), "verified": vok}
@@ -342,7 +349,9 @@ def main():
         workload = {"stree": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, LCP-skipping search over an "
                              "S-tree of 16-char SA keys (top layers LDS-staged)",
                     "plain": "configs[1]: 2^30 text in HBM, 10^7 len-32 queries, plain binary search over SA",
-                    "lcp": "configs[1] + mlr LCP skipping"}[args.algo]
+                    "lcp": "configs[1] + mlr LCP skipping",
+                    "sector": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, sector S-tree (32-B nodes, "
+                              "fused 32-char key + SA leaves, top layers LDS-staged)"}[args.algo]
         line = {
             "metric": METRIC, "value": value, "unit": "lookups/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -358,13 +367,14 @@ def main():
             "roofline": None if not whole else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "k_sa_stree" if args.algo == "stree" else "k_sa_binary",
+                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector"}.get(args.algo, "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes},
             "cpu_baseline": cpu,
             "variants": variants,
-            "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "top_levels", "iterations",
-                                            "sa_rounds", "build_sa_ns", "build_total_ns")},
+            "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
+                                            "top_levels", "iterations", "sa_rounds", "build_sa_ns",
+                                            "build_total_ns")},
             "setup_s": build_s, "verified": ok,
         }
         print(json.dumps(line), flush=True)

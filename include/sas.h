@@ -49,12 +49,15 @@ typedef struct sas_index sas_index;
 #define SAS_VALIDATE      (1u << 5)  /* search: reject query bytes > 3 (synchronises)    */
 #define SAS_BUILD_WIDE    (1u << 6)  /* build: use the n >= 2^31 two-pass doubling rounds
                                         at any n (test hook for that path)               */
+#define SAS_BUILD_SECTOR  (1u << 7)  /* also build the sector tree (SAS_ALGO_SECTOR)     */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {
     SAS_ALGO_PLAIN = 0, /* lockstep lower-bound binary search over SA (A6/A9)              */
     SAS_ALGO_LCP   = 1, /* same probes, Manber-Myers mlr LCP skipping of known chars (A21) */
-    SAS_ALGO_STREE = 2  /* S-tree over 16-char SA keys + exact tail search (K2+K3)         */
+    SAS_ALGO_STREE = 2, /* S-tree over 16-char SA keys + exact tail search (K2+K3)         */
+    SAS_ALGO_SECTOR = 3 /* sector tree: 32-B nodes (one HBM sector), 9-ary on 16-char keys,
+                           leaves fuse (32-char key, SA value) pairs: no text/SA reads for m<=32 */
 };
 
 typedef struct sas_stats {
@@ -74,6 +77,9 @@ typedef struct sas_stats {
     uint64_t rank_lo;        /* global SA rank of this index's first entry         */
     uint64_t sa_entries;     /* SA entries held (n, or a shard's rank range)       */
     uint64_t next_pos;       /* SA[rank_lo + sa_entries] (n if none)               */
+    uint64_t sector_bytes;   /* sector tree (inner nodes + fused leaves), 0 if not built */
+    uint32_t sector_layers;  /* sector tree height incl. the leaf layer           */
+    uint32_t sector_lds_layers; /* its layers served from LDS                     */
 } sas_stats;
 
 const char* sas_last_error(void);

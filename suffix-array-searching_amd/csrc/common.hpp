@@ -28,6 +28,9 @@
 #define SAS_STREE_MAX_LAYERS 16
 #define SAS_STREE_LDS_NODES 1024      // <= 64 KiB of top S-tree layers in LDS
 #define SAS_KEY_MAX 0xFFFFFFFFu       // padding key of the SA S-tree (unsigned)
+#define SAS_SECTOR_FAN 9              // sector tree: 8 separators, 9 children per 32-B node
+#define SAS_SECTOR_MAX_LAYERS 24
+#define SAS_SECTOR_LDS_NODES 2048     // <= 64 KiB of top sector-tree layers in LDS
 
 // ---------------------------------------------------------------- errors
 void sas_set_error(int code, const std::string& msg);
@@ -72,6 +75,15 @@ struct sas_index {
     uint32_t top_levels = 0;
     uint32_t iters = 0;           // ilog2(n) + 1
     uint32_t* scratch = nullptr;  // device flag word(s) for kernels (invalid query codes)
+    // sector tree (SAS_ALGO_SECTOR): 32-B nodes
+    uint32_t* sec_inner = nullptr;   // internal nodes, 8 u32 16-char separators each, root first
+    uint4* sec_leaves = nullptr;     // leaf i = 2 x uint4: {key(2i) lo,hi, key(2i+1) lo,hi}, {sa(2i), sa(2i+1), 0, 0}
+    uint64_t sec_leaf_count = 0;
+    uint64_t sec_off[SAS_SECTOR_MAX_LAYERS] = {};  // node offsets of the internal layers
+    uint32_t sec_inner_layers = 0;   // internal layers (the leaf layer not counted)
+    uint32_t sec_lds_layers = 0;
+    uint32_t sec_lds_nodes = 0;
+    uint64_t sec_inner_nodes = 0;
     sas_stats stats = {};
 };
 

@@ -510,6 +510,95 @@ static uint64_t tb_layer(uint64_t n, uint32_t h, uint32_t height) {
     return n;
 }
 
+// ------------------------------------------------------------------ sector tree
+// Leaves: leaf i = 32 B = one HBM sector = entries 2i, 2i+1 as {key lo, key hi} x2
+// then {sa, sa, 0, 0}; key = 32-char packed prefix of the suffix (zero padded),
+// padding entries key = ~0, sa = ~0.
+__global__ void k_sector_leaves(const uint64_t* __restrict__ tw, const uint32_t* __restrict__ sa, uint64_t sa_n,
+                                uint4* __restrict__ leaves, uint64_t nleaves) {
+    GRID_STRIDE(i, nleaves) {
+        uint64_t r0 = 2 * i, r1 = 2 * i + 1;
+        uint64_t k0 = ~0ull, k1 = ~0ull;
+        uint32_t s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu;
+        if (r0 < sa_n) { s0 = sa[r0]; k0 = text_chars32(tw, s0); }
+        if (r1 < sa_n) { s1 = sa[r1]; k1 = text_chars32(tw, s1); }
+        leaves[2 * i] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+        leaves[2 * i + 1] = make_uint4(s0, s1, 0u, 0u);
+    }
+}
+
+// Internal layer, left_max style (sst/s_tree.rs:163-171 with left_max = true):
+// separator j of node i = 16-char key (high word) of the LAST entry of child
+// 9i+j's subtree, so count(sep < K16) lands exactly on the child holding the
+// first entry with key16 >= K16.  child_span = leaves per child subtree.  The
+// globally last child and nonexistent children get 0xFFFFFFFF, which no query
+// key exceeds, so routing never leaves the tree.
+__global__ void k_sector_layer(uint32_t* __restrict__ inner, uint64_t oh, uint64_t layer_nodes,
+                               uint64_t child_span, uint64_t child_layer_nodes, const uint4* __restrict__ leaves,
+                               uint64_t sa_n) {
+    GRID_STRIDE(i, 8 * layer_nodes) {
+        uint64_t node = i / 8, j = i % 8;
+        uint64_t child = node * SAS_SECTOR_FAN + j;
+        uint32_t sep = 0xFFFFFFFFu;
+        if (child + 1 < child_layer_nodes) {
+            uint64_t last = 2 * (child + 1) * child_span - 1;  // last entry rank of the subtree
+            if (last >= sa_n) last = sa_n - 1;
+            uint4 v = leaves[2 * (last >> 1)];
+            sep = (last & 1) ? v.w : v.y;
+        }
+        inner[(oh + node) * 8 + j] = sep;
+    }
+}
+
+static int build_sector(sas_index* x) {
+    uint64_t sa_n = x->sa_n;
+    uint64_t nl = (sa_n + 1) / 2;
+    uint64_t sizes[SAS_SECTOR_MAX_LAYERS];
+    uint32_t H = 0;
+    uint64_t c = nl;
+    do {
+        c = (c + SAS_SECTOR_FAN - 1) / SAS_SECTOR_FAN;
+        if (H >= SAS_SECTOR_MAX_LAYERS) SAS_FAIL(ENOTSUP, "sector tree too high");
+        sizes[H++] = c;
+    } while (c > 1);
+    // sizes[] is bottom-up; store top-down
+    uint64_t tot = 0;
+    for (uint32_t h = 0; h < H; h++) {
+        x->sec_off[h] = tot;
+        tot += sizes[H - 1 - h];
+    }
+    DevBuf leaves, inner;
+    TRY(leaves.alloc(nl * 32, "sector leaves"));
+    TRY(inner.alloc(tot * 32, "sector inner nodes"));
+    hipLaunchKernelGGL(k_sector_leaves, dim3(grid_for(nl)), dim3(256), 0, 0, x->text_w, x->sa, sa_n,
+                       leaves.as<uint4>(), nl);
+    uint64_t span = 1, child_nodes = nl;
+    for (int h = (int)H - 1; h >= 0; h--) {
+        uint64_t ln = sizes[H - 1 - h];
+        hipLaunchKernelGGL(k_sector_layer, dim3(grid_for(8 * ln)), dim3(256), 0, 0, inner.as<uint32_t>(),
+                           x->sec_off[h], ln, span, child_nodes, leaves.as<uint4>(), sa_n);
+        span *= SAS_SECTOR_FAN;
+        child_nodes = ln;
+    }
+    HIP_TRY(hipGetLastError());
+    x->sec_leaves = static_cast<uint4*>(leaves.release());
+    x->sec_inner = static_cast<uint32_t*>(inner.release());
+    x->sec_leaf_count = nl;
+    x->sec_inner_layers = H;
+    x->sec_inner_nodes = tot;
+    uint32_t L = 0;
+    uint64_t ln = 0;
+    for (uint32_t h = 0; h < H; h++) {
+        uint64_t sz = sizes[H - 1 - h];
+        if (ln + sz > SAS_SECTOR_LDS_NODES) break;
+        ln += sz;
+        L++;
+    }
+    x->sec_lds_layers = L;
+    x->sec_lds_nodes = (uint32_t)ln;
+    return 0;
+}
+
 // ------------------------------------------------------------------ LDS top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
 // the leading one (0 = went left: r = mid, 1 = right: l = mid + 1).
@@ -538,7 +627,8 @@ __global__ void k_top(const uint64_t* __restrict__ tw, const uint32_t* __restric
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
-    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa, x->scratch};
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa, x->scratch, x->sec_inner,
+                     x->sec_leaves};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete x;
 }
@@ -703,6 +793,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         x->lcp = static_cast<uint32_t*>(l.release());
     }
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
+    if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
 
     // binary-search top in LDS
     {
@@ -735,6 +826,9 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.rank_lo = rank_lo;
     st.sa_entries = sa_n;
     st.next_pos = x->next_pos;
+    st.sector_bytes = (x->sec_inner_nodes + x->sec_leaf_count) * 32;
+    st.sector_layers = x->sec_leaves ? x->sec_inner_layers + 1 : 0;
+    st.sector_lds_layers = x->sec_lds_layers;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

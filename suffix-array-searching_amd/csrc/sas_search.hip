@@ -41,6 +41,12 @@ struct SearchArgs {
     uint32_t stree_height;
     uint32_t stree_lds_layers;
     uint32_t stree_lds_nodes;
+    const uint32_t* sec_inner;
+    const uint4* sec_leaves;
+    uint64_t sec_off[SAS_SECTOR_MAX_LAYERS];
+    uint32_t sec_inner_layers;
+    uint32_t sec_lds_layers;
+    uint32_t sec_lds_nodes;
     const uint8_t* qbytes;
     const uint64_t* qoff;
     const uint32_t* qlen;
@@ -242,6 +248,103 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// ------------------------------------------------------------------ SECTOR
+// Lower bound = first rank x with suffix(x) >= q.  In the sector tree that
+// predicate is read off the fused leaf entry (key = first 32 chars, sa):
+//   key != K64(q)          ->  key > K64
+//   key == K64, m <= 32    ->  n - sa >= m   (equal padded prefixes: the shorter
+//                                             suffix is a proper prefix of q)
+//   key == K64, m > 32     ->  exact compare from char 32 (text read)
+template <int QW>
+__device__ __forceinline__ bool sector_ge(uint64_t key, uint32_t p, uint64_t K64, const SearchArgs& a,
+                                          const QueryRegs<QW>& q) {
+    if (key != K64) return key > K64;
+    if (q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
+    uint32_t lcp;
+    return !suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
+}
+
+__device__ __forceinline__ void sector_entry(const uint4* __restrict__ leaves, uint64_t x, uint64_t* key, uint32_t* p) {
+    const uint64_t* kk = reinterpret_cast<const uint64_t*>(leaves + 2 * (x >> 1));
+    const uint32_t* ss = reinterpret_cast<const uint32_t*>(leaves + 2 * (x >> 1) + 1);
+    *key = kk[x & 1];
+    *p = ss[x & 1];
+}
+
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector(SearchArgs a) {
+    __shared__ uint4 s_nodes[SAS_SECTOR_LDS_NODES * 2];
+    const uint4* g = reinterpret_cast<const uint4*>(a.sec_inner);
+    for (uint32_t w = threadIdx.x; w < a.sec_lds_nodes * 2; w += blockDim.x) s_nodes[w] = g[w];
+    __syncthreads();
+    uint32_t bad = 0;
+    const uint64_t sa_n = a.sa_n;
+    const uint4* leaves = a.sec_leaves;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint32_t K16 = (uint32_t)(K64 >> 32);
+        uint32_t probes = 0;
+        uint64_t k = 0;
+        for (uint32_t h = 0; h < a.sec_inner_layers; h++) {
+            const uint4* node = (h < a.sec_lds_layers) ? s_nodes + (a.sec_off[h] + k) * 2 : g + (a.sec_off[h] + k) * 2;
+            uint4 v0 = node[0], v1 = node[1];
+            uint32_t c = (v0.x < K16) + (v0.y < K16) + (v0.z < K16) + (v0.w < K16) + (v1.x < K16) + (v1.y < K16) +
+                         (v1.z < K16) + (v1.w < K16);
+            k = k * SAS_SECTOR_FAN + c;
+            probes++;
+        }
+        // leaf k: entries 2k, 2k+1 (everything before 2k is < q)
+        uint4 kv = leaves[2 * k], sv = leaves[2 * k + 1];
+        probes++;
+        uint64_t key0 = (uint64_t)kv.x | ((uint64_t)kv.y << 32), key1 = (uint64_t)kv.z | ((uint64_t)kv.w << 32);
+        uint64_t x;
+        uint32_t px = 0;
+        if (2 * k < sa_n && sector_ge<QW>(key0, sv.x, K64, a, q)) {
+            x = 2 * k;
+            px = sv.x;
+        } else if (2 * k + 1 < sa_n && sector_ge<QW>(key1, sv.y, K64, a, q)) {
+            x = 2 * k + 1;
+            px = sv.y;
+        } else {
+            // rare: a run of entries sharing the query's 16-char key continues to the
+            // right -- exponential search, then binary search, on the leaf array
+            uint64_t lo = 2 * k + 2, step = 1, hi;
+            for (;;) {
+                hi = lo + step - 1;
+                if (hi >= sa_n) { hi = sa_n; break; }
+                uint64_t kk; uint32_t pp;
+                sector_entry(leaves, hi, &kk, &pp);
+                probes++;
+                if (sector_ge<QW>(kk, pp, K64, a, q)) break;
+                lo = hi + 1;
+                step *= 2;
+            }
+            while (lo < hi) {
+                uint64_t mid = (lo + hi) >> 1;
+                uint64_t kk; uint32_t pp;
+                sector_entry(leaves, mid, &kk, &pp);
+                probes++;
+                if (sector_ge<QW>(kk, pp, K64, a, q)) hi = mid;
+                else lo = mid + 1;
+            }
+            x = lo;
+            if (x < sa_n) {
+                uint64_t kk;
+                sector_entry(leaves, x, &kk, &px);
+            }
+        }
+        a.out_pos[i] = (x >= sa_n) ? a.next_pos : (uint64_t)px;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // ------------------------------------------------------------------ host dispatch
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     uint64_t blocks = (a.nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
@@ -262,12 +365,15 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
 #define K_LCP_TOP(Q) (k_sa_binary<Q, true, true>)
 #define K_LCP(Q) (k_sa_binary<Q, true, false>)
 #define K_STREE(Q) (k_sa_stree<Q>)
+#define K_SECTOR(Q) (k_sa_sector<Q>)
     if (algo == SAS_ALGO_PLAIN) {
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
-    } else {
+    } else if (algo == SAS_ALGO_STREE) {
         QW_CASE(K_STREE)
+    } else {
+        QW_CASE(K_SECTOR)
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -295,6 +401,12 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.stree_height = x->stree_height;
     a.stree_lds_layers = x->stree_lds_layers;
     a.stree_lds_nodes = x->stree_lds_nodes;
+    a.sec_inner = x->sec_inner;
+    a.sec_leaves = x->sec_leaves;
+    for (int h = 0; h < SAS_SECTOR_MAX_LAYERS; h++) a.sec_off[h] = x->sec_off[h];
+    a.sec_inner_layers = x->sec_inner_layers;
+    a.sec_lds_layers = x->sec_lds_layers;
+    a.sec_lds_nodes = x->sec_lds_nodes;
 }
 
 struct DeviceBuf {
@@ -308,8 +420,9 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_STREE) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_SECTOR) SAS_FAIL(EINVAL, "search: unknown algo");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "search: SAS_ALGO_STREE needs SAS_BUILD_STREE");
+    if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "search: SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
     if (nq == 0) return 0;
     if (!out_pos) SAS_FAIL(EINVAL, "search: null out_pos");
     if (!qbytes) SAS_FAIL(EINVAL, "search: null qbytes");
@@ -402,6 +515,8 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
                               double* call_ns) {
     if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
+    if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_SECTOR) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     SearchArgs a{};

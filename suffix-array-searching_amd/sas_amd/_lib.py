@@ -23,7 +23,8 @@ SAS_BUILD_VERIFY = 1 << 3
 SAS_NO_LDS_TOP = 1 << 4
 SAS_VALIDATE = 1 << 5
 SAS_BUILD_WIDE = 1 << 6
-ALGOS = {"plain": 0, "lcp": 1, "stree": 2}
+SAS_BUILD_SECTOR = 1 << 7
+ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15 = 0, 1, 2, 3
 SST_LEFT_MAX = 1 << 0
@@ -40,6 +41,7 @@ class SasStats(C.Structure):
         ("top_levels", C.c_uint32), ("iterations", C.c_uint32), ("build_sa_ns", C.c_uint64),
         ("build_total_ns", C.c_uint64), ("sa_rounds", C.c_uint32), ("reserved", C.c_uint32),
         ("rank_lo", C.c_uint64), ("sa_entries", C.c_uint64), ("next_pos", C.c_uint64),
+        ("sector_bytes", C.c_uint64), ("sector_layers", C.c_uint32), ("sector_lds_layers", C.c_uint32),
     ]
 
     def as_dict(self):

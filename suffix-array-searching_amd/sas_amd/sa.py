@@ -57,13 +57,13 @@ class SaNaive:
 
     @classmethod
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
-              rank_range: tuple[int, int] | None = None, flags: int = 0) -> "SaNaive":
+              rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
-        flags |= (_lib.SAS_BUILD_VERIFY if verify else 0)
+        flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         sa_ptr = None
         if sa is not None:
             if _is_cuda(t) != _is_cuda(sa):
