@@ -133,6 +133,19 @@ int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, 
                      int algo, uint64_t* out_pos, uint32_t* out_probes, void* stream,
                      uint32_t flags);
 
+/* Occurrence ranges (Search::search_prefix / search_range, sas/util.rs:36-46,
+ * declared but unimplemented!() in the reference): global SA ranks
+ * [out_lo[k], out_hi[k]) of the suffixes that start with query k; the count
+ * is out_hi - out_lo and the positions are SA[out_lo .. out_hi)
+ * (sas_copy_sa_range).  Needs SAS_BUILD_SECTOR.  Ragged queries as in
+ * sas_search_batch. */
+int sas_search_range(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,
+                     const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi,
+                     void* stream, uint32_t flags);
+/* Copy SA[start .. start+count) (global ranks) out: the text positions of a range. */
+int sas_copy_sa_range(const sas_index* index, uint64_t start, uint64_t count, uint32_t* dst,
+                      uint32_t flags);
+
 /* Timing helper for benches: run `reps` back-to-back fixed-length searches on
  * device buffers and report the average duration of the search kernel itself
  * (HIP events on `stream`) in *kernel_ns and of the whole call in *call_ns. */

@@ -48,6 +48,8 @@ def lib():
             getattr(L, f).restype = C.c_uint64
         L.orc_lower_bound_rank.argtypes = [C.c_void_p, C.c_uint64, u32p, C.c_void_p, C.c_uint64]
         L.orc_lower_bound_rank.restype = C.c_uint64
+        L.orc_prefix_range.argtypes = [C.c_void_p, C.c_uint64, u32p, C.c_void_p, C.c_uint64,
+                                       C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
         L.orc_search_many.argtypes = [u8p, C.c_uint64, u32p, u8p, u64p, u32p, C.c_uint64, C.c_int, u64p, C.c_int]
         L.orc_search_many.restype = C.c_uint64
         L.orc_node_find.argtypes = [u32p, C.c_uint32, C.c_uint32]
@@ -135,6 +137,17 @@ def lower_bound_rank(tpad, n, sa, q) -> int:
     qb = np.zeros(len(q) + 32, np.uint8)
     qb[: len(q)] = q
     return int(lib().orc_lower_bound_rank(tpad.ctypes.data, n, sa, qb.ctypes.data, len(q)))
+
+
+def prefix_range(tpad, n, sa, q):
+    """Ranks [lo, hi) of the suffixes starting with q (Search::search_prefix,
+    sas/util.rs:36-40)."""
+    qb = np.zeros(len(q) + 32, np.uint8)
+    qb[: len(q)] = q
+    lo, hi = C.c_uint64(0), C.c_uint64(0)
+    lib().orc_prefix_range(tpad.ctypes.data, n, np.ascontiguousarray(sa, np.uint32), qb.ctypes.data, len(q),
+                           C.byref(lo), C.byref(hi))
+    return lo.value, hi.value
 
 
 SEARCH_ALGOS = {"binary_search": 0, "binary_search_cmp": 1, "batch_c16": 2, "batch16": 3}

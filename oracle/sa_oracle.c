@@ -574,3 +574,30 @@ EXPORT void orc_sorted_query(const uint32_t* vals, uint64_t n, const uint32_t* q
                              uint32_t* out, uint64_t* rank) {
     for (uint64_t i = 0; i < nq; i++) out[i] = orc_sorted_search(vals, n, qs[i], rank ? rank + i : 0);
 }
+
+/* ------------------------------------------------------------------------ */
+/* Occurrence range (sas/util.rs:36-46 Search::search_prefix, declared but   */
+/* unimplemented!() in the reference): ranks [lo, hi) of the suffixes that   */
+/* start with q.  lo = lower bound (A6); hi = first rank whose first         */
+/* min(m, len) chars compare > q.                                            */
+/* ------------------------------------------------------------------------ */
+EXPORT void orc_prefix_range(const uint8_t* t, uint64_t n, const uint32_t* sa, const uint8_t* q, uint64_t m,
+                             uint64_t* lo_out, uint64_t* hi_out) {
+    uint64_t l = 0, r = n;
+    while (l < r) {
+        uint64_t mid = (l + r) / 2;
+        if (suffix_lt(t, n, sa[mid], q, m)) l = mid + 1;
+        else r = mid;
+    }
+    *lo_out = l;
+    r = n;
+    while (l < r) {
+        uint64_t mid = (l + r) / 2;
+        uint64_t p = sa[mid], len = n - p, k = len < m ? len : m;
+        int c = memcmp(t + p, q, k);
+        int gt = c > 0;  /* equal on k chars: starts with q (k == m) or is shorter (< q) */
+        if (!gt) l = mid + 1;
+        else r = mid;
+    }
+    *hi_out = l;
+}

@@ -862,6 +862,15 @@ extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count
     return copy_out(index->sa, dst, count * 4, flags);
 }
 
+extern "C" int sas_copy_sa_range(const sas_index* index, uint64_t start, uint64_t count, uint32_t* dst,
+                                 uint32_t flags) {
+    if (!index || (count && !dst)) SAS_FAIL(EINVAL, "sas_copy_sa_range: null argument");
+    if (start < index->rank_lo || start - index->rank_lo + count > index->sa_n)
+        SAS_FAIL(EINVAL, "sas_copy_sa_range: ranks outside this index");
+    if (count == 0) return 0;
+    return copy_out(index->sa + (start - index->rank_lo), dst, count * 4, flags);
+}
+
 extern "C" int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
     if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_lcp: null argument");
     if (!index->lcp) SAS_FAIL(EINVAL, "sas_copy_lcp: index built without SAS_BUILD_LCP");

@@ -31,6 +31,7 @@ struct SearchArgs {
     uint64_t n;          // text length
     uint64_t sa_n;       // SA entries held by this index
     uint64_t next_pos;   // answer when the lower bound is sa_n (n for a whole index)
+    uint64_t rank_lo;    // global rank of sa[0]
     const uint32_t* sa;
     const uint64_t* top_key;
     const uint32_t* top_sa;
@@ -271,15 +272,116 @@ __device__ __forceinline__ void sector_entry(const uint4* __restrict__ leaves, u
     *p = ss[x & 1];
 }
 
+// UPPER predicate for occurrence ranges: the first min(m, len) chars of
+// suffix(x) compare > q (x is past every suffix that starts with q).
+//   m <= 32: key > Q3, Q3 = q's 32-char key padded with 3s instead of 0s
+//   m >  32: key != K64 -> key > K64; else exact compare from char 32
 template <int QW>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector(SearchArgs a) {
-    __shared__ uint4 s_nodes[SAS_SECTOR_LDS_NODES * 2];
+__device__ __forceinline__ bool sector_gt_prefix(uint64_t key, uint32_t p, uint64_t K64, uint64_t Q3,
+                                                 const SearchArgs& a, const QueryRegs<QW>& q) {
+    if (q.m <= 32) return key > Q3;
+    if (key != K64) return key > K64;
+    uint32_t lcp;
+    bool lt = suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
+    return !lt && lcp < q.m;
+}
+
+// First local rank x with pred(x) (pred monotone over ranks, false before the
+// routed leaf), by descent on the 16-char key R16, the routed leaf, and an
+// exponential + binary search on the leaf array for runs that cross leaves.
+template <int QW, bool UPPER>
+__device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint4* s_nodes, const QueryRegs<QW>& q,
+                                                 uint64_t K64, uint64_t Q3, uint32_t* probes, uint32_t* px) {
+    const uint64_t sa_n = a.sa_n;
+    const uint4* leaves = a.sec_leaves;
+    const uint4* g = reinterpret_cast<const uint4*>(a.sec_inner);
+    const uint32_t R16 = (uint32_t)(((UPPER && q.m <= 32) ? Q3 : K64) >> 32);
+    auto pred = [&](uint64_t key, uint32_t p) -> bool {
+        return UPPER ? sector_gt_prefix<QW>(key, p, K64, Q3, a, q) : sector_ge<QW>(key, p, K64, a, q);
+    };
+    uint64_t k = 0;
+    for (uint32_t h = 0; h < a.sec_inner_layers; h++) {
+        const uint4* node = (h < a.sec_lds_layers) ? s_nodes + (a.sec_off[h] + k) * 2 : g + (a.sec_off[h] + k) * 2;
+        uint4 v0 = node[0], v1 = node[1];
+        uint32_t c = (v0.x < R16) + (v0.y < R16) + (v0.z < R16) + (v0.w < R16) + (v1.x < R16) + (v1.y < R16) +
+                     (v1.z < R16) + (v1.w < R16);
+        k = k * SAS_SECTOR_FAN + c;
+        (*probes)++;
+    }
+    // leaf k: entries 2k, 2k+1 (everything before 2k fails pred)
+    uint4 kv = leaves[2 * k], sv = leaves[2 * k + 1];
+    (*probes)++;
+    uint64_t key0 = (uint64_t)kv.x | ((uint64_t)kv.y << 32), key1 = (uint64_t)kv.z | ((uint64_t)kv.w << 32);
+    if (2 * k < sa_n && pred(key0, sv.x)) {
+        *px = sv.x;
+        return 2 * k;
+    }
+    if (2 * k + 1 < sa_n && pred(key1, sv.y)) {
+        *px = sv.y;
+        return 2 * k + 1;
+    }
+    // rare: a run of entries sharing the routing key continues to the right --
+    // exponential search, then binary search, on the leaf array
+    uint64_t lo = 2 * k + 2, step = 1, hi;
+    if (lo >= sa_n) return sa_n;
+    for (;;) {
+        hi = lo + step - 1;
+        if (hi >= sa_n) { hi = sa_n; break; }
+        uint64_t kk; uint32_t pp;
+        sector_entry(leaves, hi, &kk, &pp);
+        (*probes)++;
+        if (pred(kk, pp)) break;
+        lo = hi + 1;
+        step *= 2;
+    }
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        uint64_t kk; uint32_t pp;
+        sector_entry(leaves, mid, &kk, &pp);
+        (*probes)++;
+        if (pred(kk, pp)) hi = mid;
+        else lo = mid + 1;
+    }
+    if (lo < sa_n) {
+        uint64_t kk;
+        sector_entry(leaves, lo, &kk, px);
+    }
+    return lo;
+}
+
+__device__ __forceinline__ void stage_sector_top(const SearchArgs& a, uint4* s_nodes) {
     const uint4* g = reinterpret_cast<const uint4*>(a.sec_inner);
     for (uint32_t w = threadIdx.x; w < a.sec_lds_nodes * 2; w += blockDim.x) s_nodes[w] = g[w];
     __syncthreads();
+}
+
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector(SearchArgs a) {
+    __shared__ uint4 s_nodes[SAS_SECTOR_LDS_NODES * 2];
+    stage_sector_top(a, s_nodes);
     uint32_t bad = 0;
-    const uint64_t sa_n = a.sa_n;
-    const uint4* leaves = a.sec_leaves;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        uint32_t probes = 0, px = 0;
+        uint64_t x = sector_bound<QW, false>(a, s_nodes, q, q.w[0], 0, &probes, &px);
+        a.out_pos[i] = (x >= a.sa_n) ? a.next_pos : (uint64_t)px;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// Occurrence ranges: global ranks [lo, hi) of the suffixes that start with q.
+// out_pos = lo, out_hi = hi (both rank_lo-based).
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs a, uint64_t* out_hi) {
+    __shared__ uint4 s_nodes[SAS_SECTOR_LDS_NODES * 2];
+    stage_sector_top(a, s_nodes);
+    uint32_t bad = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t* qb;
@@ -288,58 +390,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector(SearchArgs a) {
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
-        const uint32_t K16 = (uint32_t)(K64 >> 32);
-        uint32_t probes = 0;
-        uint64_t k = 0;
-        for (uint32_t h = 0; h < a.sec_inner_layers; h++) {
-            const uint4* node = (h < a.sec_lds_layers) ? s_nodes + (a.sec_off[h] + k) * 2 : g + (a.sec_off[h] + k) * 2;
-            uint4 v0 = node[0], v1 = node[1];
-            uint32_t c = (v0.x < K16) + (v0.y < K16) + (v0.z < K16) + (v0.w < K16) + (v1.x < K16) + (v1.y < K16) +
-                         (v1.z < K16) + (v1.w < K16);
-            k = k * SAS_SECTOR_FAN + c;
-            probes++;
-        }
-        // leaf k: entries 2k, 2k+1 (everything before 2k is < q)
-        uint4 kv = leaves[2 * k], sv = leaves[2 * k + 1];
-        probes++;
-        uint64_t key0 = (uint64_t)kv.x | ((uint64_t)kv.y << 32), key1 = (uint64_t)kv.z | ((uint64_t)kv.w << 32);
-        uint64_t x;
-        uint32_t px = 0;
-        if (2 * k < sa_n && sector_ge<QW>(key0, sv.x, K64, a, q)) {
-            x = 2 * k;
-            px = sv.x;
-        } else if (2 * k + 1 < sa_n && sector_ge<QW>(key1, sv.y, K64, a, q)) {
-            x = 2 * k + 1;
-            px = sv.y;
-        } else {
-            // rare: a run of entries sharing the query's 16-char key continues to the
-            // right -- exponential search, then binary search, on the leaf array
-            uint64_t lo = 2 * k + 2, step = 1, hi;
-            for (;;) {
-                hi = lo + step - 1;
-                if (hi >= sa_n) { hi = sa_n; break; }
-                uint64_t kk; uint32_t pp;
-                sector_entry(leaves, hi, &kk, &pp);
-                probes++;
-                if (sector_ge<QW>(kk, pp, K64, a, q)) break;
-                lo = hi + 1;
-                step *= 2;
-            }
-            while (lo < hi) {
-                uint64_t mid = (lo + hi) >> 1;
-                uint64_t kk; uint32_t pp;
-                sector_entry(leaves, mid, &kk, &pp);
-                probes++;
-                if (sector_ge<QW>(kk, pp, K64, a, q)) hi = mid;
-                else lo = mid + 1;
-            }
-            x = lo;
-            if (x < sa_n) {
-                uint64_t kk;
-                sector_entry(leaves, x, &kk, &px);
-            }
-        }
-        a.out_pos[i] = (x >= sa_n) ? a.next_pos : (uint64_t)px;
+        const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
+        uint32_t probes = 0, px = 0;
+        uint64_t lo = sector_bound<QW, false>(a, s_nodes, q, K64, Q3, &probes, &px);
+        uint64_t hi = sector_bound<QW, true>(a, s_nodes, q, K64, Q3, &probes, &px);
+        if (hi < lo) hi = lo;
+        a.out_pos[i] = a.rank_lo + lo;
+        out_hi[i] = a.rank_lo + hi;
         if (a.out_probes) a.out_probes[i] = probes;
     }
     if (bad) atomicOr(a.bad, 1u);
@@ -391,6 +448,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.n = x->n;
     a.sa_n = x->sa_n;
     a.next_pos = x->next_pos;
+    a.rank_lo = x->rank_lo;
     a.sa = x->sa;
     a.top_key = x->top_key;
     a.top_sa = x->top_sa;
@@ -600,6 +658,77 @@ extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint3
     if (!dev) {
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMemcpy(out_shard, dout, nq * 4, hipMemcpyDeviceToHost));
+    }
+    return 0;
+}
+
+// ------------------------------------------------------------------ occurrence ranges
+extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
+                                uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
+    if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
+    if (!x->sec_leaves) SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_SECTOR");
+    if (nq == 0) return 0;
+    if (!qbytes || !qoff || !qlen || !out_lo || !out_hi) SAS_FAIL(EINVAL, "sas_search_range: null argument");
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    bool dev = flags & SAS_DEVICE_PTRS;
+    SearchArgs a{};
+    fill_args(x, a);
+    a.nq = nq;
+    a.bad = x->scratch;
+    bool check_bad = !dev || (flags & SAS_VALIDATE);
+    if (check_bad) HIP_TRY(hipMemsetAsync(x->scratch, 0, 4, st));
+    DeviceBuf bqb, bqoff, bqlen, blo, bhi;
+    uint64_t* dhi = out_hi;
+    int qw = 4;
+    if (dev) {
+        a.qbytes = qbytes;
+        a.qoff = qoff;
+        a.qlen = qlen;
+        a.out_pos = out_lo;
+    } else {
+        uint64_t span = 0, maxlen = 0;
+        for (uint64_t k = 0; k < nq; k++) {
+            uint64_t e = qoff[k] + qlen[k];
+            if (e > span) span = e;
+            if (qlen[k] > maxlen) maxlen = qlen[k];
+        }
+        qw = qw_for(maxlen);
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMalloc(&bqb.p, span + 64));
+        if (span) HIP_TRY(hipMemcpy(bqb.p, qbytes, span, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&bqoff.p, nq * 8));
+        HIP_TRY(hipMalloc(&bqlen.p, nq * 4));
+        HIP_TRY(hipMalloc(&blo.p, nq * 8));
+        HIP_TRY(hipMalloc(&bhi.p, nq * 8));
+        HIP_TRY(hipMemcpy(bqoff.p, qoff, nq * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemcpy(bqlen.p, qlen, nq * 4, hipMemcpyHostToDevice));
+        a.qbytes = static_cast<const uint8_t*>(bqb.p);
+        a.qoff = static_cast<const uint64_t*>(bqoff.p);
+        a.qlen = static_cast<const uint32_t*>(bqlen.p);
+        a.out_pos = static_cast<uint64_t*>(blo.p);
+        dhi = static_cast<uint64_t*>(bhi.p);
+    }
+    uint64_t blocks = (nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
+    if (blocks > cap) blocks = cap;
+    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
+    switch (qw) {
+        case 1: hipLaunchKernelGGL(k_sa_sector_range<1>, grid, block, 0, st, a, dhi); break;
+        case 2: hipLaunchKernelGGL(k_sa_sector_range<2>, grid, block, 0, st, a, dhi); break;
+        case 4: hipLaunchKernelGGL(k_sa_sector_range<4>, grid, block, 0, st, a, dhi); break;
+        default: hipLaunchKernelGGL(k_sa_sector_range<8>, grid, block, 0, st, a, dhi); break;
+    }
+    HIP_TRY(hipGetLastError());
+    if (check_bad || !dev) {
+        HIP_TRY(hipStreamSynchronize(st));
+        uint32_t hbad = 0;
+        HIP_TRY(hipMemcpy(&hbad, x->scratch, 4, hipMemcpyDeviceToHost));
+        if (!dev) {
+            HIP_TRY(hipMemcpy(out_lo, a.out_pos, nq * 8, hipMemcpyDeviceToHost));
+            HIP_TRY(hipMemcpy(out_hi, dhi, nq * 8, hipMemcpyDeviceToHost));
+        }
+        if (hbad) SAS_FAIL(EINVAL, "sas_search_range: query bytes must be DNA codes 0..3");
     }
     return 0;
 }

@@ -98,6 +98,8 @@ def lib():
     L.sas_get_stats.argtypes = [vp, C.POINTER(SasStats)]
     L.sas_copy_sa.argtypes = [vp, vp, u64, u32]
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]
+    L.sas_search_range.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp, u32]
+    L.sas_copy_sa_range.argtypes = [vp, u64, u64, vp, u32]
     L.sas_verify.argtypes = [vp]
     L.sas_search_batch.argtypes = [vp, vp, vp, vp, u64, i32, vp, vp, vp, u32]
     L.sas_search_fixed.argtypes = [vp, vp, u32, u64, i32, vp, vp, vp, u32]

@@ -187,6 +187,39 @@ class SaNaive:
         buf = np.concatenate(qs + [np.zeros(64, np.uint8)]) if qs else np.zeros(64, np.uint8)
         return self.search_batch(buf, off, lens, algo=algo, probes=probes)
 
+    def search_range(self, qbytes, qoff, qlen, stream=None, flags: int = 0):
+        """Occurrence ranges (Search::search_prefix, sas/util.rs:36-40): global SA
+        ranks (lo, hi) of the suffixes starting with each query; count = hi - lo."""
+        dev = _is_cuda(qbytes)
+        if dev:
+            import torch
+            nq = qoff.numel()
+            lo = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+            hi = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+            st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
+            flags |= _lib.SAS_DEVICE_PTRS
+        else:
+            qbytes = _as_u8(qbytes)
+            qoff = np.ascontiguousarray(qoff, np.uint64)
+            qlen = np.ascontiguousarray(qlen, np.uint32)
+            nq = len(qoff)
+            lo = np.zeros(max(nq, 1), np.uint64)
+            hi = np.zeros(max(nq, 1), np.uint64)
+            st = stream
+        check(lib().sas_search_range(self._h, _ptr(qbytes), _ptr(qoff), _ptr(qlen), nq, _ptr(lo), _ptr(hi), st,
+                                     flags))
+        return (lo, hi) if dev else (lo[:nq], hi[:nq])
+
+    def search_prefix(self, q) -> np.ndarray:
+        """All text positions where q occurs (Search::search_prefix, sas/util.rs:36-40)."""
+        q = _as_u8(q)
+        buf = np.concatenate([q, np.zeros(64, np.uint8)])
+        lo, hi = self.search_range(buf, np.zeros(1, np.uint64), np.array([len(q)], np.uint32))
+        cnt = int(hi[0] - lo[0])
+        out = np.zeros(max(cnt, 1), np.uint32)
+        check(lib().sas_copy_sa_range(self._h, int(lo[0]), cnt, out.ctypes.data, 0))
+        return out[:cnt]
+
     def time_fixed(self, d_qbytes, m: int, nq: int, d_out, algo="plain", reps=1, stream=None, flags=0):
         """Average (kernel_ns, call_ns) of `reps` back-to-back searches on device buffers."""
         kn, cn = C.c_double(0), C.c_double(0)

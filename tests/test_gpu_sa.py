@@ -293,3 +293,37 @@ def test_ragged_unaligned_device_queries(sas):
         assert np.array_equal(got.cpu().numpy().astype(np.uint64), expect), algo
     sa = idx.suffix_array()
     assert np.array_equal(expect, oracle_positions(t, sa, buf, off, lens))
+
+
+def test_occurrence_ranges(sas, sadef):
+    """sas_search_range (Search::search_prefix, sas/util.rs:36-40): SA[lo:hi] is
+    exactly the set of occurrences, on the definition fixtures, random texts with
+    mixed queries (vs the oracle) and long runs."""
+    for c in sadef["cases"]:
+        t = np.array(c["text"], np.uint8)
+        idx = sas.SaNaive.build(t)
+        buf, off, lens = pack([q["q"] for q in c["queries"]])
+        lo, hi = idx.search_range(buf, off, lens)
+        sa = np.array(c["sa"], np.uint32)
+        tl = c["text"]
+        for k, qd in enumerate(c["queries"]):
+            q = qd["q"]
+            assert lo[k] == qd["rank"], (c["name"], q)
+            occ = sorted(i for i in range(len(tl)) if tl[i:i + len(q)] == q) if len(q) <= len(tl) else []
+            assert sorted(sa[lo[k]:hi[k]].tolist()) == occ, (c["name"], q)
+    rng = np.random.default_rng(8)
+    for t in (sas.random_string(1 << 20, seed=77), np.zeros(50_000, np.uint8),
+              np.tile(rng.integers(0, 4, 13, dtype=np.uint8), 9000)):
+        n = len(t)
+        idx = sas.SaNaive.build(t)
+        sa = idx.suffix_array()
+        tp = O.padded(t)
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 300, 3000), rng.integers(0, 300, 3000))]
+        qs += [rng.integers(0, 4, rng.integers(1, 12), dtype=np.uint8) for _ in range(1000)]
+        buf, off, lens = pack(qs)
+        lo, hi = idx.search_range(buf, off, lens)
+        for k, q in enumerate(qs):
+            assert (lo[k], hi[k]) == O.prefix_range(tp, n, sa, q), (n, k, len(q))
+    t = np.zeros(1000, np.uint8)
+    idx = sas.SaNaive.build(t)
+    assert sorted(idx.search_prefix(np.zeros(10, np.uint8)).tolist()) == list(range(991))

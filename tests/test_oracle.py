@@ -195,3 +195,18 @@ def test_sst_differential(p):
                 assert np.array_equal(vals[np.minimum(rank, len(vals) - 1)], ref)
             t = O.STree(vals, B=B, reverse=True)
             assert np.array_equal(t.query(qs), ref)
+
+
+def test_prefix_range_matches_occurrences(sadef):
+    """orc_prefix_range: SA[lo:hi] is exactly the set of occurrence positions."""
+    for c in sadef["cases"]:
+        t = c["text"]
+        n = len(t)
+        sa = np.array(c["sa"], np.uint32)
+        tp = O.padded(np.array(t, np.uint8))
+        for qd in c["queries"]:
+            q = qd["q"]
+            lo, hi = O.prefix_range(tp, n, sa, np.array(q, np.uint8))
+            assert lo == qd["rank"]
+            occ = sorted(i for i in range(n) if t[i:i + len(q)] == q) if len(q) <= n else []
+            assert sorted(sa[lo:hi].tolist()) == occ, (c["name"], q)
