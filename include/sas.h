@@ -163,6 +163,17 @@ int sas_gen_queries(uint64_t seed, uint64_t word_pos, uint64_t n, uint64_t nq, u
                     uint32_t len_lo, uint32_t len_hi, uint64_t* off, uint32_t* len,
                     uint64_t* next_word);
 
+/* Real-data inputs.
+ * sas_read_fasta: read_fasta_file (sas/util.rs:144-169) -- records concatenated,
+ * A/C/G/T/a/c/g/t -> 0..3, every other byte -> 0; FASTA and FASTQ, no gzip.
+ * out == NULL -> only *len is computed (size the buffer, then call again). */
+int sas_read_fasta(const char* path, uint8_t* out, uint64_t cap, uint64_t* len);
+/* sas_kmer_keys: the --human u32 keys of sst/bin/bench.rs:58-76 for the S-tree:
+ * out[j] = packed chars [j, j+k) & i32::MAX, j < min(n, limit+k-1) - (k-1),
+ * out[0] = i32::MAX.  out == NULL -> only *count.  k in 1..16. */
+int sas_kmer_keys(const uint8_t* text, uint64_t n, uint32_t k, uint64_t limit, uint32_t* out,
+                  uint64_t* count, uint32_t flags);
+
 #ifdef __cplusplus
 }
 #endif

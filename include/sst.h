@@ -41,7 +41,10 @@ enum sst_layout {
     SST_SORTED    = 0, /* SortedVec: plain sorted array, binary search              */
     SST_EYTZINGER = 1, /* Eytzinger BFS layout, vals[0] = u32::MAX                  */
     SST_STREE16   = 2, /* STree<16,16>: B+ tree, 64-B nodes                          */
-    SST_STREE15   = 3  /* STree<15,16>: 15 keys + copy of the next node's first key */
+    SST_STREE15   = 3, /* STree<15,16>: 15 keys + copy of the next node's first key */
+    SST_PARTITIONED_MAP = 4 /* PartitionedSTree16M: prefix map on the top b key bits
+                               + S-tree (sst/partitioned_s_tree.rs:111-190,364-648);
+                               b = SST_PART_BITS(b) in flags                         */
 };
 
 /* layout flags (STree::new_params arguments) */
@@ -50,6 +53,8 @@ enum sst_layout {
 #define SST_FULL       (1u << 2)  /* (B+1)^h-sized layers                            */
 #define SST_DEVICE_PTRS (1u << 8) /* sst_query: qs/out_val/out_rank are device ptrs  */
 #define SST_NO_LDS_TOP (1u << 9)  /* sst_query: do not stage top layers in LDS       */
+#define SST_PART_BITS(b) (((uint32_t)(b) & 0xFFu) << 16) /* PartitionedSTree16M::new(vals, b) */
+#define SST_PART_BITS_OF(flags) (((flags) >> 16) & 0xFFu)
 
 int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, uint32_t flags, sst_index** out);
 int sst_free(sst_index* index);

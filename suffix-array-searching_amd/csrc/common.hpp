@@ -100,6 +100,10 @@ struct sst_index {
     uint32_t lds_layers = 0;
     uint32_t lds_nodes = 0;
     int num_cus = 256;
+    uint32_t* prefix_map = nullptr;  // PartitionedSTree16M
+    uint64_t pmap_words = 0;
+    uint32_t shift = 0;
+    uint32_t parts = 0;
 };
 
 // ---------------------------------------------------------------- device helpers

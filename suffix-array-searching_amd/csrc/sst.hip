@@ -31,6 +31,9 @@ struct SstArgs {
     uint64_t nq;
     uint32_t* out;
     uint64_t* rank;
+    const uint32_t* prefix_map;  // PartitionedSTree16M
+    uint32_t shift;
+    uint32_t parts;
 };
 
 // count of keys < q under SIGNED compare (find_popcnt, sst/node.rs:93-109)
@@ -69,6 +72,41 @@ __global__ __launch_bounds__(SST_BLOCK) void k_sst_stree(SstArgs a) {
         uint32_t idx = popcnt_find(g + (o + k) * 4, (int32_t)q);
         a.out[i] = a.nodes[(o + k + idx / 16) * 16 + idx % 16];
         if (a.rank) a.rank[i] = k * B + idx;
+    }
+}
+
+// PartitionedSTree16M::search (sst/partitioned_s_tree.rs:833-877): layer 0 is a
+// flat separator array entered through prefix_map[q >> shift] (a 16-key window
+// read at key granularity); below it the usual 17-ary left-max descent.
+__global__ __launch_bounds__(SST_BLOCK) void k_sst_pmap(SstArgs a) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t q = a.qs[i];
+        uint32_t p = q >> a.shift;
+        if (p >= a.parts) p = a.parts - 1;  // q above every key's prefix (UB in the reference)
+        uint64_t key = a.prefix_map[p];      // key index in layer 0
+        if (a.height >= 2) {
+            const uint32_t* l0 = a.nodes + a.off[0] * 16 + key;
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) c += (int32_t)q > (int32_t)l0[j];
+            uint64_t k = key + c;  // node index in layer 1
+            for (uint32_t h = 1; h + 1 < a.height; h++) {
+                const uint4* node = reinterpret_cast<const uint4*>(a.nodes) + (a.off[h] + k) * 4;
+                k = k * 17 + popcnt_find(node, (int32_t)q);
+            }
+            const uint4* leaf = reinterpret_cast<const uint4*>(a.nodes) + (a.off[a.height - 1] + k) * 4;
+            uint32_t idx = popcnt_find(leaf, (int32_t)q);
+            a.out[i] = a.nodes[(a.off[a.height - 1] + k) * 16 + idx];
+            if (a.rank) a.rank[i] = k * 16 + idx;
+        } else {
+            const uint32_t* l0 = a.nodes + a.off[0] * 16 + key;
+            uint32_t c = 0;
+#pragma unroll
+            for (int j = 0; j < 16; j++) c += (int32_t)q > (int32_t)l0[j];
+            a.out[i] = l0[c];
+            if (a.rank) a.rank[i] = key + c;
+        }
     }
 }
 
@@ -181,6 +219,101 @@ static int build_stree_host(const uint32_t* vals, uint64_t n, uint32_t B, bool l
     return 0;
 }
 
+// PartitionedSTree<16,16,Map>::get_part_size + try_new
+// (sst/partitioned_s_tree.rs:111-190, 364-648 with Tp = Map: not compact, L1,
+// overlap Some(0), prefix map).
+static int build_pmap_host(const uint32_t* vals, uint64_t n, uint32_t b, std::vector<uint32_t>& tree,
+                           std::vector<uint32_t>& pmap, sst_index* x) {
+    const uint64_t B = 16;
+    if (vals[n - 1] > SST_MAX) SAS_FAIL(EINVAL, "sst_build: keys must be <= i32::MAX (sst/node.rs:5)");
+    // get_part_size (:111-190)
+    uint32_t bits = 1 + (31 - __builtin_clz(vals[n - 1] ? vals[n - 1] : 1));
+    if (vals[n - 1] == 0) bits = 1;  // ilog2(0) panics in the reference; treat as 1 bit
+    auto part_sizes = [&](uint32_t shift, uint64_t parts, uint64_t* maxb) {
+        std::vector<uint64_t> bs(parts, 0);
+        for (uint64_t i = 0; i < n; i++) bs[vals[i] >> shift]++;
+        uint64_t m = 0;
+        for (uint64_t v : bs) m = v > m ? v : m;
+        *maxb = m;
+    };
+    auto get_height = [&](uint64_t xx) { return height_of((xx * 17 + 15) / 16, B); };  // MAP: x*17/16
+    uint32_t shift = bits > b ? bits - b : 0;
+    uint64_t parts = 1ull << (bits - shift);
+    uint64_t max_bucket;
+    part_sizes(shift, parts, &max_bucket);
+    uint32_t height = get_height(max_bucket);
+    uint32_t b2 = b;
+    for (;;) {
+        if (b2 == 0) break;
+        b2 -= 1;
+        if (b2 > bits) break;
+        uint32_t shift2 = bits > b2 ? bits - b2 : 0;
+        uint64_t parts2 = 1ull << (bits - shift2);
+        uint64_t mb2;
+        part_sizes(shift2, parts2, &mb2);
+        uint32_t h2 = get_height(mb2);
+        if (h2 > height) break;
+        shift = shift2;
+        parts = parts2;
+        max_bucket = mb2;
+        height = h2;
+    }
+    // try_new (:364-648), Map
+    uint64_t ls[SAS_STREE_MAX_LAYERS];
+    if (height > SAS_STREE_MAX_LAYERS) SAS_FAIL(ENOTSUP, "sst_build: tree too high");
+    for (uint32_t h = 0; h < height; h++) ls[h] = (layer_size(n, h, height, B) + B - 1) / B;
+    if (height > 1) ls[0] = ((layer_size(n, 1, height, B) + B - 1) / B + B - 1) / B;
+    uint64_t nb = 0;
+    for (uint32_t h = 0; h < height; h++) {
+        x->off[h] = nb;
+        x->layer_nodes[h] = ls[h];
+        nb += ls[h];
+    }
+    if (nb * 64 > (32ull << 30)) SAS_FAIL(ENOMEM, "sst_build: PartitionedSTree16M overhead too large (try_new -> None)");
+    tree.assign(nb * 16, SST_MAX);
+    uint64_t ol = x->off[height - 1];
+    for (uint64_t i = 0; i < n; i++) tree[(ol + i / B) * 16 + i % B] = vals[i];
+    uint64_t subtree = height == 1 ? 1 : B;
+    for (uint32_t k = 0; k + 2 < height; k++) subtree *= (B + 1);
+    for (int h = (int)height - 2; h >= 0; h--) {
+        uint64_t oh = x->off[h];
+        if (h == 0) {  // overlap Some(0): layer 0 holds the max of every layer-1 subtree
+            for (uint64_t i = 0; i + 1 < ls[1]; i++) {
+                uint64_t j = (i + 1) * subtree - 1;
+                tree[(oh + i / B) * 16 + i % B] = tree[(ol + j / B) * 16 + j % B];
+            }
+            break;
+        }
+        for (uint64_t i = 0; i < B * ls[h]; i++) {
+            uint64_t k = i / B, j = i % B;
+            k = k * (B + 1) + j + 1;
+            for (uint32_t l = (uint32_t)h; l + 2 < height; l++) k *= (B + 1);
+            tree[(oh + i / B) * 16 + i % B] = k * B < n ? tree[(ol + k - 1) * 16 + B - 1] : SST_MAX;
+        }
+    }
+    // prefix map (:605-627)
+    pmap.assign(parts, 0);
+    uint64_t max_idx = ls[0] * B - B;
+    uint64_t p = 0;
+    for (uint64_t i = 0; i < ls[0] * B; i++) {
+        uint64_t pi = tree[x->off[0] * 16 + i] >> shift;
+        while (p < pi && p + 1 < parts) {
+            p++;
+            pmap[p] = (uint32_t)(i < max_idx ? i : max_idx);
+        }
+    }
+    while (p + 1 < parts) {
+        p++;
+        pmap[p] = (uint32_t)max_idx;
+    }
+    x->height = height;
+    x->B = 16;
+    x->N = 16;
+    x->shift = shift;
+    x->parts = (uint32_t)parts;
+    return 0;
+}
+
 // Eytzinger::new (sst/eytzinger.rs:37-63), iterative in-order fill.
 static void build_eytzinger_host(const uint32_t* vals, uint64_t n, std::vector<uint32_t>& e) {
     e.assign(n + 1, 0);
@@ -214,7 +347,7 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
         x->num_cus = 256;
         if (hipGetDeviceProperties(&prop, dev) == hipSuccess) x->num_cus = prop.multiProcessorCount;
     }
-    std::vector<uint32_t> host;
+    std::vector<uint32_t> host, pmap;
     int rc = 0;
     switch (layout) {
         case SST_SORTED:
@@ -232,6 +365,9 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
             rc = build_stree_host(sorted_vals, n, layout == SST_STREE16 ? 16 : 15, flags & SST_LEFT_MAX,
                                   flags & SST_REVERSE, flags & SST_FULL, host, x);
             break;
+        case SST_PARTITIONED_MAP:
+            rc = build_pmap_host(sorted_vals, n, SST_PART_BITS_OF(flags), host, pmap, x);
+            break;
         default:
             rc = EINVAL;
             sas_set_error(EINVAL, "sst_build: unknown layout");
@@ -245,6 +381,12 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
     if (e != hipSuccess) { delete x; SAS_FAIL(ENOMEM, "sst_build: hipMalloc failed"); }
     e = hipMemcpy(x->nodes, host.data(), host.size() * 4, hipMemcpyHostToDevice);
     if (e != hipSuccess) { (void)hipFree(x->nodes); delete x; SAS_FAIL(EIO, "sst_build: upload failed"); }
+    if (!pmap.empty()) {
+        x->pmap_words = pmap.size();
+        e = hipMalloc(&x->prefix_map, pmap.size() * 4);
+        if (e == hipSuccess) e = hipMemcpy(x->prefix_map, pmap.data(), pmap.size() * 4, hipMemcpyHostToDevice);
+        if (e != hipSuccess) { (void)hipFree(x->nodes); delete x; SAS_FAIL(ENOMEM, "sst_build: prefix map upload failed"); }
+    }
     *out = x;
     return 0;
 }
@@ -252,14 +394,16 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
 extern "C" int sst_free(sst_index* x) {
     if (x) {
         if (x->nodes) (void)hipFree(x->nodes);
+        if (x->prefix_map) (void)hipFree(x->prefix_map);
         delete x;
     }
     return 0;
 }
 
 extern "C" uint64_t sst_size(const sst_index* x) {
-    // SearchIndex::size(): bytes of the node / value array (sst/lib.rs:35-36)
-    return x ? x->words * 4 : 0;
+    // SearchIndex::size(): bytes of the node / value array (sst/lib.rs:35-36), plus
+    // the prefix map for PartitionedSTree16M (sst/partitioned_s_tree.rs:100-102)
+    return x ? (x->words + x->pmap_words) * 4 : 0;
 }
 
 extern "C" uint64_t sst_layers(const sst_index* x) {
@@ -267,6 +411,7 @@ extern "C" uint64_t sst_layers(const sst_index* x) {
     switch (x->layout) {
         case SST_SORTED: return 64 - __builtin_clzll(x->n);              // ilog2(len)+1 (binary_search.rs:29-31)
         case SST_EYTZINGER: return 64 - __builtin_clzll(x->n + 1);       // ilog2(len)+1 (eytzinger.rs:72-74)
+        case SST_PARTITIONED_MAP: return x->height + 1;                  // offsets.len() + MAP (partitioned_s_tree.rs:104-106)
         default: return x->height;                                       // offsets.len() (s_tree.rs:52-54)
     }
 }
@@ -287,6 +432,8 @@ static int sst_launch(const sst_index* x, SstArgs& a, uint32_t flags, hipStream_
         hipLaunchKernelGGL(k_sst_sorted, grid, block, 0, st, a);
     } else if (x->layout == SST_EYTZINGER) {
         hipLaunchKernelGGL(k_sst_eytzinger, grid, block, 0, st, a);
+    } else if (x->layout == SST_PARTITIONED_MAP) {
+        hipLaunchKernelGGL(k_sst_pmap, grid, block, 0, st, a);
     } else if (flags & SST_NO_LDS_TOP) {
         hipLaunchKernelGGL(k_sst_stree<false>, grid, block, 0, st, a);
     } else {
@@ -310,6 +457,9 @@ static void sst_fill(const sst_index* x, SstArgs& a) {
     a.lds_layers = x->lds_layers;
     a.lds_nodes = x->lds_nodes;
     a.eyt_iters = x->height;
+    a.prefix_map = x->prefix_map;
+    a.shift = x->shift;
+    a.parts = x->parts;
 }
 
 extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, uint32_t* out_val, uint64_t* out_rank,

@@ -26,7 +26,7 @@ SAS_BUILD_WIDE = 1 << 6
 SAS_BUILD_SECTOR = 1 << 7
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3}
 
-SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15 = 0, 1, 2, 3
+SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
 SST_LEFT_MAX = 1 << 0
 SST_REVERSE = 1 << 1
 SST_FULL = 1 << 2
@@ -100,6 +100,8 @@ def lib():
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]
     L.sas_search_range.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp, u32]
     L.sas_copy_sa_range.argtypes = [vp, u64, u64, vp, u32]
+    L.sas_read_fasta.argtypes = [C.c_char_p, vp, u64, C.POINTER(u64)]
+    L.sas_kmer_keys.argtypes = [vp, u64, u32, u64, vp, C.POINTER(u64), u32]
     L.sas_verify.argtypes = [vp]
     L.sas_search_batch.argtypes = [vp, vp, vp, vp, u64, i32, vp, vp, vp, u32]
     L.sas_search_fixed.argtypes = [vp, vp, u32, u64, i32, vp, vp, vp, u32]

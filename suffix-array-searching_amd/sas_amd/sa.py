@@ -267,3 +267,25 @@ def random_queries(n: int, nq: int, seed: int = 31415, word_pos: int | None = No
     check(lib().sas_gen_queries(seed, n if word_pos is None else word_pos, n, nq, margin, len_lo, len_hi,
                                 off.ctypes.data, ln.ctypes.data, C.byref(nxt)))
     return off[:nq], ln[:nq], nxt.value
+
+
+# ---------------------------------------------------------------- real data
+def read_fasta_file(path: str) -> np.ndarray:
+    """sas/util.rs:144-169: concatenated record sequences as codes 0..3 (others -> 0)."""
+    n = C.c_uint64(0)
+    check(lib().sas_read_fasta(path.encode(), None, 0, C.byref(n)))
+    out = np.zeros(max(n.value, 1), np.uint8)
+    check(lib().sas_read_fasta(path.encode(), out.ctypes.data, n.value, C.byref(n)))
+    return out[: n.value]
+
+
+def kmer_keys(t, k: int = 16, limit: int | None = None) -> np.ndarray:
+    """sst/bin/bench.rs:58-76 (--human): u32 k-mer keys & i32::MAX, vals[0] = MAX."""
+    t = _as_u8(t)
+    n = len(t)
+    limit = n if limit is None else limit
+    cnt = C.c_uint64(0)
+    check(lib().sas_kmer_keys(t.ctypes.data, n, k, limit, None, C.byref(cnt), 0))
+    out = np.zeros(max(cnt.value, 1), np.uint32)
+    check(lib().sas_kmer_keys(t.ctypes.data, n, k, limit, out.ctypes.data, C.byref(cnt), 0))
+    return out[: cnt.value]

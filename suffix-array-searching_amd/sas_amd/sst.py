@@ -115,3 +115,14 @@ class STree16(_STree):
 
 class STree15(_STree):
     LAYOUT = _lib.SST_STREE15
+
+
+class PartitionedSTree16M(_Index):
+    """PartitionedSTree<16,16,Map> (sst/partitioned_s_tree.rs): prefix map on the
+    top b key bits + S-tree.  new(vals, b) as in the reference (test.rs uses
+    b in {0, 4, 8, 16, 20})."""
+    LAYOUT = _lib.SST_PARTITIONED_MAP
+
+    @classmethod
+    def new(cls, vals, b: int = 16):
+        return cls._build(vals, cls.LAYOUT, (b & 0xFF) << 16)

@@ -49,3 +49,33 @@ def test_error_paths_set_last_error():
     # null out pointers are rejected before any device call
     assert L.sas_build(None, 10, None, 4, 0, None) == 22
     assert L.sst_build(None, 0, 0, 0, None) == 22
+
+
+def _fasta_restated(text: str) -> list:
+    # sas/util.rs:144-169: map[A,C,G,T,a,c,g,t] = 0..3, every other byte 0; records concatenated
+    m = {c: i for i, c in enumerate("ACGT")}
+    m.update({c: i for i, c in enumerate("acgt")})
+    out = []
+    for line in text.splitlines():
+        if line.startswith(">"):
+            continue
+        out += [m.get(ch, 0) for ch in line.strip("\r")]
+    return out
+
+
+def test_read_fasta(tmp_path):
+    text = ">chr1 test\nACGTNNacgt\nRYKM\n>chr2\n\nTTTTGGGGCCCCAAAA\r\nacg\n"
+    p = tmp_path / "x.fa"
+    p.write_text(text)
+    got = sas_amd.read_fasta_file(str(p))
+    assert got.tolist() == _fasta_restated(text)
+    q = tmp_path / "x.fq"
+    q.write_text("@r1\nACGTN\n+\nIIIII\n@r2\ngggt\n+\n!!!!\n")
+    assert sas_amd.read_fasta_file(str(q)).tolist() == [0, 1, 2, 3, 0, 2, 2, 2, 3]
+    import gzip
+    g = tmp_path / "x.fa.gz"
+    g.write_bytes(gzip.compress(text.encode()))
+    with pytest.raises(sas_amd.SasError):
+        sas_amd.read_fasta_file(str(g))
+    with pytest.raises(sas_amd.SasError):
+        sas_amd.read_fasta_file(str(tmp_path / "missing.fa"))

@@ -327,3 +327,21 @@ def test_occurrence_ranges(sas, sadef):
     t = np.zeros(1000, np.uint8)
     idx = sas.SaNaive.build(t)
     assert sorted(idx.search_prefix(np.zeros(10, np.uint8)).tolist()) == list(range(991))
+
+
+def test_kmer_keys_match_reference_loop(sas):
+    """sst/bin/bench.rs:58-76 (--human keys), restated as the reference's loop."""
+    t = sas.random_string(5000, seed=2)
+    for k, limit in ((16, 5000), (16, 1000), (11, 4990), (16, 10)):
+        key, vals = 0, []
+        for i in range(k - 1):
+            key = key << 2 | int(t[i])
+        for i in range(k - 1, min(len(t), limit + k - 1)):
+            key = (key << 2 | int(t[i])) & ((1 << (2 * k)) - 1)
+            vals.append(key & 0x7FFFFFFF)
+        vals[0] = 0x7FFFFFFF
+        assert sas.kmer_keys(t, k, limit).tolist() == vals, (k, limit)
+    keys = np.sort(sas.kmer_keys(t))
+    idx = sas.STree16.new(keys)  # the S-tree the reference builds over them
+    qs = np.sort(keys)[::7]
+    assert np.array_equal(idx.query(qs), O.SortedVec(keys).query(qs))

@@ -62,6 +62,13 @@ def test_differential(sas, size):
             assert np.array_equal(v, ref), (B, lm, rev, full)
             _, orank = o.query(qs, want_rank=True)
             assert np.array_equal(r, orank)
+    # PartitionedSTree16M::new(vals, b) for the b of sst/test.rs:249-254
+    for b in (0, 4, 8, 16, 20):
+        pm = sas.PartitionedSTree16M.new(vals, b)
+        v, r = pm.query(qs, want_rank=True)
+        assert np.array_equal(v, ref), (size, b)
+        assert np.array_equal(vals[np.minimum(r, len(vals) - 1)], ref)
+        assert pm.layers() >= 1 and pm.size() >= len(vals) * 4
 
 
 def test_no_lds_and_device_path(sas):
