@@ -124,6 +124,71 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
                       f"{threads} threads, contiguous chunks (sst/bin/bench.rs:558-573)"}
 
 
+def run_sst(args, torch, sas_amd, dev, ws, rank):
+    """The u32 path (static-search-tree crate): the reference's bench sweeps sizes up to
+    2^30 bytes (sst/bin/bench.rs:455-472); this runs the largest, 2^28 keys (gen_vals:
+    uniform < i32::MAX, vals[0] = MAX, sorted; sst/util.rs:31-42) and 10^7 uniform
+    queries (gen_queries, :16-21) on every GPU layout, all checked against each other."""
+    from oracle import pyoracle as O
+    nk = args.n if args.n != 1 << 30 else 1 << 28
+    nq = args.nq
+    rng = np.random.default_rng(SEED)
+    vals = rng.integers(0, O.MAX, nk, dtype=np.uint64).astype(np.uint32)
+    vals[0] = O.MAX
+    vals.sort()
+    qs = rng.integers(0, O.MAX, nq, dtype=np.uint64).astype(np.uint32)
+    dq = torch.from_numpy(qs.view(np.int32)).to(dev)
+    dout = torch.empty(nq, dtype=torch.int32, device=dev)
+    layouts = {
+        "SortedVec": lambda: sas_amd.SortedVec.new(vals),
+        "Eytzinger": lambda: sas_amd.Eytzinger.new(vals),
+        "STree16": lambda: sas_amd.STree16.new(vals),
+        "STree16_left_max": lambda: sas_amd.STree16.new_params(vals, True, False, False),
+        "STree15": lambda: sas_amd.STree15.new(vals),
+        "PartitionedSTree16M_b16": lambda: sas_amd.PartitionedSTree16M.new(vals, 16),
+        "PartitionedSTree16M_b20": lambda: sas_amd.PartitionedSTree16M.new(vals, 20),
+    }
+    res, ref = {}, None
+    for name, mk in layouts.items():
+        idx = mk()
+        for _ in range(args.warmup):
+            idx.query(dq)
+        kns = idx.time_query(dq, dout, reps=args.steps, stream=torch.cuda.current_stream(dev).cuda_stream)
+        got = dout.cpu().numpy().view(np.uint32).copy()
+        if ref is None:
+            ref = got
+        res[name] = {"lookups_per_s": nq / (kns * 1e-9), "kernel_ms": kns * 1e-6, "layers": idx.layers(),
+                     "index_bytes": idx.size(), "agrees": bool(np.array_equal(got, ref))}
+        idx.free()
+    # CPU: the oracle's STree16 (left_max) restatement, 16 threads over contiguous chunks
+    import threading
+    tree = O.STree(vals, left_max=True)
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    sample = min(nq, 4_000_000)
+    chunks = np.array_split(qs[:sample], threads)
+    outs = [None] * threads
+
+    def work(i):
+        outs[i] = tree.query(chunks[i])
+    t0 = time.perf_counter()
+    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    [t.start() for t in th]
+    [t.join() for t in th]
+    dt = time.perf_counter() - t0
+    cpu_ok = bool(np.array_equal(np.concatenate(outs), ref[:sample]))
+    best = max(res, key=lambda k: res[k]["lookups_per_s"])
+    print(json.dumps({
+        "metric": "u32 static-search-tree lookups/s (2^28 keys = 1 GiB, 10^7 uniform queries)",
+        "value": res[best]["lookups_per_s"], "unit": "lookups/s", "n_gpus": 1, "steps": args.steps,
+        "warmup": args.warmup, "higher_is_better": True, "dtype": "u32", "vs_baseline": None,
+        "data": "synthetic: gen_vals / gen_queries shapes (sst/util.rs:16-42)",
+        "config": {"workload": "sst u32 path", "keys": nk, "queries": nq, "best": best},
+        "layouts": res,
+        "cpu_baseline": {"value": sample / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
+                         "sample": f"oracle STree16 left_max search (sst/s_tree.rs:196-206) on {sample} queries, "
+                                   f"{threads} threads", "agrees": cpu_ok}}), flush=True)
+
+
 def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     """configs[3]-shaped run: the largest text this engine indexes with a u32 SA
     (BASELINE's "64 GiB" needs a 40/64-bit SA: DESIGN.md §8) and 10^8 positive
@@ -223,7 +288,7 @@ def main():
     ap.add_argument("--variants", default="plain,lcp,stree,sector", help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workload", default="c1", choices=["c1", "c3"],
+    ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric); c3: largest u32-SA text "
                          "(2^32 - 2^20 chars), 10^8 queries of mixed length 8..256")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
@@ -245,6 +310,8 @@ def main():
     dev = torch.device("cuda", torch.cuda.current_device())
     if args.workload == "c3":
         return run_c3(args, torch, sas_amd, dev, ws, rank, dist)
+    if args.workload == "sst":
+        return run_sst(args, torch, sas_amd, dev, ws, rank)
     n, nq, m = args.n, args.nq, args.m
 
     t_build0 = time.perf_counter()
