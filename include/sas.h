@@ -50,6 +50,9 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_WIDE    (1u << 6)  /* build: use the n >= 2^31 two-pass doubling rounds
                                         at any n (test hook for that path)               */
 #define SAS_BUILD_SECTOR  (1u << 7)  /* also build the sector tree (SAS_ALGO_SECTOR)     */
+#define SAS_BUILD_SA40    (1u << 8)  /* store the SA as packed 40-bit entries and use the
+                                        bucketed 64-bit builder at any n (automatic for
+                                        n >= 2^32 - 64; test hook below that)             */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {
@@ -63,7 +66,7 @@ enum sas_algo {
 typedef struct sas_stats {
     uint64_t n;              /* text length (chars)                               */
     uint64_t text_bytes;     /* packed 2-bit text in HBM                          */
-    uint64_t sa_bytes;       /* suffix array (u32)                                */
+    uint64_t sa_bytes;       /* suffix array (sa_width bytes per entry)           */
     uint64_t lcp_bytes;      /* LCP array (u32), 0 if not built                   */
     uint64_t stree_bytes;    /* S-tree incl. 16-char key leaves, 0 if not built   */
     uint32_t stree_layers;   /* S-tree height (layers incl. leaves)               */
@@ -73,7 +76,7 @@ typedef struct sas_stats {
     uint64_t build_sa_ns;    /* wall time of the SA construction (0 if supplied)  */
     uint64_t build_total_ns; /* wall time of sas_build                            */
     uint32_t sa_rounds;      /* prefix-doubling rounds after the 32-char sort     */
-    uint32_t reserved;
+    uint32_t sa_width;       /* bytes per stored SA entry: 4 (u32) or 5 (40-bit)  */
     uint64_t rank_lo;        /* global SA rank of this index's first entry         */
     uint64_t sa_entries;     /* SA entries held (n, or a shard's rank range)       */
     uint64_t next_pos;       /* SA[rank_lo + sa_entries] (n if none)               */
@@ -84,9 +87,13 @@ typedef struct sas_stats {
 
 const char* sas_last_error(void);
 
-/* Build an index over text[0..n).  sa_or_null: caller's suffix array (u32,
- * sa_width must be 4) or NULL to construct it on the GPU (prefix doubling on
- * 32-char packed keys, n < 2^31).  The library copies everything into HBM. */
+/* Build an index over text[0..n).  sa_or_null: caller's suffix array with
+ * sa_width = 4 (u32, n < 2^32), 5 (packed 40-bit little-endian) or 8 (u64),
+ * or NULL to construct it on the GPU (prefix doubling on 32-char packed keys).
+ * n < 2^32 - 64 keeps a u32 SA; larger n (up to 2^40, as HBM allows) or
+ * SAS_BUILD_SA40 store a packed 40-bit SA, built by the bucketed builder
+ * (32-char-key buckets sorted one at a time, then doubling rounds over the
+ * tied suffixes only).  The library copies everything into HBM. */
 int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
               uint32_t flags, sas_index** out);
 int sas_free(sas_index* index);
@@ -109,8 +116,12 @@ int sas_route(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsp
 
 int sas_get_stats(const sas_index* index, sas_stats* out);
 
-/* Copy the suffix array / LCP array out (dst host or device per flags). */
+/* Copy the suffix array / LCP array out (dst host or device per flags).
+ * sas_copy_sa needs a u32 SA (sa_width 4, EINVAL otherwise); sas_copy_sa64
+ * copies global ranks [start, start+count) of either width as u64.  LCP values
+ * are u32 (capped at 2^32-1). */
 int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags);
+int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t count, uint64_t* dst, uint32_t flags);
 int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags);
 
 /* GPU check of the SA: strictly increasing adjacent suffixes (the

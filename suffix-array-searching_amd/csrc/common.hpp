@@ -5,7 +5,9 @@
 //            bits 63-2*(p%32) .. 62-2*(p%32)), followed by SAS_TEXT_PAD_WORDS
 //            zero words.  Unsigned compare of packed words == lexicographic
 //            compare of the chars (codes 0..3, sas/util.rs:9-15).
-//   sa     : u32[n] suffix array.
+//   sa     : suffix array, u32[n] (sa_w = 4) or packed 40-bit little-endian
+//            (sa_w = 5: entry i in bytes 5i..5i+4, 8 pad bytes) for n >= 2^32
+//            or SAS_BUILD_SA40.
 //   lcp    : u32[n], lcp[0] = 0, lcp[r] = lcp(SA[r-1], SA[r]).
 //   stree  : STree<16,16>-shaped B+ tree over key16[r] = first 16 chars of
 //            suffix SA[r] (zero padded), internal layers first, the leaf layer
@@ -62,7 +64,8 @@ struct sas_index {
     int num_cus = 256;
     uint64_t* text_w = nullptr;  // packed text
     uint64_t text_words = 0;
-    uint32_t* sa = nullptr;
+    uint8_t* sa = nullptr;        // sa_w bytes per entry (SaView<4> / SaView<5>)
+    uint32_t sa_w = 4;
     uint32_t* lcp = nullptr;
     uint32_t* stree = nullptr;   // all nodes, 16 u32 each
     uint64_t stree_nodes = 0;
@@ -71,13 +74,14 @@ struct sas_index {
     uint32_t stree_lds_layers = 0;
     uint32_t stree_lds_nodes = 0;
     uint64_t* top_key = nullptr;  // [SAS_TOP_NODES], index 0 unused
-    uint32_t* top_sa = nullptr;   // [SAS_TOP_NODES]
+    uint64_t* top_sa = nullptr;   // [SAS_TOP_NODES]
     uint32_t top_levels = 0;
     uint32_t iters = 0;           // ilog2(n) + 1
     uint32_t* scratch = nullptr;  // device flag word(s) for kernels (invalid query codes)
     // sector tree (SAS_ALGO_SECTOR): 32-B nodes
     uint32_t* sec_inner = nullptr;   // internal nodes, 8 u32 16-char separators each, root first
-    uint4* sec_leaves = nullptr;     // leaf i = 2 x uint4: {key(2i) lo,hi, key(2i+1) lo,hi}, {sa(2i), sa(2i+1), 0, 0}
+    uint4* sec_leaves = nullptr;     // leaf i = 2 x uint4: {key(2i) lo,hi, key(2i+1) lo,hi},
+                                     // {sa(2i) lo32, sa(2i+1) lo32, hi8(2i) | hi8(2i+1) << 8, 0}
     uint64_t sec_leaf_count = 0;
     uint64_t sec_off[SAS_SECTOR_MAX_LAYERS] = {};  // node offsets of the internal layers
     uint32_t sec_inner_layers = 0;   // internal layers (the leaf layer not counted)
@@ -105,6 +109,36 @@ struct sst_index {
     uint32_t shift = 0;
     uint32_t parts = 0;
 };
+
+// ---------------------------------------------------------------- suffix-array element access
+#define SAS_SA40_PAD 8           // bytes after a packed 40-bit SA (aligned 8-B reads)
+#define SAS_SA40_MAX (1ull << 40)
+
+template <int W>
+struct SaView {
+    const uint8_t* p;
+    __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
+        if (W == 4) return reinterpret_cast<const uint32_t*>(p)[i];
+        // 5-byte entry at byte 5i: two aligned u32 loads (same 128-B line except
+        // when straddling one) and a funnel shift
+        uint64_t o = 5 * i;
+        const uint32_t* w = reinterpret_cast<const uint32_t*>(p + (o & ~3ull));
+        uint64_t v = ((uint64_t)w[1] << 32) | w[0];
+        return (v >> (8 * (o & 3))) & (SAS_SA40_MAX - 1);
+    }
+};
+
+// Writes: byte stores, so neighbouring entries written by other lanes never race.
+template <int W>
+__device__ __forceinline__ void sa_put(uint8_t* p, uint64_t i, uint64_t v) {
+    if (W == 4) {
+        reinterpret_cast<uint32_t*>(p)[i] = (uint32_t)v;
+        return;
+    }
+    uint8_t* b = p + 5 * i;
+#pragma unroll
+    for (int k = 0; k < 5; k++) b[k] = (uint8_t)(v >> (8 * k));
+}
 
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ uint64_t chars_mask(uint32_t c) {

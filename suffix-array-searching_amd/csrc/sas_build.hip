@@ -13,6 +13,7 @@
 //      sst/s_tree.rs:72-176, unsigned keys, MAX padding),
 //   5. the LDS "top" of the lockstep binary search (Eytzinger order).
 #include "common.hpp"
+#include "build_util.hpp"
 
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -37,16 +38,6 @@ int sas_errno_of(hipError_t e) {
     return EIO;
 }
 extern "C" const char* sas_last_error(void) { return g_err.c_str(); }
-
-static unsigned grid_for(uint64_t count, unsigned block = 256) {
-    uint64_t g = (count + block - 1) / block;
-    if (g < 1) g = 1;
-    if (g > 262144) g = 262144;  // grid-stride beyond
-    return (unsigned)g;
-}
-
-#define GRID_STRIDE(i, count) \
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < (count); i += (uint64_t)gridDim.x * blockDim.x)
 
 // ------------------------------------------------------------------ text packing
 __global__ void k_pack_text(const uint8_t* __restrict__ text, uint64_t n, uint64_t* __restrict__ tw,
@@ -296,30 +287,6 @@ __global__ void k_scatter_sa(const uint32_t* __restrict__ list, uint64_t cnt, co
     GRID_STRIDE(k, cnt) sa[list[k]] = vals[k];
 }
 
-struct MaxOp {
-    __device__ __host__ uint32_t operator()(uint32_t a, uint32_t b) const { return a > b ? a : b; }
-};
-
-struct DevBuf {
-    void* p = nullptr;
-    ~DevBuf() { if (p) (void)hipFree(p); }
-    template <class T> T* as() { return static_cast<T*>(p); }
-    int alloc(size_t bytes, const char* what) {
-        if (p) { (void)hipFree(p); p = nullptr; }
-        hipError_t e = hipMalloc(&p, bytes ? bytes : 1);
-        if (e != hipSuccess) {
-            p = nullptr;
-            sas_set_error(ENOMEM, std::string("hipMalloc(") + what + ", " + std::to_string(bytes) + " B): " +
-                                      hipGetErrorString(e));
-            return ENOMEM;
-        }
-        return 0;
-    }
-    void* release() { void* q = p; p = nullptr; return q; }
-};
-
-#define TRY(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
-
 // Prefix doubling on the GPU.  sa_out: device u32[n].
 static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32_t* rounds_out, bool force_wide) {
     hipStream_t st = 0;
@@ -438,7 +405,8 @@ static int build_sa_gpu(const uint64_t* tw, uint64_t n, uint32_t* sa_out, uint32
 // ------------------------------------------------------------------ LCP, verify
 // Kernels below take the text length n (suffix lengths) and the number of SA
 // entries sa_n separately: a shard index holds a rank range of the global SA.
-__global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa, uint64_t sa_n,
+template <int W>
+__global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa, uint64_t sa_n,
                       uint32_t* __restrict__ lcp) {
     GRID_STRIDE(r, sa_n) {
         if (r == 0) { lcp[0] = 0; continue; }
@@ -450,11 +418,13 @@ __global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, const uint32_
             if (x) { l += __clzll(x) >> 1; break; }
             l += 32;
         }
-        lcp[r] = (uint32_t)(l < L ? l : L);
+        l = l < L ? l : L;
+        lcp[r] = l > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)l;
     }
 }
 
-__global__ void k_verify_adj(const uint64_t* __restrict__ tw, uint64_t n, const uint32_t* __restrict__ sa,
+template <int W>
+__global__ void k_verify_adj(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa,
                              uint64_t sa_n, uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bad) {
     GRID_STRIDE(r, sa_n) {
         uint64_t b = sa[r];
@@ -484,7 +454,8 @@ __global__ void k_count_bits(const uint32_t* __restrict__ bitmap, uint64_t words
 }
 
 // ------------------------------------------------------------------ S-tree over 16-char keys
-__global__ void k_keys16(const uint64_t* __restrict__ tw, const uint32_t* __restrict__ sa, uint64_t sa_n,
+template <int W>
+__global__ void k_keys16(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n,
                          uint32_t* __restrict__ leaves, uint64_t leaf_words) {
     GRID_STRIDE(r, leaf_words) leaves[r] = r < sa_n ? (uint32_t)(text_chars32(tw, sa[r]) >> 32) : SAS_KEY_MAX;
 }
@@ -514,16 +485,19 @@ static uint64_t tb_layer(uint64_t n, uint32_t h, uint32_t height) {
 // Leaves: leaf i = 32 B = one HBM sector = entries 2i, 2i+1 as {key lo, key hi} x2
 // then {sa, sa, 0, 0}; key = 32-char packed prefix of the suffix (zero padded),
 // padding entries key = ~0, sa = ~0.
-__global__ void k_sector_leaves(const uint64_t* __restrict__ tw, const uint32_t* __restrict__ sa, uint64_t sa_n,
+// The SA values' bits 32..39 (n >= 2^32) ride in the otherwise unused third word.
+template <int W>
+__global__ void k_sector_leaves(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n,
                                 uint4* __restrict__ leaves, uint64_t nleaves) {
     GRID_STRIDE(i, nleaves) {
         uint64_t r0 = 2 * i, r1 = 2 * i + 1;
         uint64_t k0 = ~0ull, k1 = ~0ull;
-        uint32_t s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu;
+        uint64_t s0 = 0xFFFFFFFFu, s1 = 0xFFFFFFFFu;
         if (r0 < sa_n) { s0 = sa[r0]; k0 = text_chars32(tw, s0); }
         if (r1 < sa_n) { s1 = sa[r1]; k1 = text_chars32(tw, s1); }
         leaves[2 * i] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-        leaves[2 * i + 1] = make_uint4(s0, s1, 0u, 0u);
+        uint32_t hi = (uint32_t)((s0 >> 32) & 0xFF) | ((uint32_t)((s1 >> 32) & 0xFF) << 8);
+        leaves[2 * i + 1] = make_uint4((uint32_t)s0, (uint32_t)s1, (r0 < sa_n ? hi : 0u), 0u);
     }
 }
 
@@ -570,8 +544,12 @@ static int build_sector(sas_index* x) {
     DevBuf leaves, inner;
     TRY(leaves.alloc(nl * 32, "sector leaves"));
     TRY(inner.alloc(tot * 32, "sector inner nodes"));
-    hipLaunchKernelGGL(k_sector_leaves, dim3(grid_for(nl)), dim3(256), 0, 0, x->text_w, x->sa, sa_n,
-                       leaves.as<uint4>(), nl);
+    if (x->sa_w == 5)
+        hipLaunchKernelGGL(k_sector_leaves<5>, dim3(grid_for(nl)), dim3(256), 0, 0, x->text_w, SaView<5>{x->sa},
+                           sa_n, leaves.as<uint4>(), nl);
+    else
+        hipLaunchKernelGGL(k_sector_leaves<4>, dim3(grid_for(nl)), dim3(256), 0, 0, x->text_w, SaView<4>{x->sa},
+                           sa_n, leaves.as<uint4>(), nl);
     uint64_t span = 1, child_nodes = nl;
     for (int h = (int)H - 1; h >= 0; h--) {
         uint64_t ln = sizes[H - 1 - h];
@@ -602,8 +580,9 @@ static int build_sector(sas_index* x) {
 // ------------------------------------------------------------------ LDS top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
 // the leading one (0 = went left: r = mid, 1 = right: l = mid + 1).
-__global__ void k_top(const uint64_t* __restrict__ tw, const uint32_t* __restrict__ sa, uint64_t sa_n,
-                      uint64_t* __restrict__ top_key, uint32_t* __restrict__ top_sa, uint32_t nodes) {
+template <int W>
+__global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n,
+                      uint64_t* __restrict__ top_key, uint64_t* __restrict__ top_sa, uint32_t nodes) {
     GRID_STRIDE(k, nodes) {
         if (k == 0) { top_key[0] = 0; top_sa[0] = 0xFFFFFFFFu; continue; }
         uint64_t l = 0, r = sa_n;
@@ -614,7 +593,7 @@ __global__ void k_top(const uint64_t* __restrict__ tw, const uint32_t* __restric
             if ((k >> b) & 1) l = mid + 1; else r = mid;
         }
         if (l < r) {
-            uint32_t p = sa[(l + r) >> 1];
+            uint64_t p = sa[(l + r) >> 1];
             top_sa[k] = p;
             top_key[k] = text_chars32(tw, p);
         } else {
@@ -644,7 +623,7 @@ static uint64_t now_ns() {
 }
 
 // full = the SA must be a permutation of 0..n (false for a shard's rank range)
-static int verify_sa(const uint64_t* tw, uint64_t n, const uint32_t* sa, uint64_t sa_n, bool full) {
+static int verify_sa(const uint64_t* tw, uint64_t n, const uint8_t* sa, uint32_t w, uint64_t sa_n, bool full) {
     DevBuf bitmap, bad;
     uint64_t words = (n + 31) / 32;
     if (full) {
@@ -653,8 +632,12 @@ static int verify_sa(const uint64_t* tw, uint64_t n, const uint32_t* sa, uint64_
     }
     TRY(bad.alloc(16, "verify flags"));
     HIP_TRY(hipMemset(bad.p, 0, 16));
-    hipLaunchKernelGGL(k_verify_adj, dim3(grid_for(sa_n)), dim3(256), 0, 0, tw, n, sa, sa_n,
-                       full ? bitmap.as<uint32_t>() : nullptr, bad.as<uint32_t>());
+    if (w == 5)
+        hipLaunchKernelGGL(k_verify_adj<5>, dim3(grid_for(sa_n)), dim3(256), 0, 0, tw, n, SaView<5>{sa}, sa_n,
+                           full ? bitmap.as<uint32_t>() : nullptr, bad.as<uint32_t>());
+    else
+        hipLaunchKernelGGL(k_verify_adj<4>, dim3(grid_for(sa_n)), dim3(256), 0, 0, tw, n, SaView<4>{sa}, sa_n,
+                           full ? bitmap.as<uint32_t>() : nullptr, bad.as<uint32_t>());
     if (full)
         hipLaunchKernelGGL(k_count_bits, dim3(grid_for(words)), dim3(256), 0, 0, bitmap.as<uint32_t>(), words,
                            reinterpret_cast<unsigned long long*>(bad.as<uint32_t>() + 2));
@@ -671,7 +654,7 @@ static int verify_sa(const uint64_t* tw, uint64_t n, const uint32_t* sa, uint64_
 extern "C" int sas_verify(const sas_index* index) {
     if (!index) SAS_FAIL(EINVAL, "sas_verify: null index");
     HIP_TRY(hipSetDevice(index->device));
-    return verify_sa(index->text_w, index->n, index->sa, index->sa_n, index->sa_n == index->n);
+    return verify_sa(index->text_w, index->n, index->sa, index->sa_w, index->sa_n, index->sa_n == index->n);
 }
 
 static int build_stree(sas_index* x) {
@@ -688,8 +671,12 @@ static int build_stree(sas_index* x) {
     TRY(t.alloc(tot * 64, "S-tree"));
     uint32_t* tree = t.as<uint32_t>();
     uint64_t ol = x->stree_off[height - 1];
-    hipLaunchKernelGGL(k_keys16, dim3(grid_for(ls[height - 1] * 16)), dim3(256), 0, 0, x->text_w, x->sa, nk,
-                       tree + ol * 16, ls[height - 1] * 16);
+    if (x->sa_w == 5)
+        hipLaunchKernelGGL(k_keys16<5>, dim3(grid_for(ls[height - 1] * 16)), dim3(256), 0, 0, x->text_w,
+                           SaView<5>{x->sa}, nk, tree + ol * 16, ls[height - 1] * 16);
+    else
+        hipLaunchKernelGGL(k_keys16<4>, dim3(grid_for(ls[height - 1] * 16)), dim3(256), 0, 0, x->text_w,
+                           SaView<4>{x->sa}, nk, tree + ol * 16, ls[height - 1] * 16);
     for (int h = (int)height - 2; h >= 0; h--) {
         // internal nodes: slots B..N stay MAX (B == N == 16 here, so none)
         hipLaunchKernelGGL(k_stree_layer, dim3(grid_for(16 * ls[h])), dim3(256), 0, 0, tree, x->stree_off[h],
@@ -711,6 +698,39 @@ static int build_stree(sas_index* x) {
     return 0;
 }
 
+static int copy_in_sa(const void* src, uint8_t* dst, uint64_t bytes, bool dev) {
+    HIP_TRY(hipMemcpy(dst, src, bytes, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    return 0;
+}
+
+// Caller's SA (host or device, 4 / 5 / 8 bytes per entry) -> this index's width.
+template <int WI, int WO>
+__global__ void k_convert_sa(const uint8_t* __restrict__ in, uint64_t n, uint8_t* __restrict__ out) {
+    GRID_STRIDE(i, n) {
+        uint64_t v;
+        if (WI == 8) v = reinterpret_cast<const uint64_t*>(in)[i];
+        else v = SaView<WI>{in}[i];
+        sa_put<WO>(out, i, v);
+    }
+}
+
+static int load_sa(const void* src, uint64_t n, int wi, bool dev, uint8_t* dst, uint32_t wo) {
+    const uint64_t bytes = n * (uint64_t)wi;
+    if ((uint32_t)wi == wo)
+        return copy_in_sa(src, dst, bytes, dev);
+    DevBuf staged;
+    TRY(staged.alloc(bytes + 8, "caller SA staging"));
+    TRY(copy_in_sa(src, staged.as<uint8_t>(), bytes, dev));
+    const uint8_t* in = staged.as<uint8_t>();
+    if (wi == 4 && wo == 5) hipLaunchKernelGGL((k_convert_sa<4, 5>), dim3(grid_for(n)), dim3(256), 0, 0, in, n, dst);
+    else if (wi == 5 && wo == 4) hipLaunchKernelGGL((k_convert_sa<5, 4>), dim3(grid_for(n)), dim3(256), 0, 0, in, n, dst);
+    else if (wi == 8 && wo == 4) hipLaunchKernelGGL((k_convert_sa<8, 4>), dim3(grid_for(n)), dim3(256), 0, 0, in, n, dst);
+    else hipLaunchKernelGGL((k_convert_sa<8, 5>), dim3(grid_for(n)), dim3(256), 0, 0, in, n, dst);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    return 0;
+}
+
 // Common builder.  [rank_lo, rank_hi) = the SA ranks this index holds
 // (the whole SA for sas_build, a shard's range for sas_build_shard).
 static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
@@ -719,14 +739,19 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     *out = nullptr;
     if (n == 0) SAS_FAIL(EINVAL, "sas_build: empty text");
     if (!text) SAS_FAIL(EINVAL, "sas_build: null text");
-    if (n >= (1ull << 32) - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^32 needs a 40/64-bit SA (not built yet)");
-    if (sa_or_null && sa_width != 4) SAS_FAIL(EINVAL, "sas_build: only sa_width 4 (u32) is supported");
+    if (n >= SAS_SA40_MAX - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^40 - 64");
+    const bool w5 = (flags & SAS_BUILD_SA40) || n >= (1ull << 32) - 64;
+    const uint32_t W = w5 ? 5 : 4;
+    if (sa_or_null && sa_width != 4 && sa_width != 5 && sa_width != 8)
+        SAS_FAIL(EINVAL, "sas_build: sa_width must be 4 (u32), 5 (packed 40-bit) or 8 (u64)");
+    if (sa_or_null && sa_width == 4 && n > 0xFFFFFFFFull) SAS_FAIL(EINVAL, "sas_build: a u32 SA cannot index n >= 2^32");
     if (rank_lo >= rank_hi || rank_hi > n) SAS_FAIL(EINVAL, "sas_build_shard: empty or out-of-range rank range");
     uint64_t t0 = now_ns();
     sas_index* x = new sas_index();
     x->n = n;
     x->rank_lo = rank_lo;
     x->sa_n = rank_hi - rank_lo;
+    x->sa_w = W;
     HIP_TRY(hipGetDevice(&x->device));
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, x->device) == hipSuccess) x->num_cus = prop.multiProcessorCount;
@@ -757,38 +782,54 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
 
     // global suffix array (caller's or built here), then this index's rank range
     DevBuf sa;
-    TRY(sa.alloc(n * 4, "suffix array"));
+    const uint64_t sa_bytes_full = n * W + (W == 5 ? SAS_SA40_PAD : 0);
+    TRY(sa.alloc(sa_bytes_full, "suffix array"));
     if (sa_or_null) {
-        HIP_TRY(hipMemcpy(sa.p, sa_or_null, n * 4, dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+        TRY(load_sa(sa_or_null, n, sa_width, dev, sa.as<uint8_t>(), W));
     } else {
         uint64_t s0 = now_ns();
-        TRY(build_sa_gpu(x->text_w, n, sa.as<uint32_t>(), &x->stats.sa_rounds, flags & SAS_BUILD_WIDE));
+        if (W == 5) {
+            HIP_TRY(hipMemset(sa.p, 0, sa_bytes_full));
+            uint64_t buckets = 0;
+            TRY(build_sa_gpu40(x->text_w, n, sa.as<uint8_t>(), &x->stats.sa_rounds, &buckets));
+        } else {
+            TRY(build_sa_gpu(x->text_w, n, sa.as<uint32_t>(), &x->stats.sa_rounds, flags & SAS_BUILD_WIDE));
+        }
         HIP_TRY(hipDeviceSynchronize());
         x->stats.build_sa_ns = now_ns() - s0;
     }
-    if (flags & SAS_BUILD_VERIFY) TRY(verify_sa(x->text_w, n, sa.as<uint32_t>(), n, true));
+    if (flags & SAS_BUILD_VERIFY) TRY(verify_sa(x->text_w, n, sa.as<uint8_t>(), W, n, true));
     if (rank_hi < n) {
-        uint32_t np = 0;
-        HIP_TRY(hipMemcpy(&np, sa.as<uint32_t>() + rank_hi, 4, hipMemcpyDeviceToHost));
+        uint8_t b[8] = {};
+        HIP_TRY(hipMemcpy(b, sa.as<uint8_t>() + rank_hi * W, W, hipMemcpyDeviceToHost));
+        uint64_t np = 0;
+        for (uint32_t k = 0; k < W; k++) np |= (uint64_t)b[k] << (8 * k);
         x->next_pos = np;
     } else {
         x->next_pos = n;
     }
     if (x->sa_n == n) {
-        x->sa = static_cast<uint32_t*>(sa.release());
+        x->sa = static_cast<uint8_t*>(sa.release());
     } else {
         DevBuf part;
-        TRY(part.alloc(x->sa_n * 4, "suffix array shard"));
-        HIP_TRY(hipMemcpy(part.p, sa.as<uint32_t>() + rank_lo, x->sa_n * 4, hipMemcpyDeviceToDevice));
+        const uint64_t pb = x->sa_n * W + (W == 5 ? SAS_SA40_PAD : 0);
+        TRY(part.alloc(pb, "suffix array shard"));
+        HIP_TRY(hipMemset(part.p, 0, pb));
+        HIP_TRY(hipMemcpy(part.p, sa.as<uint8_t>() + rank_lo * W, x->sa_n * W, hipMemcpyDeviceToDevice));
         sa.alloc(0, "free");
-        x->sa = static_cast<uint32_t*>(part.release());
+        x->sa = static_cast<uint8_t*>(part.release());
     }
     const uint64_t sa_n = x->sa_n;
 
     if (flags & SAS_BUILD_LCP) {
         DevBuf l;
         TRY(l.alloc(sa_n * 4, "lcp"));
-        hipLaunchKernelGGL(k_lcp, dim3(grid_for(sa_n)), dim3(256), 0, 0, x->text_w, n, x->sa, sa_n, l.as<uint32_t>());
+        if (W == 5)
+            hipLaunchKernelGGL(k_lcp<5>, dim3(grid_for(sa_n)), dim3(256), 0, 0, x->text_w, n, SaView<5>{x->sa}, sa_n,
+                               l.as<uint32_t>());
+        else
+            hipLaunchKernelGGL(k_lcp<4>, dim3(grid_for(sa_n)), dim3(256), 0, 0, x->text_w, n, SaView<4>{x->sa}, sa_n,
+                               l.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         x->lcp = static_cast<uint32_t*>(l.release());
     }
@@ -802,12 +843,16 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
         DevBuf k, s;
         TRY(k.alloc(SAS_TOP_NODES * 8, "top keys"));
-        TRY(s.alloc(SAS_TOP_NODES * 4, "top sa"));
-        hipLaunchKernelGGL(k_top, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, x->sa, sa_n,
-                           k.as<uint64_t>(), s.as<uint32_t>(), (uint32_t)SAS_TOP_NODES);
+        TRY(s.alloc(SAS_TOP_NODES * 8, "top sa"));
+        if (W == 5)
+            hipLaunchKernelGGL(k_top<5>, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, SaView<5>{x->sa},
+                               sa_n, k.as<uint64_t>(), s.as<uint64_t>(), (uint32_t)SAS_TOP_NODES);
+        else
+            hipLaunchKernelGGL(k_top<4>, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, SaView<4>{x->sa},
+                               sa_n, k.as<uint64_t>(), s.as<uint64_t>(), (uint32_t)SAS_TOP_NODES);
         HIP_TRY(hipGetLastError());
         x->top_key = static_cast<uint64_t*>(k.release());
-        x->top_sa = static_cast<uint32_t*>(s.release());
+        x->top_sa = static_cast<uint64_t*>(s.release());
     }
     HIP_TRY(hipMalloc(&x->scratch, 64));
     HIP_TRY(hipMemset(x->scratch, 0, 64));
@@ -816,7 +861,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     sas_stats& st = x->stats;
     st.n = n;
     st.text_bytes = x->text_words * 8;
-    st.sa_bytes = sa_n * 4;
+    st.sa_bytes = sa_n * W;
+    st.sa_width = W;
     st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
     st.stree_bytes = x->stree_nodes * 64;
     st.stree_layers = x->stree_height;
@@ -858,6 +904,7 @@ static int copy_out(const void* src, void* dst, uint64_t bytes, uint32_t flags) 
 
 extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
     if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_sa: null argument");
+    if (index->sa_w != 4) SAS_FAIL(EINVAL, "sas_copy_sa: the SA is 40-bit (n >= 2^32 or SAS_BUILD_SA40): use sas_copy_sa64");
     if (count > index->sa_n) SAS_FAIL(EINVAL, "sas_copy_sa: count > number of SA entries");
     return copy_out(index->sa, dst, count * 4, flags);
 }
@@ -865,10 +912,39 @@ extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count
 extern "C" int sas_copy_sa_range(const sas_index* index, uint64_t start, uint64_t count, uint32_t* dst,
                                  uint32_t flags) {
     if (!index || (count && !dst)) SAS_FAIL(EINVAL, "sas_copy_sa_range: null argument");
+    if (index->sa_w != 4) SAS_FAIL(EINVAL, "sas_copy_sa_range: the SA is 40-bit: use sas_copy_sa64");
     if (start < index->rank_lo || start - index->rank_lo + count > index->sa_n)
         SAS_FAIL(EINVAL, "sas_copy_sa_range: ranks outside this index");
     if (count == 0) return 0;
-    return copy_out(index->sa + (start - index->rank_lo), dst, count * 4, flags);
+    return copy_out(index->sa + (start - index->rank_lo) * 4, dst, count * 4, flags);
+}
+
+template <int W>
+__global__ void k_widen_sa(SaView<W> sa, uint64_t start, uint64_t count, uint64_t* __restrict__ out) {
+    GRID_STRIDE(i, count) out[i] = sa[start + i];
+}
+
+extern "C" int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t count, uint64_t* dst, uint32_t flags) {
+    if (!index || (count && !dst)) SAS_FAIL(EINVAL, "sas_copy_sa64: null argument");
+    if (start < index->rank_lo || start - index->rank_lo + count > index->sa_n)
+        SAS_FAIL(EINVAL, "sas_copy_sa64: ranks outside this index");
+    if (count == 0) return 0;
+    HIP_TRY(hipSetDevice(index->device));
+    DevBuf tmp;
+    uint64_t* out = dst;
+    if (!(flags & SAS_DEVICE_PTRS)) {
+        TRY(tmp.alloc(count * 8, "sa64 staging"));
+        out = tmp.as<uint64_t>();
+    }
+    uint64_t s0 = start - index->rank_lo;
+    if (index->sa_w == 5)
+        hipLaunchKernelGGL(k_widen_sa<5>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<5>{index->sa}, s0, count, out);
+    else
+        hipLaunchKernelGGL(k_widen_sa<4>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<4>{index->sa}, s0, count, out);
+    HIP_TRY(hipGetLastError());
+    if (!(flags & SAS_DEVICE_PTRS)) HIP_TRY(hipMemcpy(dst, out, count * 8, hipMemcpyDeviceToHost));
+    else HIP_TRY(hipDeviceSynchronize());
+    return 0;
 }
 
 extern "C" int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {

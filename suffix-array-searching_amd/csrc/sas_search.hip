@@ -21,6 +21,7 @@
 #include "common.hpp"
 
 #include <chrono>
+#include <type_traits>
 #include <vector>
 
 #define SEARCH_BLOCK 1024
@@ -32,9 +33,9 @@ struct SearchArgs {
     uint64_t sa_n;       // SA entries held by this index
     uint64_t next_pos;   // answer when the lower bound is sa_n (n for a whole index)
     uint64_t rank_lo;    // global rank of sa[0]
-    const uint32_t* sa;
+    const uint8_t* sa;       // SaView<W> (u32 or packed 40-bit)
     const uint64_t* top_key;
-    const uint32_t* top_sa;
+    const uint64_t* top_sa;
     uint32_t top_levels;
     uint32_t iters;
     const uint32_t* stree;
@@ -69,17 +70,21 @@ __device__ __forceinline__ void query_ptr(const SearchArgs& a, uint64_t i, const
 }
 
 // ------------------------------------------------------------------ PLAIN / LCP
-template <int QW, bool LCP, bool TOP>
+template <int W>
+using sa_val_t = typename std::conditional<W == 4, uint32_t, uint64_t>::type;
+
+template <int QW, bool LCP, bool TOP, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
     __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
-    __shared__ uint32_t s_sa[TOP ? SAS_TOP_NODES : 1];
+    __shared__ sa_val_t<W> s_sa[TOP ? SAS_TOP_NODES : 1];
+    const SaView<W> sa{a.sa};
     uint32_t D = 0;
     if (TOP) {
         D = a.top_levels;
         uint32_t nodes = 1u << D;
         for (uint32_t k = threadIdx.x; k < nodes; k += blockDim.x) {
             s_key[k] = a.top_key[k];
-            s_sa[k] = a.top_sa[k];
+            s_sa[k] = (sa_val_t<W>)a.top_sa[k];
         }
         __syncthreads();
     }
@@ -95,19 +100,20 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
 
         uint64_t l = 0, r = a.sa_n;
         uint32_t k = 1, probes = 0, llcp = 0, rlcp = 0;
-        uint32_t pr = 0;  // SA[r] once r has moved
+        sa_val_t<W> pr = 0;  // SA[r] once r has moved
         for (uint32_t it = 0; it < a.iters; ++it) {
             if (l < r) {
                 uint64_t mid = (l + r) >> 1;
                 uint32_t h = LCP ? (llcp < rlcp ? llcp : rlcp) : 0u;
-                uint32_t p, lcp;
+                sa_val_t<W> p;
+                uint32_t lcp;
                 bool lt;
                 if (TOP && it < D) {
                     p = s_sa[k];
                     lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
                     k = 2 * k + (lt ? 1u : 0u);
                 } else {
-                    p = a.sa[mid];
+                    p = (sa_val_t<W>)sa[mid];
                     lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
                 }
                 probes++;
@@ -165,8 +171,9 @@ __device__ __forceinline__ uint64_t stree_descend(const SearchArgs& a, const uin
     return k;
 }
 
-template <int QW>
+template <int QW, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
+    const SaView<W> sa{a.sa};
     __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.stree);
@@ -221,11 +228,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
         // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
         const uint32_t h16 = m < 16 ? m : 16;
         uint64_t l = r0, r = r1;
-        uint32_t llcp = h16, rlcp = h16, pr = 0;
+        uint32_t llcp = h16, rlcp = h16;
+        sa_val_t<W> pr = 0;
         bool have = false;
         while (l < r) {
             uint64_t mid = (l + r) >> 1;
-            uint32_t p = a.sa[mid], lcp;
+            sa_val_t<W> p = (sa_val_t<W>)sa[mid];
+            uint32_t lcp;
             uint32_t h = llcp < rlcp ? llcp : rlcp;
             bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
             probes++;
@@ -242,7 +251,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
         uint64_t pos;
         if (l >= sa_n) pos = a.next_pos;
         else if (have) pos = pr;
-        else pos = a.sa[l];
+        else pos = sa[l];
         a.out_pos[i] = pos;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -257,7 +266,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
 //                                             suffix is a proper prefix of q)
 //   key == K64, m > 32     ->  exact compare from char 32 (text read)
 template <int QW>
-__device__ __forceinline__ bool sector_ge(uint64_t key, uint32_t p, uint64_t K64, const SearchArgs& a,
+__device__ __forceinline__ bool sector_ge(uint64_t key, uint64_t p, uint64_t K64, const SearchArgs& a,
                                           const QueryRegs<QW>& q) {
     if (key != K64) return key > K64;
     if (q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
@@ -265,11 +274,16 @@ __device__ __forceinline__ bool sector_ge(uint64_t key, uint32_t p, uint64_t K64
     return !suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
 }
 
-__device__ __forceinline__ void sector_entry(const uint4* __restrict__ leaves, uint64_t x, uint64_t* key, uint32_t* p) {
+// SA value of leaf entry j (0/1) from the leaf's second 16 B: low word + bits 32..39
+__device__ __forceinline__ uint64_t sector_sa(uint4 sv, uint32_t j) {
+    uint32_t lo = j ? sv.y : sv.x;
+    return (uint64_t)lo | ((uint64_t)((sv.z >> (8 * j)) & 0xFF) << 32);
+}
+
+__device__ __forceinline__ void sector_entry(const uint4* __restrict__ leaves, uint64_t x, uint64_t* key, uint64_t* p) {
     const uint64_t* kk = reinterpret_cast<const uint64_t*>(leaves + 2 * (x >> 1));
-    const uint32_t* ss = reinterpret_cast<const uint32_t*>(leaves + 2 * (x >> 1) + 1);
     *key = kk[x & 1];
-    *p = ss[x & 1];
+    *p = sector_sa(leaves[2 * (x >> 1) + 1], (uint32_t)(x & 1));
 }
 
 // UPPER predicate for occurrence ranges: the first min(m, len) chars of
@@ -277,7 +291,7 @@ __device__ __forceinline__ void sector_entry(const uint4* __restrict__ leaves, u
 //   m <= 32: key > Q3, Q3 = q's 32-char key padded with 3s instead of 0s
 //   m >  32: key != K64 -> key > K64; else exact compare from char 32
 template <int QW>
-__device__ __forceinline__ bool sector_gt_prefix(uint64_t key, uint32_t p, uint64_t K64, uint64_t Q3,
+__device__ __forceinline__ bool sector_gt_prefix(uint64_t key, uint64_t p, uint64_t K64, uint64_t Q3,
                                                  const SearchArgs& a, const QueryRegs<QW>& q) {
     if (q.m <= 32) return key > Q3;
     if (key != K64) return key > K64;
@@ -291,12 +305,12 @@ __device__ __forceinline__ bool sector_gt_prefix(uint64_t key, uint32_t p, uint6
 // exponential + binary search on the leaf array for runs that cross leaves.
 template <int QW, bool UPPER>
 __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint4* s_nodes, const QueryRegs<QW>& q,
-                                                 uint64_t K64, uint64_t Q3, uint32_t* probes, uint32_t* px) {
+                                                 uint64_t K64, uint64_t Q3, uint32_t* probes, uint64_t* px) {
     const uint64_t sa_n = a.sa_n;
     const uint4* leaves = a.sec_leaves;
     const uint4* g = reinterpret_cast<const uint4*>(a.sec_inner);
     const uint32_t R16 = (uint32_t)(((UPPER && q.m <= 32) ? Q3 : K64) >> 32);
-    auto pred = [&](uint64_t key, uint32_t p) -> bool {
+    auto pred = [&](uint64_t key, uint64_t p) -> bool {
         return UPPER ? sector_gt_prefix<QW>(key, p, K64, Q3, a, q) : sector_ge<QW>(key, p, K64, a, q);
     };
     uint64_t k = 0;
@@ -312,12 +326,13 @@ __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint
     uint4 kv = leaves[2 * k], sv = leaves[2 * k + 1];
     (*probes)++;
     uint64_t key0 = (uint64_t)kv.x | ((uint64_t)kv.y << 32), key1 = (uint64_t)kv.z | ((uint64_t)kv.w << 32);
-    if (2 * k < sa_n && pred(key0, sv.x)) {
-        *px = sv.x;
+    const uint64_t p0 = sector_sa(sv, 0), p1 = sector_sa(sv, 1);
+    if (2 * k < sa_n && pred(key0, p0)) {
+        *px = p0;
         return 2 * k;
     }
-    if (2 * k + 1 < sa_n && pred(key1, sv.y)) {
-        *px = sv.y;
+    if (2 * k + 1 < sa_n && pred(key1, p1)) {
+        *px = p1;
         return 2 * k + 1;
     }
     // rare: a run of entries sharing the routing key continues to the right --
@@ -327,7 +342,7 @@ __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint
     for (;;) {
         hi = lo + step - 1;
         if (hi >= sa_n) { hi = sa_n; break; }
-        uint64_t kk; uint32_t pp;
+        uint64_t kk, pp;
         sector_entry(leaves, hi, &kk, &pp);
         (*probes)++;
         if (pred(kk, pp)) break;
@@ -336,7 +351,7 @@ __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint
     }
     while (lo < hi) {
         uint64_t mid = (lo + hi) >> 1;
-        uint64_t kk; uint32_t pp;
+        uint64_t kk, pp;
         sector_entry(leaves, mid, &kk, &pp);
         (*probes)++;
         if (pred(kk, pp)) hi = mid;
@@ -367,9 +382,10 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector(SearchArgs a) {
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
-        uint32_t probes = 0, px = 0;
+        uint32_t probes = 0;
+        uint64_t px = 0;
         uint64_t x = sector_bound<QW, false>(a, s_nodes, q, q.w[0], 0, &probes, &px);
-        a.out_pos[i] = (x >= a.sa_n) ? a.next_pos : (uint64_t)px;
+        a.out_pos[i] = (x >= a.sa_n) ? a.next_pos : px;
         if (a.out_probes) a.out_probes[i] = probes;
     }
     if (bad) atomicOr(a.bad, 1u);
@@ -391,7 +407,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
         const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
-        uint32_t probes = 0, px = 0;
+        uint32_t probes = 0;
+        uint64_t px = 0;
         uint64_t lo = sector_bound<QW, false>(a, s_nodes, q, K64, Q3, &probes, &px);
         uint64_t hi = sector_bound<QW, true>(a, s_nodes, q, K64, Q3, &probes, &px);
         if (hi < lo) hi = lo;
@@ -403,13 +420,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 }
 
 // ------------------------------------------------------------------ host dispatch
-static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    uint64_t blocks = (a.nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
-    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
-    if (blocks > cap) blocks = cap;
-    if (blocks == 0) return 0;
-    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    bool top = !(flags & SAS_NO_LDS_TOP);
+template <int W>
+static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
 #define QW_CASE(KERNEL_T)                                                           \
     switch (qw) {                                                                   \
         case 1: hipLaunchKernelGGL(KERNEL_T(1), grid, block, 0, st, a); break;      \
@@ -417,11 +429,11 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
         case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
         default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
     }
-#define K_PLAIN_TOP(Q) (k_sa_binary<Q, false, true>)
-#define K_PLAIN(Q) (k_sa_binary<Q, false, false>)
-#define K_LCP_TOP(Q) (k_sa_binary<Q, true, true>)
-#define K_LCP(Q) (k_sa_binary<Q, true, false>)
-#define K_STREE(Q) (k_sa_stree<Q>)
+#define K_PLAIN_TOP(Q) (k_sa_binary<Q, false, true, W>)
+#define K_PLAIN(Q) (k_sa_binary<Q, false, false, W>)
+#define K_LCP_TOP(Q) (k_sa_binary<Q, true, true, W>)
+#define K_LCP(Q) (k_sa_binary<Q, true, false, W>)
+#define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
     if (algo == SAS_ALGO_PLAIN) {
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
@@ -429,9 +441,21 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
     } else if (algo == SAS_ALGO_STREE) {
         QW_CASE(K_STREE)
-    } else {
+    } else {  // the sector kernel reads positions from its leaves: launched via W = 4 only
         QW_CASE(K_SECTOR)
     }
+#undef QW_CASE
+}
+
+static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
+    uint64_t blocks = (a.nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
+    if (blocks > cap) blocks = cap;
+    if (blocks == 0) return 0;
+    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
+    bool top = !(flags & SAS_NO_LDS_TOP);
+    if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR) launch_w<5>(algo, top, qw, grid, block, st, a);
+    else launch_w<4>(algo, top, qw, grid, block, st, a);
     HIP_TRY(hipGetLastError());
     return 0;
 }

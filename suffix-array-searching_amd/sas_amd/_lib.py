@@ -24,6 +24,7 @@ SAS_NO_LDS_TOP = 1 << 4
 SAS_VALIDATE = 1 << 5
 SAS_BUILD_WIDE = 1 << 6
 SAS_BUILD_SECTOR = 1 << 7
+SAS_BUILD_SA40 = 1 << 8
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
@@ -39,13 +40,13 @@ class SasStats(C.Structure):
         ("n", C.c_uint64), ("text_bytes", C.c_uint64), ("sa_bytes", C.c_uint64), ("lcp_bytes", C.c_uint64),
         ("stree_bytes", C.c_uint64), ("stree_layers", C.c_uint32), ("stree_lds_layers", C.c_uint32),
         ("top_levels", C.c_uint32), ("iterations", C.c_uint32), ("build_sa_ns", C.c_uint64),
-        ("build_total_ns", C.c_uint64), ("sa_rounds", C.c_uint32), ("reserved", C.c_uint32),
+        ("build_total_ns", C.c_uint64), ("sa_rounds", C.c_uint32), ("sa_width", C.c_uint32),
         ("rank_lo", C.c_uint64), ("sa_entries", C.c_uint64), ("next_pos", C.c_uint64),
         ("sector_bytes", C.c_uint64), ("sector_layers", C.c_uint32), ("sector_lds_layers", C.c_uint32),
     ]
 
     def as_dict(self):
-        return {f: getattr(self, f) for f, _ in self._fields_ if f != "reserved"}
+        return {f: getattr(self, f) for f, _ in self._fields_ }
 
 
 class SasError(RuntimeError):
@@ -100,6 +101,7 @@ def lib():
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]
     L.sas_search_range.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp, u32]
     L.sas_copy_sa_range.argtypes = [vp, u64, u64, vp, u32]
+    L.sas_copy_sa64.argtypes = [vp, u64, u64, vp, u32]
     L.sas_read_fasta.argtypes = [C.c_char_p, vp, u64, C.POINTER(u64)]
     L.sas_kmer_keys.argtypes = [vp, u64, u32, u64, vp, C.POINTER(u64), u32]
     L.sas_verify.argtypes = [vp]

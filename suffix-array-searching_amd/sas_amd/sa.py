@@ -57,27 +57,35 @@ class SaNaive:
 
     @classmethod
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
-              rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True) -> "SaNaive":
+              rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
+              sa40: bool = False) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
-        ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None."""
+        ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
+        (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
+        builder even when n < 2^32 (automatic above)."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
-        sa_ptr = None
+        flags |= _lib.SAS_BUILD_SA40 if sa40 else 0
+        sa_ptr, sa_w = None, 4
         if sa is not None:
             if _is_cuda(t) != _is_cuda(sa):
                 raise ValueError("text and sa must both be host or both be device arrays")
             if not _is_cuda(sa):
-                sa = np.ascontiguousarray(sa, np.uint32)
+                sa = np.asarray(sa)
+                sa = np.ascontiguousarray(sa, np.uint64 if sa.dtype.itemsize == 8 else np.uint32)
+                sa_w = sa.dtype.itemsize
+            else:
+                sa_w = sa.element_size()
             sa_ptr = _ptr(sa)
         if _is_cuda(t):
             flags |= _lib.SAS_DEVICE_PTRS
         h = C.c_void_p()
         if rank_range is None:
-            check(lib().sas_build(_ptr(t), n, sa_ptr, 4, flags, C.byref(h)))
+            check(lib().sas_build(_ptr(t), n, sa_ptr, sa_w, flags, C.byref(h)))
         else:
-            check(lib().sas_build_shard(_ptr(t), n, sa_ptr, 4, int(rank_range[0]), int(rank_range[1]), flags,
+            check(lib().sas_build_shard(_ptr(t), n, sa_ptr, sa_w, int(rank_range[0]), int(rank_range[1]), flags,
                                         C.byref(h)))
         return cls(h, n)
 
@@ -98,10 +106,15 @@ class SaNaive:
         check(lib().sas_get_stats(self._h, C.byref(s)))
         return s.as_dict()
 
-    def suffix_array(self, count: int | None = None) -> np.ndarray:
-        count = self.sa_n if count is None else count
-        out = np.zeros(max(count, 1), np.uint32)
-        check(lib().sas_copy_sa(self._h, out.ctypes.data, count, 0))
+    def suffix_array(self, count: int | None = None, start: int = 0) -> np.ndarray:
+        """Local SA entries [start, start+count): u32 for a u32 index, u64 for a 40-bit one."""
+        count = self.sa_n - start if count is None else count
+        if self.stats()["sa_width"] == 4 and start == 0:
+            out = np.zeros(max(count, 1), np.uint32)
+            check(lib().sas_copy_sa(self._h, out.ctypes.data, count, 0))
+            return out[:count]
+        out = np.zeros(max(count, 1), np.uint64)
+        check(lib().sas_copy_sa64(self._h, self.rank_lo + start, count, out.ctypes.data, 0))
         return out[:count]
 
     def lcp_array(self) -> np.ndarray:
@@ -216,6 +229,10 @@ class SaNaive:
         buf = np.concatenate([q, np.zeros(64, np.uint8)])
         lo, hi = self.search_range(buf, np.zeros(1, np.uint64), np.array([len(q)], np.uint32))
         cnt = int(hi[0] - lo[0])
+        if self.stats()["sa_width"] == 5:
+            out = np.zeros(max(cnt, 1), np.uint64)
+            check(lib().sas_copy_sa64(self._h, int(lo[0]), cnt, out.ctypes.data, 0))
+            return out[:cnt]
         out = np.zeros(max(cnt, 1), np.uint32)
         check(lib().sas_copy_sa_range(self._h, int(lo[0]), cnt, out.ctypes.data, 0))
         return out[:cnt]

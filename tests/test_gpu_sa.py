@@ -345,3 +345,92 @@ def test_kmer_keys_match_reference_loop(sas):
     idx = sas.STree16.new(keys)  # the S-tree the reference builds over them
     qs = np.sort(keys)[::7]
     assert np.array_equal(idx.query(qs), O.SortedVec(keys).query(qs))
+
+
+def test_sa40_matches_u32_path(sas, sadef):
+    """Packed 40-bit SA + bucketed builder (the n >= 2^32 path), forced at small
+    n: the SA is bit-identical to the oracle's, every algorithm returns the same
+    positions as the u32 index, occurrence ranges and shards agree."""
+    for c in sadef["cases"]:
+        t = np.array(c["text"], np.uint8)
+        idx = sas.SaNaive.build(t, verify=True, sa40=True)
+        assert idx.stats()["sa_width"] == 5
+        assert idx.suffix_array().tolist() == c["sa"], c["name"]
+        buf, off, lens = pack([q["q"] for q in c["queries"]])
+        expect = np.array([q["pos"] for q in c["queries"]], np.uint64)
+        for algo in ALGOS:
+            assert np.array_equal(idx.search_batch(buf, off, lens, algo=algo), expect), (c["name"], algo)
+    rng = np.random.default_rng(12)
+    blk = rng.integers(0, 4, 3000, dtype=np.uint8)
+    texts = [sas.random_string(3_000_017, seed=4), np.zeros(70_000, np.uint8),
+             np.concatenate([blk, blk, rng.integers(0, 4, 999, dtype=np.uint8), blk]),
+             np.tile(rng.integers(0, 4, 7, dtype=np.uint8), 20_000)]
+    for t in texts:
+        n = len(t)
+        a = sas.SaNaive.build(t, verify=True)
+        b = sas.SaNaive.build(t, verify=True, sa40=True)
+        sa = a.suffix_array()
+        assert np.array_equal(b.suffix_array(), sa.astype(np.uint64)), n
+        assert np.array_equal(b.lcp_array(), a.lcp_array())
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 300, 2000), rng.integers(1, 300, 2000))]
+        qs += [rng.integers(0, 4, rng.integers(1, 40), dtype=np.uint8) for _ in range(500)]
+        buf, off, lens = pack(qs)
+        expect = oracle_positions(t, sa, buf, off, lens)
+        for algo in ALGOS:
+            assert np.array_equal(b.search_batch(buf, off, lens, algo=algo), expect), (n, algo)
+        lo, hi = b.search_range(buf, off, lens)
+        lo2, hi2 = a.search_range(buf, off, lens)
+        assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2)
+        # caller-supplied u64 SA, and 40-bit shards
+        c64 = sas.SaNaive.build(t, sa=sa.astype(np.uint64), verify=True, lcp=False)
+        assert c64.stats()["sa_width"] == 4 and np.array_equal(c64.suffix_array(), sa)
+        from sas_amd.shard import shard_range
+        for g in range(2):
+            lo_r, hi_r = shard_range(n, 2, g)
+            s = sas.SaNaive.build(t, sa=sa, rank_range=(lo_r, hi_r), sa40=True)
+            assert np.array_equal(s.suffix_array(), sa[lo_r:hi_r].astype(np.uint64))
+            assert s.stats()["next_pos"] == (sa[hi_r] if hi_r < n else n)
+
+
+def test_sa_beyond_u32(sas):
+    """n > 2^32 (past the reference's u32 SA, sas/sa_search.rs:35): the 40-bit
+    builder for real.  The SA is checked on the GPU (adjacency as
+    sas/sa_search.rs:36-38 + permutation); every answer is then proven to be the
+    exact lower bound on the host text: SA[lo-1] < q <= SA[lo], pos = SA[lo]."""
+    import torch
+    n = (1 << 32) + 12345
+    t = sas.random_string(n, seed=321, device="cuda")
+    idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True)
+    st = idx.stats()
+    assert st["sa_width"] == 5 and st["n"] == n
+    ht = t.cpu().numpy()
+    del t
+    torch.cuda.empty_cache()
+    rng = np.random.default_rng(2)
+    nq = 3000
+    offs = np.concatenate([rng.integers(0, n - 300, nq - 600), rng.integers((1 << 32) - 100, n - 300, 100)])
+    qs = [ht[o:o + l] for o, l in zip(offs, rng.integers(8, 257, len(offs)))]
+    qs += [rng.integers(0, 4, rng.integers(1, 30), dtype=np.uint8) for _ in range(500)]
+    buf, off, lens = pack(qs)
+    lo, hi = idx.search_range(buf, off, lens)
+    got = {algo: idx.search_batch(buf, off, lens, algo=algo) for algo in ALGOS}
+    big = 0
+    for k, q in enumerate(qs):
+        qb = bytes(q)
+        r = int(lo[k])
+        pair = idx.suffix_array(count=2 if r > 0 else 1, start=r - 1 if r > 0 else 0)
+        cur = int(pair[-1]) if r < n else n
+        prev = int(pair[0]) if r > 0 else None
+        if r < n:
+            assert bytes(ht[cur:cur + len(q)]) >= qb, k
+        if prev is not None:
+            assert bytes(ht[prev:prev + len(q)]) < qb, k
+        for algo in ALGOS:
+            assert int(got[algo][k]) == cur, (k, algo)
+        big += cur >= (1 << 32)
+        if k < 600:
+            occ_hi = int(hi[k])
+            if occ_hi > r:
+                last = int(idx.suffix_array(count=1, start=occ_hi - 1)[0])
+                assert bytes(ht[last:last + len(q)]) == qb
+    assert big > 0  # positions above 2^32 were returned

@@ -1,0 +1,135 @@
+// treebench.hip -- price candidate search-tree layouts on MI355X before building them.
+//
+// Each lane runs one "lookup": a dependent chain of random accesses, one per tree
+// layer, each into its own region whose size is that layer's footprint and whose
+// width is that layer's node width (32 B = one sector, 128 B = one line).  The
+// chain is dependent (the next address mixes in the loaded value) like a real
+// descent.  NT = 1 issues the DRAM-level accesses (regions >= 1 GiB) as
+// non-temporal loads so they do not evict the upper layers from L2 / MALL.
+//
+//   usage: treebench <lookups> <reps> <layout>...   layout = "W:MiB,W:MiB,..." (W in bytes, MiB may be fractional)
+//   e.g.   treebench 10000000 5 32:0.285,32:2.56,32:23.1,32:207,32:1864,32:16384
+//
+// Prints one JSON line per (layout, NT): lookups/s and ns per lookup.
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/treebench tools/treebench.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+#define MAXL 12
+struct Layout {
+    int L;
+    uint64_t base[MAXL];   // byte offset of each region
+    uint64_t units[MAXL];  // number of nodes in the region
+    int width[MAXL];       // 32, 64 or 128
+    int nt[MAXL];          // non-temporal loads for this region
+};
+
+__device__ __forceinline__ uint64_t mix(uint64_t x) {
+    x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+    return x;
+}
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld(const u32x4* p) {
+    if (NT) return __builtin_nontemporal_load(p);
+    return *p;
+}
+
+__global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
+                                                   uint32_t seed, uint32_t* out) {
+    uint32_t acc = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < lookups;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
+        uint32_t dep = 0;
+        for (int l = 0; l < lay.L; l++) {
+            // one 64-bit multiply per level (cheap, like a real descent's address math);
+            // dep's top bit is 0 (buffer = 0x01): a true data dependence
+            h = h * 0x9E3779B97F4A7C15ull + l + (dep & 0x80000000u);
+            uint64_t node = ((h >> 32) * lay.units[l]) >> 32;
+            const u32x4* v = reinterpret_cast<const u32x4*>(p + lay.base[l] + node * lay.width[l]);
+            if (lay.width[l] < 16) {
+                dep = *reinterpret_cast<const uint32_t*>(v);
+                continue;
+            }
+            u32x4 t = lay.nt[l] ? ld<true>(v) : ld<false>(v);
+            if (lay.width[l] >= 32) { u32x4 t2 = lay.nt[l] ? ld<true>(v + 1) : ld<false>(v + 1); t ^= t2; }
+            if (lay.width[l] >= 64) { t ^= ld<false>(v + 2) ^ ld<false>(v + 3); }
+            if (lay.width[l] >= 128) { t ^= ld<false>(v + 4) ^ ld<false>(v + 5) ^ ld<false>(v + 6) ^ ld<false>(v + 7); }
+            dep = t.x ^ t.y ^ t.z ^ t.w;
+        }
+        acc ^= dep;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
+int main(int argc, char** argv) {
+    if (argc < 4) { fprintf(stderr, "usage: treebench <lookups> <reps> <layout>...\n"); return 2; }
+    uint64_t lookups = strtoull(argv[1], 0, 10);
+    int reps = atoi(argv[2]);
+    std::vector<Layout> lays;
+    std::vector<std::string> names;
+    uint64_t maxbytes = 0;
+    for (int a = 3; a < argc; a++) {
+        Layout L{};
+        char buf[1024];
+        strncpy(buf, argv[a], sizeof buf - 1);
+        uint64_t off = 0;
+        for (char* tok = strtok(buf, ","); tok && L.L < MAXL; tok = strtok(nullptr, ",")) {
+            int w = atoi(tok);
+            double mib = atof(strchr(tok, ':') + 1);
+            uint64_t bytes = (uint64_t)(mib * 1048576.0);
+            L.width[L.L] = w;
+            L.units[L.L] = bytes / w ? bytes / w : 1;
+            L.base[L.L] = off;
+            L.nt[L.L] = 0;
+            off += ((L.units[L.L] * w + 4095) / 4096) * 4096;
+            L.L++;
+        }
+        if (off > maxbytes) maxbytes = off;
+        lays.push_back(L);
+        names.push_back(argv[a]);
+    }
+    uint8_t* p;
+    uint32_t* out;
+    CHECK(hipMalloc(&p, maxbytes));
+    CHECK(hipMalloc(&out, 64));
+    CHECK(hipMemset(p, 1, maxbytes));
+    int cus = 256;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, 0) == hipSuccess) cus = prop.multiProcessorCount;
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    dim3 blk(1024), grd(cus * 2);
+    for (size_t k = 0; k < lays.size(); k++) {
+        for (int nt = 0; nt < 2; nt++) {
+            Layout L = lays[k];
+            for (int l = 0; l < L.L; l++) L.nt[l] = nt && (L.units[l] * L.width[l] >= (1ull << 30));
+            hipLaunchKernelGGL(k_chain, grd, blk, 0, 0, p, L, lookups, 1u, out);
+            CHECK(hipDeviceSynchronize());
+            CHECK(hipEventRecord(e0));
+            for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k_chain, grd, blk, 0, 0, p, L, lookups, 2u + r, out);
+            CHECK(hipEventRecord(e1));
+            CHECK(hipEventSynchronize(e1));
+            float ms;
+            CHECK(hipEventElapsedTime(&ms, e0, e1));
+            ms /= reps;
+            printf("{\"layout\": \"%s\", \"nt_dram\": %d, \"lookups\": %llu, \"ms\": %.4f, \"lookups_per_s\": %.4g, "
+                   "\"ps_per_lookup\": %.1f}\n",
+                   names[k].c_str(), nt, (unsigned long long)lookups, ms, lookups / (ms * 1e-3),
+                   ms * 1e9 / lookups);
+            fflush(stdout);
+        }
+    }
+    return 0;
+}
