@@ -190,15 +190,20 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
 
 
 def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
-    """configs[3]-shaped run: the largest text this engine indexes with a u32 SA
-    (BASELINE's "64 GiB" needs a 40/64-bit SA: DESIGN.md §8) and 10^8 positive
-    queries of mixed length 8..256 (random_queries with len in [8, 257)), ragged,
-    through sas_search_batch on device buffers."""
-    n = args.n if args.n != 1 << 30 else (1 << 32) - (1 << 20)
+    """configs[3]-shaped run: n = 2^34 chars (16 GiB of byte-coded text, a 40-bit SA:
+    BASELINE's "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and
+    10^8 positive queries of mixed length 8..256 (random_queries with len in
+    [8, 257)), ragged, through sas_search_batch on device buffers.  The sector tree
+    (16 B per suffix) is built only where it fits next to the SA (n <= 2^33)."""
+    n = args.n if args.n != 1 << 30 else 1 << 34
     nq = args.nq if args.nq != 10_000_000 else 100_000_000
+    sector = n <= (1 << 33)
+    main_algo = args.algo if (args.algo != "sector" or sector) else "stree"
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
-    idx = sas_amd.SaNaive.build(text, lcp=False, stree=True)
+    # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
+    idx = sas_amd.SaNaive.build(text, lcp=False, stree=not (sector and main_algo == "sector"), sector=sector,
+                                verify=True)
     stats = idx.stats()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
@@ -221,7 +226,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
     results = {}
-    for algo in [a for a in (args.algo, "plain") if a]:
+    for algo in [a for a in (main_algo, "plain", "lcp") if a]:
         if algo in results:
             continue
         def step():
@@ -232,7 +237,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
         torch.cuda.synchronize()
         ev0.record()
         tt = time.perf_counter()
-        steps = args.steps if algo == args.algo else max(2, args.steps // 4)
+        steps = args.steps if algo == main_algo else max(2, args.steps // 4)
         for _ in range(steps):
             step()
         ev1.record()
@@ -252,28 +257,36 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
         mp = float(pr.double().mean().item())
         mean_m = total / nq
         P = int(np.log2(n)) + 1
-        ab = (stats["stree_layers"] * 64 + max(0.0, mp - stats["stree_layers"]) * (4 + mean_m) + mean_m + 8
-              if algo == "stree" else P * (4 + mean_m) + mean_m + 8)
+        if algo == "stree":
+            ab = stats["stree_layers"] * 64 + max(0.0, mp - stats["stree_layers"]) * (4 + mean_m) + mean_m + 8
+        elif algo == "sector":
+            # H 32-B nodes (leaf = keys + SA), extra leaf probes x 12 B, the query, the
+            # position, and the packed text window past char 32 for the final compare
+            H = stats["sector_layers"]
+            ab = H * 32 + max(0.0, mp - H) * 12 + mean_m + 8 + max(0.0, mean_m - 32) / 4
+        else:
+            ab = P * (4 + mean_m) + mean_m + 8
         results[algo] = {"lookups_per_s": nq * steps / el, "kernel_ms": kms, "mean_probes": mp,
                          "algorithmic_bytes_per_lookup": ab, "achieved_GBps": ab * nq / (kms * 1e-3) / 1e9,
                          "verified": okc}
     if rank == 0:
-        h = results[args.algo]
+        h = results[main_algo]
         print(json.dumps({
             "metric": "pattern lookups/s (configs[3] shape)", "value": h["lookups_per_s"], "unit": "lookups/s",
             "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": nq / h["lookups_per_s"] * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
             "data": f"synthetic: random_string(ChaCha8Rng({SEED})) text, positive queries len in [8,257)",
-            "config": {"workload": f"configs[3]-shaped: n={n} (largest u32-SA text; 64 GiB needs a wider SA), "
+            "config": {"workload": f"configs[3]-shaped: n={n} chars, {stats['sa_width'] * 8}-bit SA, "
                                    f"{nq} mixed-length 8..256 queries, ragged", "n": n, "queries_per_gpu": nq,
-                       "mean_m": total / nq, "algo": args.algo},
+                       "mean_m": total / nq, "algo": main_algo},
             "roofline": {"bound": "hbm", "achieved": h["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector"}.get(args.algo, "k_sa_binary"),
+                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector"}.get(main_algo, "k_sa_binary"),
                          "kernel_ms": h["kernel_ms"]},
             "variants": results, "setup_s": setup,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
-                                            "build_sa_ns", "build_total_ns")}}), flush=True)
+                                            "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
+                                            "stree_bytes", "sector_bytes")}}), flush=True)
 
 
 def main():
