@@ -34,15 +34,18 @@ SEED = 31415  # sas/main.rs:38
 
 
 def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes: float,
-                      sector_layers: int = 0) -> float:
+                      sector_layers: int = 0, quad_layers: int = 0) -> float:
     """Bytes a lookup must move: 4 B SA word + m text bytes per
     probe, the query, the 8 B position.  PLAIN/LCP: P = ilog2(n)+1 probes.
     STREE: H 64-B nodes + measured tail probes.  SECTOR: H 32-B nodes (the
-    leaf holds the keys and the SA values) + measured extra leaf probes x 12 B."""
+    leaf holds the keys and the SA values) + measured extra leaf probes x 12 B.
+    QUAD: H 64-B nodes (4-entry leaves) + measured extra leaf probes x 64 B."""
     if algo == "stree":
         return stree_layers * 64 + tail_probes * (4 + m) + m + 8
     if algo == "sector":
         return sector_layers * 32 + tail_probes * 12 + m + 8
+    if algo == "quad":
+        return quad_layers * 64 + tail_probes * 64 + m + 8
     P = int(np.log2(n)) + 1
     return P * (4 + m) + m + 8
 
@@ -197,13 +200,13 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     (16 B per suffix) is built only where it fits next to the SA (n <= 2^33)."""
     n = args.n if args.n != 1 << 30 else 1 << 34
     nq = args.nq if args.nq != 10_000_000 else 100_000_000
-    sector = n <= (1 << 33)
-    main_algo = args.algo if (args.algo != "sector" or sector) else "stree"
+    fits = n <= (1 << 33)  # sector / quad leaves: 16 B per suffix next to the 40-bit SA
+    main_algo = args.algo if (args.algo not in ("sector", "quad") or fits) else "stree"
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
     # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
-    idx = sas_amd.SaNaive.build(text, lcp=False, stree=not (sector and main_algo == "sector"), sector=sector,
-                                verify=True)
+    idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
+                                quad=main_algo == "quad", verify=True)
     stats = idx.stats()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
@@ -259,11 +262,12 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
         P = int(np.log2(n)) + 1
         if algo == "stree":
             ab = stats["stree_layers"] * 64 + max(0.0, mp - stats["stree_layers"]) * (4 + mean_m) + mean_m + 8
-        elif algo == "sector":
-            # H 32-B nodes (leaf = keys + SA), extra leaf probes x 12 B, the query, the
-            # position, and the packed text window past char 32 for the final compare
-            H = stats["sector_layers"]
-            ab = H * 32 + max(0.0, mp - H) * 12 + mean_m + 8 + max(0.0, mean_m - 32) / 4
+        elif algo in ("sector", "quad"):
+            # H nodes (leaf = keys + SA), extra leaf probes, the query, the position, and
+            # the packed text window past char 32 for the final compare
+            H = stats[f"{algo}_layers"]
+            node, extra = (32, 12) if algo == "sector" else (64, 64)
+            ab = H * node + max(0.0, mp - H) * extra + mean_m + 8 + max(0.0, mean_m - 32) / 4
         else:
             ab = P * (4 + mean_m) + mean_m + 8
         results[algo] = {"lookups_per_s": nq * steps / el, "kernel_ms": kms, "mean_probes": mp,
@@ -281,12 +285,13 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
                        "mean_m": total / nq, "algo": main_algo},
             "roofline": {"bound": "hbm", "achieved": h["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector"}.get(main_algo, "k_sa_binary"),
+                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector",
+                                    "quad": "k_sa_quad"}.get(main_algo, "k_sa_binary"),
                          "kernel_ms": h["kernel_ms"]},
             "variants": results, "setup_s": setup,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
                                             "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
-                                            "stree_bytes", "sector_bytes")}}), flush=True)
+                                            "stree_bytes", "sector_bytes", "quad_bytes")}}), flush=True)
 
 
 def main():
@@ -297,8 +302,9 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default="sector", choices=["stree", "plain", "lcp", "sector"])
-    ap.add_argument("--variants", default="plain,lcp,stree,sector", help="other algos timed beside the headline one")
+    ap.add_argument("--algo", default="quad", choices=["stree", "plain", "lcp", "sector", "quad"])
+    ap.add_argument("--variants", default="plain,lcp,stree,sector,quad",
+                    help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
@@ -402,9 +408,10 @@ def main():
         mean_probes = float(probes.double().mean().item())
     else:
         mean_probes = float("nan")
-    layers_of = {"stree": stats["stree_layers"], "sector": stats["sector_layers"]}
+    layers_of = {"stree": stats["stree_layers"], "sector": stats["sector_layers"], "quad": stats["quad_layers"]}
     tail = max(0.0, mean_probes - layers_of[args.algo]) if args.algo in layers_of else mean_probes
-    algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail, stats["sector_layers"])
+    algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail, stats["sector_layers"],
+                                   stats["quad_layers"])
     achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
 
     variants = {}
@@ -413,7 +420,7 @@ def main():
         _, vp = idx.search_fixed(qbytes, m, algo=v, probes=True)
         vmean = float(vp.double().mean().item())
         vtail = max(0.0, vmean - layers_of[v]) if v in layers_of else vmean
-        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], vtail, stats["sector_layers"])
+        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], vtail, stats["sector_layers"], stats["quad_layers"])
         variants[v] = {"lookups_per_s": ws * nq * max(3, args.steps // 4) / vel, "kernel_ms": vk,
                        "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
                        "mean_probes": float(vp.double().mean().item()), "verified": vok}
@@ -431,7 +438,10 @@ def main():
                     "plain": "configs[1]: 2^30 text in HBM, 10^7 len-32 queries, plain binary search over SA",
                     "lcp": "configs[1] + mlr LCP skipping",
                     "sector": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, sector S-tree (32-B nodes, "
-                              "fused 32-char key + SA leaves, top layers LDS-staged)"}[args.algo]
+                              "fused 32-char key + SA leaves, top layers LDS-staged)",
+                    "quad": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, quad S-tree (17-ary 64-B nodes "
+                            "loaded by 4-lane groups in one request each, 4-entry fused 32-char key + SA leaves, "
+                            "top layers LDS-staged)"}[args.algo]
         line = {
             "metric": METRIC, "value": value, "unit": "lookups/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
@@ -447,14 +457,15 @@ def main():
             "roofline": None if not whole else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector"}.get(args.algo, "k_sa_binary"),
+                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector",
+                                    "quad": "k_sa_quad"}.get(args.algo, "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes},
             "cpu_baseline": cpu,
             "variants": variants,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
-                                            "top_levels", "iterations", "sa_rounds", "build_sa_ns",
-                                            "build_total_ns")},
+                                            "quad_layers", "quad_lds_layers", "top_levels", "iterations",
+                                            "sa_rounds", "build_sa_ns", "build_total_ns")},
             "setup_s": build_s, "verified": ok,
         }
         print(json.dumps(line), flush=True)

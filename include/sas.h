@@ -53,14 +53,17 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_SA40    (1u << 8)  /* store the SA as packed 40-bit entries and use the
                                         bucketed 64-bit builder at any n (automatic for
                                         n >= 2^32 - 64; test hook below that)             */
+#define SAS_BUILD_QUAD    (1u << 9)  /* also build the quad tree (SAS_ALGO_QUAD)         */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {
     SAS_ALGO_PLAIN = 0, /* lockstep lower-bound binary search over SA (A6/A9)              */
     SAS_ALGO_LCP   = 1, /* same probes, Manber-Myers mlr LCP skipping of known chars (A21) */
     SAS_ALGO_STREE = 2, /* S-tree over 16-char SA keys + exact tail search (K2+K3)         */
-    SAS_ALGO_SECTOR = 3 /* sector tree: 32-B nodes (one HBM sector), 9-ary on 16-char keys,
+    SAS_ALGO_SECTOR = 3, /* sector tree: 32-B nodes (one HBM sector), 9-ary on 16-char keys,
                            leaves fuse (32-char key, SA value) pairs: no text/SA reads for m<=32 */
+    SAS_ALGO_QUAD = 4   /* quad tree: 4 lanes per query load each 64-B node in one request;
+                           17-ary on 16-char keys, leaves = 4 fused (32-char key, SA) entries  */
 };
 
 typedef struct sas_stats {
@@ -83,6 +86,9 @@ typedef struct sas_stats {
     uint64_t sector_bytes;   /* sector tree (inner nodes + fused leaves), 0 if not built */
     uint32_t sector_layers;  /* sector tree height incl. the leaf layer           */
     uint32_t sector_lds_layers; /* its layers served from LDS                     */
+    uint64_t quad_bytes;     /* quad tree (inner nodes + leaves), 0 if not built   */
+    uint32_t quad_layers;    /* quad tree height incl. the leaf layer              */
+    uint32_t quad_lds_layers; /* its layers served from LDS                       */
 } sas_stats;
 
 const char* sas_last_error(void);

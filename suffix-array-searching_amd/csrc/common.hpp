@@ -33,6 +33,9 @@
 #define SAS_SECTOR_FAN 9              // sector tree: 8 separators, 9 children per 32-B node
 #define SAS_SECTOR_MAX_LAYERS 24
 #define SAS_SECTOR_LDS_NODES 2048     // <= 64 KiB of top sector-tree layers in LDS
+#define SAS_QUAD_FAN 17               // quad tree: 16 separators, 17 children per 64-B node
+#define SAS_QUAD_MAX_LAYERS 16
+#define SAS_QUAD_LDS_NODES 1024       // <= 64 KiB of top quad-tree layers in LDS
 
 // ---------------------------------------------------------------- errors
 void sas_set_error(int code, const std::string& msg);
@@ -88,6 +91,15 @@ struct sas_index {
     uint32_t sec_lds_layers = 0;
     uint32_t sec_lds_nodes = 0;
     uint64_t sec_inner_nodes = 0;
+    // quad tree (SAS_ALGO_QUAD): 64-B nodes, one 4-lane cooperative load each
+    uint4* quad_inner = nullptr;     // internal nodes, 16 u32 16-char separators (4 x uint4), root first
+    uint4* quad_leaves = nullptr;    // entry x = {key lo, key hi, sa lo32, sa bits 32..39}; leaf = 4 entries
+    uint64_t quad_leaf_count = 0;
+    uint64_t quad_off[SAS_QUAD_MAX_LAYERS] = {};
+    uint32_t quad_inner_layers = 0;
+    uint32_t quad_lds_layers = 0;
+    uint32_t quad_lds_nodes = 0;
+    uint64_t quad_inner_nodes = 0;
     sas_stats stats = {};
 };
 

@@ -577,6 +577,94 @@ static int build_sector(sas_index* x) {
     return 0;
 }
 
+// ------------------------------------------------------------------ quad tree
+// Leaf entry x (16 B) = {key64 lo, key64 hi, SA lo32, SA bits 32..39} for rank x;
+// leaf i = entries 4i..4i+3 = 64 B, so lane j of a 4-lane group loads entry j
+// and the group's load is one 64-B request.  Padding entries are all ones.
+template <int W>
+__global__ void k_quad_leaves(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n,
+                              uint4* __restrict__ leaves, uint64_t entries) {
+    GRID_STRIDE(x, entries) {
+        if (x < sa_n) {
+            uint64_t p = sa[x];
+            uint64_t k = text_chars32(tw, p);
+            leaves[x] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), (uint32_t)p, (uint32_t)(p >> 32));
+        } else {
+            leaves[x] = make_uint4(~0u, ~0u, ~0u, ~0u);
+        }
+    }
+}
+
+// Internal layer, left-max (as k_sector_layer, 17-ary): separator j of node i =
+// 16-char key of the last entry of child 17i+j's subtree (child_span leaves),
+// 0xFFFFFFFF for the globally last child and beyond.
+__global__ void k_quad_layer(uint32_t* __restrict__ inner, uint64_t oh, uint64_t layer_nodes, uint64_t child_span,
+                             uint64_t child_layer_nodes, const uint4* __restrict__ leaves, uint64_t sa_n) {
+    GRID_STRIDE(i, 16 * layer_nodes) {
+        uint64_t node = i / 16, j = i % 16;
+        uint64_t child = node * SAS_QUAD_FAN + j;
+        uint32_t sep = 0xFFFFFFFFu;
+        if (child + 1 < child_layer_nodes) {
+            uint64_t last = 4 * (child + 1) * child_span - 1;
+            if (last >= sa_n) last = sa_n - 1;
+            sep = leaves[last].y;
+        }
+        inner[(oh + node) * 16 + j] = sep;
+    }
+}
+
+static int build_quad(sas_index* x) {
+    const uint64_t sa_n = x->sa_n;
+    const uint64_t nl = (sa_n + 3) / 4;
+    uint64_t sizes[SAS_QUAD_MAX_LAYERS];
+    uint32_t H = 0;
+    uint64_t c = nl;
+    do {
+        c = (c + SAS_QUAD_FAN - 1) / SAS_QUAD_FAN;
+        if (H >= SAS_QUAD_MAX_LAYERS) SAS_FAIL(ENOTSUP, "quad tree too high");
+        sizes[H++] = c;
+    } while (c > 1);
+    uint64_t tot = 0;
+    for (uint32_t h = 0; h < H; h++) {
+        x->quad_off[h] = tot;
+        tot += sizes[H - 1 - h];
+    }
+    DevBuf leaves, inner;
+    TRY(leaves.alloc(nl * 64, "quad leaves"));
+    TRY(inner.alloc(tot * 64, "quad inner nodes"));
+    if (x->sa_w == 5)
+        hipLaunchKernelGGL(k_quad_leaves<5>, dim3(grid_for(4 * nl)), dim3(256), 0, 0, x->text_w, SaView<5>{x->sa},
+                           sa_n, leaves.as<uint4>(), 4 * nl);
+    else
+        hipLaunchKernelGGL(k_quad_leaves<4>, dim3(grid_for(4 * nl)), dim3(256), 0, 0, x->text_w, SaView<4>{x->sa},
+                           sa_n, leaves.as<uint4>(), 4 * nl);
+    uint64_t span = 1, child_nodes = nl;
+    for (int h = (int)H - 1; h >= 0; h--) {
+        uint64_t ln = sizes[H - 1 - h];
+        hipLaunchKernelGGL(k_quad_layer, dim3(grid_for(16 * ln)), dim3(256), 0, 0, inner.as<uint32_t>(),
+                           x->quad_off[h], ln, span, child_nodes, leaves.as<uint4>(), sa_n);
+        span *= SAS_QUAD_FAN;
+        child_nodes = ln;
+    }
+    HIP_TRY(hipGetLastError());
+    x->quad_leaves = static_cast<uint4*>(leaves.release());
+    x->quad_inner = static_cast<uint4*>(inner.release());
+    x->quad_leaf_count = nl;
+    x->quad_inner_layers = H;
+    x->quad_inner_nodes = tot;
+    uint32_t L = 0;
+    uint64_t ln = 0;
+    for (uint32_t h = 0; h < H; h++) {
+        uint64_t sz = sizes[H - 1 - h];
+        if (ln + sz > SAS_QUAD_LDS_NODES) break;
+        ln += sz;
+        L++;
+    }
+    x->quad_lds_layers = L;
+    x->quad_lds_nodes = (uint32_t)ln;
+    return 0;
+}
+
 // ------------------------------------------------------------------ LDS top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
 // the leading one (0 = went left: r = mid, 1 = right: l = mid + 1).
@@ -607,7 +695,7 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
 static void free_index(sas_index* x) {
     if (!x) return;
     void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa, x->scratch, x->sec_inner,
-                     x->sec_leaves};
+                     x->sec_leaves, x->quad_inner, x->quad_leaves};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete x;
 }
@@ -835,6 +923,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     }
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
     if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
+    if (flags & SAS_BUILD_QUAD) TRY(build_quad(x));
 
     // binary-search top in LDS
     {
@@ -875,6 +964,9 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.sector_bytes = (x->sec_inner_nodes + x->sec_leaf_count) * 32;
     st.sector_layers = x->sec_leaves ? x->sec_inner_layers + 1 : 0;
     st.sector_lds_layers = x->sec_lds_layers;
+    st.quad_bytes = (x->quad_inner_nodes + x->quad_leaf_count) * 64;
+    st.quad_layers = x->quad_leaves ? x->quad_inner_layers + 1 : 0;
+    st.quad_lds_layers = x->quad_lds_layers;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -49,6 +49,13 @@ struct SearchArgs {
     uint32_t sec_inner_layers;
     uint32_t sec_lds_layers;
     uint32_t sec_lds_nodes;
+    const uint4* quad_inner;
+    const uint4* quad_leaves;
+    uint64_t quad_off[SAS_QUAD_MAX_LAYERS];
+    uint64_t quad_leaf_count;
+    uint32_t quad_inner_layers;
+    uint32_t quad_lds_layers;
+    uint32_t quad_lds_nodes;
     const uint8_t* qbytes;
     const uint64_t* qoff;
     const uint32_t* qlen;
@@ -419,6 +426,112 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// ------------------------------------------------------------------ QUAD
+// A 4-lane group per query.  Every node is 64 B and the group loads it with one
+// 16-B load per lane, which the memory system serves as ONE request (a per-lane
+// 32-B node costs two): tools/treebench measured 19-22 ps per DRAM-level 64-B
+// group load vs 26.5 ps for a per-lane 32-B node.  Inner nodes: 16 left-max
+// 16-char separators, 17-ary; lane j counts its 4, the group sums by shuffles.
+// Leaves: 4 entries {key64, SA}, lane j evaluates entry j, a group ballot picks
+// the first entry >= q.  All branches are group-uniform.
+#define QUAD_G 4
+
+__device__ __forceinline__ uint32_t quad_sum(uint32_t c) {
+    c += __shfl_xor(c, 1, QUAD_G);
+    c += __shfl_xor(c, 2, QUAD_G);
+    return c;
+}
+
+// 4-bit mask of the group's lanes with b set (bit j = lane j of the group)
+__device__ __forceinline__ uint32_t quad_mask(bool b) {
+    uint64_t bal = __ballot(b);
+    return (uint32_t)(bal >> (threadIdx.x & 60)) & 0xFu;
+}
+
+// Evaluate leaf L: mask of its entries x (< sa_n) with suffix(x) >= q; *p = this lane's SA value.
+template <int QW>
+__device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64, uint64_t L,
+                                              uint32_t sub, uint64_t* p) {
+    const uint64_t x = 4 * L + sub;
+    const uint4 e = a.quad_leaves[x];
+    const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+    const uint64_t pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+    *p = pp;
+    return quad_mask(x < a.sa_n && sector_ge<QW>(key, pp, K64, a, q));
+}
+
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
+    __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
+    for (uint32_t w = threadIdx.x; w < a.quad_lds_nodes * 4; w += blockDim.x) s_nodes[w] = a.quad_inner[w];
+    __syncthreads();
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const uint64_t nl = a.quad_leaf_count;
+    uint32_t bad = 0;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint32_t R16 = (uint32_t)(K64 >> 32);
+        uint32_t probes = 0;
+        uint64_t k = 0;
+        for (uint32_t h = 0; h < a.quad_inner_layers; h++) {
+            const uint4* node = ((h < a.quad_lds_layers) ? s_nodes : a.quad_inner) + (a.quad_off[h] + k) * 4;
+            const uint4 v = node[sub];
+            const uint32_t c = quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+            k = k * SAS_QUAD_FAN + c;
+            probes++;
+        }
+        // routed leaf k: every entry before it fails the predicate
+        uint64_t pl;
+        uint32_t mk = quad_leaf<QW>(a, q, K64, k, sub, &pl);
+        probes++;
+        uint64_t L = k;
+        if (!mk) {
+            // rare: a run of entries sharing the routing key continues past leaf k --
+            // exponential, then binary search over leaves for the first leaf holding
+            // an entry >= q (leaf nl = virtual: past every entry)
+            uint64_t lo = k + 1, step = 1, hi = nl;
+            while (lo < nl) {
+                hi = lo + step - 1;
+                if (hi >= nl) { hi = nl; break; }
+                uint64_t pp;
+                probes++;
+                if (quad_leaf<QW>(a, q, K64, hi, sub, &pp)) break;
+                lo = hi + 1;
+                step *= 2;
+                hi = nl;
+            }
+            while (lo < hi) {
+                uint64_t mid = (lo + hi) >> 1;
+                uint64_t pp;
+                probes++;
+                if (quad_leaf<QW>(a, q, K64, mid, sub, &pp)) hi = mid;
+                else lo = mid + 1;
+            }
+            L = lo;
+            if (L < nl) {
+                mk = quad_leaf<QW>(a, q, K64, L, sub, &pl);
+                probes++;
+            }
+        }
+        uint64_t pos = a.next_pos;
+        if (mk) {
+            const uint32_t f = __builtin_ctz(mk);
+            pos = __shfl((unsigned long long)pl, (int)f, QUAD_G);
+        }
+        if (sub == 0) {
+            a.out_pos[i] = pos;
+            if (a.out_probes) a.out_probes[i] = probes;
+        }
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // ------------------------------------------------------------------ host dispatch
 template <int W>
 static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
@@ -435,26 +548,30 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 #define K_LCP(Q) (k_sa_binary<Q, true, false, W>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
+#define K_QUAD(Q) (k_sa_quad<Q>)
     if (algo == SAS_ALGO_PLAIN) {
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
     } else if (algo == SAS_ALGO_STREE) {
         QW_CASE(K_STREE)
-    } else {  // the sector kernel reads positions from its leaves: launched via W = 4 only
+    } else if (algo == SAS_ALGO_SECTOR) {  // sector/quad read positions from their leaves: W = 4 only
         QW_CASE(K_SECTOR)
+    } else {
+        QW_CASE(K_QUAD)
     }
 #undef QW_CASE
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    uint64_t blocks = (a.nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    const uint64_t lanes = a.nq * (algo == SAS_ALGO_QUAD ? QUAD_G : 1);
+    uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     if (blocks == 0) return 0;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
-    if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR) launch_w<5>(algo, top, qw, grid, block, st, a);
+    if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR && algo != SAS_ALGO_QUAD) launch_w<5>(algo, top, qw, grid, block, st, a);
     else launch_w<4>(algo, top, qw, grid, block, st, a);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -489,6 +606,13 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.sec_inner_layers = x->sec_inner_layers;
     a.sec_lds_layers = x->sec_lds_layers;
     a.sec_lds_nodes = x->sec_lds_nodes;
+    a.quad_inner = x->quad_inner;
+    a.quad_leaves = x->quad_leaves;
+    for (int h = 0; h < SAS_QUAD_MAX_LAYERS; h++) a.quad_off[h] = x->quad_off[h];
+    a.quad_leaf_count = x->quad_leaf_count;
+    a.quad_inner_layers = x->quad_inner_layers;
+    a.quad_lds_layers = x->quad_lds_layers;
+    a.quad_lds_nodes = x->quad_lds_nodes;
 }
 
 struct DeviceBuf {
@@ -502,7 +626,8 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_SECTOR) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_QUAD) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo == SAS_ALGO_QUAD && !x->quad_leaves) SAS_FAIL(EINVAL, "search: SAS_ALGO_QUAD needs SAS_BUILD_QUAD");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "search: SAS_ALGO_STREE needs SAS_BUILD_STREE");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "search: SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
     if (nq == 0) return 0;
@@ -598,7 +723,8 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_SECTOR) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_QUAD) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if (algo == SAS_ALGO_QUAD && !x->quad_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no quad tree");
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     SearchArgs a{};

@@ -58,7 +58,7 @@ class SaNaive:
     @classmethod
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
-              sa40: bool = False) -> "SaNaive":
+              sa40: bool = False, quad: bool = True) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
@@ -68,6 +68,7 @@ class SaNaive:
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         flags |= _lib.SAS_BUILD_SA40 if sa40 else 0
+        flags |= _lib.SAS_BUILD_QUAD if quad else 0
         sa_ptr, sa_w = None, 4
         if sa is not None:
             if _is_cuda(t) != _is_cuda(sa):

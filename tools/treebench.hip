@@ -8,6 +8,8 @@
 // non-temporal loads so they do not evict the upper layers from L2 / MALL.
 //
 //   usage: treebench <lookups> <reps> <layout>...   layout = "W:MiB,W:MiB,..." (W in bytes, MiB may be fractional)
+//   W = 1064 / 1128: a 64-B / 128-B node loaded cooperatively by 4 / 8 lanes (16 B each, one
+//   request), the lanes of a group sharing one lookup (ps are then per lookup, not per lane)
 //   e.g.   treebench 10000000 5 32:0.285,32:2.56,32:23.1,32:207,32:1864,32:16384
 //
 // Prints one JSON line per (layout, NT): lookups/s and ns per lookup.
@@ -38,17 +40,22 @@ __device__ __forceinline__ uint64_t mix(uint64_t x) {
     return x;
 }
 
+__device__ __forceinline__ uint64_t node_idx_coop(uint64_t h, uint64_t units) { return ((h >> 32) * units) >> 32; }
+
 template <bool NT>
 __device__ __forceinline__ u32x4 ld(const u32x4* p) {
     if (NT) return __builtin_nontemporal_load(p);
     return *p;
 }
 
+template <int G>
 __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
                                                    uint32_t seed, uint32_t* out) {
     uint32_t acc = 0;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < lookups;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint32_t sub = threadIdx.x % G;  // lane within a cooperative group of G lanes
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < lookups * G;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t i = t / G;
         uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
         uint32_t dep = 0;
         for (int l = 0; l < lay.L; l++) {
@@ -59,6 +66,15 @@ __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p
             const u32x4* v = reinterpret_cast<const u32x4*>(p + lay.base[l] + node * lay.width[l]);
             if (lay.width[l] < 16) {
                 dep = *reinterpret_cast<const uint32_t*>(v);
+                continue;
+            }
+            if (lay.width[l] > 1000) {  // cooperative: 16 B per lane, combine over the group
+                int wb = lay.width[l] - 1000;
+                const u32x4* node = reinterpret_cast<const u32x4*>(p + lay.base[l] + node_idx_coop(h, lay.units[l]) * wb);
+                u32x4 t = node[sub % (wb / 16)];
+                uint32_t d = t.x ^ t.y ^ t.z ^ t.w;
+                for (int o = 1; o < G; o <<= 1) d ^= __shfl_xor(d, o, G);
+                dep = d;
                 continue;
             }
             u32x4 t = lay.nt[l] ? ld<true>(v) : ld<false>(v);
@@ -88,11 +104,12 @@ int main(int argc, char** argv) {
             int w = atoi(tok);
             double mib = atof(strchr(tok, ':') + 1);
             uint64_t bytes = (uint64_t)(mib * 1048576.0);
+            int wb = w > 1000 ? w - 1000 : w;
             L.width[L.L] = w;
-            L.units[L.L] = bytes / w ? bytes / w : 1;
+            L.units[L.L] = bytes / wb ? bytes / wb : 1;
             L.base[L.L] = off;
             L.nt[L.L] = 0;
-            off += ((L.units[L.L] * w + 4095) / 4096) * 4096;
+            off += ((L.units[L.L] * wb + 4095) / 4096) * 4096;
             L.L++;
         }
         if (off > maxbytes) maxbytes = off;
@@ -112,13 +129,20 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&e1));
     dim3 blk(1024), grd(cus * 2);
     for (size_t k = 0; k < lays.size(); k++) {
-        for (int nt = 0; nt < 2; nt++) {
+        for (int nt = 0; nt < 1; nt++) {
             Layout L = lays[k];
-            for (int l = 0; l < L.L; l++) L.nt[l] = nt && (L.units[l] * L.width[l] >= (1ull << 30));
-            hipLaunchKernelGGL(k_chain, grd, blk, 0, 0, p, L, lookups, 1u, out);
+            for (int l = 0; l < L.L; l++) L.nt[l] = nt && L.width[l] < 1000 && (L.units[l] * L.width[l] >= (1ull << 30));
+            int G = 1;
+            for (int l = 0; l < L.L; l++) if (L.width[l] > 1000) G = (L.width[l] - 1000) / 16 > G ? (L.width[l] - 1000) / 16 : G;
+            auto launch = [&](uint32_t sd) {
+                if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out);
+                else if (G == 4) hipLaunchKernelGGL(k_chain<4>, grd, blk, 0, 0, p, L, lookups, sd, out);
+                else hipLaunchKernelGGL(k_chain<1>, grd, blk, 0, 0, p, L, lookups, sd, out);
+            };
+            launch(1u);
             CHECK(hipDeviceSynchronize());
             CHECK(hipEventRecord(e0));
-            for (int r = 0; r < reps; r++) hipLaunchKernelGGL(k_chain, grd, blk, 0, 0, p, L, lookups, 2u + r, out);
+            for (int r = 0; r < reps; r++) launch(2u + r);
             CHECK(hipEventRecord(e1));
             CHECK(hipEventSynchronize(e1));
             float ms;
