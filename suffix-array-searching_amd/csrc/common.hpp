@@ -203,9 +203,10 @@ static __device__ __forceinline__ uint64_t pack_query_word_slow(const uint8_t* _
     // c valid bytes (each block holds at least one valid byte, so it can never
     // touch a page outside the buffer) and realign with v_alignbyte_b32.
     uint32_t c = m - base < 32 ? m - base : 32;
-    uintptr_t addr = (uintptr_t)(q + base);
-    const uint4* p = reinterpret_cast<const uint4*>(addr & ~(uintptr_t)15);
-    uint32_t s = (uint32_t)(addr & 15);
+    // aligned block pointer by pointer arithmetic (an int-to-pointer cast would drop
+    // the global address space and compile to FLAT loads)
+    uint32_t s = (uint32_t)(((uintptr_t)(q + base)) & 15);
+    const uint4* p = reinterpret_cast<const uint4*>(q + base - s);
     const uint4 z = make_uint4(0, 0, 0, 0);
     uint4 b0 = p[0];
     uint4 b1 = (s + c > 16) ? p[1] : z;

@@ -169,12 +169,11 @@ __device__ __forceinline__ uint64_t stree_descend(const SearchArgs& a, const uin
                                                   uint32_t* probes) {
     uint64_t k = 0;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
-    for (uint32_t h = 0; h + 1 < a.stree_height; h++) {
-        const uint4* node = (h < a.stree_lds_layers) ? s_nodes + (a.stree_off[h] + k) * 4
-                                                     : g + (a.stree_off[h] + k) * 4;
-        k = k * (SAS_STREE_B + 1) + cnt_lt_node(node, K);
-        (*probes)++;
-    }
+    uint32_t h = 0;
+    for (; h < a.stree_lds_layers && h + 1 < a.stree_height; h++)
+        k = k * (SAS_STREE_B + 1) + cnt_lt_node(s_nodes + (a.stree_off[h] + k) * 4, K);
+    for (; h + 1 < a.stree_height; h++) k = k * (SAS_STREE_B + 1) + cnt_lt_node(g + (a.stree_off[h] + k) * 4, K);
+    *probes += a.stree_height - 1;
     return k;
 }
 
@@ -321,14 +320,21 @@ __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint
         return UPPER ? sector_gt_prefix<QW>(key, p, K64, Q3, a, q) : sector_ge<QW>(key, p, K64, a, q);
     };
     uint64_t k = 0;
-    for (uint32_t h = 0; h < a.sec_inner_layers; h++) {
-        const uint4* node = (h < a.sec_lds_layers) ? s_nodes + (a.sec_off[h] + k) * 2 : g + (a.sec_off[h] + k) * 2;
-        uint4 v0 = node[0], v1 = node[1];
-        uint32_t c = (v0.x < R16) + (v0.y < R16) + (v0.z < R16) + (v0.w < R16) + (v1.x < R16) + (v1.y < R16) +
-                     (v1.z < R16) + (v1.w < R16);
-        k = k * SAS_SECTOR_FAN + c;
-        (*probes)++;
+    auto count8 = [&](uint4 v0, uint4 v1) -> uint32_t {
+        return (v0.x < R16) + (v0.y < R16) + (v0.z < R16) + (v0.w < R16) + (v1.x < R16) + (v1.y < R16) +
+               (v1.z < R16) + (v1.w < R16);
+    };
+    // LDS layers, then HBM layers (separate loops: ds_read / global_load, not FLAT)
+    uint32_t h = 0;
+    for (; h < a.sec_lds_layers; h++) {
+        const uint4* node = s_nodes + (a.sec_off[h] + k) * 2;
+        k = k * SAS_SECTOR_FAN + count8(node[0], node[1]);
     }
+    for (; h < a.sec_inner_layers; h++) {
+        const uint4* node = g + (a.sec_off[h] + k) * 2;
+        k = k * SAS_SECTOR_FAN + count8(node[0], node[1]);
+    }
+    *probes += a.sec_inner_layers;
     // leaf k: entries 2k, 2k+1 (everything before 2k fails pred)
     uint4 kv = leaves[2 * k], sv = leaves[2 * k + 1];
     (*probes)++;
@@ -436,9 +442,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 // the first entry >= q.  All branches are group-uniform.
 #define QUAD_G 4
 
+// Sum over the 4 lanes of a quad with DPP quad_perm moves (VALU, no LDS crossbar):
+// [1,0,3,2] = lane ^ 1 (0xB1), [2,3,0,1] = lane ^ 2 (0x4E).
 __device__ __forceinline__ uint32_t quad_sum(uint32_t c) {
-    c += __shfl_xor(c, 1, QUAD_G);
-    c += __shfl_xor(c, 2, QUAD_G);
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);
     return c;
 }
 
@@ -479,13 +487,18 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
         const uint32_t R16 = (uint32_t)(K64 >> 32);
         uint32_t probes = 0;
         uint64_t k = 0;
-        for (uint32_t h = 0; h < a.quad_inner_layers; h++) {
-            const uint4* node = ((h < a.quad_lds_layers) ? s_nodes : a.quad_inner) + (a.quad_off[h] + k) * 4;
-            const uint4 v = node[sub];
-            const uint32_t c = quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-            k = k * SAS_QUAD_FAN + c;
-            probes++;
+        // LDS layers, then HBM layers: separate loops keep the loads ds_read / global_load
+        // (a pointer select between the two address spaces compiles to FLAT loads)
+        uint32_t h = 0;
+        for (; h < a.quad_lds_layers; h++) {
+            const uint4 v = s_nodes[(a.quad_off[h] + k) * 4 + sub];
+            k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
         }
+        for (; h < a.quad_inner_layers; h++) {
+            const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
+            k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+        }
+        probes += a.quad_inner_layers;
         // routed leaf k: every entry before it fails the predicate
         uint64_t pl;
         uint32_t mk = quad_leaf<QW>(a, q, K64, k, sub, &pl);

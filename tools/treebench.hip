@@ -88,6 +88,33 @@ __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// Two independent lookups per lane group, their levels interleaved (ILP = 2):
+// cooperative 64-B levels only (W = 1064), G = 4.
+__global__ __launch_bounds__(1024, 8) void k_chain_ilp2(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
+                                                        uint32_t seed, uint32_t* out) {
+    const int G = 4;
+    uint32_t acc = 0;
+    const uint32_t sub = threadIdx.x % G;
+    const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) / G;
+    for (uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; 2 * g < lookups; g += groups) {
+        uint64_t ha = mix((2 * g) * 0x9E3779B97F4A7C15ull + seed), hb = mix((2 * g + 1) * 0x9E3779B97F4A7C15ull + seed);
+        uint32_t da = 0, db = 0;
+        for (int l = 0; l < lay.L; l++) {
+            ha = ha * 0x9E3779B97F4A7C15ull + l + (da & 0x80000000u);
+            hb = hb * 0x9E3779B97F4A7C15ull + l + (db & 0x80000000u);
+            int wb = lay.width[l] - 1000;
+            const u32x4* na = reinterpret_cast<const u32x4*>(p + lay.base[l] + node_idx_coop(ha, lay.units[l]) * wb);
+            const u32x4* nb = reinterpret_cast<const u32x4*>(p + lay.base[l] + node_idx_coop(hb, lay.units[l]) * wb);
+            u32x4 ta = na[sub % (wb / 16)], tb = nb[sub % (wb / 16)];
+            uint32_t xa = ta.x ^ ta.y ^ ta.z ^ ta.w, xb = tb.x ^ tb.y ^ tb.z ^ tb.w;
+            for (int o = 1; o < G; o <<= 1) { xa ^= __shfl_xor(xa, o, G); xb ^= __shfl_xor(xb, o, G); }
+            da = xa; db = xb;
+        }
+        acc ^= da ^ db;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) { fprintf(stderr, "usage: treebench <lookups> <reps> <layout>...\n"); return 2; }
     uint64_t lookups = strtoull(argv[1], 0, 10);
@@ -134,8 +161,10 @@ int main(int argc, char** argv) {
             for (int l = 0; l < L.L; l++) L.nt[l] = nt && L.width[l] < 1000 && (L.units[l] * L.width[l] >= (1ull << 30));
             int G = 1;
             for (int l = 0; l < L.L; l++) if (L.width[l] > 1000) G = (L.width[l] - 1000) / 16 > G ? (L.width[l] - 1000) / 16 : G;
+            bool ilp2 = getenv("TB_ILP2") != nullptr;
             auto launch = [&](uint32_t sd) {
-                if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out);
+                if (ilp2) hipLaunchKernelGGL(k_chain_ilp2, grd, blk, 0, 0, p, L, lookups, sd, out);
+                else if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else if (G == 4) hipLaunchKernelGGL(k_chain<4>, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else hipLaunchKernelGGL(k_chain<1>, grd, blk, 0, 0, p, L, lookups, sd, out);
             };
