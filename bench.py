@@ -95,6 +95,16 @@ def load_traffic(algo: str, n: int, nq: int, m: int):
     return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
 
 
+def host_cpu() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
     """The oracle's restatement of the reference CPU search, timed on this host's
     cores on a bounded sample of the same queries (rank 0, N=1 only)."""
@@ -120,7 +130,14 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
         if best is None or rate > best[0]:
             best = (rate, algo, sample, dt)
     rate, algo, sample, dt = best
+    # one thread on a smaller sample of the same queries (1 thread and all cores)
+    s1 = min(nq, max(1000, int(sample * (seconds / 8) / max(dt * threads, 1e-3))))
+    qb = np.concatenate([qbytes_dev[: s1 * m].cpu().numpy(), np.zeros(64, np.uint8)])
+    t0 = time.perf_counter()
+    O.search_many(t, n, sa, qb, np.arange(s1, dtype=np.uint64) * m, np.full(s1, m, np.uint32), algo, 1)
+    one = s1 / (time.perf_counter() - t0)
     return {"value": rate, "unit": "lookups/s", "cores": threads, "kind": "port",
+            "single_thread_value": one, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
             "sample": f"oracle/{algo} (restates sas/sa_search.rs "
                       f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
                       f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA, {dt:.1f} s, "
@@ -139,7 +156,10 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
     vals = rng.integers(0, O.MAX, nk, dtype=np.uint64).astype(np.uint32)
     vals[0] = O.MAX
     vals.sort()
-    qs = rng.integers(0, O.MAX, nq, dtype=np.uint64).astype(np.uint32)
+    if args.positive:  # gen_positive_queries (sst/util.rs:23-28)
+        qs = vals[rng.integers(0, nk, nq)]
+    else:  # gen_queries (sst/util.rs:16-21)
+        qs = rng.integers(0, O.MAX, nq, dtype=np.uint64).astype(np.uint32)
     dq = torch.from_numpy(qs.view(np.int32)).to(dev)
     dout = torch.empty(nq, dtype=torch.int32, device=dev)
     layouts = {
@@ -163,6 +183,22 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         res[name] = {"lookups_per_s": nq / (kns * 1e-9), "kernel_ms": kns * 1e-6, "layers": idx.layers(),
                      "index_bytes": idx.size(), "agrees": bool(np.array_equal(got, ref))}
         idx.free()
+    # --range mode (sst/bin/bench.rs:84-109): the interleaved [q, q+1] stream through
+    # STree16 left_max; rank(q+1) - rank(q) = number of keys equal to q (checked)
+    rq = np.stack([qs, np.minimum(qs.astype(np.uint64) + 1, O.MAX).astype(np.uint32)], 1).reshape(-1)
+    drq = torch.from_numpy(rq.view(np.int32)).to(dev)
+    drout = torch.empty(2 * nq, dtype=torch.int32, device=dev)
+    st16 = sas_amd.STree16.new_params(vals, True, False, False)
+    for _ in range(args.warmup):
+        st16.query(drq)
+    rkns = st16.time_query(drq, drout, reps=args.steps, stream=torch.cuda.current_stream(dev).cuda_stream)
+    sample = rq[: 2 * min(nq, 100_000)]
+    _, rk = st16.query(sample, want_rank=True)
+    cnt = rk[1::2].astype(np.int64) - rk[0::2].astype(np.int64)
+    expect = np.searchsorted(vals, sample[1::2], "left") - np.searchsorted(vals, sample[0::2], "left")
+    range_res = {"queries": 2 * nq, "lookups_per_s": 2 * nq / (rkns * 1e-9), "kernel_ms": rkns * 1e-6,
+                 "ranges_per_s": nq / (rkns * 1e-9), "counts_verified": bool(np.array_equal(cnt, expect))}
+    st16.free()
     # CPU: the oracle's STree16 (left_max) restatement, 16 threads over contiguous chunks
     import threading
     tree = O.STree(vals, left_max=True)
@@ -187,6 +223,8 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         "data": "synthetic: gen_vals / gen_queries shapes (sst/util.rs:16-42)",
         "config": {"workload": "sst u32 path", "keys": nk, "queries": nq, "best": best},
         "layouts": res,
+        "range_mode": range_res,
+        "queries_kind": "positive" if args.positive else "uniform",
         "cpu_baseline": {"value": sample / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
                          "sample": f"oracle STree16 left_max search (sst/s_tree.rs:196-206) on {sample} queries, "
                                    f"{threads} threads", "agrees": cpu_ok}}), flush=True)
@@ -310,6 +348,7 @@ def main():
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric); c3: largest u32-SA text "
                          "(2^32 - 2^20 chars), 10^8 queries of mixed length 8..256")
+    ap.add_argument("--positive", action="store_true", help="sst workload: queries drawn from the keys")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
@@ -400,6 +439,20 @@ def main():
     el, kernel_ms, ok = run_algo(args.algo, args.steps, args.warmup)
     if not ok:
         raise SystemExit(f"bench: {args.algo} returned a non-occurrence position")
+    # end to end from host buffers: pageable queries H2D, the search, positions
+    # D2H, as a caller handing host memory through the C ABI would see it.  Never `value`.
+    e2e = None
+    if args.mode == "replicated":
+        hq = qbytes.cpu().numpy()
+        best = None
+        for _ in range(2):
+            t0 = time.perf_counter()
+            hpos = idx.search_fixed(hq, m, algo=args.algo)
+            dt = time.perf_counter() - t0
+            best = dt if best is None else min(best, dt)
+        e2e = {"lookups_per_s": nq / best, "ms": best * 1e3,
+               "matches_device_run": bool(np.array_equal(hpos, out.cpu().numpy().astype(np.uint64))),
+               "path": "host query bytes -> sas_search_fixed (staging hipMalloc + H2D, kernel, D2H)"}
     # probes -> tail probes for the algorithmic byte count (untimed pass; a shard of a
     # multi-GPU sharded run only holds part of the SA, so the pass needs the whole index)
     whole = args.mode == "replicated" or ws == 1
@@ -462,6 +515,7 @@ def main():
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes},
             "cpu_baseline": cpu,
+            "e2e_host": e2e,
             "variants": variants,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
                                             "quad_layers", "quad_lds_layers", "top_levels", "iterations",
