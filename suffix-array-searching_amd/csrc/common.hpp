@@ -152,6 +152,23 @@ __device__ __forceinline__ void sa_put(uint8_t* p, uint64_t i, uint64_t v) {
     for (int k = 0; k < 5; k++) b[k] = (uint8_t)(v >> (8 * k));
 }
 
+// ---------------------------------------------------------------- 4-lane (quad) groups
+#define QUAD_G 4
+
+// Sum over the 4 lanes of a quad with DPP quad_perm moves (VALU, no LDS crossbar):
+// [1,0,3,2] = lane ^ 1 (0xB1), [2,3,0,1] = lane ^ 2 (0x4E).
+__device__ __forceinline__ uint32_t quad_sum(uint32_t c) {
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);
+    return c;
+}
+
+// 4-bit mask of the group's lanes with b set (bit j = lane j of the group)
+__device__ __forceinline__ uint32_t quad_mask(bool b) {
+    uint64_t bal = __ballot(b);
+    return (uint32_t)(bal >> (threadIdx.x & 60)) & 0xFu;
+}
+
 // ---------------------------------------------------------------- device helpers
 __device__ __forceinline__ uint64_t chars_mask(uint32_t c) {
     // top 2c bits set, c in [0, 32]

@@ -440,22 +440,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 // 16-char separators, 17-ary; lane j counts its 4, the group sums by shuffles.
 // Leaves: 4 entries {key64, SA}, lane j evaluates entry j, a group ballot picks
 // the first entry >= q.  All branches are group-uniform.
-#define QUAD_G 4
-
-// Sum over the 4 lanes of a quad with DPP quad_perm moves (VALU, no LDS crossbar):
-// [1,0,3,2] = lane ^ 1 (0xB1), [2,3,0,1] = lane ^ 2 (0x4E).
-__device__ __forceinline__ uint32_t quad_sum(uint32_t c) {
-    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);
-    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);
-    return c;
-}
-
-// 4-bit mask of the group's lanes with b set (bit j = lane j of the group)
-__device__ __forceinline__ uint32_t quad_mask(bool b) {
-    uint64_t bal = __ballot(b);
-    return (uint32_t)(bal >> (threadIdx.x & 60)) & 0xFu;
-}
-
 // Evaluate leaf L: mask of its entries x (< sa_n) with suffix(x) >= q; *p = this lane's SA value.
 template <int QW>
 __device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64, uint64_t L,

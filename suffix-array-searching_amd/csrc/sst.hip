@@ -75,6 +75,51 @@ __global__ __launch_bounds__(SST_BLOCK) void k_sst_stree(SstArgs a) {
     }
 }
 
+// Same search, 4 lanes per query: lane j loads keys 4j..4j+3 of each 64-B node,
+// so a node costs one memory request instead of four (treebench);
+// the group sums its counts with DPP.  The answer key is taken from the lane that
+// holds it (no reload of the leaf); only idx == 16 (every key of the leaf < q,
+// STree16) reads the next leaf's first key, as the reference does.
+template <bool TOP>
+__global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_stree4(SstArgs a) {
+    __shared__ uint4 s_nodes[TOP ? SAS_STREE_LDS_NODES * 4 : 1];
+    const uint4* g = reinterpret_cast<const uint4*>(a.nodes);
+    if (TOP) {
+        for (uint32_t h = 0; h < a.lds_layers; h++) {
+            uint32_t cnt = ((h + 1 < a.lds_layers) ? a.lds_off[h + 1] : a.lds_nodes) - a.lds_off[h];
+            for (uint32_t w = threadIdx.x; w < cnt * 4; w += blockDim.x)
+                s_nodes[a.lds_off[h] * 4 + w] = g[a.off[h] * 4 + w];
+        }
+        __syncthreads();
+    }
+    const uint32_t B = a.B, sub = threadIdx.x & (QUAD_G - 1);
+    const uint32_t lds_layers = TOP ? a.lds_layers : 0;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
+        const int32_t q = (int32_t)a.qs[i];
+        auto cnt4 = [&](uint4 v) -> uint32_t {
+            return quad_sum((q > (int32_t)v.x) + (q > (int32_t)v.y) + (q > (int32_t)v.z) + (q > (int32_t)v.w));
+        };
+        uint64_t k = 0;
+        uint32_t h = 0;
+        for (; h < lds_layers && h + 1 < a.height; h++) k = k * (B + 1) + cnt4(s_nodes[(a.lds_off[h] + k) * 4 + sub]);
+        for (; h + 1 < a.height; h++) k = k * (B + 1) + cnt4(g[(a.off[h] + k) * 4 + sub]);
+        const uint64_t o = a.off[a.height - 1];
+        const uint4 v = g[(o + k) * 4 + sub];
+        const uint32_t idx = cnt4(v);
+        // this lane's candidate key for idx % 4, then taken from lane idx / 4 of the group
+        const uint32_t r = idx & 3;
+        uint32_t mine = r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w;
+        const int src = (int)((threadIdx.x & 63) & ~3u) + (int)((idx >> 2) & 3);
+        uint32_t val = (uint32_t)__shfl((int)mine, src, 64);
+        if (sub == 0) {
+            if (idx >= 16) val = a.nodes[(o + k + 1) * 16];
+            a.out[i] = val;
+            if (a.rank) a.rank[i] = k * B + idx;
+        }
+    }
+}
+
 // PartitionedSTree16M::search (sst/partitioned_s_tree.rs:833-877): layer 0 is a
 // flat separator array entered through prefix_map[q >> shift] (a 16-key window
 // read at key granularity); below it the usual 17-ary left-max descent.
@@ -106,6 +151,50 @@ __global__ __launch_bounds__(SST_BLOCK) void k_sst_pmap(SstArgs a) {
             for (int j = 0; j < 16; j++) c += (int32_t)q > (int32_t)l0[j];
             a.out[i] = l0[c];
             if (a.rank) a.rank[i] = key + c;
+        }
+    }
+}
+
+// 4-lane cooperative version: the 16-key window (lane j: keys 4j..4j+3, any
+// alignment) and every 64-B node are one request per group.
+__global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_pmap4(SstArgs a) {
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
+        const int32_t q = (int32_t)a.qs[i];
+        uint32_t p = (uint32_t)q >> a.shift;
+        if (p >= a.parts) p = a.parts - 1;  // q above every key's prefix (UB in the reference)
+        const uint64_t key = a.prefix_map[p];
+        const uint32_t* l0 = a.nodes + a.off[0] * 16 + key + 4 * sub;
+        const uint32_t w0 = l0[0], w1 = l0[1], w2 = l0[2], w3 = l0[3];
+        const uint32_t c0 = quad_sum((q > (int32_t)w0) + (q > (int32_t)w1) + (q > (int32_t)w2) + (q > (int32_t)w3));
+        uint32_t val;
+        uint64_t rank;
+        if (a.height >= 2) {
+            uint64_t k = key + c0;  // node index in layer 1
+            auto cnt4 = [&](uint4 v) -> uint32_t {
+                return quad_sum((q > (int32_t)v.x) + (q > (int32_t)v.y) + (q > (int32_t)v.z) + (q > (int32_t)v.w));
+            };
+            const uint4* g = reinterpret_cast<const uint4*>(a.nodes);
+            for (uint32_t h = 1; h + 1 < a.height; h++) k = k * 17 + cnt4(g[(a.off[h] + k) * 4 + sub]);
+            const uint64_t o = a.off[a.height - 1];
+            const uint4 v = g[(o + k) * 4 + sub];
+            const uint32_t idx = cnt4(v);
+            const uint32_t r = idx & 3;
+            uint32_t mine = r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w;
+            val = (uint32_t)__shfl((int)mine, (int)((threadIdx.x & 63) & ~3u) + (int)((idx >> 2) & 3), 64);
+            if (idx >= 16) val = a.nodes[(o + k + 1) * 16];
+            rank = k * 16 + idx;
+        } else {
+            const uint32_t r = c0 & 3;
+            uint32_t mine = r == 0 ? w0 : r == 1 ? w1 : r == 2 ? w2 : w3;
+            val = (uint32_t)__shfl((int)mine, (int)((threadIdx.x & 63) & ~3u) + (int)((c0 >> 2) & 3), 64);
+            if (c0 >= 16) val = a.nodes[a.off[0] * 16 + key + 16];
+            rank = key + c0;
+        }
+        if (sub == 0) {
+            a.out[i] = val;
+            if (a.rank) a.rank[i] = rank;
         }
     }
 }
@@ -432,12 +521,13 @@ static int sst_launch(const sst_index* x, SstArgs& a, uint32_t flags, hipStream_
         hipLaunchKernelGGL(k_sst_sorted, grid, block, 0, st, a);
     } else if (x->layout == SST_EYTZINGER) {
         hipLaunchKernelGGL(k_sst_eytzinger, grid, block, 0, st, a);
-    } else if (x->layout == SST_PARTITIONED_MAP) {
-        hipLaunchKernelGGL(k_sst_pmap, grid, block, 0, st, a);
-    } else if (flags & SST_NO_LDS_TOP) {
-        hipLaunchKernelGGL(k_sst_stree<false>, grid, block, 0, st, a);
     } else {
-        hipLaunchKernelGGL(k_sst_stree<true>, grid, block, 0, st, a);
+        // S-tree layouts: the 4-lane cooperative kernels (one request per node)
+        uint64_t b4 = (a.nq * QUAD_G + SST_BLOCK - 1) / SST_BLOCK;
+        dim3 grid4((unsigned)(b4 < cap ? b4 : cap));
+        if (x->layout == SST_PARTITIONED_MAP) hipLaunchKernelGGL(k_sst_pmap4, grid4, block, 0, st, a);
+        else if (flags & SST_NO_LDS_TOP) hipLaunchKernelGGL(k_sst_stree4<false>, grid4, block, 0, st, a);
+        else hipLaunchKernelGGL(k_sst_stree4<true>, grid4, block, 0, st, a);
     }
     HIP_TRY(hipGetLastError());
     return 0;
