@@ -141,42 +141,32 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
 }
 
 // ------------------------------------------------------------------ STREE
-__device__ __forceinline__ void cnt_node(const uint4* node, uint32_t K, uint32_t* lt, uint32_t* eq) {
-    uint32_t c = 0, e = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        uint4 v = node[j];
-        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
-        e += (v.x == K) + (v.y == K) + (v.z == K) + (v.w == K);
-    }
-    *lt = c;
-    *eq = e;
+// 4-lane cooperative node reads (one request per 64-B node): lane
+// j holds keys 4j..4j+3, the group sums its counts with DPP.
+__device__ __forceinline__ uint32_t quad_cnt_lt(uint4 v, uint32_t K) {
+    return quad_sum((v.x < K) + (v.y < K) + (v.z < K) + (v.w < K));
 }
-
-__device__ __forceinline__ uint32_t cnt_lt_node(const uint4* node, uint32_t K) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        uint4 v = node[j];
-        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
-    }
-    return c;
+__device__ __forceinline__ uint32_t quad_cnt_eq(uint4 v, uint32_t K) {
+    return quad_sum((v.x == K) + (v.y == K) + (v.z == K) + (v.w == K));
 }
 
 // Descend the internal layers for key K; returns the leaf node index (within
-// the leaf layer).  sst/s_tree.rs:196-203 with unsigned keys.
+// the leaf layer).  sst/s_tree.rs:196-203 with unsigned keys.  LDS layers, then
+// HBM layers (separate loops: ds_read / global_load, not FLAT).
 __device__ __forceinline__ uint64_t stree_descend(const SearchArgs& a, const uint4* s_nodes, uint32_t K,
-                                                  uint32_t* probes) {
+                                                  uint32_t sub) {
     uint64_t k = 0;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
     uint32_t h = 0;
     for (; h < a.stree_lds_layers && h + 1 < a.stree_height; h++)
-        k = k * (SAS_STREE_B + 1) + cnt_lt_node(s_nodes + (a.stree_off[h] + k) * 4, K);
-    for (; h + 1 < a.stree_height; h++) k = k * (SAS_STREE_B + 1) + cnt_lt_node(g + (a.stree_off[h] + k) * 4, K);
-    *probes += a.stree_height - 1;
+        k = k * (SAS_STREE_B + 1) + quad_cnt_lt(s_nodes[(a.stree_off[h] + k) * 4 + sub], K);
+    for (; h + 1 < a.stree_height; h++) k = k * (SAS_STREE_B + 1) + quad_cnt_lt(g[(a.stree_off[h] + k) * 4 + sub], K);
     return k;
 }
 
+// One 4-lane group per query.  The S-tree descent and the leaf scans are
+// cooperative; the exact tail search in [r0, r1] (SA + text reads) runs on all
+// four lanes identically, so its loads coalesce to one request each.
 template <int QW, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
     const SaView<W> sa{a.sa};
@@ -187,24 +177,25 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
         __syncthreads();
     }
     uint32_t bad = 0;
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
     const uint64_t n = a.n;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
     const uint64_t ol = a.stree_off[a.stree_height - 1];
     const uint64_t sa_n = a.sa_n;
     const uint64_t leaf_nodes = (sa_n + 15) / 16;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
         const uint32_t K = (uint32_t)(q.w[0] >> 32);  // padded 16-char key of q
-        uint32_t probes = 0;
+        uint32_t probes = a.stree_height - 1;
 
-        uint64_t k = stree_descend(a, s_nodes, K, &probes);
-        uint32_t c, e;
-        cnt_node(g + (ol + k) * 4, K, &c, &e);
+        uint64_t k = stree_descend(a, s_nodes, K, sub);
+        const uint4 lv = g[(ol + k) * 4 + sub];
+        const uint32_t c = quad_cnt_lt(lv, K), e = quad_cnt_eq(lv, K);
         probes++;
         uint64_t r0 = k * 16 + c;
         uint64_t r1 = r0 + e;
@@ -212,8 +203,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
             uint64_t kk = k + 1;
             int steps = 0;
             for (; kk < leaf_nodes && steps < 4; kk++, steps++) {
-                uint32_t c2, e2;
-                cnt_node(g + (ol + kk) * 4, K, &c2, &e2);
+                const uint32_t e2 = quad_cnt_eq(g[(ol + kk) * 4 + sub], K);
                 probes++;
                 r1 += e2;
                 if (e2 < 16) break;
@@ -222,8 +212,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
                 if (K == SAS_KEY_MAX) {
                     r1 = sa_n;
                 } else {
-                    uint64_t k2 = stree_descend(a, s_nodes, K + 1, &probes);
-                    r1 = k2 * 16 + cnt_lt_node(g + (ol + k2) * 4, K + 1);
+                    uint64_t k2 = stree_descend(a, s_nodes, K + 1, sub);
+                    probes += a.stree_height - 1;
+                    r1 = k2 * 16 + quad_cnt_lt(g[(ol + k2) * 4 + sub], K + 1);
                     probes++;
                 }
             }
@@ -258,8 +249,10 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
         if (l >= sa_n) pos = a.next_pos;
         else if (have) pos = pr;
         else pos = sa[l];
-        a.out_pos[i] = pos;
-        if (a.out_probes) a.out_probes[i] = probes;
+        if (sub == 0) {
+            a.out_pos[i] = pos;
+            if (a.out_probes) a.out_probes[i] = probes;
+        }
     }
     if (bad) atomicOr(a.bad, 1u);
 }
@@ -561,7 +554,7 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    const uint64_t lanes = a.nq * (algo == SAS_ALGO_QUAD ? QUAD_G : 1);
+    const uint64_t lanes = a.nq * ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) ? QUAD_G : 1);
     uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;

@@ -16,7 +16,7 @@ off, _, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=200, le
 src = torch.from_numpy(off.astype(np.int64)).cuda()
 qb = t[(src[:, None] + torch.arange(m, device="cuda")[None, :]).reshape(-1)].contiguous()
 out = torch.empty(nq, dtype=torch.int64, device="cuda")
-kw = dict(sector=algo == "sector", stree=False, lcp=False, quad=algo == "quad")
+kw = dict(sector=algo == "sector", stree=algo == "stree", lcp=False, quad=algo == "quad")
 idx = sas_amd.SaNaive.build(t, **kw)
 for rep in range(3):
     idx.time_fixed(qb, m, nq, out, algo=algo, reps=3)
