@@ -154,7 +154,7 @@ int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, 
  * declared but unimplemented!() in the reference): global SA ranks
  * [out_lo[k], out_hi[k]) of the suffixes that start with query k; the count
  * is out_hi - out_lo and the positions are SA[out_lo .. out_hi)
- * (sas_copy_sa_range).  Needs SAS_BUILD_SECTOR.  Ragged queries as in
+ * (sas_copy_sa_range).  Needs SAS_BUILD_QUAD (used if present) or SAS_BUILD_SECTOR.  Ragged queries as in
  * sas_search_batch. */
 int sas_search_range(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,
                      const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi,

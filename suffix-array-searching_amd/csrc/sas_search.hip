@@ -433,25 +433,119 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 // 16-char separators, 17-ary; lane j counts its 4, the group sums by shuffles.
 // Leaves: 4 entries {key64, SA}, lane j evaluates entry j, a group ballot picks
 // the first entry >= q.  All branches are group-uniform.
-// Evaluate leaf L: mask of its entries x (< sa_n) with suffix(x) >= q; *p = this lane's SA value.
-template <int QW>
-__device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64, uint64_t L,
-                                              uint32_t sub, uint64_t* p) {
+// Evaluate leaf L: mask of its entries x (< sa_n) satisfying the bound's predicate
+// (UPPER = false: suffix(x) >= q; UPPER = true: the first min(m, len) chars of
+// suffix(x) are > q, sector_gt_prefix); *p = this lane's SA value.
+template <int QW, bool UPPER>
+__device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64, uint64_t Q3,
+                                              uint64_t L, uint32_t sub, uint64_t* p) {
     const uint64_t x = 4 * L + sub;
     const uint4 e = a.quad_leaves[x];
     const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
     const uint64_t pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
     *p = pp;
-    return quad_mask(x < a.sa_n && sector_ge<QW>(key, pp, K64, a, q));
+    // short-circuit: padding entries (x >= sa_n) carry SA = all ones and must never
+    // reach the predicate (its m > 32 text compare would read past the text)
+    const bool t = x < a.sa_n &&
+                   (UPPER ? sector_gt_prefix<QW>(key, pp, K64, Q3, a, q) : sector_ge<QW>(key, pp, K64, a, q));
+    return quad_mask(t);
+}
+
+// First local rank with the bound's predicate (monotone over ranks): descent on the
+// 16-char routing key, the routed leaf, then (rare) an exponential + binary search
+// over later leaves for a run of equal routing keys that crosses leaves.  Returns
+// sa_n if no entry qualifies; *px = SA at the returned rank (group-uniform).
+template <int QW, bool UPPER>
+__device__ __forceinline__ uint64_t quad_bound(const SearchArgs& a, const uint4* s_nodes, const QueryRegs<QW>& q,
+                                               uint64_t K64, uint64_t Q3, uint32_t sub, uint32_t* probes,
+                                               uint64_t* px) {
+    const uint32_t R16 = (uint32_t)(((UPPER && q.m <= 32) ? Q3 : K64) >> 32);
+    const uint64_t nl = a.quad_leaf_count;
+    uint64_t k = 0;
+    // LDS layers, then HBM layers: separate loops keep the loads ds_read / global_load
+    // (a pointer select between the two address spaces compiles to FLAT loads)
+    uint32_t h = 0;
+    for (; h < a.quad_lds_layers; h++) {
+        const uint4 v = s_nodes[(a.quad_off[h] + k) * 4 + sub];
+        k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+    }
+    for (; h < a.quad_inner_layers; h++) {
+        const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
+        k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+    }
+    *probes += a.quad_inner_layers + 1;
+    // routed leaf k: every entry before it fails the predicate
+    uint64_t pl;
+    uint32_t mk = quad_leaf<QW, UPPER>(a, q, K64, Q3, k, sub, &pl);
+    uint64_t L = k;
+    if (!mk) {
+        // leaf nl = virtual: past every entry
+        uint64_t lo = k + 1, step = 1, hi = nl;
+        while (lo < nl) {
+            hi = lo + step - 1;
+            if (hi >= nl) { hi = nl; break; }
+            uint64_t pp;
+            (*probes)++;
+            if (quad_leaf<QW, UPPER>(a, q, K64, Q3, hi, sub, &pp)) break;
+            lo = hi + 1;
+            step *= 2;
+            hi = nl;
+        }
+        while (lo < hi) {
+            uint64_t mid = (lo + hi) >> 1;
+            uint64_t pp;
+            (*probes)++;
+            if (quad_leaf<QW, UPPER>(a, q, K64, Q3, mid, sub, &pp)) hi = mid;
+            else lo = mid + 1;
+        }
+        L = lo;
+        if (L < nl) {
+            mk = quad_leaf<QW, UPPER>(a, q, K64, Q3, L, sub, &pl);
+            (*probes)++;
+        }
+    }
+    if (!mk) return a.sa_n;
+    const uint32_t f = __builtin_ctz(mk);
+    *px = __shfl((unsigned long long)pl, (int)(((threadIdx.x & 63) & ~3u) + f), 64);
+    return 4 * L + f;
+}
+
+__device__ __forceinline__ void stage_quad_top(const SearchArgs& a, uint4* s_nodes) {
+    for (uint32_t w = threadIdx.x; w < a.quad_lds_nodes * 4; w += blockDim.x) s_nodes[w] = a.quad_inner[w];
+    __syncthreads();
 }
 
 template <int QW>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
     __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
-    for (uint32_t w = threadIdx.x; w < a.quad_lds_nodes * 4; w += blockDim.x) s_nodes[w] = a.quad_inner[w];
-    __syncthreads();
+    stage_quad_top(a, s_nodes);
     const uint32_t sub = threadIdx.x & (QUAD_G - 1);
-    const uint64_t nl = a.quad_leaf_count;
+    uint32_t bad = 0;
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        uint32_t probes = 0;
+        uint64_t px = 0;
+        const uint64_t x = quad_bound<QW, false>(a, s_nodes, q, q.w[0], 0, sub, &probes, &px);
+        if (sub == 0) {
+            a.out_pos[i] = (x >= a.sa_n) ? a.next_pos : px;
+            if (a.out_probes) a.out_probes[i] = probes;
+        }
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// Occurrence ranges on the quad tree: global ranks [lo, hi) of the suffixes
+// that start with q (out_pos = lo, out_hi = hi), as k_sa_sector_range.
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a, uint64_t* out_hi) {
+    __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
+    stage_quad_top(a, s_nodes);
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
     uint32_t bad = 0;
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
     for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
@@ -461,61 +555,15 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
-        const uint32_t R16 = (uint32_t)(K64 >> 32);
+        const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
         uint32_t probes = 0;
-        uint64_t k = 0;
-        // LDS layers, then HBM layers: separate loops keep the loads ds_read / global_load
-        // (a pointer select between the two address spaces compiles to FLAT loads)
-        uint32_t h = 0;
-        for (; h < a.quad_lds_layers; h++) {
-            const uint4 v = s_nodes[(a.quad_off[h] + k) * 4 + sub];
-            k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-        }
-        for (; h < a.quad_inner_layers; h++) {
-            const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
-            k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-        }
-        probes += a.quad_inner_layers;
-        // routed leaf k: every entry before it fails the predicate
-        uint64_t pl;
-        uint32_t mk = quad_leaf<QW>(a, q, K64, k, sub, &pl);
-        probes++;
-        uint64_t L = k;
-        if (!mk) {
-            // rare: a run of entries sharing the routing key continues past leaf k --
-            // exponential, then binary search over leaves for the first leaf holding
-            // an entry >= q (leaf nl = virtual: past every entry)
-            uint64_t lo = k + 1, step = 1, hi = nl;
-            while (lo < nl) {
-                hi = lo + step - 1;
-                if (hi >= nl) { hi = nl; break; }
-                uint64_t pp;
-                probes++;
-                if (quad_leaf<QW>(a, q, K64, hi, sub, &pp)) break;
-                lo = hi + 1;
-                step *= 2;
-                hi = nl;
-            }
-            while (lo < hi) {
-                uint64_t mid = (lo + hi) >> 1;
-                uint64_t pp;
-                probes++;
-                if (quad_leaf<QW>(a, q, K64, mid, sub, &pp)) hi = mid;
-                else lo = mid + 1;
-            }
-            L = lo;
-            if (L < nl) {
-                mk = quad_leaf<QW>(a, q, K64, L, sub, &pl);
-                probes++;
-            }
-        }
-        uint64_t pos = a.next_pos;
-        if (mk) {
-            const uint32_t f = __builtin_ctz(mk);
-            pos = __shfl((unsigned long long)pl, (int)f, QUAD_G);
-        }
+        uint64_t px = 0;
+        const uint64_t lo = quad_bound<QW, false>(a, s_nodes, q, K64, Q3, sub, &probes, &px);
+        uint64_t hi = quad_bound<QW, true>(a, s_nodes, q, K64, Q3, sub, &probes, &px);
+        if (hi < lo) hi = lo;
         if (sub == 0) {
-            a.out_pos[i] = pos;
+            a.out_pos[i] = a.rank_lo + lo;
+            out_hi[i] = a.rank_lo + hi;
             if (a.out_probes) a.out_probes[i] = probes;
         }
     }
@@ -806,7 +854,9 @@ extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint3
 extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
                                 uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
-    if (!x->sec_leaves) SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_SECTOR");
+    if (!x->sec_leaves && !x->quad_leaves)
+        SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_QUAD or SAS_BUILD_SECTOR");
+    const bool quad = x->quad_leaves != nullptr;
     if (nq == 0) return 0;
     if (!qbytes || !qoff || !qlen || !out_lo || !out_hi) SAS_FAIL(EINVAL, "sas_search_range: null argument");
     HIP_TRY(hipSetDevice(x->device));
@@ -849,15 +899,24 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
         a.out_pos = static_cast<uint64_t*>(blo.p);
         dhi = static_cast<uint64_t*>(bhi.p);
     }
-    uint64_t blocks = (nq + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    uint64_t blocks = (nq * (quad ? QUAD_G : 1) + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    switch (qw) {
-        case 1: hipLaunchKernelGGL(k_sa_sector_range<1>, grid, block, 0, st, a, dhi); break;
-        case 2: hipLaunchKernelGGL(k_sa_sector_range<2>, grid, block, 0, st, a, dhi); break;
-        case 4: hipLaunchKernelGGL(k_sa_sector_range<4>, grid, block, 0, st, a, dhi); break;
-        default: hipLaunchKernelGGL(k_sa_sector_range<8>, grid, block, 0, st, a, dhi); break;
+    if (quad) {
+        switch (qw) {
+            case 1: hipLaunchKernelGGL(k_sa_quad_range<1>, grid, block, 0, st, a, dhi); break;
+            case 2: hipLaunchKernelGGL(k_sa_quad_range<2>, grid, block, 0, st, a, dhi); break;
+            case 4: hipLaunchKernelGGL(k_sa_quad_range<4>, grid, block, 0, st, a, dhi); break;
+            default: hipLaunchKernelGGL(k_sa_quad_range<8>, grid, block, 0, st, a, dhi); break;
+        }
+    } else {
+        switch (qw) {
+            case 1: hipLaunchKernelGGL(k_sa_sector_range<1>, grid, block, 0, st, a, dhi); break;
+            case 2: hipLaunchKernelGGL(k_sa_sector_range<2>, grid, block, 0, st, a, dhi); break;
+            case 4: hipLaunchKernelGGL(k_sa_sector_range<4>, grid, block, 0, st, a, dhi); break;
+            default: hipLaunchKernelGGL(k_sa_sector_range<8>, grid, block, 0, st, a, dhi); break;
+        }
     }
     HIP_TRY(hipGetLastError());
     if (check_bad || !dev) {

@@ -329,6 +329,29 @@ def test_occurrence_ranges(sas, sadef):
     assert sorted(idx.search_prefix(np.zeros(10, np.uint8)).tolist()) == list(range(991))
 
 
+def test_occurrence_ranges_both_trees(sas, sadef):
+    """sas_search_range runs on the quad tree when it is built (k_sa_quad_range) and on
+    the sector tree otherwise (k_sa_sector_range): both give identical ranges, including
+    above-every-suffix, empty and long queries, and a quad-only index searches."""
+    rng = np.random.default_rng(21)
+    cases = [np.array(c["text"], np.uint8) for c in sadef["cases"]]
+    cases += [sas.random_string(300_000, seed=5), np.zeros(20_000, np.uint8),
+              np.tile(rng.integers(0, 4, 5, dtype=np.uint8), 4000)]
+    for t in cases:
+        n = len(t)
+        q_only = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=True)
+        s_only = sas.SaNaive.build(t, lcp=False, stree=False, sector=True, quad=False)
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, max(1, n - 1), 400), rng.integers(0, 300, 400))]
+        qs += [np.full(l, 3, np.uint8) for l in (1, 16, 31, 32, 33, 64, 200)]  # above every suffix
+        qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(0, 70, 200)]
+        buf, off, lens = pack(qs)
+        lq, hq = q_only.search_range(buf, off, lens)
+        ls, hs = s_only.search_range(buf, off, lens)
+        assert np.array_equal(lq, ls) and np.array_equal(hq, hs), n
+        assert np.array_equal(q_only.search_batch(buf, off, lens, algo="quad"),
+                              s_only.search_batch(buf, off, lens, algo="sector")), n
+
+
 def test_kmer_keys_match_reference_loop(sas):
     """sst/bin/bench.rs:58-76 (--human keys), restated as the reference's loop."""
     t = sas.random_string(5000, seed=2)
