@@ -457,3 +457,44 @@ def test_sa_beyond_u32(sas):
                 last = int(idx.suffix_array(count=1, start=occ_hi - 1)[0])
                 assert bytes(ht[last:last + len(q)]) == qb
     assert big > 0  # positions above 2^32 were returned
+
+
+def test_fasta_genome_like_end_to_end(sas, tmp_path):
+    """read_fasta_file (sas/util.rs:144-169) -> GPU SA -> every algorithm vs the oracle,
+    on a genome-shaped FASTA: several records, soft-masked (lowercase) runs, long N
+    stretches (-> code 0, so long runs of equal keys), tandem and interspersed repeats."""
+    rng = np.random.default_rng(17)
+    alpha = np.array(list("ACGT"))
+    unit = "".join(alpha[rng.integers(0, 4, 300)])
+    recs = []
+    for r in range(4):
+        parts = []
+        for _ in range(30):
+            kind = rng.integers(0, 4)
+            if kind == 0:
+                parts.append("".join(alpha[rng.integers(0, 4, rng.integers(500, 3000))]))
+            elif kind == 1:
+                parts.append("N" * int(rng.integers(50, 2000)))
+            elif kind == 2:
+                parts.append(unit * int(rng.integers(1, 6)))
+            else:
+                parts.append("".join(alpha[rng.integers(0, 4, rng.integers(100, 800))]).lower())
+        seq = "".join(parts)
+        recs.append(f">chr{r} synthetic\n" + "\n".join(seq[i:i + 60] for i in range(0, len(seq), 60)))
+    path = tmp_path / "genome.fa"
+    path.write_text("\n".join(recs) + "\n")
+    t = sas.read_fasta_file(str(path))
+    n = len(t)
+    sa_ref = O.build_sa(t)
+    idx = sas.SaNaive.build(t, verify=True)
+    assert np.array_equal(idx.suffix_array(), sa_ref)
+    qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 400, 3000), rng.integers(1, 400, 3000))]
+    qs += [np.zeros(l, np.uint8) for l in (5, 40, 100, 1999, 2500)]  # inside / beyond the N runs
+    buf, off, lens = pack(qs)
+    expect = oracle_positions(t, sa_ref, buf, off, lens)
+    for algo in ALGOS:
+        assert np.array_equal(idx.search_batch(buf, off, lens, algo=algo), expect), algo
+    lo, hi = idx.search_range(buf, off, lens)
+    tp = O.padded(t)
+    for k in range(0, len(qs), 7):
+        assert (lo[k], hi[k]) == O.prefix_range(tp, n, sa_ref, qs[k])
