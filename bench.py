@@ -46,6 +46,9 @@ def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes:
         return sector_layers * 32 + tail_probes * 12 + m + 8
     if algo == "quad":
         return quad_layers * 64 + tail_probes * 64 + m + 8
+    if algo == "inline":  # P probes of one 16-B fused (key, SA) entry
+        P = int(np.log2(n)) + 1
+        return P * 16 + m + 8
     P = int(np.log2(n)) + 1
     return P * (4 + m) + m + 8
 
@@ -239,12 +242,12 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     n = args.n if args.n != 1 << 30 else 1 << 34
     nq = args.nq if args.nq != 10_000_000 else 100_000_000
     fits = n <= (1 << 33)  # sector / quad leaves: 16 B per suffix next to the 40-bit SA
-    main_algo = args.algo if (args.algo not in ("sector", "quad") or fits) else "stree"
+    main_algo = args.algo if (args.algo not in ("sector", "quad", "inline") or fits) else "stree"
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
     # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
     idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
-                                quad=main_algo == "quad", verify=True)
+                                quad=main_algo in ("quad", "inline"), verify=True)
     stats = idx.stats()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
@@ -340,8 +343,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default="quad", choices=["stree", "plain", "lcp", "sector", "quad"])
-    ap.add_argument("--variants", default="plain,lcp,stree,sector,quad",
+    ap.add_argument("--algo", default="quad", choices=["stree", "plain", "lcp", "sector", "quad", "inline"])
+    ap.add_argument("--variants", default="plain,lcp,stree,sector,quad,inline",
                     help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -492,6 +495,8 @@ def main():
                     "lcp": "configs[1] + mlr LCP skipping",
                     "sector": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, sector S-tree (32-B nodes, "
                               "fused 32-char key + SA leaves, top layers LDS-staged)",
+                    "inline": "configs[1] probe sequence (binary_search_batch) over fused 32-char key + SA "
+                              "entries, 2^30 text in HBM, 10^7 len-32 queries",
                     "quad": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, quad S-tree (17-ary 64-B nodes "
                             "loaded by 4-lane groups in one request each, 4-entry fused 32-char key + SA leaves, "
                             "top layers LDS-staged)"}[args.algo]
@@ -510,8 +515,8 @@ def main():
             "roofline": None if not whole else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector",
-                                    "quad": "k_sa_quad"}.get(args.algo, "k_sa_binary"),
+                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad",
+                                    "inline": "k_sa_inline"}.get(args.algo, "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes},
             "cpu_baseline": cpu,

@@ -62,8 +62,11 @@ enum sas_algo {
     SAS_ALGO_STREE = 2, /* S-tree over 16-char SA keys + exact tail search (K2+K3)         */
     SAS_ALGO_SECTOR = 3, /* sector tree: 32-B nodes (one HBM sector), 9-ary on 16-char keys,
                            leaves fuse (32-char key, SA value) pairs: no text/SA reads for m<=32 */
-    SAS_ALGO_QUAD = 4   /* quad tree: 4 lanes per query load each 64-B node in one request;
+    SAS_ALGO_QUAD = 4,  /* quad tree: 4 lanes per query load each 64-B node in one request;
                            17-ary on 16-char keys, leaves = 4 fused (32-char key, SA) entries  */
+    SAS_ALGO_INLINE = 5 /* PLAIN's probe sequence (binary_search_batch) over the quad tree's
+                           fused (32-char key, SA) entries: one 16-B read per probe instead of
+                           an SA word + text words ("inlining values", todo.org:18-19)     */
 };
 
 typedef struct sas_stats {

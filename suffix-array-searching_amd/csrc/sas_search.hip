@@ -570,6 +570,65 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a,
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// ------------------------------------------------------------------ INLINE
+// binary_search_batch<64>'s probes (sas/sa_search.rs:157-196: same mids, same
+// ilog2(n)+1 lockstep iterations, same LDS top as PLAIN) but each probe reads the
+// fused 16-B entry {key64, SA} of the quad leaves: the 32-char key decides unless
+// it equals the query's (then the text from char 32), so a len-32 probe is one
+// memory request instead of an SA word + two text words.
+template <int QW, bool TOP>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
+    __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
+    __shared__ uint64_t s_sa[TOP ? SAS_TOP_NODES : 1];
+    uint32_t D = 0;
+    if (TOP) {
+        D = a.top_levels;
+        for (uint32_t k = threadIdx.x; k < (1u << D); k += blockDim.x) {
+            s_key[k] = a.top_key[k];
+            s_sa[k] = a.top_sa[k];
+        }
+        __syncthreads();
+    }
+    uint32_t bad = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        uint64_t l = 0, r = a.sa_n, pr = 0;
+        uint32_t k = 1, probes = 0;
+        for (uint32_t it = 0; it < a.iters; ++it) {
+            if (l < r) {
+                const uint64_t mid = (l + r) >> 1;
+                uint64_t key, p;
+                if (TOP && it < D) {
+                    key = s_key[k];
+                    p = s_sa[k];
+                } else {
+                    const uint4 e = a.quad_leaves[mid];
+                    key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                    p = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+                }
+                const bool ge = sector_ge<QW>(key, p, K64, a, q);
+                if (TOP && it < D) k = 2 * k + (ge ? 0u : 1u);
+                probes++;
+                if (ge) {
+                    r = mid;
+                    pr = p;
+                } else {
+                    l = mid + 1;
+                }
+            }
+        }
+        a.out_pos[i] = (r >= a.sa_n) ? a.next_pos : pr;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // ------------------------------------------------------------------ host dispatch
 template <int W>
 static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
@@ -587,16 +646,20 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 #define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
 #define K_QUAD(Q) (k_sa_quad<Q>)
+#define K_INLINE_TOP(Q) (k_sa_inline<Q, true>)
+#define K_INLINE(Q) (k_sa_inline<Q, false>)
     if (algo == SAS_ALGO_PLAIN) {
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
     } else if (algo == SAS_ALGO_STREE) {
         QW_CASE(K_STREE)
-    } else if (algo == SAS_ALGO_SECTOR) {  // sector/quad read positions from their leaves: W = 4 only
+    } else if (algo == SAS_ALGO_SECTOR) {  // sector/quad/inline read positions from leaves: W = 4 only
         QW_CASE(K_SECTOR)
-    } else {
+    } else if (algo == SAS_ALGO_QUAD) {
         QW_CASE(K_QUAD)
+    } else {
+        if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
     }
 #undef QW_CASE
 }
@@ -609,7 +672,7 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     if (blocks == 0) return 0;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
-    if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR && algo != SAS_ALGO_QUAD) launch_w<5>(algo, top, qw, grid, block, st, a);
+    if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR && algo != SAS_ALGO_QUAD && algo != SAS_ALGO_INLINE) launch_w<5>(algo, top, qw, grid, block, st, a);
     else launch_w<4>(algo, top, qw, grid, block, st, a);
     HIP_TRY(hipGetLastError());
     return 0;
@@ -664,8 +727,9 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_QUAD) SAS_FAIL(EINVAL, "search: unknown algo");
-    if (algo == SAS_ALGO_QUAD && !x->quad_leaves) SAS_FAIL(EINVAL, "search: SAS_ALGO_QUAD needs SAS_BUILD_QUAD");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_INLINE) SAS_FAIL(EINVAL, "search: unknown algo");
+    if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
+        SAS_FAIL(EINVAL, "search: SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "search: SAS_ALGO_STREE needs SAS_BUILD_STREE");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "search: SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
     if (nq == 0) return 0;
@@ -761,8 +825,9 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_QUAD) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
-    if (algo == SAS_ALGO_QUAD && !x->quad_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no quad tree");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_INLINE) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
+        SAS_FAIL(EINVAL, "sas_time_fixed: index has no quad tree");
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     SearchArgs a{};

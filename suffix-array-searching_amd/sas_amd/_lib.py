@@ -26,7 +26,7 @@ SAS_BUILD_WIDE = 1 << 6
 SAS_BUILD_SECTOR = 1 << 7
 SAS_BUILD_SA40 = 1 << 8
 SAS_BUILD_QUAD = 1 << 9
-ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4}
+ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
 SST_LEFT_MAX = 1 << 0

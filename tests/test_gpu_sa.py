@@ -19,7 +19,7 @@ from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("plain", "lcp", "stree", "sector", "quad")
+ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline")
 
 
 @pytest.fixture(scope="module")
