@@ -257,6 +257,131 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+__device__ __forceinline__ void cnt_node(const uint4* node, uint32_t K, uint32_t* lt, uint32_t* eq) {
+    uint32_t c = 0, e = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint4 v = node[j];
+        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
+        e += (v.x == K) + (v.y == K) + (v.z == K) + (v.w == K);
+    }
+    *lt = c;
+    *eq = e;
+}
+
+__device__ __forceinline__ uint32_t cnt_lt_node(const uint4* node, uint32_t K) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        uint4 v = node[j];
+        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
+    }
+    return c;
+}
+
+// Per-lane S-tree (one lane per query), used for long queries (QW > 1): the exact
+// tail's text compares dominate there, and four redundant lanes would quadruple them.
+// Descend the internal layers for key K; returns the leaf node index (within
+// the leaf layer).  sst/s_tree.rs:196-203 with unsigned keys.
+__device__ __forceinline__ uint64_t stree_descend1(const SearchArgs& a, const uint4* s_nodes, uint32_t K,
+                                                  uint32_t* probes) {
+    uint64_t k = 0;
+    const uint4* g = reinterpret_cast<const uint4*>(a.stree);
+    uint32_t h = 0;
+    for (; h < a.stree_lds_layers && h + 1 < a.stree_height; h++)
+        k = k * (SAS_STREE_B + 1) + cnt_lt_node(s_nodes + (a.stree_off[h] + k) * 4, K);
+    for (; h + 1 < a.stree_height; h++) k = k * (SAS_STREE_B + 1) + cnt_lt_node(g + (a.stree_off[h] + k) * 4, K);
+    *probes += a.stree_height - 1;
+    return k;
+}
+
+template <int QW, int W>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree1(SearchArgs a) {
+    const SaView<W> sa{a.sa};
+    __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
+    {
+        const uint4* g = reinterpret_cast<const uint4*>(a.stree);
+        for (uint32_t w = threadIdx.x; w < a.stree_lds_nodes * 4; w += blockDim.x) s_nodes[w] = g[w];
+        __syncthreads();
+    }
+    uint32_t bad = 0;
+    const uint64_t n = a.n;
+    const uint4* g = reinterpret_cast<const uint4*>(a.stree);
+    const uint64_t ol = a.stree_off[a.stree_height - 1];
+    const uint64_t sa_n = a.sa_n;
+    const uint64_t leaf_nodes = (sa_n + 15) / 16;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint32_t K = (uint32_t)(q.w[0] >> 32);  // padded 16-char key of q
+        uint32_t probes = 0;
+
+        uint64_t k = stree_descend1(a, s_nodes, K, &probes);
+        uint32_t c, e;
+        cnt_node(g + (ol + k) * 4, K, &c, &e);
+        probes++;
+        uint64_t r0 = k * 16 + c;
+        uint64_t r1 = r0 + e;
+        if (c + e == 16) {  // the run of equal keys may continue in the next leaves
+            uint64_t kk = k + 1;
+            int steps = 0;
+            for (; kk < leaf_nodes && steps < 4; kk++, steps++) {
+                uint32_t c2, e2;
+                cnt_node(g + (ol + kk) * 4, K, &c2, &e2);
+                probes++;
+                r1 += e2;
+                if (e2 < 16) break;
+            }
+            if (kk < leaf_nodes && steps == 4) {  // long run: lower_bound(K + 1)
+                if (K == SAS_KEY_MAX) {
+                    r1 = sa_n;
+                } else {
+                    uint64_t k2 = stree_descend1(a, s_nodes, K + 1, &probes);
+                    r1 = k2 * 16 + cnt_lt_node(g + (ol + k2) * 4, K + 1);
+                    probes++;
+                }
+            }
+        }
+        if (r0 > sa_n) r0 = sa_n;
+        if (r1 > sa_n) r1 = sa_n;
+
+        // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
+        const uint32_t h16 = m < 16 ? m : 16;
+        uint64_t l = r0, r = r1;
+        uint32_t llcp = h16, rlcp = h16;
+        sa_val_t<W> pr = 0;
+        bool have = false;
+        while (l < r) {
+            uint64_t mid = (l + r) >> 1;
+            sa_val_t<W> p = (sa_val_t<W>)sa[mid];
+            uint32_t lcp;
+            uint32_t h = llcp < rlcp ? llcp : rlcp;
+            bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
+            probes++;
+            if (lt) {
+                l = mid + 1;
+                llcp = lcp;
+            } else {
+                r = mid;
+                rlcp = lcp;
+                pr = p;
+                have = true;
+            }
+        }
+        uint64_t pos;
+        if (l >= sa_n) pos = a.next_pos;
+        else if (have) pos = pr;
+        else pos = sa[l];
+        a.out_pos[i] = pos;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // ------------------------------------------------------------------ SECTOR
 // Lower bound = first rank x with suffix(x) >= q.  In the sector tree that
 // predicate is read off the fused leaf entry (key = first 32 chars, sa):
@@ -644,6 +769,7 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 #define K_LCP_TOP(Q) (k_sa_binary<Q, true, true, W>)
 #define K_LCP(Q) (k_sa_binary<Q, true, false, W>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
+#define K_STREE1(Q) (k_sa_stree1<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
 #define K_QUAD(Q) (k_sa_quad<Q>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true>)
@@ -653,7 +779,9 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
     } else if (algo == SAS_ALGO_LCP) {
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
     } else if (algo == SAS_ALGO_STREE) {
-        QW_CASE(K_STREE)
+        // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
+        if (qw == 1) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
+        else { QW_CASE(K_STREE1) }
     } else if (algo == SAS_ALGO_SECTOR) {  // sector/quad/inline read positions from leaves: W = 4 only
         QW_CASE(K_SECTOR)
     } else if (algo == SAS_ALGO_QUAD) {
@@ -665,7 +793,8 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    const uint64_t lanes = a.nq * ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) ? QUAD_G : 1);
+    const bool coop = algo == SAS_ALGO_QUAD || (algo == SAS_ALGO_STREE && qw == 1);
+    const uint64_t lanes = a.nq * (coop ? QUAD_G : 1);
     uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
