@@ -288,14 +288,22 @@ __device__ __forceinline__ bool suffix_less_from(const uint64_t* __restrict__ tw
                                                  const QueryRegs<QW>& q, uint32_t h, uint32_t* lcp) {
     uint64_t lenS = n - p;
     uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
-    for (uint32_t off = h; off < L; off += 32) {
-        uint32_t c = L - off < 32 ? L - off : 32;
-        uint64_t mk = chars_mask(c);
-        uint64_t a = text_chars32(tw, p + off) & mk;
-        uint64_t b = q.chars32(off) & mk;
-        if (a != b) {
-            *lcp = off + (uint32_t)(__clzll(a ^ b) >> 1);
-            return a < b;
+    if (h < L) {
+        // consecutive 32-char windows share a text word: carry it, one new load per window
+        uint64_t w = (p + h) >> 5;
+        const uint32_t sh = (uint32_t)((p + h) & 31) << 1;
+        uint64_t lo = tw[w];
+        for (uint32_t off = h; off < L; off += 32) {
+            const uint64_t hi = tw[++w];
+            const uint32_t c = L - off < 32 ? L - off : 32;
+            const uint64_t mk = chars_mask(c);
+            const uint64_t a = (sh ? ((lo << sh) | (hi >> (64 - sh))) : lo) & mk;
+            const uint64_t b = q.chars32(off) & mk;
+            if (a != b) {
+                *lcp = off + (uint32_t)(__clzll(a ^ b) >> 1);
+                return a < b;
+            }
+            lo = hi;
         }
     }
     *lcp = L;

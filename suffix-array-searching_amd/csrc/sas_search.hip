@@ -393,7 +393,8 @@ template <int QW>
 __device__ __forceinline__ bool sector_ge(uint64_t key, uint64_t p, uint64_t K64, const SearchArgs& a,
                                           const QueryRegs<QW>& q) {
     if (key != K64) return key > K64;
-    if (q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
+    // QW == 1 is only dispatched for m <= 32 (qw_for): the text compare is dead code there
+    if (QW == 1 || q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
     uint32_t lcp;
     return !suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
 }
@@ -417,7 +418,7 @@ __device__ __forceinline__ void sector_entry(const uint4* __restrict__ leaves, u
 template <int QW>
 __device__ __forceinline__ bool sector_gt_prefix(uint64_t key, uint64_t p, uint64_t K64, uint64_t Q3,
                                                  const SearchArgs& a, const QueryRegs<QW>& q) {
-    if (q.m <= 32) return key > Q3;
+    if (QW == 1 || q.m <= 32) return key > Q3;
     if (key != K64) return key > K64;
     uint32_t lcp;
     bool lt = suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
