@@ -378,8 +378,9 @@ def main():
     t_build0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)  # sas/util.rs:9-15, identical on every rank
     if args.mode == "shard":
-        from sas_amd.shard import ShardedSearch, shard_range
-        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, rank_range=shard_range(n, ws, rank))
+        from sas_amd.shard import ShardedSearch
+        # each rank builds ONLY its own SA rank range (sas_build_part: no whole-SA step)
+        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True)
         if dist is None:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

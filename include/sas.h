@@ -115,6 +115,17 @@ int sas_free(sas_index* index);
 int sas_build_shard(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
                     uint64_t rank_lo, uint64_t rank_hi, uint32_t flags, sas_index** out);
 
+/* Sharded-text mode without any whole-SA step: part `part` of `parts` builds ONLY
+ * its own SA rank range, so the text size is not capped by one GPU's memory for
+ * a full SA.  Every part takes the same contiguous range of
+ * 7-char-prefix bins from the text's histogram (balanced to bin granularity, so
+ * the range is chosen by the library: sas_get_stats -> rank_lo, sa_entries,
+ * next_pos), ties on 32-char keys are resolved inside the part by text windows.
+ * The SA is stored 40-bit.  ENOTSUP for a text whose repeated prefixes exceed
+ * 2^21 chars (use sas_build_shard), EINVAL for an empty part. */
+int sas_build_part(const uint8_t* text, uint64_t n, uint32_t part, uint32_t parts, uint32_t flags,
+                   sas_index** out);
+
 /* Query routing for the sharded mode: out_shard[k] = number of splitter
  * suffixes (text positions splitter_pos[0..nsplit), in increasing suffix
  * order: the first suffix of shards 1..W-1) that are < query k.  Fixed-length

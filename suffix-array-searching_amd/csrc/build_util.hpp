@@ -44,3 +44,8 @@ struct DevBuf {
 // Declared here, defined in sas_build40.hip: the bucketed builder of a packed
 // 40-bit SA (n up to 2^40 as HBM allows).  sa5: device, 5*n + SAS_SA40_PAD bytes.
 int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* rounds_out, uint64_t* buckets_out);
+// Part builder (sas_build_part): the SA rank range of part `part` of `parts`
+// (contiguous 7-mer bins), packed 40-bit; returns the device buffer, the range and
+// SA[rank_hi] (n if none).
+int build_sa_part40(const uint64_t* tw, uint64_t n, uint32_t part, uint32_t parts, uint8_t** sa5_out,
+                    uint64_t* rank_lo, uint64_t* count, uint64_t* next_pos, uint32_t* rounds_out);

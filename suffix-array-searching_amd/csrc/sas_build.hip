@@ -822,13 +822,13 @@ static int load_sa(const void* src, uint64_t n, int wi, bool dev, uint8_t* dst, 
 // Common builder.  [rank_lo, rank_hi) = the SA ranks this index holds
 // (the whole SA for sas_build, a shard's range for sas_build_shard).
 static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
-                      uint64_t rank_lo, uint64_t rank_hi, sas_index** out) {
+                      uint64_t rank_lo, uint64_t rank_hi, sas_index** out, uint32_t part = 0, uint32_t parts = 0) {
     if (!out) SAS_FAIL(EINVAL, "sas_build: null out");
     *out = nullptr;
     if (n == 0) SAS_FAIL(EINVAL, "sas_build: empty text");
     if (!text) SAS_FAIL(EINVAL, "sas_build: null text");
     if (n >= SAS_SA40_MAX - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^40 - 64");
-    const bool w5 = (flags & SAS_BUILD_SA40) || n >= (1ull << 32) - 64;
+    const bool w5 = (flags & SAS_BUILD_SA40) || n >= (1ull << 32) - 64 || parts > 0;
     const uint32_t W = w5 ? 5 : 4;
     if (sa_or_null && sa_width != 4 && sa_width != 5 && sa_width != 8)
         SAS_FAIL(EINVAL, "sas_build: sa_width must be 4 (u32), 5 (packed 40-bit) or 8 (u64)");
@@ -868,6 +868,19 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     x->text_w = tw.as<uint64_t>();
     tw.release();
 
+    if (parts > 0) {
+        // part mode: only this part's SA rank range is ever built (sas_build40.hip)
+        uint64_t s0 = now_ns(), lo = 0, cnt = 0, np = 0;
+        uint8_t* local = nullptr;
+        TRY(build_sa_part40(x->text_w, n, part, parts, &local, &lo, &cnt, &np, &x->stats.sa_rounds));
+        x->sa = local;
+        x->rank_lo = lo;
+        x->sa_n = cnt;
+        x->next_pos = np;
+        HIP_TRY(hipDeviceSynchronize());
+        x->stats.build_sa_ns = now_ns() - s0;
+        if (flags & SAS_BUILD_VERIFY) TRY(verify_sa(x->text_w, n, x->sa, W, x->sa_n, false));
+    } else {
     // global suffix array (caller's or built here), then this index's rank range
     DevBuf sa;
     const uint64_t sa_bytes_full = n * W + (W == 5 ? SAS_SA40_PAD : 0);
@@ -907,7 +920,9 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         sa.alloc(0, "free");
         x->sa = static_cast<uint8_t*>(part.release());
     }
+    }  // part mode
     const uint64_t sa_n = x->sa_n;
+    rank_lo = x->rank_lo;
 
     if (flags & SAS_BUILD_LCP) {
         DevBuf l;
@@ -981,6 +996,12 @@ extern "C" int sas_build(const uint8_t* text, uint64_t n, const void* sa_or_null
 extern "C" int sas_build_shard(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width,
                                uint64_t rank_lo, uint64_t rank_hi, uint32_t flags, sas_index** out) {
     return build_impl(text, n, sa_or_null, sa_width, flags, rank_lo, rank_hi, out);
+}
+
+extern "C" int sas_build_part(const uint8_t* text, uint64_t n, uint32_t part, uint32_t parts, uint32_t flags,
+                              sas_index** out) {
+    if (parts == 0 || part >= parts) SAS_FAIL(EINVAL, "sas_build_part: need part < parts");
+    return build_impl(text, n, nullptr, 5, flags, 0, n, out, part, parts);
 }
 
 extern "C" int sas_get_stats(const sas_index* index, sas_stats* out) {

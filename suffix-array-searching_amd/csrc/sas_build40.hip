@@ -133,7 +133,7 @@ __global__ void k_b_emit(const uint64_t* __restrict__ keys, const uint64_t* __re
     GRID_STRIDE(j, c) {
         uint64_t p = vals[j];
         sa_put<5>(sa5, off + j, p);
-        sa_put<5>(rank5, p, group[j]);
+        if (rank5) sa_put<5>(rank5, p, group[j]);
         bool h0 = (j == 0) || keys[j] != keys[j - 1];
         bool h1 = (j + 1 == c) || keys[j + 1] != keys[j];
         tied[j] = !(h0 && h1);
@@ -365,5 +365,326 @@ int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* round
     }
     HIP_TRY(hipStreamSynchronize(st));
     *rounds_out = rounds;
+    return 0;
+}
+
+// ======================================================================
+// Part builder (sharded text): part g of P builds ONLY its own SA
+// rank range.  Every part computes the same histogram from the full text and
+// takes the contiguous bins [B_g, B_{g+1}) whose cumulative counts straddle
+// g*n/P, so its suffixes are exactly the global ranks [cum(B_g), cum(B_{g+1})).
+// Suffixes that tie on their 32-char key share a bin, hence a part, so ties are
+// resolved locally, by text windows instead of the global rank array: round w
+// stably sorts each tied group by the next 32 chars (zero padded) and then by
+// how many of them exist (a proper prefix sorts first, Rust slice order).
+// Rounds = longest tied prefix / 32, capped (ENOTSUP past the cap: such a text
+// needs the whole-SA builder, sas_build_shard).
+// ======================================================================
+#define PART_MAX_ROUNDS (1u << 16)
+
+// Window of the tied element k at offset o: key = chars [p+o, p+o+32) (zero
+// padded), len = min(n - p, o + 32).  Group members agree on their first o chars
+// (zero padded), so ordering by (key, len) is slice order: equal keys with a
+// shorter length mean a proper prefix (the padding zeros stand for real zeros in
+// the longer suffix); equal keys and len = o + 32 stay tied for the next window.
+__global__ void k_w_keys(const uint64_t* __restrict__ list, uint64_t cnt, SaView<5> sa, const uint64_t* tw,
+                         uint64_t n, uint64_t o, uint64_t* __restrict__ pos, uint64_t* __restrict__ key,
+                         uint64_t* __restrict__ lc, uint64_t* __restrict__ perm) {
+    GRID_STRIDE(k, cnt) {
+        uint64_t p = sa[list[k]];
+        pos[k] = p;
+        key[k] = (p + o < n) ? text_chars32(tw, p + o) : 0ull;
+        const uint64_t len = n - p;
+        lc[k] = len < o + 32 ? len : o + 32;
+        perm[k] = k;
+    }
+}
+
+__global__ void k_gather64(const uint64_t* __restrict__ src, const uint64_t* __restrict__ perm, uint64_t cnt,
+                           uint64_t* __restrict__ dst) {
+    GRID_STRIDE(k, cnt) dst[k] = src[perm[k]];
+}
+
+__global__ void k_w_heads(const uint64_t* __restrict__ perm, uint64_t cnt, const uint64_t* __restrict__ grp,
+                          const uint64_t* __restrict__ key, const uint64_t* __restrict__ lc,
+                          const uint64_t* __restrict__ list, uint64_t* __restrict__ headpos,
+                          uint8_t* __restrict__ head) {
+    GRID_STRIDE(k, cnt) {
+        bool hd = true;
+        if (k > 0) {
+            uint64_t a = perm[k], b = perm[k - 1];
+            hd = grp[a] != grp[b] || key[a] != key[b] || lc[a] != lc[b];
+        }
+        head[k] = hd;
+        headpos[k] = hd ? list[k] : 0ull;
+    }
+}
+
+__global__ void k_w_scatter(const uint64_t* __restrict__ list, const uint64_t* __restrict__ perm,
+                            const uint64_t* __restrict__ pos, uint64_t cnt, const uint8_t* __restrict__ head,
+                            uint8_t* __restrict__ sa5, uint8_t* __restrict__ unresolved) {
+    GRID_STRIDE(k, cnt) {
+        sa_put<5>(sa5, list[k], pos[perm[k]]);
+        bool h1 = (k + 1 == cnt) || head[k + 1];
+        unresolved[k] = !(head[k] && h1);
+    }
+}
+
+// Resolve tied groups in place.  list: ascending SA slots of the tied entries,
+// grp: their group ids (slot of the group's first entry), both device, cnt entries;
+// sa5: the (local) SA whose slots they index.  Consumes list / grp.
+static int resolve_ties_windows(const uint64_t* tw, uint64_t n, uint8_t* sa5, DevBuf& list, DevBuf& grp, uint64_t cnt,
+                                uint32_t* rounds_out) {
+    hipStream_t st = 0;
+    uint32_t rounds = 0;
+    if (cnt == 0) {
+        *rounds_out = 0;
+        return 0;
+    }
+    DevBuf pos, key, lc, perm, perm2, kbuf, kbuf2, hp, hd, uf, list2, grp2, tmp, cnt_d;
+    TRY(pos.alloc(cnt * 8, "tie positions"));
+    TRY(key.alloc(cnt * 8, "tie window keys"));
+    TRY(lc.alloc(cnt * 8, "tie window lengths"));
+    TRY(perm.alloc(cnt * 8, "tie order"));
+    TRY(perm2.alloc(cnt * 8, "tie order alt"));
+    TRY(kbuf.alloc(cnt * 8, "tie sort keys"));
+    TRY(kbuf2.alloc(cnt * 8, "tie sort keys alt"));
+    TRY(hp.alloc(cnt * 8, "tie groups"));
+    TRY(hd.alloc(cnt, "tie heads"));
+    TRY(uf.alloc(cnt, "tie flags"));
+    TRY(list2.alloc(cnt * 8, "tie list alt"));
+    TRY(grp2.alloc(cnt * 8, "tie group alt"));
+    TRY(cnt_d.alloc(16, "counter"));
+    size_t tmp_have = 0;
+    SaView<5> sav{sa5};
+    uint64_t* L = list.as<uint64_t>();
+    uint64_t* G = grp.as<uint64_t>();
+    uint64_t* Ln = list2.as<uint64_t>();
+    uint64_t* Gn = grp2.as<uint64_t>();
+    for (uint64_t o = 32; cnt > 0; o += 32) {
+        if (++rounds > PART_MAX_ROUNDS)
+            SAS_FAIL(ENOTSUP, "sas_build_part: suffixes share prefixes longer than " +
+                                  std::to_string(32ull * PART_MAX_ROUNDS) + " chars; use sas_build_shard");
+        hipLaunchKernelGGL(k_w_keys, dim3(grid_for(cnt)), dim3(256), 0, st, L, cnt, sav, tw, n, o, pos.as<uint64_t>(),
+                           key.as<uint64_t>(), lc.as<uint64_t>(), perm.as<uint64_t>());
+        // stable LSD: window length, then window key, then group (outermost)
+        const uint64_t* srcs[3] = {lc.as<uint64_t>(), key.as<uint64_t>(), G};
+        const int bits[3] = {41, 64, 40};
+        uint64_t* pa = perm.as<uint64_t>();
+        uint64_t* pb = perm2.as<uint64_t>();
+        for (int pass = 0; pass < 3; pass++) {
+            hipLaunchKernelGGL(k_gather64, dim3(grid_for(cnt)), dim3(256), 0, st, srcs[pass], pa, cnt,
+                               kbuf.as<uint64_t>());
+            rocprim::double_buffer<uint64_t> kd(kbuf.as<uint64_t>(), kbuf2.as<uint64_t>());
+            rocprim::double_buffer<uint64_t> vd(pa, pb);
+            const int nb = bits[pass];
+            TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+                return rocprim::radix_sort_pairs(t, sz, kd, vd, (size_t)cnt, 0, nb, st);
+            }));
+            if (vd.current() != pa) { uint64_t* t = pa; pa = pb; pb = t; }
+        }
+        hipLaunchKernelGGL(k_w_heads, dim3(grid_for(cnt)), dim3(256), 0, st, pa, cnt, G, key.as<uint64_t>(),
+                           lc.as<uint64_t>(), L, hp.as<uint64_t>(), hd.as<uint8_t>());
+        hipLaunchKernelGGL(k_w_scatter, dim3(grid_for(cnt)), dim3(256), 0, st, L, pa, pos.as<uint64_t>(), cnt,
+                           hd.as<uint8_t>(), sa5, uf.as<uint8_t>());
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::inclusive_scan(t, sz, hp.as<uint64_t>(), hp.as<uint64_t>(), (size_t)cnt, MaxOp64(), st);
+        }));
+        HIP_TRY(hipGetLastError());
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::select(t, sz, hp.as<uint64_t>(), uf.as<uint8_t>(), Gn, cnt_d.as<uint64_t>(), (size_t)cnt, st);
+        }));
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::select(t, sz, L, uf.as<uint8_t>(), Ln, cnt_d.as<uint64_t>(), (size_t)cnt, st);
+        }));
+        HIP_TRY(hipMemcpy(&cnt, cnt_d.p, 8, hipMemcpyDeviceToHost));
+        uint64_t* t1 = L; L = Ln; Ln = t1;
+        uint64_t* t2 = G; G = Gn; Gn = t2;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    *rounds_out = rounds;
+    return 0;
+}
+
+static int histogram(const uint64_t* tw, uint64_t n, std::vector<uint64_t>& h) {
+    DevBuf hist;
+    TRY(hist.alloc(HIST_BINS * 8, "histogram"));
+    HIP_TRY(hipMemset(hist.p, 0, HIST_BINS * 8));
+    unsigned g = grid_for(n, 1024);
+    hipLaunchKernelGGL(k_hist, dim3(g < 1024 ? g : 1024), dim3(1024), 0, 0, tw, n, hist.as<unsigned long long>());
+    HIP_TRY(hipGetLastError());
+    h.assign(HIST_BINS, 0);
+    HIP_TRY(hipMemcpy(h.data(), hist.p, HIST_BINS * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
+
+// Tied entries collected while sorting buckets: ascending SA slots + group ids.
+struct TiedSink {
+    DevBuf list, grp;
+    uint64_t cap = 0, cnt = 0;
+};
+
+static int append_dev(DevBuf& dst, uint64_t& cap, uint64_t have, const uint64_t* src, uint64_t d, const char* what) {
+    if (have + d > cap) {
+        uint64_t nc = cap ? cap : 1024;
+        while (nc < have + d) nc *= 2;
+        DevBuf grown;
+        TRY(grown.alloc(nc * 8, what));
+        if (have) HIP_TRY(hipMemcpy(grown.p, dst.p, have * 8, hipMemcpyDeviceToDevice));
+        dst.alloc(0, "free");
+        dst.p = grown.release();
+        cap = nc;
+    }
+    if (d) HIP_TRY(hipMemcpy(dst.as<uint64_t>() + have, src, d * 8, hipMemcpyDeviceToDevice));
+    return 0;
+}
+
+// Sorted (key, position) pairs of the suffixes in bins [lo, hi) -> SA slots
+// off0.. of sa5; entries whose 32-char key repeats go to `ties`.
+static int sort_bins_into(const uint64_t* tw, uint64_t n, const std::vector<uint64_t>& h, uint32_t lo, uint32_t hi,
+                          uint64_t cap, uint8_t* sa5, uint64_t off0, TiedSink& ties) {
+    hipStream_t st = 0;
+    uint64_t bucket_max = 0, acc = 0;
+    std::vector<uint32_t> edges{lo};
+    for (uint32_t b = lo; b < hi; b++) {
+        if (acc + h[b] > cap && acc) {
+            edges.push_back(b);
+            bucket_max = acc > bucket_max ? acc : bucket_max;
+            acc = 0;
+        }
+        acc += h[b];
+    }
+    edges.push_back(hi);
+    bucket_max = acc > bucket_max ? acc : bucket_max;
+    if (bucket_max == 0) return 0;
+    DevBuf ka, kb, va, vb, grp, flg, bcnt, cnt_d, tmp;
+    size_t tmp_have = 0;
+    TRY(ka.alloc(bucket_max * 8, "bucket keys"));
+    TRY(kb.alloc(bucket_max * 8, "bucket keys alt"));
+    TRY(va.alloc(bucket_max * 8, "bucket positions"));
+    TRY(vb.alloc(bucket_max * 8, "bucket positions alt"));
+    TRY(grp.alloc(bucket_max * 8, "bucket groups"));
+    TRY(flg.alloc(bucket_max, "bucket tied flags"));
+    const uint64_t nblk = (n + COLLECT_CHUNK - 1) / COLLECT_CHUNK;
+    TRY(bcnt.alloc(nblk * 8, "block counts"));
+    TRY(cnt_d.alloc(16, "counter"));
+    uint64_t off = off0;
+    for (size_t b = 0; b + 1 < edges.size(); b++) {
+        uint32_t blo = edges[b], bhi = edges[b + 1];
+        uint64_t c = 0;
+        for (uint32_t i = blo; i < bhi; i++) c += h[i];
+        if (c == 0) continue;
+        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
+                           bcnt.as<uint64_t>());
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::exclusive_scan(t, sz, bcnt.as<uint64_t>(), bcnt.as<uint64_t>(), (uint64_t)0,
+                                           (size_t)nblk, rocprim::plus<uint64_t>(), st);
+        }));
+        hipLaunchKernelGGL(k_bucket_collect, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
+                           bcnt.as<uint64_t>(), ka.as<uint64_t>(), va.as<uint64_t>());
+        rocprim::double_buffer<uint64_t> kdb(ka.as<uint64_t>(), kb.as<uint64_t>());
+        rocprim::double_buffer<uint64_t> vdb(va.as<uint64_t>(), vb.as<uint64_t>());
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::radix_sort_pairs(t, sz, kdb, vdb, (size_t)c, 0, 64, st);
+        }));
+        const uint64_t* sk = kdb.current();
+        const uint64_t* sv = vdb.current();
+        uint64_t* free_k = (sk == ka.as<uint64_t>()) ? kb.as<uint64_t>() : ka.as<uint64_t>();
+        uint64_t* free_v = (sv == va.as<uint64_t>()) ? vb.as<uint64_t>() : va.as<uint64_t>();
+        hipLaunchKernelGGL(k_b_heads, dim3(grid_for(c)), dim3(256), 0, st, sk, c, off, grp.as<uint64_t>());
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::inclusive_scan(t, sz, grp.as<uint64_t>(), grp.as<uint64_t>(), (size_t)c, MaxOp64(), st);
+        }));
+        hipLaunchKernelGGL(k_b_emit, dim3(grid_for(c)), dim3(256), 0, st, sk, sv, grp.as<uint64_t>(), c, off, sa5,
+                           (uint8_t*)nullptr, flg.as<uint8_t>());
+        HIP_TRY(hipGetLastError());
+        rocprim::counting_iterator<uint64_t> cit(off);
+        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+            return rocprim::select(t, sz, cit, flg.as<uint8_t>(), free_k, cnt_d.as<uint64_t>(), (size_t)c, st);
+        }));
+        uint64_t d = 0;
+        HIP_TRY(hipMemcpy(&d, cnt_d.p, 8, hipMemcpyDeviceToHost));
+        if (d) {
+            TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+                return rocprim::select(t, sz, grp.as<uint64_t>(), flg.as<uint8_t>(), free_v, cnt_d.as<uint64_t>(),
+                                       (size_t)c, st);
+            }));
+            uint64_t cap_l = ties.cap, cap_g = ties.cap;
+            TRY(append_dev(ties.list, cap_l, ties.cnt, free_k, d, "tied list"));
+            TRY(append_dev(ties.grp, cap_g, ties.cnt, free_v, d, "tied groups"));
+            ties.cap = cap_l;
+            ties.cnt += d;
+        }
+        off += c;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return 0;
+}
+
+// The smallest suffix among those whose bin is >= b_from (the first suffix of the
+// next part): its bin is the first non-empty one; sort that bin and resolve the
+// ties of its first key group.
+static int min_suffix_from(const uint64_t* tw, uint64_t n, const std::vector<uint64_t>& h, uint32_t b_from,
+                           uint64_t cap, uint64_t* out) {
+    uint32_t b = b_from;
+    while (b < HIST_BINS && h[b] == 0) b++;
+    if (b >= HIST_BINS) {
+        *out = n;
+        return 0;
+    }
+    const uint64_t c = h[b];
+    DevBuf sa;
+    TRY(sa.alloc(c * 5 + SAS_SA40_PAD, "next-part bin SA"));
+    HIP_TRY(hipMemset(sa.p, 0, c * 5 + SAS_SA40_PAD));
+    TiedSink ties;
+    TRY(sort_bins_into(tw, n, h, b, b + 1, cap, sa.as<uint8_t>(), 0, ties));
+    uint32_t r = 0;
+    TRY(resolve_ties_windows(tw, n, sa.as<uint8_t>(), ties.list, ties.grp, ties.cnt, &r));
+    uint8_t bytes[8] = {};
+    HIP_TRY(hipMemcpy(bytes, sa.p, 5, hipMemcpyDeviceToHost));
+    uint64_t v = 0;
+    for (int k = 0; k < 5; k++) v |= (uint64_t)bytes[k] << (8 * k);
+    *out = v;
+    return 0;
+}
+
+int build_sa_part40(const uint64_t* tw, uint64_t n, uint32_t part, uint32_t parts, uint8_t** sa5_out,
+                    uint64_t* rank_lo, uint64_t* count, uint64_t* next_pos, uint32_t* rounds_out) {
+    std::vector<uint64_t> h;
+    TRY(histogram(tw, n, h));
+    // part boundaries: B_g = first bin whose preceding count reaches g*n/P
+    std::vector<uint64_t> cum(HIST_BINS + 1, 0);
+    for (uint32_t b = 0; b < HIST_BINS; b++) cum[b + 1] = cum[b] + h[b];
+    auto bound = [&](uint32_t g) -> uint32_t {
+        if (g == 0) return 0;
+        if (g >= parts) return HIST_BINS;
+        const uint64_t target = (uint64_t)(((unsigned __int128)n * g) / parts);
+        uint32_t b = 0;
+        while (b < HIST_BINS && cum[b] < target) b++;
+        return b;
+    };
+    const uint32_t lo = bound(part), hi = bound(part + 1);
+    *rank_lo = cum[lo];
+    *count = cum[hi] - cum[lo];
+    if (*count == 0)
+        SAS_FAIL(EINVAL, "sas_build_part: part " + std::to_string(part) + " of " + std::to_string(parts) +
+                             " holds no suffixes (too many parts for this text)");
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    uint64_t cap = (uint64_t)(free_b * 0.45) / 42;
+    uint64_t maxbin = 0;
+    for (uint32_t b = lo; b < hi; b++) maxbin = h[b] > maxbin ? h[b] : maxbin;
+    if (cap > (1ull << 31)) cap = 1ull << 31;
+    if (maxbin > cap)
+        SAS_FAIL(ENOTSUP, "sas_build_part: " + std::to_string(maxbin) + " suffixes share one 7-char prefix");
+    if (cap < maxbin) cap = maxbin;
+    DevBuf sa;
+    TRY(sa.alloc(*count * 5 + SAS_SA40_PAD, "suffix array part"));
+    HIP_TRY(hipMemset(sa.p, 0, *count * 5 + SAS_SA40_PAD));
+    TiedSink ties;
+    TRY(sort_bins_into(tw, n, h, lo, hi, cap, sa.as<uint8_t>(), 0, ties));
+    TRY(resolve_ties_windows(tw, n, sa.as<uint8_t>(), ties.list, ties.grp, ties.cnt, rounds_out));
+    TRY(min_suffix_from(tw, n, h, hi, cap, next_pos));
+    *sa5_out = static_cast<uint8_t*>(sa.release());
     return 0;
 }

@@ -90,6 +90,23 @@ class SaNaive:
                                         C.byref(h)))
         return cls(h, n)
 
+    @classmethod
+    def build_part(cls, t, part: int, parts: int, lcp: bool = True, stree: bool = True, verify: bool = False,
+                   flags: int = 0, sector: bool = True, quad: bool = True) -> "SaNaive":
+        """Sharded-text index that builds ONLY its own SA rank range (sas_build_part):
+        part `part` of `parts` contiguous 7-char-prefix bin ranges.  The range is
+        chosen by the library (stats: rank_lo, sa_entries, next_pos)."""
+        t = _as_u8(t)
+        n = int(t.numel() if _is_cuda(t) else len(t))
+        flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
+        flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
+        flags |= _lib.SAS_BUILD_QUAD if quad else 0
+        if _is_cuda(t):
+            flags |= _lib.SAS_DEVICE_PTRS
+        h = C.c_void_p()
+        check(lib().sas_build_part(_ptr(t), n, int(part), int(parts), flags, C.byref(h)))
+        return cls(h, n)
+
     def free(self):
         if self._h:
             lib().sas_free(self._h)

@@ -498,3 +498,71 @@ def test_fasta_genome_like_end_to_end(sas, tmp_path):
     tp = O.padded(t)
     for k in range(0, len(qs), 7):
         assert (lo[k], hi[k]) == O.prefix_range(tp, n, sa_ref, qs[k])
+
+
+@pytest.mark.parametrize("parts", [1, 2, 3, 5])
+def test_part_builds_concatenate_to_full_sa(sas, parts):
+    """sas_build_part: each part builds only its own SA rank range (no whole-SA
+    step).  The parts' SAs concatenate to the oracle's SA, the ranges are
+    contiguous, next_pos = SA[rank_hi], and routed lookups on the parts equal the
+    whole index on mixed queries (sharded-text mode)."""
+    rng = np.random.default_rng(parts)
+    blk = rng.integers(0, 4, 700, dtype=np.uint8)
+    texts = [sas.random_string(1_000_003, seed=9),
+             np.concatenate([blk, rng.integers(0, 4, 5000, dtype=np.uint8), blk, blk,
+                             rng.integers(0, 4, 3000, dtype=np.uint8), np.zeros(900, np.uint8), blk]),
+             np.tile(rng.integers(0, 4, 7, dtype=np.uint8), 3000)]
+    if parts == 1:
+        texts.append(np.zeros(5000, np.uint8))
+    for t in texts:
+        n = len(t)
+        sa_ref = O.build_sa(t)
+        idxs = [sas.SaNaive.build_part(t, g, parts, verify=True) for g in range(parts)]
+        st = [ix.stats() for ix in idxs]
+        assert st[0]["rank_lo"] == 0 and sum(s["sa_entries"] for s in st) == n
+        for g in range(parts):
+            lo, cnt = st[g]["rank_lo"], st[g]["sa_entries"]
+            assert st[g]["sa_width"] == 5
+            if g + 1 < parts:
+                assert st[g + 1]["rank_lo"] == lo + cnt
+            assert np.array_equal(idxs[g].suffix_array(), sa_ref[lo:lo + cnt].astype(np.uint64)), (n, g)
+            assert st[g]["next_pos"] == (sa_ref[lo + cnt] if lo + cnt < n else n)
+        full = sas.SaNaive.build(t)
+        m = 24
+        offs = rng.integers(0, n - m, 3000)
+        qb = np.concatenate([t[o:o + m] for o in offs] + [rng.integers(0, 4, 1000 * m, dtype=np.uint8)])
+        nq = len(qb) // m
+        expect = full.search_fixed(qb, m, algo="plain")
+        splitters = np.array([idxs[g].suffix_array(1)[0] for g in range(1, parts)], np.uint64)
+        dest = idxs[0].route(splitters, qb, m) if parts > 1 else np.zeros(nq, np.uint32)
+        got = np.zeros(nq, np.uint64)
+        for g in range(parts):
+            sel = np.nonzero(dest == g)[0]
+            if len(sel) == 0:
+                continue
+            sub = qb.reshape(nq, m)[sel].reshape(-1)
+            for algo in ("quad", "plain", "stree"):
+                assert np.array_equal(idxs[g].search_fixed(sub, m, algo=algo), expect[sel]), (n, g, algo)
+            got[sel] = idxs[g].search_fixed(sub, m, algo="quad")
+        assert np.array_equal(got, expect)
+
+
+def test_part_builds_at_scale(sas):
+    """n = 2^28 + 5, 3 parts: every part's SA equals the matching slice of the
+    whole-SA builder's output; the ranges tile [0, n); next_pos links the parts."""
+    n = (1 << 28) + 5
+    t = sas.random_string(n, seed=44, device="cuda")
+    full = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=False)
+    sa = full.suffix_array()
+    full.free()
+    lo_expect = 0
+    for g in range(3):
+        ix = sas.SaNaive.build_part(t, g, 3, lcp=False, stree=False, sector=False, quad=True, verify=True)
+        st = ix.stats()
+        lo, cnt = st["rank_lo"], st["sa_entries"]
+        assert lo == lo_expect and cnt > n // 4
+        assert np.array_equal(ix.suffix_array(), sa[lo:lo + cnt].astype(np.uint64)), g
+        assert st["next_pos"] == (int(sa[lo + cnt]) if lo + cnt < n else n)
+        lo_expect = lo + cnt
+        ix.free()
+    assert lo_expect == n
