@@ -46,6 +46,17 @@ def reference_kats() -> dict:
             {"cite": "sst/s_tree.rs:887-895, sst/btree.rs:179-187", "node": list(range(1, 16)) + [I32_MAX],
              "q": 1, "expect": 0},
         ],
+        # SortedVec::binary_search results pinned by the interpolation-search tests
+        # (their expected values are binary_search's; q = 9 there reads vals[n], out
+        # of bounds, and is left out) and the btree tests (same values as s_tree's)
+        "sorted_search": [
+            {"cite": "sst/interp_search.rs:258-266 (interppolation_vs_binsearch)",
+             "input": list(range(1, 16)), "qs": [5], "expect": [5]},
+            {"cite": "sst/interp_search.rs:268-276 (normal_vs_batched, q < 9)",
+             "input": list(range(1, 9)), "qs": [0, 1, 2, 3, 4, 5, 6], "expect": [1, 1, 2, 3, 4, 5, 6]},
+            {"cite": "sst/btree.rs:153-177 (test_btree_search_bottom_layer / _top_node)",
+             "input": "range(1,2000) + [MAX]", "qs": [452, 289], "expect": [452, 289]},
+        ],
     }
 
 

@@ -32,6 +32,13 @@ def test_kats(sas, golden_dir):
         assert e.nodes().tolist() == c["vals"]
     for c in k["eytzinger_search"]:
         assert sas.Eytzinger.new(c["input"]).query_one(c["q"]) == c["expect"]
+    for c in k["sorted_search"]:
+        inp = list(range(1, 2000)) + [O.MAX] if c["input"] == "range(1,2000) + [MAX]" else c["input"]
+        assert sas.SortedVec.new(inp).query(c["qs"]).tolist() == c["expect"], c["cite"]
+        if inp[-1] != O.MAX:
+            inp = inp + [O.MAX]
+        for cls in (sas.STree16, sas.STree15, sas.Eytzinger, sas.PartitionedSTree16M):
+            assert cls.new(inp).query(c["qs"]).tolist() == c["expect"], (cls.__name__, c["cite"])
     vals = list(range(1, 2000)) + [O.MAX]
     for cls in (sas.STree16, sas.STree15, sas.SortedVec, sas.Eytzinger):
         idx = cls.new(vals)

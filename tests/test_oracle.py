@@ -67,6 +67,18 @@ def test_kat_stree_search(kats):
         assert int(t.query([k["q"]])[0]) == k["expect"] == int(O.SortedVec(vals).query([k["q"]])[0]), k["cite"]
 
 
+def _kat_input(k):
+    return list(range(1, 2000)) + [O.MAX] if k["input"] == "range(1,2000) + [MAX]" else k["input"]
+
+
+def test_kat_sorted_search(kats):
+    for k in kats["sorted_search"]:
+        got = O.SortedVec(_kat_input(k)).query(k["qs"])
+        assert got.tolist() == k["expect"], k["cite"]
+        assert O.STree(_kat_input(k) if _kat_input(k)[-1] == O.MAX else _kat_input(k) + [O.MAX]).query(
+            k["qs"]).tolist() == k["expect"], k["cite"]
+
+
 def test_kat_node_find(kats):
     for k in kats["node_find"]:
         assert O.node_find(k["node"], k["q"]) == k["expect"]
