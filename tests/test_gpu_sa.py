@@ -566,3 +566,28 @@ def test_part_builds_at_scale(sas):
         lo_expect = lo + cnt
         ix.free()
     assert lo_expect == n
+
+
+def test_probe_counts_match_reference_counter(sas):
+    """out_probes of PLAIN / LCP = the reference's `cnt` of binary_search
+    (sas/sa_search.rs:104: one per loop iteration while l < r), query by query,
+    on the oracle's restatement; the Counter mirror sums them."""
+    n = 200_003
+    t = sas.random_string(n, seed=19)
+    idx = sas.SaNaive.build(t)
+    sa = idx.suffix_array()
+    tp = O.padded(t)
+    rng = np.random.default_rng(3)
+    qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 100, 300), rng.integers(1, 80, 300))]
+    qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(1, 30, 200)]
+    qs += [np.full(40, 3, np.uint8), np.zeros(0, np.uint8), t[n - 5:]]
+    buf, off, lens = pack(qs)
+    expect = [O.search_one(tp, n, sa, np.asarray(q, np.uint8), "binary_search") for q in qs]
+    for algo in ("plain", "lcp"):
+        pos, probes = idx.search_batch(buf, off, lens, algo=algo, probes=True)
+        assert pos.tolist() == [e[0] for e in expect], algo
+        assert probes.tolist() == [e[1] for e in expect], algo
+    cnt = sas.Counter()
+    for q, e in zip(qs[:50], expect[:50]):
+        assert sas.binary_search(idx, q, cnt) == e[0]
+    assert cnt.value == sum(e[1] for e in expect[:50])
