@@ -559,6 +559,28 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 // 16-char separators, 17-ary; lane j counts its 4, the group sums by shuffles.
 // Leaves: 4 entries {key64, SA}, lane j evaluates entry j, a group ballot picks
 // the first entry >= q.  All branches are group-uniform.
+// m <= 32 queries at an 8-B aligned address with m % 8 == 0 (the headline shape):
+// lane j of the group loads bytes 8j..8j+7 (one contiguous 32-B request per query
+// instead of two 16-B halves per lane) and packs them to 16 bits; the group ORs the
+// four parts with DPP quad_perm moves.
+__device__ __forceinline__ uint64_t quad_key32(const uint8_t* __restrict__ qb, uint32_t m, uint32_t sub,
+                                               uint32_t* bad) {
+    uint32_t part = 0;
+    if (8 * sub < m) {
+        const uint2 v = *reinterpret_cast<const uint2*>(qb + 8 * sub);
+        *bad |= (v.x | v.y) & 0xFCFCFCFCu;
+        part = (pack4(v.x) << 8) | pack4(v.y);
+    }
+    // chars 8j..8j+7 -> bits 63-16j .. 48-16j
+    uint32_t hi = (sub < 2) ? (part << (16 - 16 * sub)) : 0u;
+    uint32_t lo = (sub >= 2) ? (part << (16 - 16 * (sub - 2))) : 0u;
+    hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false);
+    lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false);
+    hi |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false);
+    lo |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false);
+    return ((uint64_t)hi << 32) | lo;
+}
+
 // Evaluate leaf L: mask of its entries x (< sa_n) satisfying the bound's predicate
 // (UPPER = false: suffix(x) >= q; UPPER = true: the first min(m, len) chars of
 // suffix(x) are > q, sector_gt_prefix); *p = this lane's SA value.
@@ -653,7 +675,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
-        q.load(qb, m, &bad);
+        if (QW == 1 && a.qoff == nullptr && (m & 7) == 0 && (((uintptr_t)qb) & 7) == 0) {
+            q.bytes = qb;
+            q.m = m;
+            q.w[0] = quad_key32(qb, m, sub, &bad);
+        } else {
+            q.load(qb, m, &bad);
+        }
         uint32_t probes = 0;
         uint64_t px = 0;
         const uint64_t x = quad_bound<QW, false>(a, s_nodes, q, q.w[0], 0, sub, &probes, &px);
