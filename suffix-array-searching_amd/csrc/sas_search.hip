@@ -389,12 +389,44 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree1(SearchArgs a) {
 //   key == K64, m <= 32    ->  n - sa >= m   (equal padded prefixes: the shorter
 //                                             suffix is a proper prefix of q)
 //   key == K64, m > 32     ->  exact compare from char 32 (text read)
+// suffix(p) < q when the first 32 chars are known equal (m > 32).  The windows
+// past char 32 are all needed when q occurs at p (every positive answer), so the
+// text words are loaded in chunks of up to 4 windows before any compare: their
+// latencies overlap instead of chaining load -> compare -> branch per window.
 template <int QW>
+__device__ __forceinline__ bool tail_less32(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
+                                            const QueryRegs<QW>& q) {
+    const uint64_t lenS = n - p;
+    const uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
+    const uint64_t w0 = (p + 32) >> 5;
+    const uint32_t sh = (uint32_t)(p & 31) << 1;
+    for (uint32_t off = 32, wi = 0; off < L; off += 128, wi += 4) {
+        uint64_t wd[5];
+#pragma unroll
+        for (int i = 0; i < 5; i++) wd[i] = (off + 32 * i <= L + 31) ? tw[w0 + wi + i] : 0ull;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint32_t o = off + 32 * i;
+            if (o >= L) break;
+            const uint32_t c = L - o < 32 ? L - o : 32;
+            const uint64_t mk = chars_mask(c);
+            const uint64_t t = (sh ? ((wd[i] << sh) | (wd[i + 1] >> (64 - sh))) : wd[i]) & mk;
+            const uint64_t b = q.chars32(o) & mk;
+            if (t != b) return t < b;
+        }
+    }
+    return lenS < (uint64_t)q.m;
+}
+
+// PREFETCH: load the tail's text words up front (tail_less32); measured faster for
+// the per-lane sector kernel, slower for the 4-lane quad kernel (register spills).
+template <int QW, bool PREFETCH = false>
 __device__ __forceinline__ bool sector_ge(uint64_t key, uint64_t p, uint64_t K64, const SearchArgs& a,
                                           const QueryRegs<QW>& q) {
     if (key != K64) return key > K64;
     // QW == 1 is only dispatched for m <= 32 (qw_for): the text compare is dead code there
     if (QW == 1 || q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
+    if (PREFETCH) return !tail_less32<QW>(a.tw, a.n, p, q);
     uint32_t lcp;
     return !suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
 }
@@ -436,7 +468,7 @@ __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint
     const uint4* g = reinterpret_cast<const uint4*>(a.sec_inner);
     const uint32_t R16 = (uint32_t)(((UPPER && q.m <= 32) ? Q3 : K64) >> 32);
     auto pred = [&](uint64_t key, uint64_t p) -> bool {
-        return UPPER ? sector_gt_prefix<QW>(key, p, K64, Q3, a, q) : sector_ge<QW>(key, p, K64, a, q);
+        return UPPER ? sector_gt_prefix<QW>(key, p, K64, Q3, a, q) : sector_ge<QW, true>(key, p, K64, a, q);
     };
     uint64_t k = 0;
     auto count8 = [&](uint4 v0, uint4 v1) -> uint32_t {
