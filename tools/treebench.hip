@@ -90,6 +90,34 @@ __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p
 
 // Two independent lookups per lane group, their levels interleaved (ILP = 2):
 // cooperative 64-B levels only (W = 1064), G = 4.
+// XCD-partitioned replay (G = 4): workgroups are dispatched round-robin to the 8
+// XCDs, so block b runs on XCD b % 8; its lookups only touch that XCD's eighth of
+// every level (as if the queries had been bucketed by key range per XCD).
+__global__ __launch_bounds__(1024, 8) void k_chain_xcd(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
+                                                       uint32_t seed, uint32_t* out) {
+    const int G = 4;
+    uint32_t acc = 0;
+    const uint32_t sub = threadIdx.x % G, xcd = blockIdx.x % 8;
+    const uint64_t groups = ((uint64_t)gridDim.x * blockDim.x) / G;
+    for (uint64_t g = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; g < lookups; g += groups) {
+        uint64_t h = mix(g * 0x9E3779B97F4A7C15ull + seed);
+        uint32_t dep = 0;
+        for (int l = 0; l < lay.L; l++) {
+            h = h * 0x9E3779B97F4A7C15ull + l + (dep & 0x80000000u);
+            const int wb = lay.width[l] - 1000;
+            const uint64_t part = lay.units[l] / 8 ? lay.units[l] / 8 : 1;
+            const uint64_t node = (lay.units[l] >= 8 ? xcd * part : 0) + (((h >> 32) * part) >> 32);
+            const u32x4* v = reinterpret_cast<const u32x4*>(p + lay.base[l] + node * wb);
+            u32x4 t = v[sub % (wb / 16)];
+            uint32_t d = t.x ^ t.y ^ t.z ^ t.w;
+            for (int o = 1; o < G; o <<= 1) d ^= __shfl_xor(d, o, G);
+            dep = d;
+        }
+        acc ^= dep;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 __global__ __launch_bounds__(1024, 8) void k_chain_ilp2(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
                                                         uint32_t seed, uint32_t* out) {
     const int G = 4;
@@ -162,8 +190,10 @@ int main(int argc, char** argv) {
             int G = 1;
             for (int l = 0; l < L.L; l++) if (L.width[l] > 1000) G = (L.width[l] - 1000) / 16 > G ? (L.width[l] - 1000) / 16 : G;
             bool ilp2 = getenv("TB_ILP2") != nullptr;
+            bool xcdp = getenv("TB_XCD") != nullptr;
             auto launch = [&](uint32_t sd) {
-                if (ilp2) hipLaunchKernelGGL(k_chain_ilp2, grd, blk, 0, 0, p, L, lookups, sd, out);
+                if (xcdp) hipLaunchKernelGGL(k_chain_xcd, grd, blk, 0, 0, p, L, lookups, sd, out);
+                else if (ilp2) hipLaunchKernelGGL(k_chain_ilp2, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else if (G == 4) hipLaunchKernelGGL(k_chain<4>, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else hipLaunchKernelGGL(k_chain<1>, grd, blk, 0, 0, p, L, lookups, sd, out);
