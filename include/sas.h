@@ -134,6 +134,17 @@ int sas_route(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsp
               const uint8_t* qbytes, uint32_t m, uint64_t nq, uint32_t* out_shard,
               void* stream, uint32_t flags);
 
+/* One sharded step's send side, fused on the GPU (device pointers only,
+ * SAS_DEVICE_PTRS): route each fixed-length query (as sas_route), group the
+ * queries by destination shard (counting sort) and copy their bytes into
+ * out_send, bucket after bucket.  out_counts[w] = queries for shard w
+ * (w < nsplit + 1); out_slot[k] = send position of query k, so the positions
+ * that come back in send order are gathered with it.  Order inside a bucket is
+ * unspecified. */
+int sas_route_pack(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsplit,
+                   const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_counts,
+                   uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags);
+
 int sas_get_stats(const sas_index* index, sas_stats* out);
 
 /* Copy the suffix array / LCP array out (dst host or device per flags).

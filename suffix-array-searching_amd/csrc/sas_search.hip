@@ -20,6 +20,8 @@
 // Text compares are 2-bit packed: 32 chars per u64 compare.
 #include "common.hpp"
 
+#include <rocprim/device/device_scan.hpp>
+
 #include <chrono>
 #include <type_traits>
 #include <vector>
@@ -1102,6 +1104,113 @@ extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint3
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMemcpy(out_shard, dout, nq * 4, hipMemcpyDeviceToHost));
     }
+    return 0;
+}
+
+// ------------------------------------------------------------------ route + pack (sharded step)
+// One sharded-mode step needs the queries grouped by destination shard.  This is
+// a counting sort by destination, fused with the routing and the byte copy:
+//   k_route          dest[i] (as in sas_route)
+//   k_pack_count     per-block histogram of dest (LDS atomics) -> cnt[w * nblk + b]
+//   exclusive scan   -> base[w * nblk + b] = first send slot of (bucket w, block b)
+//   k_pack_scatter   slot = base + LDS-atomic rank; copy the query's m bytes to
+//                    send[slot * m]; slot_of[i] = slot (positions come back in
+//                    send order and are gathered with it)
+// Order inside a bucket is not stable (it need not be: every slot is recorded).
+#define PACK_BLOCK 1024
+#define PACK_ITEMS 8
+#define PACK_CHUNK (PACK_BLOCK * PACK_ITEMS)
+
+__global__ __launch_bounds__(PACK_BLOCK) void k_pack_count(const uint32_t* __restrict__ dest, uint64_t nq, uint32_t W,
+                                                           uint64_t nblk, uint64_t* __restrict__ cnt) {
+    __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
+    for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * PACK_CHUNK;
+    for (int it = 0; it < PACK_ITEMS; it++) {
+        const uint64_t i = base + (uint64_t)it * PACK_BLOCK + threadIdx.x;
+        if (i < nq) atomicAdd(&h[dest[i]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) cnt[(uint64_t)w * nblk + blockIdx.x] = h[w];
+}
+
+__global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __restrict__ dest, uint64_t nq,
+                                                             uint32_t W, uint64_t nblk,
+                                                             const uint64_t* __restrict__ base_slot,
+                                                             const uint8_t* __restrict__ qbytes, uint32_t m,
+                                                             uint8_t* __restrict__ send,
+                                                             uint64_t* __restrict__ slot_of) {
+    __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
+    for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * PACK_CHUNK;
+    const bool vec = (m & 15) == 0 && ((((uintptr_t)qbytes) | ((uintptr_t)send)) & 15) == 0;
+    for (int it = 0; it < PACK_ITEMS; it++) {
+        const uint64_t i = base + (uint64_t)it * PACK_BLOCK + threadIdx.x;
+        if (i >= nq) continue;
+        const uint32_t w = dest[i];
+        const uint64_t slot = base_slot[(uint64_t)w * nblk + blockIdx.x] + atomicAdd(&h[w], 1u);
+        slot_of[i] = slot;
+        const uint8_t* src = qbytes + i * (uint64_t)m;
+        uint8_t* dst = send + slot * (uint64_t)m;
+        if (vec) {
+            for (uint32_t k = 0; k < m; k += 16)
+                *reinterpret_cast<uint4*>(dst + k) = *reinterpret_cast<const uint4*>(src + k);
+        } else {
+            for (uint32_t k = 0; k < m; k++) dst[k] = src[k];
+        }
+    }
+}
+
+__global__ void k_pack_totals(const uint64_t* __restrict__ base_slot, uint32_t W, uint64_t nblk, uint64_t nq,
+                              uint64_t* __restrict__ out_counts) {
+    for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
+        const uint64_t lo = base_slot[(uint64_t)w * nblk];
+        const uint64_t hi = (w + 1 < W) ? base_slot[(uint64_t)(w + 1) * nblk] : nq;
+        out_counts[w] = hi - lo;
+    }
+}
+
+extern "C" int sas_route_pack(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
+                              const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_counts,
+                              uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
+    if (!x || (nsplit && !splitter_pos) || !out_counts || (nq && (!qbytes || !out_send || !out_slot)))
+        SAS_FAIL(EINVAL, "sas_route_pack: null argument");
+    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_route_pack: device pointers only (SAS_DEVICE_PTRS)");
+    if (nsplit > SAS_MAX_SPLIT) SAS_FAIL(EINVAL, "sas_route_pack: too many splitters");
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint32_t W = nsplit + 1;
+    if (nq == 0) {
+        HIP_TRY(hipMemsetAsync(out_counts, 0, W * 8, st));
+        return 0;
+    }
+    const uint64_t nblk = (nq + PACK_CHUNK - 1) / PACK_CHUNK;
+    void* dest = nullptr;
+    void* cnt = nullptr;
+    void* tmp = nullptr;
+    size_t tbytes = 0;
+    HIP_TRY(rocprim::exclusive_scan(nullptr, tbytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0,
+                                    (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
+    HIP_TRY(hipMallocAsync(&dest, nq * 4, st));
+    HIP_TRY(hipMallocAsync(&cnt, nblk * W * 8, st));
+    HIP_TRY(hipMallocAsync(&tmp, tbytes ? tbytes : 8, st));
+    uint64_t rb = (nq + 255) / 256;
+    if (rb > 65536) rb = 65536;
+    hipLaunchKernelGGL(k_route, dim3((unsigned)rb), dim3(256), 0, st, x->text_w, x->n, splitter_pos, nsplit, qbytes,
+                       m, nq, static_cast<uint32_t*>(dest), x->scratch);
+    hipLaunchKernelGGL(k_pack_count, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest), nq,
+                       W, nblk, static_cast<uint64_t*>(cnt));
+    HIP_TRY(rocprim::exclusive_scan(tmp, tbytes, static_cast<uint64_t*>(cnt), static_cast<uint64_t*>(cnt),
+                                    (uint64_t)0, (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
+    hipLaunchKernelGGL(k_pack_scatter, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest),
+                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot);
+    hipLaunchKernelGGL(k_pack_totals, dim3(1), dim3(256), 0, st, static_cast<uint64_t*>(cnt), W, nblk, nq, out_counts);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipFreeAsync(dest, st));
+    HIP_TRY(hipFreeAsync(cnt, st));
+    HIP_TRY(hipFreeAsync(tmp, st));
     return 0;
 }
 

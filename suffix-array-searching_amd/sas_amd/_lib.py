@@ -99,6 +99,7 @@ def lib():
     L.sas_build_shard.argtypes = [vp, u64, vp, i32, u64, u64, u32, C.POINTER(vp)]
     L.sas_build_part.argtypes = [vp, u64, u32, u32, u32, C.POINTER(vp)]
     L.sas_route.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, u32]
+    L.sas_route_pack.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, vp, vp, u32]
     L.sas_get_stats.argtypes = [vp, C.POINTER(SasStats)]
     L.sas_copy_sa.argtypes = [vp, vp, u64, u32]
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]

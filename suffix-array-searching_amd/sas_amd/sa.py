@@ -159,6 +159,22 @@ class SaNaive:
                               out.ctypes.data, stream, 0))
         return out[:nq]
 
+    def route_pack(self, splitter_pos, qbytes, m: int, stream=None):
+        """Send side of one sharded step, fused on the GPU (sas_route_pack): CUDA
+        tensors in -> (counts int64 [W], send uint8 [nq*m] grouped by shard,
+        slot int64 [nq] = send position of each query)."""
+        import torch
+        nq = qbytes.numel() // m
+        W = splitter_pos.numel() + 1
+        counts = torch.empty(W, dtype=torch.int64, device=qbytes.device)
+        send = torch.empty(max(nq * m, 1), dtype=torch.uint8, device=qbytes.device)
+        slot = torch.empty(max(nq, 1), dtype=torch.int64, device=qbytes.device)
+        st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
+        check(lib().sas_route_pack(self._h, splitter_pos.data_ptr() if W > 1 else None, W - 1, qbytes.data_ptr(), m,
+                                   nq, counts.data_ptr(), send.data_ptr(), slot.data_ptr(), st,
+                                   _lib.SAS_DEVICE_PTRS))
+        return counts, send[: nq * m], slot[:nq]
+
     def verify(self):
         check(lib().sas_verify(self._h))
 

@@ -39,21 +39,25 @@ class ShardedSearch:
     def search_fixed(self, qbytes, m: int):
         """qbytes: uint8 tensor [nq*m] of this rank's queries -> int64 positions."""
         import torch
-        dist, W = self.dist, self.world
-        nq = qbytes.numel() // m
-        dest = self.index.route(self.splitters, qbytes, m).to(torch.int64)
-        order = torch.argsort(dest, stable=True)
-        send = torch.bincount(dest, minlength=W)
+        dist = self.dist
+        if hasattr(self.index, "route_pack"):
+            # GPU: routing, grouping by shard and the byte copy in one fused call
+            send, qsend, slot = self.index.route_pack(self.splitters, qbytes, m)
+        else:  # CPU stand-ins (tests): the same grouping with torch ops
+            nq = qbytes.numel() // m
+            dest = self.index.route(self.splitters, qbytes, m).to(torch.int64)
+            order = torch.argsort(dest, stable=True)
+            send = torch.bincount(dest, minlength=self.world)
+            qsend = qbytes.view(nq, m).index_select(0, order).reshape(-1)
+            slot = torch.empty_like(order)
+            slot[order] = torch.arange(nq, device=order.device)
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send, group=self.group)
         send_l, recv_l = send.tolist(), recv.tolist()
-        qsend = qbytes.view(nq, m).index_select(0, order).reshape(-1)
         qrecv = torch.empty(sum(recv_l) * m, dtype=torch.uint8, device=qbytes.device)
         dist.all_to_all_single(qrecv, qsend, [c * m for c in recv_l], [c * m for c in send_l], group=self.group)
         local = self.index.search_fixed(qrecv, m, algo=self.algo) if sum(recv_l) else \
             torch.empty(0, dtype=torch.int64, device=qbytes.device)
-        back = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+        back = torch.empty(sum(send_l), dtype=torch.int64, device=qbytes.device)
         dist.all_to_all_single(back, local.to(torch.int64), send_l, recv_l, group=self.group)
-        out = torch.empty_like(back)
-        out[order] = back
-        return out
+        return back.index_select(0, slot)  # positions come back in send order

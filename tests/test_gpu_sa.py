@@ -591,3 +591,26 @@ def test_probe_counts_match_reference_counter(sas):
     for q, e in zip(qs[:50], expect[:50]):
         assert sas.binary_search(idx, q, cnt) == e[0]
     assert cnt.value == sum(e[1] for e in expect[:50])
+
+
+def test_route_pack(sas):
+    """sas_route_pack: counts = histogram of sas_route's shards, slots are a
+    permutation, every query's bytes sit at its slot inside its shard's bucket."""
+    import torch
+    n, m, W = 300_007, 24, 5
+    t = sas.random_string(n, seed=61)
+    idxs = [sas.SaNaive.build_part(t, g, W, lcp=False, stree=False, sector=False) for g in range(W)]
+    splitters = torch.tensor([int(ix.suffix_array(1)[0]) for ix in idxs[1:]], dtype=torch.int64).cuda()
+    rng = np.random.default_rng(2)
+    offs = rng.integers(0, n - m, 20_000)
+    qb = np.concatenate([t[o:o + m] for o in offs] + [rng.integers(0, 4, 5000 * m, dtype=np.uint8)])
+    nq = len(qb) // m
+    dq = torch.from_numpy(qb).cuda()
+    dest = idxs[0].route(splitters, dq, m).cpu().numpy()
+    counts, send, slot = idxs[0].route_pack(splitters, dq, m)
+    counts, send, slot = counts.cpu().numpy(), send.cpu().numpy(), slot.cpu().numpy()
+    assert counts.tolist() == np.bincount(dest, minlength=W).tolist()
+    assert np.array_equal(np.sort(slot), np.arange(nq))
+    starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
+    assert ((slot >= starts[dest]) & (slot < starts[dest] + counts[dest])).all()
+    assert np.array_equal(send.reshape(nq, m)[slot], qb.reshape(nq, m))
