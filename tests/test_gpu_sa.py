@@ -614,3 +614,40 @@ def test_route_pack(sas):
     starts = np.concatenate([[0], np.cumsum(counts)[:-1]])
     assert ((slot >= starts[dest]) & (slot < starts[dest] + counts[dest])).all()
     assert np.array_equal(send.reshape(nq, m)[slot], qb.reshape(nq, m))
+
+
+def test_full_size_algorithms_agree_and_are_lower_bounds(sas):
+    """BASELINE size (n = 2^30, 10^6 mixed queries: positive len 32 as in the bench,
+    random negatives, other lengths): all algorithms return identical positions; a
+    sample is proven exact on the host text (SA[lo-1] < q <= SA[lo], pos = SA[lo])."""
+    import torch
+    n = 1 << 30
+    t = sas.random_string(n, seed=31415, device="cuda")
+    idx = sas.SaNaive.build(t)
+    ht = t.cpu().numpy()
+    rng = np.random.default_rng(30)
+    offs = rng.integers(0, n - 200, 700_000)
+    qs = [ht[o:o + 32] for o in offs[:500_000]]
+    qs += [ht[o:o + l] for o, l in zip(offs[500_000:], rng.integers(1, 160, 200_000))]
+    qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(1, 40, 300_000)]
+    buf, off, lens = pack(qs)
+    dbuf = torch.from_numpy(buf).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    dlen = torch.from_numpy(lens.view(np.int32)).cuda()
+    res = {}
+    for algo in ALGOS:
+        res[algo] = idx.search_batch(dbuf, doff, dlen, algo=algo).cpu().numpy()
+    for algo in ALGOS:
+        assert np.array_equal(res[algo], res["plain"]), algo
+    lo, hi = idx.search_range(dbuf, doff, dlen)
+    lo = lo.cpu().numpy()
+    for k in rng.choice(len(qs), 3000, replace=False):
+        q = bytes(qs[k])
+        r = int(lo[k])
+        cur = int(idx.suffix_array(count=1, start=r)[0]) if r < n else n
+        assert int(res["plain"][k]) == cur
+        if r < n:
+            assert bytes(ht[cur:cur + len(q)]) >= q
+        if r > 0:
+            prev = int(idx.suffix_array(count=1, start=r - 1)[0])
+            assert bytes(ht[prev:prev + len(q)]) < q
