@@ -48,9 +48,13 @@ __device__ __forceinline__ u32x4 ld(const u32x4* p) {
     return *p;
 }
 
+// io != nullptr: each lookup also streams its 32-B query in (8 B per lane of the
+// group) and writes an 8-B result (lane 0), as the real search kernels do.
+struct Io { const uint8_t* q; uint64_t* res; };
+
 template <int G>
 __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
-                                                   uint32_t seed, uint32_t* out) {
+                                                   uint32_t seed, uint32_t* out, Io io = Io{nullptr, nullptr}) {
     uint32_t acc = 0;
     const uint32_t sub = threadIdx.x % G;  // lane within a cooperative group of G lanes
     for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < lookups * G;
@@ -58,6 +62,10 @@ __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p
         uint64_t i = t / G;
         uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
         uint32_t dep = 0;
+        if (io.q) {
+            const uint2 qv = *reinterpret_cast<const uint2*>(io.q + i * 32 + 8 * (sub % 4));
+            h ^= (uint64_t)(qv.x & 0x80000000u);  // qv top bit 0: a data dependence, no value change
+        }
         for (int l = 0; l < lay.L; l++) {
             // one 64-bit multiply per level (cheap, like a real descent's address math);
             // dep's top bit is 0 (buffer = 0x01): a true data dependence
@@ -83,6 +91,7 @@ __global__ __launch_bounds__(1024, 8) void k_chain(const uint8_t* __restrict__ p
             if (lay.width[l] >= 128) { t ^= ld<false>(v + 4) ^ ld<false>(v + 5) ^ ld<false>(v + 6) ^ ld<false>(v + 7); }
             dep = t.x ^ t.y ^ t.z ^ t.w;
         }
+        if (io.res && sub == 0) io.res[i] = dep;
         acc ^= dep;
     }
     if (acc == 0x12345678u) out[0] = acc;
@@ -183,6 +192,15 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
     dim3 blk(1024), grd(cus * 2);
+    Io io{nullptr, nullptr};
+    if (getenv("TB_IO")) {
+        uint8_t* qbuf;
+        uint64_t* rbuf;
+        CHECK(hipMalloc(&qbuf, lookups * 32 + 64));
+        CHECK(hipMemset(qbuf, 1, lookups * 32 + 64));
+        CHECK(hipMalloc(&rbuf, lookups * 8));
+        io = Io{qbuf, rbuf};
+    }
     for (size_t k = 0; k < lays.size(); k++) {
         for (int nt = 0; nt < 1; nt++) {
             Layout L = lays[k];
@@ -194,9 +212,9 @@ int main(int argc, char** argv) {
             auto launch = [&](uint32_t sd) {
                 if (xcdp) hipLaunchKernelGGL(k_chain_xcd, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else if (ilp2) hipLaunchKernelGGL(k_chain_ilp2, grd, blk, 0, 0, p, L, lookups, sd, out);
-                else if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out);
-                else if (G == 4) hipLaunchKernelGGL(k_chain<4>, grd, blk, 0, 0, p, L, lookups, sd, out);
-                else hipLaunchKernelGGL(k_chain<1>, grd, blk, 0, 0, p, L, lookups, sd, out);
+                else if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out, io);
+                else if (G == 4) hipLaunchKernelGGL(k_chain<4>, grd, blk, 0, 0, p, L, lookups, sd, out, io);
+                else hipLaunchKernelGGL(k_chain<1>, grd, blk, 0, 0, p, L, lookups, sd, out, io);
             };
             launch(1u);
             CHECK(hipDeviceSynchronize());
