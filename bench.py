@@ -202,22 +202,20 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
     range_res = {"queries": 2 * nq, "lookups_per_s": 2 * nq / (rkns * 1e-9), "kernel_ms": rkns * 1e-6,
                  "ranges_per_s": nq / (rkns * 1e-9), "counts_verified": bool(np.array_equal(cnt, expect))}
     st16.free()
-    # CPU: the oracle's STree16 (left_max) restatement, 16 threads over contiguous chunks
-    import threading
+    # CPU: the oracle's restatement of the reference's bench variant, STree16 left_max
+    # + batch_final::<128> (sst/bin/bench.rs:96; sst/s_tree.rs:303-326), contiguous
+    # per-thread chunks (sst/bin/bench.rs:558-573); 16 threads and 1 thread
     tree = O.STree(vals, left_max=True)
     threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    sample = min(nq, 4_000_000)
-    chunks = np.array_split(qs[:sample], threads)
-    outs = [None] * threads
-
-    def work(i):
-        outs[i] = tree.query(chunks[i])
+    sample = nq
     t0 = time.perf_counter()
-    th = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    [t.start() for t in th]
-    [t.join() for t in th]
+    cpu_out = tree.query_batch(qs[:sample], threads)
     dt = time.perf_counter() - t0
-    cpu_ok = bool(np.array_equal(np.concatenate(outs), ref[:sample]))
+    s1 = min(nq, 2_000_000)
+    t1 = time.perf_counter()
+    tree.query_batch(qs[:s1], 1)
+    one = s1 / (time.perf_counter() - t1)
+    cpu_ok = bool(np.array_equal(cpu_out, ref[:sample]))
     best = max(res, key=lambda k: res[k]["lookups_per_s"])
     print(json.dumps({
         "metric": "u32 static-search-tree lookups/s (2^28 keys = 1 GiB, 10^7 uniform queries)",
@@ -229,8 +227,10 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         "range_mode": range_res,
         "queries_kind": "positive" if args.positive else "uniform",
         "cpu_baseline": {"value": sample / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
-                         "sample": f"oracle STree16 left_max search (sst/s_tree.rs:196-206) on {sample} queries, "
-                                   f"{threads} threads", "agrees": cpu_ok}}), flush=True)
+                         "single_thread_value": one, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
+                         "sample": f"oracle STree16 left_max + batch_final::<128> restatement (sst/s_tree.rs:303-326) "
+                                   f"on all {sample} queries, {threads} threads, {dt:.2f} s", "agrees": cpu_ok}}),
+          flush=True)
 
 
 def run_c3(args, torch, sas_amd, dev, ws, rank, dist):

@@ -58,6 +58,7 @@ def lib():
         L.orc_stree_dims.restype = C.c_uint32
         L.orc_stree_build.argtypes = [u32p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int, u32p, u64p]
         L.orc_stree_query.argtypes = [u32p, u64p, C.c_uint32, C.c_uint32, C.c_uint32, u32p, C.c_uint64, u32p, C.c_void_p]
+        L.orc_stree_batch_mt.argtypes = [u32p, u64p, C.c_uint32, C.c_uint32, u32p, C.c_uint64, u32p, C.c_uint32]
         L.orc_eytzinger_build.argtypes = [u32p, C.c_uint64, u32p]
         L.orc_eytzinger_query.argtypes = [u32p, C.c_uint64, u32p, C.c_uint64, C.c_int, u32p]
         L.orc_sorted_query.argtypes = [u32p, C.c_uint64, u32p, C.c_uint64, u32p, C.c_void_p]
@@ -191,6 +192,15 @@ class STree:
 
     def nodes(self):
         return self.tree.reshape(-1, self.N)
+
+    def query_batch(self, qs, threads: int = 1):
+        """batch_final::<128> restatement (sst/s_tree.rs:303-326) over contiguous
+        per-thread chunks (sst/bin/bench.rs:558-573); same results as query()."""
+        assert self.N == 16
+        qs = np.ascontiguousarray(qs, np.uint32)
+        out = np.zeros(max(len(qs), 1), np.uint32)
+        lib().orc_stree_batch_mt(self.tree, self.offsets, self.height, self.B, qs, len(qs), out, threads)
+        return out[: len(qs)]
 
     def query(self, qs, want_rank=False):
         qs = np.ascontiguousarray(qs, np.uint32)

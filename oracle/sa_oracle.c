@@ -560,6 +560,79 @@ EXPORT uint32_t orc_sorted_search(const uint32_t* vals, uint64_t n, uint32_t q, 
     return l < n ? vals[l] : UINT32_MAX;
 }
 
+/* sst/s_tree.rs:303-326 batch_final::<P> (the reference's bench variant, run with
+ * P = 128, sst/bin/bench.rs:96): P queries descend layer by layer; after each
+ * node a query's next node is prefetched, so P independent loads are in flight.
+ * Node compare = find_popcnt with SSE2 signed compares (sst/node.rs:93-109). */
+static inline uint32_t node_find16_sse(const uint32_t* node, uint32_t q) {
+    const __m128i qv = _mm_set1_epi32((int32_t)q);
+    uint32_t c = 0;
+    for (int j = 0; j < 4; j++) {
+        __m128i v = _mm_loadu_si128((const __m128i*)(node + 4 * j));
+        c += (uint32_t)__builtin_popcount(_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpgt_epi32(qv, v))));
+    }
+    return c;
+}
+
+EXPORT void orc_stree_batch(const uint32_t* tree, const uint64_t* offsets, uint32_t height, uint32_t B,
+                            const uint32_t* qs, uint64_t nq, uint32_t* out) {
+    enum { P = 128 };
+    uint64_t k[P];
+    for (uint64_t base = 0; base < nq; base += P) {
+        const uint64_t cnt = nq - base < P ? nq - base : P;
+        for (uint64_t i = 0; i < cnt; i++) k[i] = 0;
+        for (uint32_t h = 0; h + 1 < height; h++) {
+            const uint32_t* o = tree + offsets[h] * 16;
+            const uint32_t* o2 = tree + offsets[h + 1] * 16;
+            for (uint64_t i = 0; i < cnt; i++) {
+                k[i] = k[i] * (B + 1) + node_find16_sse(o + k[i] * 16, qs[base + i]);
+                __builtin_prefetch(o2 + k[i] * 16);
+            }
+        }
+        const uint32_t* o = tree + offsets[height - 1] * 16;
+        for (uint64_t i = 0; i < cnt; i++) {
+            const uint32_t idx = node_find16_sse(o + k[i] * 16, qs[base + i]);
+            out[base + i] = o[k[i] * 16 + idx];
+        }
+    }
+}
+
+struct StreeJob {
+    const uint32_t* tree;
+    const uint64_t* offsets;
+    uint32_t height, B;
+    const uint32_t* qs;
+    uint64_t nq;
+    uint32_t* out;
+};
+static void* stree_worker(void* arg) {
+    struct StreeJob* j = (struct StreeJob*)arg;
+    orc_stree_batch(j->tree, j->offsets, j->height, j->B, j->qs, j->nq, j->out);
+    return NULL;
+}
+/* Contiguous query chunks per thread (sst/bin/bench.rs:558-573). */
+EXPORT void orc_stree_batch_mt(const uint32_t* tree, const uint64_t* offsets, uint32_t height, uint32_t B,
+                               const uint32_t* qs, uint64_t nq, uint32_t* out, uint32_t threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    struct StreeJob jobs[256];
+    const uint64_t chunk = (nq + threads - 1) / threads;
+    uint32_t started = 0;
+    for (uint32_t t = 0; t < threads; t++) {
+        const uint64_t lo = t * chunk, hi = lo + chunk < nq ? lo + chunk : nq;
+        if (lo >= hi) break;
+        jobs[t] = (struct StreeJob){tree, offsets, height, B, qs + lo, hi - lo, out + lo};
+        if (pthread_create(&th[t], NULL, stree_worker, &jobs[t]) != 0) {
+            stree_worker(&jobs[t]);
+            th[t] = 0;
+        }
+        started = t + 1;
+    }
+    for (uint32_t t = 0; t < started; t++)
+        if (th[t]) pthread_join(th[t], NULL);
+}
+
 /* Batch helpers so Python tests do not loop per query. */
 EXPORT void orc_stree_query(const uint32_t* tree, const uint64_t* offsets, uint32_t height, uint32_t B,
                             uint32_t N, const uint32_t* qs, uint64_t nq, uint32_t* out, uint64_t* rank) {

@@ -222,3 +222,18 @@ def test_prefix_range_matches_occurrences(sadef):
             assert lo == qd["rank"]
             occ = sorted(i for i in range(n) if t[i:i + len(q)] == q) if len(q) <= n else []
             assert sorted(sa[lo:hi].tolist()) == occ, (c["name"], q)
+
+
+def test_stree_batch_final_restatement_matches_search():
+    """orc_stree_batch (batch_final::<128>, sst/s_tree.rs:303-326; the u32 CPU
+    baseline) returns exactly STree::search's values, single- and multi-threaded."""
+    rng = np.random.default_rng(5)
+    for size in (17, 1000, 70_001):
+        vals = gen_vals(size, rng)
+        qs = rng.integers(0, O.MAX, 5000, dtype=np.uint64).astype(np.uint32)
+        for B in (16, 15):
+            for lm, rev in ((False, False), (True, False), (False, True)):
+                t = O.STree(vals, B=B, left_max=lm, reverse=rev)
+                ref = t.query(qs)
+                assert np.array_equal(t.query_batch(qs), ref), (size, B, lm, rev)
+                assert np.array_equal(t.query_batch(qs, threads=3), ref)
