@@ -513,7 +513,8 @@ def main():
                                        if args.mode == "replicated" else
                                        f"SA rank ranges over {ws} GPUs, sas_route + RCCL all_to_all_single "
                                        f"(queries out, positions back)")},
-            "roofline": None if not whole else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            # shard mode: the events bracket route + exchanges + search, not one kernel
+            "roofline": None if args.mode != "replicated" else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad",
