@@ -200,50 +200,63 @@ static int with_temp(DevBuf& tmp, size_t& have, Fn fn) {
     return 0;
 }
 
-int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* rounds_out, uint64_t* buckets_out) {
-    hipStream_t st = 0;
-    DevBuf tmp;
-    size_t tmp_have = 0;
-
-    // 1) histogram of the first 7 chars
+static int histogram(const uint64_t* tw, uint64_t n, std::vector<uint64_t>& h) {
     DevBuf hist;
     TRY(hist.alloc(HIST_BINS * 8, "histogram"));
-    HIP_TRY(hipMemsetAsync(hist.p, 0, HIST_BINS * 8, st));
-    hipLaunchKernelGGL(k_hist, dim3(grid_for(n, 1024) < 1024 ? grid_for(n, 1024) : 1024), dim3(1024), 0, st, tw, n,
-                       hist.as<unsigned long long>());
+    HIP_TRY(hipMemset(hist.p, 0, HIST_BINS * 8));
+    unsigned g = grid_for(n, 1024);
+    hipLaunchKernelGGL(k_hist, dim3(g < 1024 ? g : 1024), dim3(1024), 0, 0, tw, n, hist.as<unsigned long long>());
     HIP_TRY(hipGetLastError());
-    std::vector<uint64_t> h(HIST_BINS);
+    h.assign(HIST_BINS, 0);
     HIP_TRY(hipMemcpy(h.data(), hist.p, HIST_BINS * 8, hipMemcpyDeviceToHost));
+    return 0;
+}
 
-    // rank array, then size the buckets from what HBM has left
-    DevBuf rank;
-    TRY(rank.alloc(5 * n + SAS_SA40_PAD, "rank (40-bit)"));
-    size_t free_b = 0, total_b = 0;
-    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
-    uint64_t cap = (uint64_t)(free_b * 0.55) / 42;  // keys x2, vals x2, group, flags, sort temp
-    if (cap > n) cap = n;
-    uint64_t maxbin = 0;
-    for (uint64_t c : h) maxbin = c > maxbin ? c : maxbin;
-    if (maxbin > cap)
-        SAS_FAIL(ENOTSUP, "sas_build (40-bit): " + std::to_string(maxbin) +
-                              " suffixes share one 7-char prefix, more than one bucket (" + std::to_string(cap) +
-                              ") fits in free HBM");
-    if (cap < maxbin) cap = maxbin;
-    std::vector<uint32_t> edges{0};  // bucket b = bins [edges[b], edges[b+1])
-    uint64_t acc = 0, bucket_max = 0;
-    for (uint32_t b = 0; b < HIST_BINS; b++) {
-        if (acc + h[b] > cap) {
+// Tied entries collected while sorting buckets: ascending SA slots + group ids.
+struct TiedSink {
+    DevBuf list, grp;
+    uint64_t cap = 0, cnt = 0;
+};
+
+static int append_dev(DevBuf& dst, uint64_t& cap, uint64_t have, const uint64_t* src, uint64_t d, const char* what) {
+    if (have + d > cap) {
+        uint64_t nc = cap ? cap : 1024;
+        while (nc < have + d) nc *= 2;
+        DevBuf grown;
+        TRY(grown.alloc(nc * 8, what));
+        if (have) HIP_TRY(hipMemcpy(grown.p, dst.p, have * 8, hipMemcpyDeviceToDevice));
+        dst.alloc(0, "free");
+        dst.p = grown.release();
+        cap = nc;
+    }
+    if (d) HIP_TRY(hipMemcpy(dst.as<uint64_t>() + have, src, d * 8, hipMemcpyDeviceToDevice));
+    return 0;
+}
+
+// Sorted (key, position) pairs of the suffixes in bins [lo, hi) -> SA slots
+// off0.. of sa5; entries whose 32-char key repeats go to `ties`.
+// rank5 (optional): also write the 40-bit group id of every suffix (the whole-SA
+// builder's doubling rounds read it); nbuckets (optional): buckets sorted.
+static int sort_bins_into(const uint64_t* tw, uint64_t n, const std::vector<uint64_t>& h, uint32_t lo, uint32_t hi,
+                          uint64_t cap, uint8_t* sa5, uint64_t off0, TiedSink& ties, uint8_t* rank5 = nullptr,
+                          uint64_t* nbuckets = nullptr) {
+    hipStream_t st = 0;
+    uint64_t bucket_max = 0, acc = 0;
+    std::vector<uint32_t> edges{lo};
+    for (uint32_t b = lo; b < hi; b++) {
+        if (acc + h[b] > cap && acc) {
             edges.push_back(b);
             bucket_max = acc > bucket_max ? acc : bucket_max;
             acc = 0;
         }
         acc += h[b];
     }
-    edges.push_back(HIST_BINS);
+    edges.push_back(hi);
     bucket_max = acc > bucket_max ? acc : bucket_max;
-    *buckets_out = edges.size() - 1;
-
-    DevBuf ka, kb, va, vb, grp, flg, bcnt, cnt_d, list, list_alt;
+    if (nbuckets) *nbuckets = edges.size() - 1;
+    if (bucket_max == 0) return 0;
+    DevBuf ka, kb, va, vb, grp, flg, bcnt, cnt_d, tmp;
+    size_t tmp_have = 0;
     TRY(ka.alloc(bucket_max * 8, "bucket keys"));
     TRY(kb.alloc(bucket_max * 8, "bucket keys alt"));
     TRY(va.alloc(bucket_max * 8, "bucket positions"));
@@ -253,25 +266,20 @@ int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* round
     const uint64_t nblk = (n + COLLECT_CHUNK - 1) / COLLECT_CHUNK;
     TRY(bcnt.alloc(nblk * 8, "block counts"));
     TRY(cnt_d.alloc(16, "counter"));
-    uint64_t list_cap = 1 << 20, tied = 0;
-    TRY(list.alloc(list_cap * 8, "tied list"));
-
-    // 2) buckets in key order
-    uint64_t off = 0;
+    uint64_t off = off0;
     for (size_t b = 0; b + 1 < edges.size(); b++) {
-        uint32_t lo = edges[b], hi = edges[b + 1];
+        uint32_t blo = edges[b], bhi = edges[b + 1];
         uint64_t c = 0;
-        for (uint32_t i = lo; i < hi; i++) c += h[i];
+        for (uint32_t i = blo; i < bhi; i++) c += h[i];
         if (c == 0) continue;
-        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, lo, hi,
+        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
                            bcnt.as<uint64_t>());
         TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
             return rocprim::exclusive_scan(t, sz, bcnt.as<uint64_t>(), bcnt.as<uint64_t>(), (uint64_t)0,
                                            (size_t)nblk, rocprim::plus<uint64_t>(), st);
         }));
-        hipLaunchKernelGGL(k_bucket_collect, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, lo, hi,
+        hipLaunchKernelGGL(k_bucket_collect, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
                            bcnt.as<uint64_t>(), ka.as<uint64_t>(), va.as<uint64_t>());
-        HIP_TRY(hipGetLastError());
         rocprim::double_buffer<uint64_t> kdb(ka.as<uint64_t>(), kb.as<uint64_t>());
         rocprim::double_buffer<uint64_t> vdb(va.as<uint64_t>(), vb.as<uint64_t>());
         TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
@@ -280,12 +288,13 @@ int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* round
         const uint64_t* sk = kdb.current();
         const uint64_t* sv = vdb.current();
         uint64_t* free_k = (sk == ka.as<uint64_t>()) ? kb.as<uint64_t>() : ka.as<uint64_t>();
+        uint64_t* free_v = (sv == va.as<uint64_t>()) ? vb.as<uint64_t>() : va.as<uint64_t>();
         hipLaunchKernelGGL(k_b_heads, dim3(grid_for(c)), dim3(256), 0, st, sk, c, off, grp.as<uint64_t>());
         TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
             return rocprim::inclusive_scan(t, sz, grp.as<uint64_t>(), grp.as<uint64_t>(), (size_t)c, MaxOp64(), st);
         }));
         hipLaunchKernelGGL(k_b_emit, dim3(grid_for(c)), dim3(256), 0, st, sk, sv, grp.as<uint64_t>(), c, off, sa5,
-                           rank.as<uint8_t>(), flg.as<uint8_t>());
+                           rank5, flg.as<uint8_t>());
         HIP_TRY(hipGetLastError());
         rocprim::counting_iterator<uint64_t> cit(off);
         TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
@@ -294,25 +303,54 @@ int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* round
         uint64_t d = 0;
         HIP_TRY(hipMemcpy(&d, cnt_d.p, 8, hipMemcpyDeviceToHost));
         if (d) {
-            if (tied + d > list_cap) {
-                uint64_t nc = list_cap;
-                while (nc < tied + d) nc *= 2;
-                DevBuf grown;
-                TRY(grown.alloc(nc * 8, "tied list"));
-                HIP_TRY(hipMemcpyAsync(grown.p, list.p, tied * 8, hipMemcpyDeviceToDevice, st));
-                list.alloc(0, "free");
-                list.p = grown.release();
-                list_cap = nc;
-            }
-            HIP_TRY(hipMemcpyAsync(list.as<uint64_t>() + tied, free_k, d * 8, hipMemcpyDeviceToDevice, st));
-            tied += d;
+            TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
+                return rocprim::select(t, sz, grp.as<uint64_t>(), flg.as<uint8_t>(), free_v, cnt_d.as<uint64_t>(),
+                                       (size_t)c, st);
+            }));
+            uint64_t cap_l = ties.cap, cap_g = ties.cap;
+            TRY(append_dev(ties.list, cap_l, ties.cnt, free_k, d, "tied list"));
+            TRY(append_dev(ties.grp, cap_g, ties.cnt, free_v, d, "tied groups"));
+            ties.cap = cap_l;
+            ties.cnt += d;
         }
         off += c;
     }
     HIP_TRY(hipStreamSynchronize(st));
-    if (off != n) SAS_FAIL(EIO, "sas_build (40-bit): buckets cover " + std::to_string(off) + " of n suffixes");
-    ka.alloc(0, "free"); kb.alloc(0, "free"); va.alloc(0, "free"); vb.alloc(0, "free");
-    grp.alloc(0, "free"); flg.alloc(0, "free"); bcnt.alloc(0, "free");
+    return 0;
+}
+
+int build_sa_gpu40(const uint64_t* tw, uint64_t n, uint8_t* sa5, uint32_t* rounds_out, uint64_t* buckets_out) {
+    hipStream_t st = 0;
+    DevBuf tmp;
+    size_t tmp_have = 0;
+
+    // 1) histogram of the first 7 chars
+    std::vector<uint64_t> h;
+    TRY(histogram(tw, n, h));
+
+    // rank array, then size the buckets from what HBM has left
+    DevBuf rank;
+    TRY(rank.alloc(5 * n + SAS_SA40_PAD, "rank (40-bit)"));
+    size_t free_b = 0, total_b = 0;
+    HIP_TRY(hipMemGetInfo(&free_b, &total_b));
+    uint64_t cap = (uint64_t)(free_b * 0.55) / 42;  // keys x2, vals x2, group, flags, sort temp
+    if (cap > n) cap = n;
+    if (cap > (1ull << 31)) cap = 1ull << 31;       // one radix sort stays below 2^31 pairs
+    uint64_t maxbin = 0;
+    for (uint64_t c : h) maxbin = c > maxbin ? c : maxbin;
+    if (maxbin > cap)
+        SAS_FAIL(ENOTSUP, "sas_build (40-bit): " + std::to_string(maxbin) +
+                              " suffixes share one 7-char prefix, more than one bucket (" + std::to_string(cap) +
+                              ") fits in free HBM");
+    if (cap < maxbin) cap = maxbin;
+
+    // 2) buckets in key order: SA, 40-bit group ids, tied ranks
+    TiedSink ties;
+    TRY(sort_bins_into(tw, n, h, 0, HIST_BINS, cap, sa5, 0, ties, rank.as<uint8_t>(), buckets_out));
+    DevBuf& list = ties.list;
+    DevBuf list_alt, cnt_d;
+    TRY(cnt_d.alloc(16, "counter"));
+    const uint64_t tied = ties.cnt;
 
     // 3) doubling rounds over the tied ranks
     uint32_t rounds = 0;
@@ -503,121 +541,6 @@ static int resolve_ties_windows(const uint64_t* tw, uint64_t n, uint8_t* sa5, De
     }
     HIP_TRY(hipStreamSynchronize(st));
     *rounds_out = rounds;
-    return 0;
-}
-
-static int histogram(const uint64_t* tw, uint64_t n, std::vector<uint64_t>& h) {
-    DevBuf hist;
-    TRY(hist.alloc(HIST_BINS * 8, "histogram"));
-    HIP_TRY(hipMemset(hist.p, 0, HIST_BINS * 8));
-    unsigned g = grid_for(n, 1024);
-    hipLaunchKernelGGL(k_hist, dim3(g < 1024 ? g : 1024), dim3(1024), 0, 0, tw, n, hist.as<unsigned long long>());
-    HIP_TRY(hipGetLastError());
-    h.assign(HIST_BINS, 0);
-    HIP_TRY(hipMemcpy(h.data(), hist.p, HIST_BINS * 8, hipMemcpyDeviceToHost));
-    return 0;
-}
-
-// Tied entries collected while sorting buckets: ascending SA slots + group ids.
-struct TiedSink {
-    DevBuf list, grp;
-    uint64_t cap = 0, cnt = 0;
-};
-
-static int append_dev(DevBuf& dst, uint64_t& cap, uint64_t have, const uint64_t* src, uint64_t d, const char* what) {
-    if (have + d > cap) {
-        uint64_t nc = cap ? cap : 1024;
-        while (nc < have + d) nc *= 2;
-        DevBuf grown;
-        TRY(grown.alloc(nc * 8, what));
-        if (have) HIP_TRY(hipMemcpy(grown.p, dst.p, have * 8, hipMemcpyDeviceToDevice));
-        dst.alloc(0, "free");
-        dst.p = grown.release();
-        cap = nc;
-    }
-    if (d) HIP_TRY(hipMemcpy(dst.as<uint64_t>() + have, src, d * 8, hipMemcpyDeviceToDevice));
-    return 0;
-}
-
-// Sorted (key, position) pairs of the suffixes in bins [lo, hi) -> SA slots
-// off0.. of sa5; entries whose 32-char key repeats go to `ties`.
-static int sort_bins_into(const uint64_t* tw, uint64_t n, const std::vector<uint64_t>& h, uint32_t lo, uint32_t hi,
-                          uint64_t cap, uint8_t* sa5, uint64_t off0, TiedSink& ties) {
-    hipStream_t st = 0;
-    uint64_t bucket_max = 0, acc = 0;
-    std::vector<uint32_t> edges{lo};
-    for (uint32_t b = lo; b < hi; b++) {
-        if (acc + h[b] > cap && acc) {
-            edges.push_back(b);
-            bucket_max = acc > bucket_max ? acc : bucket_max;
-            acc = 0;
-        }
-        acc += h[b];
-    }
-    edges.push_back(hi);
-    bucket_max = acc > bucket_max ? acc : bucket_max;
-    if (bucket_max == 0) return 0;
-    DevBuf ka, kb, va, vb, grp, flg, bcnt, cnt_d, tmp;
-    size_t tmp_have = 0;
-    TRY(ka.alloc(bucket_max * 8, "bucket keys"));
-    TRY(kb.alloc(bucket_max * 8, "bucket keys alt"));
-    TRY(va.alloc(bucket_max * 8, "bucket positions"));
-    TRY(vb.alloc(bucket_max * 8, "bucket positions alt"));
-    TRY(grp.alloc(bucket_max * 8, "bucket groups"));
-    TRY(flg.alloc(bucket_max, "bucket tied flags"));
-    const uint64_t nblk = (n + COLLECT_CHUNK - 1) / COLLECT_CHUNK;
-    TRY(bcnt.alloc(nblk * 8, "block counts"));
-    TRY(cnt_d.alloc(16, "counter"));
-    uint64_t off = off0;
-    for (size_t b = 0; b + 1 < edges.size(); b++) {
-        uint32_t blo = edges[b], bhi = edges[b + 1];
-        uint64_t c = 0;
-        for (uint32_t i = blo; i < bhi; i++) c += h[i];
-        if (c == 0) continue;
-        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
-                           bcnt.as<uint64_t>());
-        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
-            return rocprim::exclusive_scan(t, sz, bcnt.as<uint64_t>(), bcnt.as<uint64_t>(), (uint64_t)0,
-                                           (size_t)nblk, rocprim::plus<uint64_t>(), st);
-        }));
-        hipLaunchKernelGGL(k_bucket_collect, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
-                           bcnt.as<uint64_t>(), ka.as<uint64_t>(), va.as<uint64_t>());
-        rocprim::double_buffer<uint64_t> kdb(ka.as<uint64_t>(), kb.as<uint64_t>());
-        rocprim::double_buffer<uint64_t> vdb(va.as<uint64_t>(), vb.as<uint64_t>());
-        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
-            return rocprim::radix_sort_pairs(t, sz, kdb, vdb, (size_t)c, 0, 64, st);
-        }));
-        const uint64_t* sk = kdb.current();
-        const uint64_t* sv = vdb.current();
-        uint64_t* free_k = (sk == ka.as<uint64_t>()) ? kb.as<uint64_t>() : ka.as<uint64_t>();
-        uint64_t* free_v = (sv == va.as<uint64_t>()) ? vb.as<uint64_t>() : va.as<uint64_t>();
-        hipLaunchKernelGGL(k_b_heads, dim3(grid_for(c)), dim3(256), 0, st, sk, c, off, grp.as<uint64_t>());
-        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
-            return rocprim::inclusive_scan(t, sz, grp.as<uint64_t>(), grp.as<uint64_t>(), (size_t)c, MaxOp64(), st);
-        }));
-        hipLaunchKernelGGL(k_b_emit, dim3(grid_for(c)), dim3(256), 0, st, sk, sv, grp.as<uint64_t>(), c, off, sa5,
-                           (uint8_t*)nullptr, flg.as<uint8_t>());
-        HIP_TRY(hipGetLastError());
-        rocprim::counting_iterator<uint64_t> cit(off);
-        TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
-            return rocprim::select(t, sz, cit, flg.as<uint8_t>(), free_k, cnt_d.as<uint64_t>(), (size_t)c, st);
-        }));
-        uint64_t d = 0;
-        HIP_TRY(hipMemcpy(&d, cnt_d.p, 8, hipMemcpyDeviceToHost));
-        if (d) {
-            TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
-                return rocprim::select(t, sz, grp.as<uint64_t>(), flg.as<uint8_t>(), free_v, cnt_d.as<uint64_t>(),
-                                       (size_t)c, st);
-            }));
-            uint64_t cap_l = ties.cap, cap_g = ties.cap;
-            TRY(append_dev(ties.list, cap_l, ties.cnt, free_k, d, "tied list"));
-            TRY(append_dev(ties.grp, cap_g, ties.cnt, free_v, d, "tied groups"));
-            ties.cap = cap_l;
-            ties.cnt += d;
-        }
-        off += c;
-    }
-    HIP_TRY(hipStreamSynchronize(st));
     return 0;
 }
 
