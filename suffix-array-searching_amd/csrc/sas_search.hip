@@ -259,46 +259,16 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
-__device__ __forceinline__ void cnt_node(const uint4* node, uint32_t K, uint32_t* lt, uint32_t* eq) {
-    uint32_t c = 0, e = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        uint4 v = node[j];
-        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
-        e += (v.x == K) + (v.y == K) + (v.z == K) + (v.w == K);
-    }
-    *lt = c;
-    *eq = e;
-}
 
-__device__ __forceinline__ uint32_t cnt_lt_node(const uint4* node, uint32_t K) {
-    uint32_t c = 0;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        uint4 v = node[j];
-        c += (v.x < K) + (v.y < K) + (v.z < K) + (v.w < K);
-    }
-    return c;
-}
 
-// Per-lane S-tree (one lane per query), used for long queries (QW > 1): the exact
-// tail's text compares dominate there, and four redundant lanes would quadruple them.
-// Descend the internal layers for key K; returns the leaf node index (within
-// the leaf layer).  sst/s_tree.rs:196-203 with unsigned keys.
-__device__ __forceinline__ uint64_t stree_descend1(const SearchArgs& a, const uint4* s_nodes, uint32_t K,
-                                                  uint32_t* probes) {
-    uint64_t k = 0;
-    const uint4* g = reinterpret_cast<const uint4*>(a.stree);
-    uint32_t h = 0;
-    for (; h < a.stree_lds_layers && h + 1 < a.stree_height; h++)
-        k = k * (SAS_STREE_B + 1) + cnt_lt_node(s_nodes + (a.stree_off[h] + k) * 4, K);
-    for (; h + 1 < a.stree_height; h++) k = k * (SAS_STREE_B + 1) + cnt_lt_node(g + (a.stree_off[h] + k) * 4, K);
-    *probes += a.stree_height - 1;
-    return k;
-}
-
+// Long queries (QW > 1): one query per LANE, four queries per 4-lane group.
+// The group walks the S-tree cooperatively for each of its four queries in turn
+// (one request per 64-B node, the 16-char key taken from the owning lane), then
+// every lane runs the exact tail search of its own query in parallel: the descent
+// costs one request per node as in k_sa_stree, and the tail keeps the per-lane
+// parallelism of k_sa_stree1 (where the text compares of long queries dominate).
 template <int QW, int W>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree1(SearchArgs a) {
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree4x(SearchArgs a) {
     const SaView<W> sa{a.sa};
     __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
     {
@@ -307,62 +277,79 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree1(SearchArgs a) {
         __syncthreads();
     }
     uint32_t bad = 0;
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const int lane0 = (int)((threadIdx.x & 63) & ~3u);
     const uint64_t n = a.n;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
     const uint64_t ol = a.stree_off[a.stree_height - 1];
     const uint64_t sa_n = a.sa_n;
     const uint64_t leaf_nodes = (sa_n + 15) / 16;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
-         i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // the loop runs while ANY query of the group is in range (group-uniform)
+    for (uint64_t gi = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) - sub; gi < a.nq; gi += stride) {
+        const uint64_t i = gi + sub;
+        const bool mine = i < a.nq;
         const uint8_t* qb;
-        uint32_t m;
-        query_ptr(a, i, &qb, &m);
+        uint32_t m = 0;
         QueryRegs<QW> q;
-        q.load(qb, m, &bad);
-        const uint32_t K = (uint32_t)(q.w[0] >> 32);  // padded 16-char key of q
+        if (mine) {
+            query_ptr(a, i, &qb, &m);
+            q.load(qb, m, &bad);
+        } else {
+            q.bytes = a.qbytes;
+            q.m = 0;
+            for (int j = 0; j < QW; j++) q.w[j] = 0;
+        }
+        const uint32_t Kmine = (uint32_t)(q.w[0] >> 32);  // padded 16-char key of this lane's query
         uint32_t probes = 0;
-
-        uint64_t k = stree_descend1(a, s_nodes, K, &probes);
-        uint32_t c, e;
-        cnt_node(g + (ol + k) * 4, K, &c, &e);
-        probes++;
-        uint64_t r0 = k * 16 + c;
-        uint64_t r1 = r0 + e;
-        if (c + e == 16) {  // the run of equal keys may continue in the next leaves
-            uint64_t kk = k + 1;
-            int steps = 0;
-            for (; kk < leaf_nodes && steps < 4; kk++, steps++) {
-                uint32_t c2, e2;
-                cnt_node(g + (ol + kk) * 4, K, &c2, &e2);
-                probes++;
-                r1 += e2;
-                if (e2 < 16) break;
-            }
-            if (kk < leaf_nodes && steps == 4) {  // long run: lower_bound(K + 1)
-                if (K == SAS_KEY_MAX) {
-                    r1 = sa_n;
-                } else {
-                    uint64_t k2 = stree_descend1(a, s_nodes, K + 1, &probes);
-                    r1 = k2 * 16 + cnt_lt_node(g + (ol + k2) * 4, K + 1);
-                    probes++;
+        uint64_t my_r0 = 0, my_r1 = 0;
+        for (uint32_t j = 0; j < QUAD_G; j++) {
+            if (gi + j >= a.nq) break;  // group-uniform
+            const uint32_t K = (uint32_t)__shfl((int)Kmine, lane0 + (int)j, 64);
+            uint32_t pr_j = a.stree_height - 1;
+            const uint64_t k = stree_descend(a, s_nodes, K, sub);
+            const uint4 lv = g[(ol + k) * 4 + sub];
+            const uint32_t c = quad_cnt_lt(lv, K), e = quad_cnt_eq(lv, K);
+            pr_j++;
+            uint64_t r0 = k * 16 + c, r1 = r0 + e;
+            if (c + e == 16) {
+                uint64_t kk = k + 1;
+                int steps = 0;
+                for (; kk < leaf_nodes && steps < 4; kk++, steps++) {
+                    const uint32_t e2 = quad_cnt_eq(g[(ol + kk) * 4 + sub], K);
+                    pr_j++;
+                    r1 += e2;
+                    if (e2 < 16) break;
+                }
+                if (kk < leaf_nodes && steps == 4) {
+                    if (K == SAS_KEY_MAX) {
+                        r1 = sa_n;
+                    } else {
+                        const uint64_t k2 = stree_descend(a, s_nodes, K + 1, sub);
+                        pr_j += a.stree_height;
+                        r1 = k2 * 16 + quad_cnt_lt(g[(ol + k2) * 4 + sub], K + 1);
+                    }
                 }
             }
+            if (sub == j) {
+                my_r0 = r0 > sa_n ? sa_n : r0;
+                my_r1 = r1 > sa_n ? sa_n : r1;
+                probes = pr_j;
+            }
         }
-        if (r0 > sa_n) r0 = sa_n;
-        if (r1 > sa_n) r1 = sa_n;
-
-        // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
+        if (!mine) continue;
+        // exact lower bound of this lane's query inside [r0, r1] (per lane)
         const uint32_t h16 = m < 16 ? m : 16;
-        uint64_t l = r0, r = r1;
+        uint64_t l = my_r0, r = my_r1;
         uint32_t llcp = h16, rlcp = h16;
         sa_val_t<W> pr = 0;
         bool have = false;
         while (l < r) {
-            uint64_t mid = (l + r) >> 1;
-            sa_val_t<W> p = (sa_val_t<W>)sa[mid];
+            const uint64_t mid = (l + r) >> 1;
+            const sa_val_t<W> p = (sa_val_t<W>)sa[mid];
             uint32_t lcp;
-            uint32_t h = llcp < rlcp ? llcp : rlcp;
-            bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
+            const uint32_t h = llcp < rlcp ? llcp : rlcp;
+            const bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
             probes++;
             if (lt) {
                 l = mid + 1;
@@ -832,7 +819,7 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 #define K_LCP_TOP(Q) (k_sa_binary<Q, true, true, W>)
 #define K_LCP(Q) (k_sa_binary<Q, true, false, W>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
-#define K_STREE1(Q) (k_sa_stree1<Q, W>)
+#define K_STREE4X(Q) (k_sa_stree4x<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
 #define K_QUAD(Q) (k_sa_quad<Q>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true>)
@@ -844,7 +831,7 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
     } else if (algo == SAS_ALGO_STREE) {
         // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
         if (qw == 1) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
-        else { QW_CASE(K_STREE1) }
+        else { QW_CASE(K_STREE4X) }
     } else if (algo == SAS_ALGO_SECTOR) {  // sector/quad/inline read positions from leaves: W = 4 only
         QW_CASE(K_SECTOR)
     } else if (algo == SAS_ALGO_QUAD) {

@@ -1,5 +1,5 @@
 set -e
-for a in "plain c1" "lcp c1" "stree c1" "plain c3" "stree c3" "sector c3" "quad c1"; do
+for a in "stree c3" "stree c1"; do
   set -- $a
   timeout -k 10 200 python3 tools/ab_old_new.py old $1 $2 2>&1 | grep " ms" | tail -1
   timeout -k 10 200 python3 tools/ab_old_new.py new $1 $2 2>&1 | grep " ms" | tail -1
