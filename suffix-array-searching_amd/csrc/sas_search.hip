@@ -266,7 +266,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
 // (one request per 64-B node, the 16-char key taken from the owning lane), then
 // every lane runs the exact tail search of its own query in parallel: the descent
 // costs one request per node as in k_sa_stree, and the tail keeps the per-lane
-// parallelism of k_sa_stree1 (where the text compares of long queries dominate).
+// parallelism of a one-lane-per-query search (the text compares of long queries dominate).
 template <int QW, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree4x(SearchArgs a) {
     const SaView<W> sa{a.sa};
