@@ -238,16 +238,19 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     BASELINE's "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and
     10^8 positive queries of mixed length 8..256 (random_queries with len in
     [8, 257)), ragged, through sas_search_batch on device buffers.  The sector tree
-    (16 B per suffix) is built only where it fits next to the SA (n <= 2^33)."""
+    and the fused quad leaves (16 B per suffix) fit next to the SA only up to n = 2^33;
+    above, QUAD / INLINE run on compact key-only quad leaves (8 B per suffix,
+    SAS_BUILD_QUAD_COMPACT) and SECTOR falls back to STREE."""
     n = args.n if args.n != 1 << 30 else 1 << 34
     nq = args.nq if args.nq != 10_000_000 else 100_000_000
-    fits = n <= (1 << 33)  # sector / quad leaves: 16 B per suffix next to the 40-bit SA
-    main_algo = args.algo if (args.algo not in ("sector", "quad", "inline") or fits) else "stree"
+    fits = n <= (1 << 33)  # 16 B per suffix next to the 40-bit SA
+    main_algo = args.algo if (args.algo != "sector" or fits) else "stree"
+    quad_mode = ("compact" if (args.quad_compact or not fits) else True) if main_algo in ("quad", "inline") else False
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
     # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
     idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
-                                quad=main_algo in ("quad", "inline"), verify=True)
+                                quad=quad_mode, verify=True)
     stats = idx.stats()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
@@ -305,10 +308,13 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
             ab = stats["stree_layers"] * 64 + max(0.0, mp - stats["stree_layers"]) * (4 + mean_m) + mean_m + 8
         elif algo in ("sector", "quad"):
             # H nodes (leaf = keys + SA), extra leaf probes, the query, the position, and
-            # the packed text window past char 32 for the final compare
+            # the packed text window past char 32 for the final compare (+ the 5-B SA
+            # entry for compact key-only quad leaves)
             H = stats[f"{algo}_layers"]
             node, extra = (32, 12) if algo == "sector" else (64, 64)
             ab = H * node + max(0.0, mp - H) * extra + mean_m + 8 + max(0.0, mean_m - 32) / 4
+            if algo == "quad" and stats["quad_entry_bytes"] == 8:
+                ab += stats["sa_width"]
         else:
             ab = P * (4 + mean_m) + mean_m + 8
         results[algo] = {"lookups_per_s": nq * steps / el, "kernel_ms": kms, "mean_probes": mp,
@@ -326,13 +332,14 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
                        "mean_m": total / nq, "algo": main_algo},
             "roofline": {"bound": "hbm", "achieved": h["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": None,
-                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector",
-                                    "quad": "k_sa_quad"}.get(main_algo, "k_sa_binary"),
+                         "kernel": {"stree": "k_sa_stree4x", "sector": "k_sa_sector", "quad": "k_sa_quad4x",
+                                    "inline": "k_sa_inline"}.get(main_algo, "k_sa_binary"),
                          "kernel_ms": h["kernel_ms"]},
             "variants": results, "setup_s": setup,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
                                             "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
-                                            "stree_bytes", "sector_bytes", "quad_bytes")}}), flush=True)
+                                            "stree_bytes", "sector_bytes", "quad_bytes",
+                                            "quad_entry_bytes")}}), flush=True)
 
 
 def main():
@@ -351,6 +358,8 @@ def main():
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric); c3: largest u32-SA text "
                          "(2^32 - 2^20 chars), 10^8 queries of mixed length 8..256")
+    ap.add_argument("--quad-compact", action="store_true",
+                    help="c3: key-only quad leaves even where the fused ones fit (n <= 2^33)")
     ap.add_argument("--positive", action="store_true", help="sst workload: queries drawn from the keys")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "

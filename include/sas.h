@@ -54,6 +54,11 @@ typedef struct sas_index sas_index;
                                         bucketed 64-bit builder at any n (automatic for
                                         n >= 2^32 - 64; test hook below that)             */
 #define SAS_BUILD_QUAD    (1u << 9)  /* also build the quad tree (SAS_ALGO_QUAD)         */
+#define SAS_BUILD_QUAD_COMPACT (1u << 10) /* build the quad tree with key-only leaves: 8 B
+                                        per suffix (eight 32-char keys per 64-B leaf) instead
+                                        of 16, SA values read from the SA array.  Fits next to
+                                        a 40-bit SA at n = 2^34 in one GPU's HBM.  Implies
+                                        SAS_BUILD_QUAD                                     */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {
@@ -92,6 +97,8 @@ typedef struct sas_stats {
     uint64_t quad_bytes;     /* quad tree (inner nodes + leaves), 0 if not built   */
     uint32_t quad_layers;    /* quad tree height incl. the leaf layer              */
     uint32_t quad_lds_layers; /* its layers served from LDS                       */
+    uint32_t quad_entry_bytes; /* quad leaf bytes per suffix: 16 (fused key + SA),
+                                  8 (SAS_BUILD_QUAD_COMPACT), 0 if not built        */
 } sas_stats;
 
 const char* sas_last_error(void);

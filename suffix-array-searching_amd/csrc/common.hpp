@@ -94,6 +94,8 @@ struct sas_index {
     // quad tree (SAS_ALGO_QUAD): 64-B nodes, one 4-lane cooperative load each
     uint4* quad_inner = nullptr;     // internal nodes, 16 u32 16-char separators (4 x uint4), root first
     uint4* quad_leaves = nullptr;    // entry x = {key lo, key hi, sa lo32, sa bits 32..39}; leaf = 4 entries
+                                     // compact (SAS_BUILD_QUAD_COMPACT): entry x = key64 only; leaf = 8 entries
+    uint32_t quad_compact = 0;       // 1: key-only leaves, SA values read from `sa`
     uint64_t quad_leaf_count = 0;
     uint64_t quad_off[SAS_QUAD_MAX_LAYERS] = {};
     uint32_t quad_inner_layers = 0;

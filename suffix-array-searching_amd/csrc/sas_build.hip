@@ -595,27 +595,38 @@ __global__ void k_quad_leaves(const uint64_t* __restrict__ tw, SaView<W> sa, uin
     }
 }
 
+// Compact leaves: entry x = key64 of rank x only; leaf i = entries 8i..8i+7 (lane j
+// of a group loads keys 2j, 2j+1).  Padding keys are all ones.
+template <int W>
+__global__ void k_quad_keys(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n,
+                            uint64_t* __restrict__ keys, uint64_t entries) {
+    GRID_STRIDE(x, entries) keys[x] = x < sa_n ? text_chars32(tw, sa[x]) : ~0ull;
+}
+
 // Internal layer, left-max (as k_sector_layer, 17-ary): separator j of node i =
-// 16-char key of the last entry of child 17i+j's subtree (child_span leaves),
-// 0xFFFFFFFF for the globally last child and beyond.
+// 16-char key of the last entry of child 17i+j's subtree (child_span leaves of epl
+// entries), 0xFFFFFFFF for the globally last child and beyond.  Fused leaves hold
+// the key's high word at uint32 4x+1, compact ones at 2x+1.
 __global__ void k_quad_layer(uint32_t* __restrict__ inner, uint64_t oh, uint64_t layer_nodes, uint64_t child_span,
-                             uint64_t child_layer_nodes, const uint4* __restrict__ leaves, uint64_t sa_n) {
+                             uint64_t child_layer_nodes, const uint32_t* __restrict__ leaves, uint64_t sa_n,
+                             uint32_t epl) {
     GRID_STRIDE(i, 16 * layer_nodes) {
         uint64_t node = i / 16, j = i % 16;
         uint64_t child = node * SAS_QUAD_FAN + j;
         uint32_t sep = 0xFFFFFFFFu;
         if (child + 1 < child_layer_nodes) {
-            uint64_t last = 4 * (child + 1) * child_span - 1;
+            uint64_t last = epl * (child + 1) * child_span - 1;
             if (last >= sa_n) last = sa_n - 1;
-            sep = leaves[last].y;
+            sep = leaves[(epl == 4 ? 4 : 2) * last + 1];
         }
         inner[(oh + node) * 16 + j] = sep;
     }
 }
 
-static int build_quad(sas_index* x) {
+static int build_quad(sas_index* x, bool compact) {
     const uint64_t sa_n = x->sa_n;
-    const uint64_t nl = (sa_n + 3) / 4;
+    const uint32_t epl = compact ? 8 : 4;  // entries per 64-B leaf
+    const uint64_t nl = (sa_n + epl - 1) / epl;
     uint64_t sizes[SAS_QUAD_MAX_LAYERS];
     uint32_t H = 0;
     uint64_t c = nl;
@@ -632,17 +643,20 @@ static int build_quad(sas_index* x) {
     DevBuf leaves, inner;
     TRY(leaves.alloc(nl * 64, "quad leaves"));
     TRY(inner.alloc(tot * 64, "quad inner nodes"));
-    if (x->sa_w == 5)
-        hipLaunchKernelGGL(k_quad_leaves<5>, dim3(grid_for(4 * nl)), dim3(256), 0, 0, x->text_w, SaView<5>{x->sa},
-                           sa_n, leaves.as<uint4>(), 4 * nl);
+    const dim3 lg(grid_for(epl * nl)), lb(256);
+    if (compact && x->sa_w == 5)
+        hipLaunchKernelGGL(k_quad_keys<5>, lg, lb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, leaves.as<uint64_t>(), 8 * nl);
+    else if (compact)
+        hipLaunchKernelGGL(k_quad_keys<4>, lg, lb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, leaves.as<uint64_t>(), 8 * nl);
+    else if (x->sa_w == 5)
+        hipLaunchKernelGGL(k_quad_leaves<5>, lg, lb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, leaves.as<uint4>(), 4 * nl);
     else
-        hipLaunchKernelGGL(k_quad_leaves<4>, dim3(grid_for(4 * nl)), dim3(256), 0, 0, x->text_w, SaView<4>{x->sa},
-                           sa_n, leaves.as<uint4>(), 4 * nl);
+        hipLaunchKernelGGL(k_quad_leaves<4>, lg, lb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, leaves.as<uint4>(), 4 * nl);
     uint64_t span = 1, child_nodes = nl;
     for (int h = (int)H - 1; h >= 0; h--) {
         uint64_t ln = sizes[H - 1 - h];
         hipLaunchKernelGGL(k_quad_layer, dim3(grid_for(16 * ln)), dim3(256), 0, 0, inner.as<uint32_t>(),
-                           x->quad_off[h], ln, span, child_nodes, leaves.as<uint4>(), sa_n);
+                           x->quad_off[h], ln, span, child_nodes, leaves.as<uint32_t>(), sa_n, epl);
         span *= SAS_QUAD_FAN;
         child_nodes = ln;
     }
@@ -650,6 +664,7 @@ static int build_quad(sas_index* x) {
     x->quad_leaves = static_cast<uint4*>(leaves.release());
     x->quad_inner = static_cast<uint4*>(inner.release());
     x->quad_leaf_count = nl;
+    x->quad_compact = compact ? 1 : 0;
     x->quad_inner_layers = H;
     x->quad_inner_nodes = tot;
     uint32_t L = 0;
@@ -938,7 +953,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     }
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
     if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
-    if (flags & SAS_BUILD_QUAD) TRY(build_quad(x));
+    if (flags & (SAS_BUILD_QUAD | SAS_BUILD_QUAD_COMPACT)) TRY(build_quad(x, (flags & SAS_BUILD_QUAD_COMPACT) != 0));
 
     // binary-search top in LDS
     {
@@ -982,6 +997,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.quad_bytes = (x->quad_inner_nodes + x->quad_leaf_count) * 64;
     st.quad_layers = x->quad_leaves ? x->quad_inner_layers + 1 : 0;
     st.quad_lds_layers = x->quad_lds_layers;
+    st.quad_entry_bytes = x->quad_leaves ? (x->quad_compact ? 8 : 16) : 0;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -602,32 +602,80 @@ __device__ __forceinline__ uint64_t quad_key32(const uint8_t* __restrict__ qb, u
     return ((uint64_t)hi << 32) | lo;
 }
 
-// Evaluate leaf L: mask of its entries x (< sa_n) satisfying the bound's predicate
-// (UPPER = false: suffix(x) >= q; UPPER = true: the first min(m, len) chars of
-// suffix(x) are > q, sector_gt_prefix); *p = this lane's SA value.
-template <int QW, bool UPPER>
+// Leaf formats (KO = key-only, SAS_BUILD_QUAD_COMPACT):
+//   fused: entry x = 16 B {key64, SA lo32, SA bits 32..39}, 4 per 64-B leaf
+//   KO:    entry x = key64, 8 per 64-B leaf; SA values come from the SA array
+// Per-lane reads of one entry (the tails of the 4x kernel, INLINE's probes):
+template <bool KO>
+__device__ __forceinline__ uint64_t quad_entry_key(const SearchArgs& a, uint64_t x) {
+    if (KO) return reinterpret_cast<const uint64_t*>(a.quad_leaves)[x];
+    const uint2 k = reinterpret_cast<const uint2*>(a.quad_leaves)[2 * x];
+    return (uint64_t)k.x | ((uint64_t)k.y << 32);
+}
+template <bool KO, int W>
+__device__ __forceinline__ uint64_t quad_entry_sa(const SearchArgs& a, uint64_t x) {
+    if (KO) return SaView<W>{a.sa}[x];
+    const uint2 s = reinterpret_cast<const uint2*>(a.quad_leaves)[2 * x + 1];
+    return (uint64_t)s.x | ((uint64_t)(s.y & 0xFFu) << 32);
+}
+
+#define QUAD_NO_SA (~0ull)  // "SA value not read yet" (never a valid 40-bit SA)
+
+// Evaluate leaf L for the bound's predicate (UPPER = false: suffix(x) >= q;
+// UPPER = true: the first min(m, len) chars of suffix(x) are > q, sector_gt_prefix).
+// Returns the first qualifying entry of the leaf (EPL if none; entries x >= sa_n
+// never qualify) and *p = its SA value, group-uniform (KO: QUAD_NO_SA when the
+// predicate did not need it).  Fused leaves: lane j holds entry j; KO leaves: lane j
+// holds entries 2j, 2j+1 and reads an SA value only for an entry whose key ties q's.
+template <int QW, bool UPPER, bool KO, int W>
 __device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64, uint64_t Q3,
                                               uint64_t L, uint32_t sub, uint64_t* p) {
-    const uint64_t x = 4 * L + sub;
-    const uint4 e = a.quad_leaves[x];
-    const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
-    const uint64_t pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
-    *p = pp;
-    // short-circuit: padding entries (x >= sa_n) carry SA = all ones and must never
+    const int lane0 = (int)((threadIdx.x & 63) & ~3u);
+    const uint4 e = a.quad_leaves[4 * L + sub];
+    // short-circuit: padding entries (x >= sa_n) carry all-ones keys/SA and must never
     // reach the predicate (its m > 32 text compare would read past the text)
-    const bool t = x < a.sa_n &&
-                   (UPPER ? sector_gt_prefix<QW>(key, pp, K64, Q3, a, q) : sector_ge<QW>(key, pp, K64, a, q));
-    return quad_mask(t);
+    auto pred = [&](uint64_t key, uint64_t pp) -> bool {
+        return UPPER ? sector_gt_prefix<QW>(key, pp, K64, Q3, a, q) : sector_ge<QW>(key, pp, K64, a, q);
+    };
+    if (!KO) {
+        const uint64_t x = 4 * L + sub;
+        const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        const uint64_t pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+        const uint32_t mk = quad_mask(x < a.sa_n && pred(key, pp));
+        const uint32_t f = mk ? (uint32_t)__builtin_ctz(mk) : 4u;
+        *p = __shfl((unsigned long long)pp, lane0 + (int)(f & 3), 64);
+        return f;
+    }
+    const uint64_t x0 = 8 * L + 2 * sub;
+    const uint64_t k0 = (uint64_t)e.x | ((uint64_t)e.y << 32), k1 = (uint64_t)e.z | ((uint64_t)e.w << 32);
+    // the SA value matters only on a tie with q's 32-char key (UPPER with m <= 32: never)
+    const bool tie_ok = !(UPPER && q.m <= 32);
+    uint64_t p0 = QUAD_NO_SA, p1 = QUAD_NO_SA;
+    if (tie_ok && k0 == K64 && x0 < a.sa_n) p0 = quad_entry_sa<true, W>(a, x0);
+    if (tie_ok && k1 == K64 && x0 + 1 < a.sa_n) p1 = quad_entry_sa<true, W>(a, x0 + 1);
+    const bool t0 = x0 < a.sa_n && pred(k0, p0);
+    const bool t1 = x0 + 1 < a.sa_n && pred(k1, p1);
+    const uint32_t many = quad_mask(t0 || t1), m0 = quad_mask(t0);
+    if (!many) {
+        *p = QUAD_NO_SA;
+        return 8;
+    }
+    const uint32_t j = (uint32_t)__builtin_ctz(many);
+    const uint32_t s = ((m0 >> j) & 1u) ? 0u : 1u;  // entry 2j (t0) or 2j+1
+    *p = __shfl((unsigned long long)(s ? p1 : p0), lane0 + (int)j, 64);
+    return 2 * j + s;
 }
 
 // First local rank with the bound's predicate (monotone over ranks): descent on the
 // 16-char routing key, the routed leaf, then (rare) an exponential + binary search
 // over later leaves for a run of equal routing keys that crosses leaves.  Returns
-// sa_n if no entry qualifies; *px = SA at the returned rank (group-uniform).
-template <int QW, bool UPPER>
+// sa_n if no entry qualifies; *px = SA at the returned rank (group-uniform;
+// QUAD_NO_SA if a KO leaf did not need it).
+template <int QW, bool UPPER, bool KO, int W>
 __device__ __forceinline__ uint64_t quad_bound(const SearchArgs& a, const uint4* s_nodes, const QueryRegs<QW>& q,
                                                uint64_t K64, uint64_t Q3, uint32_t sub, uint32_t* probes,
                                                uint64_t* px) {
+    constexpr uint32_t EPL = KO ? 8 : 4;
     const uint32_t R16 = (uint32_t)(((UPPER && q.m <= 32) ? Q3 : K64) >> 32);
     const uint64_t nl = a.quad_leaf_count;
     uint64_t k = 0;
@@ -645,9 +693,9 @@ __device__ __forceinline__ uint64_t quad_bound(const SearchArgs& a, const uint4*
     *probes += a.quad_inner_layers + 1;
     // routed leaf k: every entry before it fails the predicate
     uint64_t pl;
-    uint32_t mk = quad_leaf<QW, UPPER>(a, q, K64, Q3, k, sub, &pl);
+    uint32_t f = quad_leaf<QW, UPPER, KO, W>(a, q, K64, Q3, k, sub, &pl);
     uint64_t L = k;
-    if (!mk) {
+    if (f == EPL) {
         // leaf nl = virtual: past every entry
         uint64_t lo = k + 1, step = 1, hi = nl;
         while (lo < nl) {
@@ -655,7 +703,7 @@ __device__ __forceinline__ uint64_t quad_bound(const SearchArgs& a, const uint4*
             if (hi >= nl) { hi = nl; break; }
             uint64_t pp;
             (*probes)++;
-            if (quad_leaf<QW, UPPER>(a, q, K64, Q3, hi, sub, &pp)) break;
+            if (quad_leaf<QW, UPPER, KO, W>(a, q, K64, Q3, hi, sub, &pp) < EPL) break;
             lo = hi + 1;
             step *= 2;
             hi = nl;
@@ -664,19 +712,18 @@ __device__ __forceinline__ uint64_t quad_bound(const SearchArgs& a, const uint4*
             uint64_t mid = (lo + hi) >> 1;
             uint64_t pp;
             (*probes)++;
-            if (quad_leaf<QW, UPPER>(a, q, K64, Q3, mid, sub, &pp)) hi = mid;
+            if (quad_leaf<QW, UPPER, KO, W>(a, q, K64, Q3, mid, sub, &pp) < EPL) hi = mid;
             else lo = mid + 1;
         }
         L = lo;
         if (L < nl) {
-            mk = quad_leaf<QW, UPPER>(a, q, K64, Q3, L, sub, &pl);
+            f = quad_leaf<QW, UPPER, KO, W>(a, q, K64, Q3, L, sub, &pl);
             (*probes)++;
         }
     }
-    if (!mk) return a.sa_n;
-    const uint32_t f = __builtin_ctz(mk);
-    *px = __shfl((unsigned long long)pl, (int)(((threadIdx.x & 63) & ~3u) + f), 64);
-    return 4 * L + f;
+    if (f == EPL) return a.sa_n;
+    *px = pl;
+    return EPL * L + f;
 }
 
 __device__ __forceinline__ void stage_quad_top(const SearchArgs& a, uint4* s_nodes) {
@@ -684,7 +731,7 @@ __device__ __forceinline__ void stage_quad_top(const SearchArgs& a, uint4* s_nod
     __syncthreads();
 }
 
-template <int QW>
+template <int QW, bool KO, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
     __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
     stage_quad_top(a, s_nodes);
@@ -705,7 +752,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
         }
         uint32_t probes = 0;
         uint64_t px = 0;
-        const uint64_t x = quad_bound<QW, false>(a, s_nodes, q, q.w[0], 0, sub, &probes, &px);
+        const uint64_t x = quad_bound<QW, false, KO, W>(a, s_nodes, q, q.w[0], 0, sub, &probes, &px);
+        if (KO && x < a.sa_n && px == QUAD_NO_SA) px = quad_entry_sa<true, W>(a, x);  // group-uniform address
         if (sub == 0) {
             a.out_pos[i] = (x >= a.sa_n) ? a.next_pos : px;
             if (a.out_probes) a.out_probes[i] = probes;
@@ -714,9 +762,132 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// Long queries (QW > 1), as k_sa_stree4x: one query per LANE, four per 4-lane group.
+// The group descends the quad tree and reads the routed leaf cooperatively for each
+// of its four queries in turn (one request per 64-B node), which places each query
+// at x0 = the first entry of that leaf whose 32-char key is >= its own (the entry's
+// key and fused SA value travel to the owning lane by a shuffle).  Every entry
+// before x0 is < q.  Then every lane finishes its own query: the predicate at x0
+// (typically a key tie -> one text compare from char 32, the part that dominates for
+// long queries), and in the rare case it fails an exponential + binary search over
+// the following entries.
+template <int QW, bool KO, int W>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
+    constexpr uint32_t EPL = KO ? 8 : 4;
+    __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
+    stage_quad_top(a, s_nodes);
+    uint32_t bad = 0;
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const int lane0 = (int)((threadIdx.x & 63) & ~3u);
+    const uint64_t sa_n = a.sa_n;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    // the loop runs while ANY query of the group is in range (group-uniform)
+    for (uint64_t gi = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) - sub; gi < a.nq; gi += stride) {
+        const uint64_t i = gi + sub;
+        const bool mine = i < a.nq;
+        const uint8_t* qb;
+        uint32_t m = 0;
+        QueryRegs<QW> q;
+        if (mine) {
+            query_ptr(a, i, &qb, &m);
+            q.load(qb, m, &bad);
+        } else {
+            q.bytes = a.qbytes;
+            q.m = 0;
+            for (int j = 0; j < QW; j++) q.w[j] = 0;
+        }
+        const uint64_t Kmine = q.w[0];  // padded 32-char key of this lane's query
+        uint32_t probes = a.quad_inner_layers + 1;
+        uint64_t x0 = 0, key0 = 0, p0 = QUAD_NO_SA;
+        bool known = false;
+        for (uint32_t j = 0; j < QUAD_G; j++) {
+            if (gi + j >= a.nq) break;  // group-uniform
+            const uint64_t K64 = __shfl((unsigned long long)Kmine, lane0 + (int)j, 64);
+            const uint32_t R16 = (uint32_t)(K64 >> 32);
+            uint64_t k = 0;
+            uint32_t h = 0;
+            for (; h < a.quad_lds_layers; h++) {
+                const uint4 v = s_nodes[(a.quad_off[h] + k) * 4 + sub];
+                k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+            }
+            for (; h < a.quad_inner_layers; h++) {
+                const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
+                k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+            }
+            const uint4 e = a.quad_leaves[4 * k + sub];
+            uint64_t ksel, psel = QUAD_NO_SA;
+            uint32_t c;
+            if (KO) {
+                const uint64_t ka = (uint64_t)e.x | ((uint64_t)e.y << 32), kb = (uint64_t)e.z | ((uint64_t)e.w << 32);
+                c = quad_sum((ka < K64) + (kb < K64));
+                ksel = (c & 1) ? kb : ka;
+            } else {
+                ksel = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                psel = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+                c = quad_sum(ksel < K64);
+            }
+            const int src = lane0 + (int)((KO ? c >> 1 : c) & 3);
+            const uint64_t kc = __shfl((unsigned long long)ksel, src, 64);
+            const uint64_t pc = KO ? QUAD_NO_SA : __shfl((unsigned long long)psel, src, 64);
+            if (sub == j) {
+                x0 = EPL * k + c;
+                known = c < EPL;  // else x0 starts the next leaf: nothing read for it yet
+                key0 = kc;
+                p0 = known ? pc : QUAD_NO_SA;
+            }
+        }
+        if (!mine) continue;
+        const uint64_t K64 = Kmine;
+        // predicate at x0 with the values the leaf read already delivered
+        bool ok = false;
+        if (x0 < sa_n) {
+            const uint64_t key = known ? key0 : quad_entry_key<KO>(a, x0);
+            if (key != K64) {
+                ok = key > K64;
+            } else {
+                if (p0 == QUAD_NO_SA) p0 = quad_entry_sa<KO, W>(a, x0);
+                ok = sector_ge<QW, true>(key, p0, K64, a, q);
+            }
+            if (!known) probes++;
+        }
+        uint64_t x = x0;
+        if (!ok && x0 < sa_n) {  // rare: exponential + binary search over x0+1 ..
+            auto pred = [&](uint64_t y) -> bool {
+                const uint64_t key = quad_entry_key<KO>(a, y);
+                if (key != K64) return key > K64;
+                return sector_ge<QW, true>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
+            };
+            uint64_t lo = x0 + 1, hi = sa_n, step = 1;
+            while (lo < sa_n) {
+                hi = lo + step - 1;
+                if (hi >= sa_n) { hi = sa_n; break; }
+                probes++;
+                if (pred(hi)) break;
+                lo = hi + 1;
+                step *= 2;
+                hi = sa_n;
+            }
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                probes++;
+                if (pred(mid)) hi = mid;
+                else lo = mid + 1;
+            }
+            x = lo;
+            p0 = QUAD_NO_SA;
+        }
+        uint64_t pos;
+        if (x >= sa_n) pos = a.next_pos;
+        else pos = (p0 != QUAD_NO_SA) ? p0 : quad_entry_sa<KO, W>(a, x);
+        a.out_pos[i] = pos;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // Occurrence ranges on the quad tree: global ranks [lo, hi) of the suffixes
 // that start with q (out_pos = lo, out_hi = hi), as k_sa_sector_range.
-template <int QW>
+template <int QW, bool KO, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a, uint64_t* out_hi) {
     __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
     stage_quad_top(a, s_nodes);
@@ -733,8 +904,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a,
         const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
         uint32_t probes = 0;
         uint64_t px = 0;
-        const uint64_t lo = quad_bound<QW, false>(a, s_nodes, q, K64, Q3, sub, &probes, &px);
-        uint64_t hi = quad_bound<QW, true>(a, s_nodes, q, K64, Q3, sub, &probes, &px);
+        const uint64_t lo = quad_bound<QW, false, KO, W>(a, s_nodes, q, K64, Q3, sub, &probes, &px);
+        uint64_t hi = quad_bound<QW, true, KO, W>(a, s_nodes, q, K64, Q3, sub, &probes, &px);
         if (hi < lo) hi = lo;
         if (sub == 0) {
             a.out_pos[i] = a.rank_lo + lo;
@@ -748,10 +919,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a,
 // ------------------------------------------------------------------ INLINE
 // binary_search_batch<64>'s probes (sas/sa_search.rs:157-196: same mids, same
 // ilog2(n)+1 lockstep iterations, same LDS top as PLAIN) but each probe reads the
-// fused 16-B entry {key64, SA} of the quad leaves: the 32-char key decides unless
-// it equals the query's (then the text from char 32), so a len-32 probe is one
-// memory request instead of an SA word + two text words.
-template <int QW, bool TOP>
+// quad leaves' entry: the 32-char key decides unless it equals the query's (then
+// the SA value -- in the fused entry, or from the SA array for KO leaves -- and the
+// text from char 32), so a len-32 probe is one memory request instead of an SA
+// word + two text words.
+template <int QW, bool TOP, bool KO, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
     __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
     __shared__ uint64_t s_sa[TOP ? SAS_TOP_NODES : 1];
@@ -773,7 +945,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
-        uint64_t l = 0, r = a.sa_n, pr = 0;
+        uint64_t l = 0, r = a.sa_n, pr = QUAD_NO_SA;
         uint32_t k = 1, probes = 0;
         for (uint32_t it = 0; it < a.iters; ++it) {
             if (l < r) {
@@ -782,6 +954,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                 if (TOP && it < D) {
                     key = s_key[k];
                     p = s_sa[k];
+                } else if (KO) {
+                    key = quad_entry_key<true>(a, mid);
+                    p = key == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
                 } else {
                     const uint4 e = a.quad_leaves[mid];
                     key = (uint64_t)e.x | ((uint64_t)e.y << 32);
@@ -798,7 +973,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                 }
             }
         }
-        a.out_pos[i] = (r >= a.sa_n) ? a.next_pos : pr;
+        if (r >= a.sa_n) pr = a.next_pos;
+        else if (KO && pr == QUAD_NO_SA) pr = quad_entry_sa<true, W>(a, r);
+        a.out_pos[i] = pr;
         if (a.out_probes) a.out_probes[i] = probes;
     }
     if (bad) atomicOr(a.bad, 1u);
@@ -821,9 +998,6 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 #define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_STREE4X(Q) (k_sa_stree4x<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
-#define K_QUAD(Q) (k_sa_quad<Q>)
-#define K_INLINE_TOP(Q) (k_sa_inline<Q, true>)
-#define K_INLINE(Q) (k_sa_inline<Q, false>)
     if (algo == SAS_ALGO_PLAIN) {
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
@@ -832,10 +1006,30 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
         // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
         if (qw == 1) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
         else { QW_CASE(K_STREE4X) }
-    } else if (algo == SAS_ALGO_SECTOR) {  // sector/quad/inline read positions from leaves: W = 4 only
+    } else {  // SAS_ALGO_SECTOR: positions come from the fused leaves, W = 4 only
         QW_CASE(K_SECTOR)
-    } else if (algo == SAS_ALGO_QUAD) {
-        QW_CASE(K_QUAD)
+    }
+#undef QW_CASE
+}
+
+// QUAD / INLINE: fused leaves read no SA (W = 4 instantiation only); KO leaves read
+// SA values through SaView<W>.
+template <bool KO, int W>
+static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
+#define QW_CASE(KERNEL_T)                                                           \
+    switch (qw) {                                                                   \
+        case 1: hipLaunchKernelGGL(KERNEL_T(1), grid, block, 0, st, a); break;      \
+        case 2: hipLaunchKernelGGL(KERNEL_T(2), grid, block, 0, st, a); break;      \
+        case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
+        default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
+    }
+#define K_QUAD4X(Q) (k_sa_quad4x<Q, KO, W>)
+#define K_INLINE_TOP(Q) (k_sa_inline<Q, true, KO, W>)
+#define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
+    if (algo == SAS_ALGO_QUAD) {
+        // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
+        if (qw == 1) hipLaunchKernelGGL((k_sa_quad<1, KO, W>), grid, block, 0, st, a);
+        else { QW_CASE(K_QUAD4X) }
     } else {
         if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
     }
@@ -843,7 +1037,7 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    const bool coop = algo == SAS_ALGO_QUAD || (algo == SAS_ALGO_STREE && qw == 1);
+    const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
     const uint64_t lanes = a.nq * (coop ? QUAD_G : 1);
     uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
@@ -851,8 +1045,15 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     if (blocks == 0) return 0;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
-    if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR && algo != SAS_ALGO_QUAD && algo != SAS_ALGO_INLINE) launch_w<5>(algo, top, qw, grid, block, st, a);
-    else launch_w<4>(algo, top, qw, grid, block, st, a);
+    if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) {
+        if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
+        else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);
+        else launch_quad<true, 4>(algo, top, qw, grid, block, st, a);
+    } else if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR) {
+        launch_w<5>(algo, top, qw, grid, block, st, a);
+    } else {
+        launch_w<4>(algo, top, qw, grid, block, st, a);
+    }
     HIP_TRY(hipGetLastError());
     return 0;
 }
@@ -1202,6 +1403,16 @@ extern "C" int sas_route_pack(const sas_index* x, const uint64_t* splitter_pos, 
 }
 
 // ------------------------------------------------------------------ occurrence ranges
+template <bool KO, int W>
+static void launch_quad_range(int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a, uint64_t* dhi) {
+    switch (qw) {
+        case 1: hipLaunchKernelGGL((k_sa_quad_range<1, KO, W>), grid, block, 0, st, a, dhi); break;
+        case 2: hipLaunchKernelGGL((k_sa_quad_range<2, KO, W>), grid, block, 0, st, a, dhi); break;
+        case 4: hipLaunchKernelGGL((k_sa_quad_range<4, KO, W>), grid, block, 0, st, a, dhi); break;
+        default: hipLaunchKernelGGL((k_sa_quad_range<8, KO, W>), grid, block, 0, st, a, dhi); break;
+    }
+}
+
 extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
                                 uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
@@ -1254,13 +1465,11 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    if (quad) {
-        switch (qw) {
-            case 1: hipLaunchKernelGGL(k_sa_quad_range<1>, grid, block, 0, st, a, dhi); break;
-            case 2: hipLaunchKernelGGL(k_sa_quad_range<2>, grid, block, 0, st, a, dhi); break;
-            case 4: hipLaunchKernelGGL(k_sa_quad_range<4>, grid, block, 0, st, a, dhi); break;
-            default: hipLaunchKernelGGL(k_sa_quad_range<8>, grid, block, 0, st, a, dhi); break;
-        }
+    if (quad && !x->quad_compact) {
+        launch_quad_range<false, 4>(qw, grid, block, st, a, dhi);
+    } else if (quad) {
+        if (x->sa_w == 5) launch_quad_range<true, 5>(qw, grid, block, st, a, dhi);
+        else launch_quad_range<true, 4>(qw, grid, block, st, a, dhi);
     } else {
         switch (qw) {
             case 1: hipLaunchKernelGGL(k_sa_sector_range<1>, grid, block, 0, st, a, dhi); break;

@@ -45,6 +45,14 @@ def _as_u8(x):
     return np.ascontiguousarray(np.frombuffer(x, np.uint8) if isinstance(x, (bytes, bytearray)) else x, np.uint8)
 
 
+def _quad_flags(quad) -> int:
+    if quad == "compact":
+        return _lib.SAS_BUILD_QUAD_COMPACT
+    if quad in (True, False):
+        return _lib.SAS_BUILD_QUAD if quad else 0
+    raise ValueError(f"quad must be True, False or 'compact', not {quad!r}")
+
+
 class SaNaive:
     """GPU-resident suffix-array index: 2-bit packed text, u32 SA, optional LCP
     array and S-tree over 16-char SA keys, all in HBM."""
@@ -58,17 +66,18 @@ class SaNaive:
     @classmethod
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
-              sa40: bool = False, quad: bool = True) -> "SaNaive":
+              sa40: bool = False, quad: bool | str = True) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
-        builder even when n < 2^32 (automatic above)."""
+        builder even when n < 2^32 (automatic above).  quad="compact": key-only quad
+        leaves (8 B per suffix, SA values read from the SA array; SAS_BUILD_QUAD_COMPACT)."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         flags |= _lib.SAS_BUILD_SA40 if sa40 else 0
-        flags |= _lib.SAS_BUILD_QUAD if quad else 0
+        flags |= _quad_flags(quad)
         sa_ptr, sa_w = None, 4
         if sa is not None:
             if _is_cuda(t) != _is_cuda(sa):
@@ -92,7 +101,7 @@ class SaNaive:
 
     @classmethod
     def build_part(cls, t, part: int, parts: int, lcp: bool = True, stree: bool = True, verify: bool = False,
-                   flags: int = 0, sector: bool = True, quad: bool = True) -> "SaNaive":
+                   flags: int = 0, sector: bool = True, quad: bool | str = True) -> "SaNaive":
         """Sharded-text index that builds ONLY its own SA rank range (sas_build_part):
         part `part` of `parts` contiguous 7-char-prefix bin ranges.  The range is
         chosen by the library (stats: rank_lo, sa_entries, next_pos)."""
@@ -100,7 +109,7 @@ class SaNaive:
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
-        flags |= _lib.SAS_BUILD_QUAD if quad else 0
+        flags |= _quad_flags(quad)
         if _is_cuda(t):
             flags |= _lib.SAS_DEVICE_PTRS
         h = C.c_void_p()

@@ -352,6 +352,53 @@ def test_occurrence_ranges_both_trees(sas, sadef):
                               s_only.search_batch(buf, off, lens, algo="sector")), n
 
 
+def test_compact_quad_leaves(sas, sadef):
+    """SAS_BUILD_QUAD_COMPACT: key-only quad leaves (8 per 64-B leaf, SA values from the
+    SA array), u32 and 40-bit SA.  QUAD (cooperative m <= 32 kernel and the 4x kernel
+    for longer queries), INLINE and occurrence ranges equal the oracle / the fused
+    index on the definition fixtures, random, all-zero, periodic and repeat texts."""
+    rng = np.random.default_rng(44)
+    for c in sadef["cases"]:
+        t = np.array(c["text"], np.uint8)
+        buf, off, lens = pack([q["q"] for q in c["queries"]])
+        expect = np.array([q["pos"] for q in c["queries"]], np.uint64)
+        for sa40 in (False, True):
+            idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad="compact", sa40=sa40)
+            assert idx.stats()["quad_entry_bytes"] == 8
+            for algo in ("quad", "inline"):
+                assert np.array_equal(idx.search_batch(buf, off, lens, algo=algo), expect), (c["name"], sa40, algo)
+            lo, _ = idx.search_range(buf, off, lens)
+            assert lo.tolist() == [q["rank"] for q in c["queries"]], c["name"]
+    blk = rng.integers(0, 4, 3000, dtype=np.uint8)
+    texts = [sas.random_string(2_000_003, seed=9), np.zeros(40_000, np.uint8),
+             np.tile(rng.integers(0, 4, 7, dtype=np.uint8), 12_000),
+             np.concatenate([blk, blk, rng.integers(0, 4, 999, dtype=np.uint8), blk, blk[:1777]])]
+    for t in texts:
+        n = len(t)
+        fused = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=True)
+        sa = fused.suffix_array()
+        assert fused.stats()["quad_entry_bytes"] == 16
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 300, 3000), rng.integers(1, 300, 3000))]
+        qs += [rng.integers(0, 4, rng.integers(0, 70), dtype=np.uint8) for _ in range(800)]
+        qs += [np.full(l, 3, np.uint8) for l in (1, 31, 32, 33, 200)] + [t[n - k:] for k in (1, 5, 32, 40)]
+        buf, off, lens = pack(qs)
+        expect = oracle_positions(t, sa, buf, off, lens)
+        q32 = [t[o:o + 32] for o in rng.integers(0, n - 32, 3000)] + [np.full(32, 3, np.uint8)]
+        b32 = np.concatenate(q32)
+        e32 = oracle_positions(t, sa, b32, np.arange(len(q32), dtype=np.uint64) * 32,
+                               np.full(len(q32), 32, np.uint32))
+        flo, fhi = fused.search_range(buf, off, lens)
+        for sa40 in (False, True):
+            idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad="compact", sa40=sa40)
+            st = idx.stats()
+            assert st["quad_bytes"] < fused.stats()["quad_bytes"] * 0.6
+            for algo in ("quad", "inline"):
+                assert np.array_equal(idx.search_batch(buf, off, lens, algo=algo), expect), (n, sa40, algo)
+                assert np.array_equal(idx.search_fixed(b32, 32, algo=algo), e32), (n, sa40, algo)
+            lo, hi = idx.search_range(buf, off, lens)
+            assert np.array_equal(lo, flo) and np.array_equal(hi, fhi), (n, sa40)
+
+
 def test_kmer_keys_match_reference_loop(sas):
     """sst/bin/bench.rs:58-76 (--human keys), restated as the reference's loop."""
     t = sas.random_string(5000, seed=2)
@@ -457,6 +504,17 @@ def test_sa_beyond_u32(sas):
                 last = int(idx.suffix_array(count=1, start=occ_hi - 1)[0])
                 assert bytes(ht[last:last + len(q)]) == qb
     assert big > 0  # positions above 2^32 were returned
+    # compact quad leaves at the same n: SA values (above 2^32) come from the 40-bit array
+    del idx
+    torch.cuda.empty_cache()
+    tc = torch.from_numpy(ht).cuda()
+    cidx = sas.SaNaive.build(tc, lcp=False, stree=False, sector=False, quad="compact")
+    del tc
+    assert cidx.stats()["quad_entry_bytes"] == 8
+    for algo in ("quad", "inline"):
+        assert np.array_equal(cidx.search_batch(buf, off, lens, algo=algo), got["plain"]), algo
+    clo, chi = cidx.search_range(buf, off, lens)
+    assert np.array_equal(clo, lo) and np.array_equal(chi, hi)
 
 
 def test_fasta_genome_like_end_to_end(sas, tmp_path):

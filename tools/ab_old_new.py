@@ -4,6 +4,7 @@ import sys, os
 which = sys.argv[1]
 algo = sys.argv[2] if len(sys.argv) > 2 else "sector"
 shape = sys.argv[3] if len(sys.argv) > 3 else "c1"   # c1: len-32 fixed; c3: ragged 8..256
+qmode = sys.argv[4] if len(sys.argv) > 4 else "fused"  # quad leaves: fused | compact
 root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_old" if which == "old" else "..")
 sys.path.insert(0, os.path.join(root, "suffix-array-searching_amd"))
 import numpy as np
@@ -28,7 +29,7 @@ else:
     qb = torch.cat([t[src[rep] + within], torch.zeros(64, dtype=torch.uint8, device="cuda")])
     qlen = lens.to(torch.int32)
 out = torch.empty(nq, dtype=torch.int64, device="cuda")
-kw = dict(sector=algo == "sector", stree=algo == "stree", lcp=False, quad=algo in ("quad", "inline"))
+kw = dict(sector=algo == "sector", stree=algo == "stree", lcp=False, quad=("compact" if qmode == "compact" else True) if algo in ("quad", "inline") else False)
 idx = sas_amd.SaNaive.build(t, **kw)
 import time
 for r in range(3):
@@ -45,5 +46,5 @@ for r in range(3):
         e1.record()
         torch.cuda.synchronize()
         kns = e0.elapsed_time(e1) / 5 * 1e6
-    print(which, algo, shape, f"{kns / 1e6:.4f} ms", flush=True)
-np.save(f"/tmp/ab_{which}_{algo}_{shape}.npy", out.cpu().numpy())
+    print(which, algo, shape, qmode, f"{kns / 1e6:.4f} ms", flush=True)
+np.save(f"/tmp/ab_{which}_{algo}_{shape}_{qmode}.npy", out.cpu().numpy())
