@@ -409,12 +409,13 @@ __device__ __forceinline__ bool tail_less32(const uint64_t* __restrict__ tw, uin
 
 // PREFETCH: load the tail's text words up front (tail_less32); measured faster for
 // the per-lane sector kernel, slower for the 4-lane quad kernel (register spills).
-template <int QW, bool PREFETCH = false>
+// SHORT1: QW == 1 means m <= 32 (qw_for), so the text compare is dead code there;
+// false for kernels that hold fewer query words in registers than the query has.
+template <int QW, bool PREFETCH = false, bool SHORT1 = true>
 __device__ __forceinline__ bool sector_ge(uint64_t key, uint64_t p, uint64_t K64, const SearchArgs& a,
                                           const QueryRegs<QW>& q) {
     if (key != K64) return key > K64;
-    // QW == 1 is only dispatched for m <= 32 (qw_for): the text compare is dead code there
-    if (QW == 1 || q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
+    if ((SHORT1 && QW == 1) || q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
     if (PREFETCH) return !tail_less32<QW>(a.tw, a.n, p, q);
     uint32_t lcp;
     return !suffix_less_from<QW>(a.tw, a.n, p, q, 32, &lcp);
@@ -762,6 +763,15 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// tail_less32 prefetch in the 4x tails: measured 4-6% slower (more spills), so off
+// query words the 4x kernel holds in registers (later words are repacked from the
+// bytes): 2 measured ~2% faster than 4/8 (fewer spills) on ragged 8..256 queries
+#ifndef SAS_QUAD4X_MAXREGS
+#define SAS_QUAD4X_MAXREGS 2
+#endif
+#ifndef SAS_QUAD4X_PREFETCH
+#define SAS_QUAD4X_PREFETCH false
+#endif
 // Long queries (QW > 1), as k_sa_stree4x: one query per LANE, four per 4-lane group.
 // The group descends the quad tree and reads the routed leaf cooperatively for each
 // of its four queries in turn (one request per 64-B node), which places each query
@@ -846,7 +856,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
                 ok = key > K64;
             } else {
                 if (p0 == QUAD_NO_SA) p0 = quad_entry_sa<KO, W>(a, x0);
-                ok = sector_ge<QW, true>(key, p0, K64, a, q);
+                ok = sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, p0, K64, a, q);
             }
             if (!known) probes++;
         }
@@ -855,7 +865,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
             auto pred = [&](uint64_t y) -> bool {
                 const uint64_t key = quad_entry_key<KO>(a, y);
                 if (key != K64) return key > K64;
-                return sector_ge<QW, true>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
+                return sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
             };
             uint64_t lo = x0 + 1, hi = sa_n, step = 1;
             while (lo < sa_n) {
@@ -1023,7 +1033,7 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
         case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
         default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
     }
-#define K_QUAD4X(Q) (k_sa_quad4x<Q, KO, W>)
+#define K_QUAD4X(Q) (k_sa_quad4x<(Q < SAS_QUAD4X_MAXREGS ? Q : SAS_QUAD4X_MAXREGS), KO, W>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true, KO, W>)
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
     if (algo == SAS_ALGO_QUAD) {

@@ -5,7 +5,7 @@ which = sys.argv[1]
 algo = sys.argv[2] if len(sys.argv) > 2 else "sector"
 shape = sys.argv[3] if len(sys.argv) > 3 else "c1"   # c1: len-32 fixed; c3: ragged 8..256
 qmode = sys.argv[4] if len(sys.argv) > 4 else "fused"  # quad leaves: fused | compact
-root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_old" if which == "old" else "..")
+root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_" + which if which.startswith("old") else "..")
 sys.path.insert(0, os.path.join(root, "suffix-array-searching_amd"))
 import numpy as np
 import torch
