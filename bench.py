@@ -340,7 +340,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
             "variants": results, "setup_s": setup,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
                                             "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
-                                            "stree_bytes", "sector_bytes", "quad_bytes",
+                                            "stree_bytes", "sector_bytes", "quad_bytes", "quad_fan",
                                             "quad_entry_bytes")}}), flush=True)
 
 
@@ -536,7 +536,7 @@ def main():
             "e2e_host": e2e,
             "variants": variants,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
-                                            "quad_layers", "quad_lds_layers", "top_levels", "iterations",
+                                            "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "iterations",
                                             "sa_rounds", "build_sa_ns", "build_total_ns")},
             "setup_s": build_s, "verified": ok,
         }

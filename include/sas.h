@@ -59,6 +59,14 @@ typedef struct sas_index sas_index;
                                         of 16, SA values read from the SA array.  Fits next to
                                         a 40-bit SA at n = 2^34 in one GPU's HBM.  Implies
                                         SAS_BUILD_QUAD                                     */
+#define SAS_BUILD_QUAD_ABS (1u << 11) /* quad tree inner nodes in the absolute layout: 16 u32
+                                        16-char separators, 17-ary                        */
+#define SAS_BUILD_QUAD_REL (1u << 12) /* quad tree inner nodes in the prefix-relative layout:
+                                        the node's shared d-char prefix + 30 u16 separators
+                                        over the next 8 chars, 31-ary.  Neither flag: the
+                                        layout with fewer levels larger than the 256 MiB
+                                        Infinity Cache (absolute on a tie; n = 2^30 builds
+                                        absolute, n = 2^34 compact builds relative)        */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {
@@ -68,7 +76,9 @@ enum sas_algo {
     SAS_ALGO_SECTOR = 3, /* sector tree: 32-B nodes (one HBM sector), 9-ary on 16-char keys,
                            leaves fuse (32-char key, SA value) pairs: no text/SA reads for m<=32 */
     SAS_ALGO_QUAD = 4,  /* quad tree: 4 lanes per query load each 64-B node in one request;
-                           17-ary on 16-char keys, leaves = 4 fused (32-char key, SA) entries  */
+                           31-ary on the 8 chars after each node's shared prefix (17-ary on
+                           16-char keys with SAS_BUILD_QUAD_ABS), leaves = 4 fused (32-char
+                           key, SA) entries                                                  */
     SAS_ALGO_INLINE = 5 /* PLAIN's probe sequence (binary_search_batch) over the quad tree's
                            fused (32-char key, SA) entries: one 16-B read per probe instead of
                            an SA word + text words ("inlining values", todo.org:18-19)     */
@@ -99,6 +109,8 @@ typedef struct sas_stats {
     uint32_t quad_lds_layers; /* its layers served from LDS                       */
     uint32_t quad_entry_bytes; /* quad leaf bytes per suffix: 16 (fused key + SA),
                                   8 (SAS_BUILD_QUAD_COMPACT), 0 if not built        */
+    uint32_t quad_fan;       /* quad inner-node fan-out: 31 (prefix-relative nodes) or
+                                17 (SAS_BUILD_QUAD_ABS), 0 if not built              */
 } sas_stats;
 
 const char* sas_last_error(void);

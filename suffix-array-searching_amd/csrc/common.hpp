@@ -33,7 +33,11 @@
 #define SAS_SECTOR_FAN 9              // sector tree: 8 separators, 9 children per 32-B node
 #define SAS_SECTOR_MAX_LAYERS 24
 #define SAS_SECTOR_LDS_NODES 2048     // <= 64 KiB of top sector-tree layers in LDS
-#define SAS_QUAD_FAN 17               // quad tree: 16 separators, 17 children per 64-B node
+#define SAS_QUAD_FAN 17               // quad tree, absolute nodes: 16 u32 separators, 17 children
+#define SAS_QUAD_RFAN 31              // quad tree, prefix-relative nodes: 30 u16 separators, 31 children
+#define SAS_QUAD_RMAXD 13             // relative nodes: at most 13 shared chars in the 27-bit header
+#define SAS_QUAD_MAX_INNER 10         // inner layers the (unrolled) descent supports; leaf index < 2^32
+#define SAS_QUAD_MAX_LDS 4            // of which at most this many LDS-staged
 #define SAS_QUAD_MAX_LAYERS 16
 #define SAS_QUAD_LDS_NODES 1024       // <= 64 KiB of top quad-tree layers in LDS
 
@@ -92,12 +96,14 @@ struct sas_index {
     uint32_t sec_lds_nodes = 0;
     uint64_t sec_inner_nodes = 0;
     // quad tree (SAS_ALGO_QUAD): 64-B nodes, one 4-lane cooperative load each
-    uint4* quad_inner = nullptr;     // internal nodes, 16 u32 16-char separators (4 x uint4), root first
+    uint4* quad_inner = nullptr;     // internal nodes (4 x uint4 each), root first: prefix-relative
+                                     // (quad_fan 31) or 16 u32 16-char separators (quad_fan 17)
     uint4* quad_leaves = nullptr;    // entry x = {key lo, key hi, sa lo32, sa bits 32..39}; leaf = 4 entries
                                      // compact (SAS_BUILD_QUAD_COMPACT): entry x = key64 only; leaf = 8 entries
     uint32_t quad_compact = 0;       // 1: key-only leaves, SA values read from `sa`
     uint64_t quad_leaf_count = 0;
     uint64_t quad_off[SAS_QUAD_MAX_LAYERS] = {};
+    uint32_t quad_fan = SAS_QUAD_RFAN;  // children per inner node; 31 = prefix-relative layout
     uint32_t quad_inner_layers = 0;
     uint32_t quad_lds_layers = 0;
     uint32_t quad_lds_nodes = 0;

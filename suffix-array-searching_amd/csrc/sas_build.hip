@@ -623,18 +623,90 @@ __global__ void k_quad_layer(uint32_t* __restrict__ inner, uint64_t oh, uint64_t
     }
 }
 
-static int build_quad(sas_index* x, bool compact) {
+// Prefix-relative internal layer (quad_fan 31).  A node's whole subtree shares its
+// first d chars P (d = LCP of the subtree's first and last 32-char keys, capped at
+// SAS_QUAD_RMAXD), so its separators only need the 8 chars after them:
+//   word 0   = d << 27 | P (2d bits, right-aligned): u16 slots 0 and 1
+//   u16 slot 2 + s (s = 0..29) = chars [d, d+8) of the key of the LAST entry of child
+//            31i+s (left-max, as k_quad_layer), 0xFFFF for the globally last child and
+//            beyond; stored XOR 0x8000 so that a saturating packed i16 subtract compares
+//            two of them at once (quad_rel_child).
+// Within the subtree these 16-bit windows are monotone in rank (the keys agree on
+// chars [0, d)), so "window < q's window" still implies "suffix < q" for a query
+// whose first d chars equal P; the search decides the other two cases from P alone
+// ("above P" = every entry < q: the last child).  The LAST node of a layer may have
+// fewer than 31 children, so it always gets d = 0 (its windows are the first 8 chars,
+// still monotone): "above P" cannot happen there and no child index leaves the layer.
+__device__ __forceinline__ uint64_t quad_key_at(const uint32_t* __restrict__ leaves, uint32_t epl, uint64_t x) {
+    const uint2 k = reinterpret_cast<const uint2*>(leaves)[epl == 4 ? 2 * x : x];
+    return (uint64_t)k.x | ((uint64_t)k.y << 32);
+}
+
+__global__ void k_quad_rel_layer(uint32_t* __restrict__ inner, uint64_t oh, uint64_t layer_nodes,
+                                 uint64_t child_span, uint64_t child_layer_nodes,
+                                 const uint32_t* __restrict__ leaves, uint64_t sa_n, uint32_t epl) {
+    GRID_STRIDE(i, 16 * layer_nodes) {
+        const uint64_t node = i / 16, w = i % 16;
+        const uint64_t span = epl * child_span;  // entries per child
+        const uint64_t first = node * SAS_QUAD_RFAN * span;
+        uint64_t last = (node + 1) * SAS_QUAD_RFAN * span;
+        last = (last < sa_n ? last : sa_n) - 1;
+        const uint64_t kf = quad_key_at(leaves, epl, first), kl = quad_key_at(leaves, epl, last);
+        uint32_t d = (kf == kl) ? 32u : (uint32_t)__builtin_clzll(kf ^ kl) / 2;
+        if (d > SAS_QUAD_RMAXD) d = SAS_QUAD_RMAXD;
+        if (node + 1 == layer_nodes) d = 0;
+        uint32_t word;
+        if (w == 0) {
+            word = (d << 27) | (d ? (uint32_t)(kf >> (64 - 2 * d)) : 0u);
+        } else {
+            uint32_t half[2];
+            for (int e = 0; e < 2; e++) {
+                const uint64_t child = node * SAS_QUAD_RFAN + (2 * w - 2 + e);
+                half[e] = 0xFFFFu;
+                if (child + 1 < child_layer_nodes)
+                    half[e] = (uint32_t)(quad_key_at(leaves, epl, (child + 1) * span - 1) >> (48 - 2 * d)) & 0xFFFFu;
+            }
+            word = (half[0] | (half[1] << 16)) ^ 0x80008000u;
+        }
+        inner[(oh + node) * 16 + w] = word;
+    }
+}
+
+// Levels (inner layers and the leaf layer) whose 64-B nodes outgrow the 256 MiB
+// Infinity Cache: each costs one DRAM-level request per lookup.
+static uint32_t quad_dram_levels(uint64_t nl, uint32_t fan) {
+    const uint64_t mall_nodes = (256ull << 20) / 64;
+    uint32_t cnt = 0;
+    for (uint64_t c = nl;; c = (c + fan - 1) / fan) {
+        cnt += c > mall_nodes;
+        if (c <= 1) break;
+    }
+    return cnt;
+}
+
+// mode: SAS_BUILD_QUAD_ABS / SAS_BUILD_QUAD_REL force a layout; neither = the one
+// with fewer levels beyond the Infinity Cache, the absolute layout on a tie
+// (measured: at n = 2^30 both have two such levels and the absolute one is ~4%
+// faster; at n = 2^34 with compact leaves the relative one saves a level, -8% on
+// ragged 8..256 queries; tools/ab_quad_rel.py).
+static int build_quad(sas_index* x, bool compact, uint32_t mode) {
     const uint64_t sa_n = x->sa_n;
     const uint32_t epl = compact ? 8 : 4;  // entries per 64-B leaf
     const uint64_t nl = (sa_n + epl - 1) / epl;
+    bool absolute = true;
+    if (mode & SAS_BUILD_QUAD_REL) absolute = false;
+    else if (!(mode & SAS_BUILD_QUAD_ABS))
+        absolute = quad_dram_levels(nl, SAS_QUAD_RFAN) >= quad_dram_levels(nl, SAS_QUAD_FAN);
+    const uint32_t fan = absolute ? SAS_QUAD_FAN : SAS_QUAD_RFAN;
     uint64_t sizes[SAS_QUAD_MAX_LAYERS];
     uint32_t H = 0;
     uint64_t c = nl;
     do {
-        c = (c + SAS_QUAD_FAN - 1) / SAS_QUAD_FAN;
+        c = (c + fan - 1) / fan;
         if (H >= SAS_QUAD_MAX_LAYERS) SAS_FAIL(ENOTSUP, "quad tree too high");
         sizes[H++] = c;
     } while (c > 1);
+    if (H > SAS_QUAD_MAX_INNER || nl > (1ull << 32)) SAS_FAIL(ENOTSUP, "quad tree: more than 2^32 leaves");
     uint64_t tot = 0;
     for (uint32_t h = 0; h < H; h++) {
         x->quad_off[h] = tot;
@@ -655,9 +727,13 @@ static int build_quad(sas_index* x, bool compact) {
     uint64_t span = 1, child_nodes = nl;
     for (int h = (int)H - 1; h >= 0; h--) {
         uint64_t ln = sizes[H - 1 - h];
-        hipLaunchKernelGGL(k_quad_layer, dim3(grid_for(16 * ln)), dim3(256), 0, 0, inner.as<uint32_t>(),
-                           x->quad_off[h], ln, span, child_nodes, leaves.as<uint32_t>(), sa_n, epl);
-        span *= SAS_QUAD_FAN;
+        if (absolute)
+            hipLaunchKernelGGL(k_quad_layer, dim3(grid_for(16 * ln)), dim3(256), 0, 0, inner.as<uint32_t>(),
+                               x->quad_off[h], ln, span, child_nodes, leaves.as<uint32_t>(), sa_n, epl);
+        else
+            hipLaunchKernelGGL(k_quad_rel_layer, dim3(grid_for(16 * ln)), dim3(256), 0, 0, inner.as<uint32_t>(),
+                               x->quad_off[h], ln, span, child_nodes, leaves.as<uint32_t>(), sa_n, epl);
+        span *= fan;
         child_nodes = ln;
     }
     HIP_TRY(hipGetLastError());
@@ -665,13 +741,14 @@ static int build_quad(sas_index* x, bool compact) {
     x->quad_inner = static_cast<uint4*>(inner.release());
     x->quad_leaf_count = nl;
     x->quad_compact = compact ? 1 : 0;
+    x->quad_fan = fan;
     x->quad_inner_layers = H;
     x->quad_inner_nodes = tot;
     uint32_t L = 0;
     uint64_t ln = 0;
     for (uint32_t h = 0; h < H; h++) {
         uint64_t sz = sizes[H - 1 - h];
-        if (ln + sz > SAS_QUAD_LDS_NODES) break;
+        if (ln + sz > SAS_QUAD_LDS_NODES || L == SAS_QUAD_MAX_LDS) break;
         ln += sz;
         L++;
     }
@@ -953,7 +1030,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     }
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
     if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
-    if (flags & (SAS_BUILD_QUAD | SAS_BUILD_QUAD_COMPACT)) TRY(build_quad(x, (flags & SAS_BUILD_QUAD_COMPACT) != 0));
+    if (flags & (SAS_BUILD_QUAD | SAS_BUILD_QUAD_COMPACT)) TRY(build_quad(x, (flags & SAS_BUILD_QUAD_COMPACT) != 0, flags & (SAS_BUILD_QUAD_ABS | SAS_BUILD_QUAD_REL)));
 
     // binary-search top in LDS
     {
@@ -998,6 +1075,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.quad_layers = x->quad_leaves ? x->quad_inner_layers + 1 : 0;
     st.quad_lds_layers = x->quad_lds_layers;
     st.quad_entry_bytes = x->quad_leaves ? (x->quad_compact ? 8 : 16) : 0;
+    st.quad_fan = x->quad_leaves ? x->quad_fan : 0;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -55,6 +55,7 @@ struct SearchArgs {
     const uint4* quad_leaves;
     uint64_t quad_off[SAS_QUAD_MAX_LAYERS];
     uint64_t quad_leaf_count;
+    uint32_t quad_fan;
     uint32_t quad_inner_layers;
     uint32_t quad_lds_layers;
     uint32_t quad_lds_nodes;
@@ -667,6 +668,75 @@ __device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRe
     return 2 * j + s;
 }
 
+// Inner-node descent of the 4-lane group to the leaf for routing key R (a padded
+// 32-char key).  Absolute nodes (quad_fan 17): lane j counts its 4 of the 16 u32
+// 16-char separators < R's first 16 chars.  Prefix-relative nodes (quad_fan 31,
+// k_quad_rel_layer): lane 0's word 0 is the header {d, P}, broadcast to the group;
+// if R's first d chars equal P, the child is the count of 16-bit separators below
+// R's chars [d, d+8); if they are below P every entry of the subtree is >= R (child
+// 0), if above, every entry is < R (the last child; a layer's last node, which may
+// have fewer children, has d = 0, so it never answers "above").  Either way every
+// entry before the chosen child is < R, the invariant the leaf search needs.
+typedef short quad_short2 __attribute__((ext_vector_type(2)));
+// sign bits (15, 31) of the saturating packed i16 difference w - tt: set where the
+// 16-bit half of w is below tt's (both stored XOR 0x8000, so signed order = unsigned)
+__device__ __forceinline__ uint32_t lt2_signs(uint32_t w, uint32_t tt) {
+    const quad_short2 d = __builtin_elementwise_sub_sat(__builtin_bit_cast(quad_short2, w),
+                                                        __builtin_bit_cast(quad_short2, tt));
+    return __builtin_bit_cast(uint32_t, d);
+}
+
+// m0 = 0 on lane 0 of the group (its word 0 is the header), 0x80008000 elsewhere
+__device__ __forceinline__ uint32_t quad_rel_child(uint4 v, uint64_t R, uint32_t m0) {
+    const uint32_t hdr = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v.x, 0x00, 0xF, 0xF, false);
+    const uint64_t full = R >> (48 - ((hdr >> 26) & 62u));  // R's chars [0, d + 8)
+    const uint32_t Qd = (uint32_t)(full >> 16), P = hdr & 0x7FFFFFFu;
+    const uint32_t T = (uint32_t)full & 0xFFFFu;
+    const uint32_t tt = (T | (T << 16)) ^ 0x80008000u;
+    uint32_t c = __builtin_popcount(lt2_signs(v.x, tt) & m0);
+    c += __builtin_popcount(lt2_signs(v.y, tt) & 0x80008000u);
+    c += __builtin_popcount(lt2_signs(v.z, tt) & 0x80008000u);
+    c += __builtin_popcount(lt2_signs(v.w, tt) & 0x80008000u);
+    c = quad_sum(c);
+    return Qd == P ? c : (Qd < P ? 0u : SAS_QUAD_RFAN - 1);
+}
+
+__device__ __forceinline__ uint32_t quad_abs_child(uint4 v, uint32_t R16) {
+    return quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
+}
+
+// Both loops are unrolled over the layer index so the per-layer offsets (kernel
+// arguments) are loop-invariant scalar loads hoisted out of the query loop; the leaf
+// index fits 32 bits (build_quad refuses more than 2^32 leaves).
+template <bool REL>
+__device__ __forceinline__ uint32_t quad_descend_t(const SearchArgs& a, const uint4* s_nodes, uint64_t R, uint32_t sub) {
+    const uint32_t R16 = (uint32_t)(R >> 32);
+    const uint32_t m0 = sub ? 0x80008000u : 0u;
+    uint32_t k = 0;
+    // LDS layers, then HBM layers: separate loops keep the loads ds_read / global_load
+    // (a pointer select between the two address spaces compiles to FLAT loads)
+#pragma unroll
+    for (uint32_t h = 0; h < SAS_QUAD_MAX_LDS; h++) {
+        if (h < a.quad_lds_layers) {
+            const uint4 v = s_nodes[((uint32_t)a.quad_off[h] + k) * 4 + sub];
+            k = REL ? k * SAS_QUAD_RFAN + quad_rel_child(v, R, m0) : k * SAS_QUAD_FAN + quad_abs_child(v, R16);
+        }
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < SAS_QUAD_MAX_INNER; h++) {
+        if (h >= a.quad_lds_layers && h < a.quad_inner_layers) {
+            const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
+            k = REL ? k * SAS_QUAD_RFAN + quad_rel_child(v, R, m0) : k * SAS_QUAD_FAN + quad_abs_child(v, R16);
+        }
+    }
+    return k;
+}
+
+__device__ __forceinline__ uint64_t quad_descend(const SearchArgs& a, const uint4* s_nodes, uint64_t R, uint32_t sub) {
+    return a.quad_fan == SAS_QUAD_RFAN ? quad_descend_t<true>(a, s_nodes, R, sub)
+                                       : quad_descend_t<false>(a, s_nodes, R, sub);
+}
+
 // First local rank with the bound's predicate (monotone over ranks): descent on the
 // 16-char routing key, the routed leaf, then (rare) an exponential + binary search
 // over later leaves for a run of equal routing keys that crosses leaves.  Returns
@@ -677,20 +747,8 @@ __device__ __forceinline__ uint64_t quad_bound(const SearchArgs& a, const uint4*
                                                uint64_t K64, uint64_t Q3, uint32_t sub, uint32_t* probes,
                                                uint64_t* px) {
     constexpr uint32_t EPL = KO ? 8 : 4;
-    const uint32_t R16 = (uint32_t)(((UPPER && q.m <= 32) ? Q3 : K64) >> 32);
     const uint64_t nl = a.quad_leaf_count;
-    uint64_t k = 0;
-    // LDS layers, then HBM layers: separate loops keep the loads ds_read / global_load
-    // (a pointer select between the two address spaces compiles to FLAT loads)
-    uint32_t h = 0;
-    for (; h < a.quad_lds_layers; h++) {
-        const uint4 v = s_nodes[(a.quad_off[h] + k) * 4 + sub];
-        k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-    }
-    for (; h < a.quad_inner_layers; h++) {
-        const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
-        k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-    }
+    const uint64_t k = quad_descend(a, s_nodes, (UPPER && q.m <= 32) ? Q3 : K64, sub);
     *probes += a.quad_inner_layers + 1;
     // routed leaf k: every entry before it fails the predicate
     uint64_t pl;
@@ -813,17 +871,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
         for (uint32_t j = 0; j < QUAD_G; j++) {
             if (gi + j >= a.nq) break;  // group-uniform
             const uint64_t K64 = __shfl((unsigned long long)Kmine, lane0 + (int)j, 64);
-            const uint32_t R16 = (uint32_t)(K64 >> 32);
-            uint64_t k = 0;
-            uint32_t h = 0;
-            for (; h < a.quad_lds_layers; h++) {
-                const uint4 v = s_nodes[(a.quad_off[h] + k) * 4 + sub];
-                k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-            }
-            for (; h < a.quad_inner_layers; h++) {
-                const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
-                k = k * SAS_QUAD_FAN + quad_sum((v.x < R16) + (v.y < R16) + (v.z < R16) + (v.w < R16));
-            }
+            const uint64_t k = quad_descend(a, s_nodes, K64, sub);
             const uint4 e = a.quad_leaves[4 * k + sub];
             uint64_t ksel, psel = QUAD_NO_SA;
             uint32_t c;
@@ -1100,6 +1148,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.quad_inner = x->quad_inner;
     a.quad_leaves = x->quad_leaves;
     for (int h = 0; h < SAS_QUAD_MAX_LAYERS; h++) a.quad_off[h] = x->quad_off[h];
+    a.quad_fan = x->quad_fan;
     a.quad_leaf_count = x->quad_leaf_count;
     a.quad_inner_layers = x->quad_inner_layers;
     a.quad_lds_layers = x->quad_lds_layers;

@@ -27,6 +27,8 @@ SAS_BUILD_SECTOR = 1 << 7
 SAS_BUILD_SA40 = 1 << 8
 SAS_BUILD_QUAD = 1 << 9
 SAS_BUILD_QUAD_COMPACT = 1 << 10
+SAS_BUILD_QUAD_ABS = 1 << 11
+SAS_BUILD_QUAD_REL = 1 << 12
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
@@ -47,6 +49,7 @@ class SasStats(C.Structure):
         ("sector_bytes", C.c_uint64), ("sector_layers", C.c_uint32), ("sector_lds_layers", C.c_uint32),
         ("quad_bytes", C.c_uint64), ("quad_layers", C.c_uint32), ("quad_lds_layers", C.c_uint32),
         ("quad_entry_bytes", C.c_uint32),
+        ("quad_fan", C.c_uint32),
     ]
 
     def as_dict(self):

@@ -46,11 +46,24 @@ def _as_u8(x):
 
 
 def _quad_flags(quad) -> int:
-    if quad == "compact":
-        return _lib.SAS_BUILD_QUAD_COMPACT
-    if quad in (True, False):
-        return _lib.SAS_BUILD_QUAD if quad else 0
-    raise ValueError(f"quad must be True, False or 'compact', not {quad!r}")
+    """True: fused leaves; "compact": key-only leaves.  The inner-node layout is picked
+    by the library (SAS_BUILD_QUAD_ABS / _REL in sas.h) unless a suffix forces it:
+    "abs" / "rel" (fused) or "compact-abs" / "compact-rel"."""
+    if quad is False:
+        return 0
+    if quad is True:
+        quad = "fused"
+    if not isinstance(quad, str):
+        raise ValueError(f"quad must be a bool or a string, not {quad!r}")
+    leaves, _, layout = quad.partition("-") if quad.startswith("compact") else ("fused", "", quad)
+    if layout == "fused":
+        layout = ""
+    flags = {"fused": _lib.SAS_BUILD_QUAD, "compact": _lib.SAS_BUILD_QUAD_COMPACT}.get(leaves)
+    lay = {"": 0, "abs": _lib.SAS_BUILD_QUAD_ABS, "rel": _lib.SAS_BUILD_QUAD_REL}.get(layout)
+    if flags is None or lay is None:
+        raise ValueError(f"quad must be True, False, 'compact', 'abs', 'rel', 'compact-abs' or "
+                         f"'compact-rel', not {quad!r}")
+    return flags | lay
 
 
 class SaNaive:

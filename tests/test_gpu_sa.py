@@ -352,6 +352,59 @@ def test_occurrence_ranges_both_trees(sas, sadef):
                               s_only.search_batch(buf, off, lens, algo="sector")), n
 
 
+def test_quad_relative_nodes(sas, sadef):
+    """Quad inner nodes: prefix-relative (SAS_BUILD_QUAD_REL, 31-ary: a node's shared
+    d-char prefix + 30 16-bit separators over the next 8 chars) and absolute
+    (SAS_BUILD_QUAD_ABS, 17-ary 16-char separators) must both give the oracle's
+    positions and identical ranges; the automatic choice is absolute at these sizes.
+    Queries mutated at chars 0..24 land between separators at every depth and exercise
+    the below/above-prefix cases; leaf counts of 31^k + 1 leave a one-child last node
+    per layer (the clamp), and a near-periodic text pins d at its 13-char cap."""
+    rng = np.random.default_rng(31)
+    per = np.tile(rng.integers(0, 4, 16, dtype=np.uint8), 4000)
+    per[rng.integers(0, len(per), 300)] = rng.integers(0, 4, 300, dtype=np.uint8)
+    texts = [sas.random_string(1_000_003, seed=12), sas.random_string(4 * 31 ** 3 + 1, seed=13),
+             sas.random_string(4 * 31 ** 2 + 3, seed=14), np.zeros(50_000, np.uint8), per,
+             np.tile(rng.integers(0, 4, 13, dtype=np.uint8), 7000)]
+    texts += [np.array(c["text"], np.uint8) for c in sadef["cases"]]
+    assert sas.SaNaive.build(texts[0], lcp=False, stree=False, sector=False).stats()["quad_fan"] == 17
+    for t in texts:
+        n = len(t)
+        for leaves in ("", "compact-"):
+            rel = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=leaves + "rel")
+            ab = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=leaves + "abs")
+            assert rel.stats()["quad_fan"] == 31 and ab.stats()["quad_fan"] == 17
+            quad = leaves or "fused"
+            sa = rel.suffix_array()
+            qs = []
+            for o, l in zip(rng.integers(0, max(1, n - 40), 1500), rng.integers(1, 40, 1500)):
+                q = t[o:o + l].copy()
+                if len(q):
+                    j = rng.integers(0, len(q))
+                    q[j] = (q[j] + rng.integers(1, 4)) % 4
+                qs.append(q)
+            qs += [t[o:o + l] for o, l in zip(rng.integers(0, max(1, n - 300), 800), rng.integers(0, 300, 800))]
+            qs += [np.full(l, 3, np.uint8) for l in (1, 8, 13, 31, 32, 33, 200)] + [np.zeros(0, np.uint8)]
+            qs += [t[n - k:] for k in (1, 5, 32, 40) if k <= n]
+            buf, off, lens = pack(qs)
+            expect = oracle_positions(t, sa, buf, off, lens)
+            for idx in (rel, ab):
+                assert np.array_equal(idx.search_batch(buf, off, lens, algo="quad"), expect), (n, quad)
+            if n >= 64:
+                q32 = [t[o:o + 32].copy() for o in rng.integers(0, n - 32, 1500)]
+                for q in q32[::2]:
+                    j = rng.integers(0, 32)
+                    q[j] = (q[j] + 1) % 4
+                q32 += [np.full(32, 3, np.uint8)]
+                b32 = np.concatenate(q32)
+                e32 = oracle_positions(t, sa, b32, np.arange(len(q32), dtype=np.uint64) * 32,
+                                       np.full(len(q32), 32, np.uint32))
+                assert np.array_equal(rel.search_fixed(b32, 32, algo="quad"), e32), (n, quad)
+            lr, hr = rel.search_range(buf, off, lens)
+            la, ha = ab.search_range(buf, off, lens)
+            assert np.array_equal(lr, la) and np.array_equal(hr, ha), (n, quad)
+
+
 def test_compact_quad_leaves(sas, sadef):
     """SAS_BUILD_QUAD_COMPACT: key-only quad leaves (8 per 64-B leaf, SA values from the
     SA array), u32 and 40-bit SA.  QUAD (cooperative m <= 32 kernel and the 4x kernel
