@@ -182,9 +182,25 @@ int main(int argc, char** argv) {
     }
     uint8_t* p;
     uint32_t* out;
-    CHECK(hipMalloc(&p, maxbytes));
     CHECK(hipMalloc(&out, 64));
-    CHECK(hipMemset(p, 1, maxbytes));
+    // TB_SEPARATE=1: every level in its own allocation, as the real index arrays are
+    // (p = 0, base[l] = the level's device address)
+    const bool separate = getenv("TB_SEPARATE") != nullptr;
+    if (!separate) {
+        CHECK(hipMalloc(&p, maxbytes));
+        CHECK(hipMemset(p, 1, maxbytes));
+    } else {
+        p = nullptr;
+        for (auto& L : lays) {
+            for (int l = 0; l < L.L; l++) {
+                const int wb = L.width[l] > 1000 ? L.width[l] - 1000 : L.width[l];
+                uint8_t* q;
+                CHECK(hipMalloc(&q, L.units[l] * wb + 64));
+                CHECK(hipMemset(q, 1, L.units[l] * wb + 64));
+                L.base[l] = (uint64_t)(uintptr_t)q;
+            }
+        }
+    }
     int cus = 256;
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, 0) == hipSuccess) cus = prop.multiProcessorCount;
