@@ -56,6 +56,8 @@ struct SearchArgs {
     uint64_t quad_off[SAS_QUAD_MAX_LAYERS];
     uint64_t quad_leaf_count;
     uint32_t quad_fan;
+    uint32_t quad_nt_from;   // first inner layer read with non-temporal loads
+    uint32_t quad_leaf_nt;   // leaves read with non-temporal loads
     uint32_t quad_inner_layers;
     uint32_t quad_lds_layers;
     uint32_t quad_lds_nodes;
@@ -575,6 +577,24 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 }
 
 // ------------------------------------------------------------------ QUAD
+// Levels far larger than the 256 MiB Infinity Cache (quad_nt_from.., the leaves when
+// quad_leaf_nt) are read with non-temporal loads so they do not evict the upper layers
+// from L2; the query stream and the positions likewise (SAS_QUAD_NT_IO).  Same-box
+// A/B at n = 2^30 (tools/ab_nt.sh): absolute layout 0.760 -> 0.713 ms, relative
+// 0.790 -> 0.734 ms; NT on a level that partly fits the Infinity Cache (the 554 MB
+// relative leaf-parent layer, the 59 MB absolute one) made it slower.
+#ifndef SAS_QUAD_NT_IO
+#define SAS_QUAD_NT_IO 1
+#endif
+typedef unsigned int quad_u32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ uint4 nt_load4(const uint4* p) {
+    const quad_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const quad_u32x4*>(p));
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint4 quad_leaf_load(const SearchArgs& a, const uint4* p) {
+    return a.quad_leaf_nt ? nt_load4(p) : *p;
+}
+
 // A 4-lane group per query.  Every node is 64 B and the group loads it with one
 // 16-B load per lane, which the memory system serves as ONE request (a per-lane
 // 32-B node costs two): tools/treebench measured 19-22 ps per DRAM-level 64-B
@@ -590,7 +610,13 @@ __device__ __forceinline__ uint64_t quad_key32(const uint8_t* __restrict__ qb, u
                                                uint32_t* bad) {
     uint32_t part = 0;
     if (8 * sub < m) {
-        const uint2 v = *reinterpret_cast<const uint2*>(qb + 8 * sub);
+        uint2 v;
+        if (SAS_QUAD_NT_IO) {  // the query stream is read once: keep it out of L2
+            const uint64_t w = __builtin_nontemporal_load(reinterpret_cast<const uint64_t*>(qb + 8 * sub));
+            v = make_uint2((uint32_t)w, (uint32_t)(w >> 32));
+        } else {
+            v = *reinterpret_cast<const uint2*>(qb + 8 * sub);
+        }
         *bad |= (v.x | v.y) & 0xFCFCFCFCu;
         part = (pack4(v.x) << 8) | pack4(v.y);
     }
@@ -633,7 +659,7 @@ template <int QW, bool UPPER, bool KO, int W>
 __device__ __forceinline__ uint32_t quad_leaf(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64, uint64_t Q3,
                                               uint64_t L, uint32_t sub, uint64_t* p) {
     const int lane0 = (int)((threadIdx.x & 63) & ~3u);
-    const uint4 e = a.quad_leaves[4 * L + sub];
+    const uint4 e = quad_leaf_load(a, a.quad_leaves + 4 * L + sub);
     // short-circuit: padding entries (x >= sa_n) carry all-ones keys/SA and must never
     // reach the predicate (its m > 32 text compare would read past the text)
     auto pred = [&](uint64_t key, uint64_t pp) -> bool {
@@ -725,7 +751,8 @@ __device__ __forceinline__ uint32_t quad_descend_t(const SearchArgs& a, const ui
 #pragma unroll
     for (uint32_t h = 0; h < SAS_QUAD_MAX_INNER; h++) {
         if (h >= a.quad_lds_layers && h < a.quad_inner_layers) {
-            const uint4 v = a.quad_inner[(a.quad_off[h] + k) * 4 + sub];
+            const uint4* pv = a.quad_inner + (a.quad_off[h] + k) * 4 + sub;
+            const uint4 v = h >= a.quad_nt_from ? nt_load4(pv) : *pv;
             k = REL ? k * SAS_QUAD_RFAN + quad_rel_child(v, R, m0) : k * SAS_QUAD_FAN + quad_abs_child(v, R16);
         }
     }
@@ -814,7 +841,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
         const uint64_t x = quad_bound<QW, false, KO, W>(a, s_nodes, q, q.w[0], 0, sub, &probes, &px);
         if (KO && x < a.sa_n && px == QUAD_NO_SA) px = quad_entry_sa<true, W>(a, x);  // group-uniform address
         if (sub == 0) {
-            a.out_pos[i] = (x >= a.sa_n) ? a.next_pos : px;
+            const uint64_t res = (x >= a.sa_n) ? a.next_pos : px;
+            if (SAS_QUAD_NT_IO) __builtin_nontemporal_store(res, a.out_pos + i);
+            else a.out_pos[i] = res;
             if (a.out_probes) a.out_probes[i] = probes;
         }
     }
@@ -872,7 +901,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
             if (gi + j >= a.nq) break;  // group-uniform
             const uint64_t K64 = __shfl((unsigned long long)Kmine, lane0 + (int)j, 64);
             const uint64_t k = quad_descend(a, s_nodes, K64, sub);
-            const uint4 e = a.quad_leaves[4 * k + sub];
+            const uint4 e = quad_leaf_load(a, a.quad_leaves + 4 * k + sub);
             uint64_t ksel, psel = QUAD_NO_SA;
             uint32_t c;
             if (KO) {
@@ -1149,6 +1178,17 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.quad_leaves = x->quad_leaves;
     for (int h = 0; h < SAS_QUAD_MAX_LAYERS; h++) a.quad_off[h] = x->quad_off[h];
     a.quad_fan = x->quad_fan;
+    {
+        // non-temporal levels: footprint > 3x the 256 MiB Infinity Cache (see nt_load4)
+        const uint64_t big = 3ull * (256ull << 20) / 64;  // in 64-B nodes
+        const uint32_t H = x->quad_inner_layers;
+        a.quad_nt_from = H;
+        for (uint32_t h = 0; h < H; h++) {
+            const uint64_t sz = (h + 1 < H ? x->quad_off[h + 1] : x->quad_inner_nodes) - x->quad_off[h];
+            if (sz > big) { a.quad_nt_from = h; break; }
+        }
+        a.quad_leaf_nt = x->quad_leaf_count > big;
+    }
     a.quad_leaf_count = x->quad_leaf_count;
     a.quad_inner_layers = x->quad_inner_layers;
     a.quad_lds_layers = x->quad_lds_layers;

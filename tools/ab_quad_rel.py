@@ -5,7 +5,9 @@ the two indexes so box drift hits both; checks the positions are identical."""
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "suffix-array-searching_amd"))
+# AB_PKG: another build of the package (tools/mk_variant.sh) to time instead of this tree's
+sys.path.insert(0, os.environ.get("AB_PKG") or
+                os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "suffix-array-searching_amd"))
 import numpy as np
 import torch
 

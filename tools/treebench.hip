@@ -186,6 +186,19 @@ int main(int argc, char** argv) {
     // TB_SEPARATE=1: every level in its own allocation, as the real index arrays are
     // (p = 0, base[l] = the level's device address)
     const bool separate = getenv("TB_SEPARATE") != nullptr;
+    // TB_FRAG=<KiB>: before the levels are allocated, fill ~48 GiB with chunks of that
+    // size and free every other one, so the levels land on scattered physical memory
+    std::vector<void*> frag;
+    if (getenv("TB_FRAG")) {
+        const size_t chunk = (size_t)atoll(getenv("TB_FRAG")) << 10;
+        for (size_t tot = 0; tot < (48ull << 30); tot += chunk) {
+            void* q;
+            if (hipMalloc(&q, chunk) != hipSuccess) break;
+            frag.push_back(q);
+        }
+        for (size_t i = 0; i < frag.size(); i += 2) CHECK(hipFree(frag[i]));
+        fprintf(stderr, "TB_FRAG: %zu chunks of %zu KiB, freed every other\n", frag.size(), chunk >> 10);
+    }
     if (!separate) {
         CHECK(hipMalloc(&p, maxbytes));
         CHECK(hipMemset(p, 1, maxbytes));
