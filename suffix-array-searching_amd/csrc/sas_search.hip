@@ -55,6 +55,7 @@ struct SearchArgs {
     const uint4* quad_leaves;
     uint64_t quad_off[SAS_QUAD_MAX_LAYERS];
     uint64_t quad_leaf_count;
+    uint32_t stree_leaf_nt;  // S-tree leaf layer (16-char keys) read non-temporal
     uint32_t quad_fan;
     uint32_t quad_nt_from;   // first inner layer read with non-temporal loads
     uint32_t quad_leaf_nt;   // leaves read with non-temporal loads
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
         uint32_t probes = a.stree_height - 1;
 
         uint64_t k = stree_descend(a, s_nodes, K, sub);
-        const uint4 lv = g[(ol + k) * 4 + sub];
+        const uint4 lv = load4(g + (ol + k) * 4 + sub, a.stree_leaf_nt);
         const uint32_t c = quad_cnt_lt(lv, K), e = quad_cnt_eq(lv, K);
         probes++;
         uint64_t r0 = k * 16 + c;
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree4x(SearchArgs a) {
             const uint32_t K = (uint32_t)__shfl((int)Kmine, lane0 + (int)j, 64);
             uint32_t pr_j = a.stree_height - 1;
             const uint64_t k = stree_descend(a, s_nodes, K, sub);
-            const uint4 lv = g[(ol + k) * 4 + sub];
+            const uint4 lv = load4(g + (ol + k) * 4 + sub, a.stree_leaf_nt);
             const uint32_t c = quad_cnt_lt(lv, K), e = quad_cnt_eq(lv, K);
             pr_j++;
             uint64_t r0 = k * 16 + c, r1 = r0 + e;
@@ -480,6 +481,7 @@ __device__ __forceinline__ uint64_t sector_bound(const SearchArgs& a, const uint
     }
     *probes += a.sec_inner_layers;
     // leaf k: entries 2k, 2k+1 (everything before 2k fails pred)
+    // (non-temporal loads here measured 8% slower: tools/ab_nt2.sh)
     uint4 kv = leaves[2 * k], sv = leaves[2 * k + 1];
     (*probes)++;
     uint64_t key0 = (uint64_t)kv.x | ((uint64_t)kv.y << 32), key1 = (uint64_t)kv.z | ((uint64_t)kv.w << 32);
@@ -586,11 +588,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_sector_range(SearchArgs 
 #ifndef SAS_QUAD_NT_IO
 #define SAS_QUAD_NT_IO 1
 #endif
-typedef unsigned int quad_u32x4 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint4 nt_load4(const uint4* p) {
-    const quad_u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const quad_u32x4*>(p));
-    return make_uint4(v.x, v.y, v.z, v.w);
-}
 __device__ __forceinline__ uint4 quad_leaf_load(const SearchArgs& a, const uint4* p) {
     return a.quad_leaf_nt ? nt_load4(p) : *p;
 }
@@ -1174,13 +1171,15 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.sec_inner_layers = x->sec_inner_layers;
     a.sec_lds_layers = x->sec_lds_layers;
     a.sec_lds_nodes = x->sec_lds_nodes;
+    // non-temporal levels, as for the quad tree below
+    a.stree_leaf_nt = (x->sa_n + 15) / 16 * 64 > SAS_NT_BYTES;
     a.quad_inner = x->quad_inner;
     a.quad_leaves = x->quad_leaves;
     for (int h = 0; h < SAS_QUAD_MAX_LAYERS; h++) a.quad_off[h] = x->quad_off[h];
     a.quad_fan = x->quad_fan;
     {
         // non-temporal levels: footprint > 3x the 256 MiB Infinity Cache (see nt_load4)
-        const uint64_t big = 3ull * (256ull << 20) / 64;  // in 64-B nodes
+        const uint64_t big = SAS_NT_BYTES / 64;  // in 64-B nodes
         const uint32_t H = x->quad_inner_layers;
         a.quad_nt_from = H;
         for (uint32_t h = 0; h < H; h++) {

@@ -34,6 +34,7 @@ struct SstArgs {
     const uint32_t* prefix_map;  // PartitionedSTree16M
     uint32_t shift;
     uint32_t parts;
+    uint32_t leaf_nt;  // leaf layer read non-temporal (> SAS_NT_BYTES)
 };
 
 // count of keys < q under SIGNED compare (find_popcnt, sst/node.rs:93-109)
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_stree4(SstArgs a) {
         for (; h < lds_layers && h + 1 < a.height; h++) k = k * (B + 1) + cnt4(s_nodes[(a.lds_off[h] + k) * 4 + sub]);
         for (; h + 1 < a.height; h++) k = k * (B + 1) + cnt4(g[(a.off[h] + k) * 4 + sub]);
         const uint64_t o = a.off[a.height - 1];
-        const uint4 v = g[(o + k) * 4 + sub];
+        const uint4 v = load4(g + (o + k) * 4 + sub, a.leaf_nt);
         const uint32_t idx = cnt4(v);
         // this lane's candidate key for idx % 4, then taken from lane idx / 4 of the group
         const uint32_t r = idx & 3;
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_pmap4(SstArgs a) {
             const uint4* g = reinterpret_cast<const uint4*>(a.nodes);
             for (uint32_t h = 1; h + 1 < a.height; h++) k = k * 17 + cnt4(g[(a.off[h] + k) * 4 + sub]);
             const uint64_t o = a.off[a.height - 1];
-            const uint4 v = g[(o + k) * 4 + sub];
+            const uint4 v = load4(g + (o + k) * 4 + sub, a.leaf_nt);
             const uint32_t idx = cnt4(v);
             const uint32_t r = idx & 3;
             uint32_t mine = r == 0 ? v.x : r == 1 ? v.y : r == 2 ? v.z : v.w;
@@ -550,6 +551,7 @@ static void sst_fill(const sst_index* x, SstArgs& a) {
     a.prefix_map = x->prefix_map;
     a.shift = x->shift;
     a.parts = x->parts;
+    a.leaf_nt = x->height > 0 && x->layer_nodes[x->height - 1] * 64 > SAS_NT_BYTES;
 }
 
 extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, uint32_t* out_val, uint64_t* out_rank,
