@@ -536,7 +536,7 @@ def main():
             "e2e_host": e2e,
             "variants": variants,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
-                                            "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "iterations",
+                                            "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "iterations",
                                             "sa_rounds", "build_sa_ns", "build_total_ns")},
             "setup_s": build_s, "verified": ok,
         }

@@ -111,6 +111,8 @@ typedef struct sas_stats {
                                   8 (SAS_BUILD_QUAD_COMPACT), 0 if not built        */
     uint32_t quad_fan;       /* quad inner-node fan-out: 31 (prefix-relative nodes) or
                                 17 (SAS_BUILD_QUAD_ABS), 0 if not built              */
+    uint32_t top2_levels;    /* binary-search levels whose pivots come from LDS or the
+                                cache-resident pivot array (PLAIN/LCP/INLINE)        */
 } sas_stats;
 
 const char* sas_last_error(void);

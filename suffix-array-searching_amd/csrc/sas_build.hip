@@ -757,36 +757,33 @@ static int build_quad(sas_index* x, bool compact, uint32_t mode) {
     return 0;
 }
 
-// ------------------------------------------------------------------ LDS top of the binary search
+// ------------------------------------------------------------------ top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
-// the leading one (0 = went left: r = mid, 1 = right: l = mid + 1).
+// the leading one (0 = went left: r = mid, 1 = right: l = mid + 1); entry k =
+// {32-char key, SA value} of that state's pivot SA[(l + r) / 2].
 template <int W>
-__global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n,
-                      uint64_t* __restrict__ top_key, uint64_t* __restrict__ top_sa, uint32_t nodes) {
+__global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint4* __restrict__ top2,
+                      uint32_t nodes) {
     GRID_STRIDE(k, nodes) {
-        if (k == 0) { top_key[0] = 0; top_sa[0] = 0xFFFFFFFFu; continue; }
-        uint64_t l = 0, r = sa_n;
-        int depth = 63 - __clzll(k);
+        uint64_t l = 0, r = sa_n, p = 0xFFFFFFFFu, key = 0;
+        int depth = k ? 63 - __clzll(k) : 0;
         for (int b = depth - 1; b >= 0; b--) {
             uint64_t mid = (l + r) >> 1;
             if (l >= r) break;
             if ((k >> b) & 1) l = mid + 1; else r = mid;
         }
-        if (l < r) {
-            uint64_t p = sa[(l + r) >> 1];
-            top_sa[k] = p;
-            top_key[k] = text_chars32(tw, p);
-        } else {
-            top_sa[k] = 0xFFFFFFFFu;
-            top_key[k] = 0;
+        if (k && l < r) {
+            p = sa[(l + r) >> 1];
+            key = text_chars32(tw, p);
         }
+        top2[k] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
     }
 }
 
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
-    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top_key, x->top_sa, x->scratch, x->sec_inner,
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top2, x->scratch, x->sec_inner,
                      x->sec_leaves, x->quad_inner, x->quad_leaves};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete x;
@@ -1037,18 +1034,18 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         uint32_t iters = 64 - __builtin_clzll(sa_n);  // ilog2(len) + 1 (sas/sa_search.rs:171)
         x->iters = iters;
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
-        DevBuf k, s;
-        TRY(k.alloc(SAS_TOP_NODES * 8, "top keys"));
-        TRY(s.alloc(SAS_TOP_NODES * 8, "top sa"));
+        x->top2_levels = iters < SAS_TOP2_LEVELS ? iters : SAS_TOP2_LEVELS;
+        DevBuf t2;
+        TRY(t2.alloc(SAS_TOP2_NODES * 16, "top2"));
+        const dim3 tg(grid_for(SAS_TOP2_NODES)), tb(256);
         if (W == 5)
-            hipLaunchKernelGGL(k_top<5>, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, SaView<5>{x->sa},
-                               sa_n, k.as<uint64_t>(), s.as<uint64_t>(), (uint32_t)SAS_TOP_NODES);
+            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(),
+                               (uint32_t)SAS_TOP2_NODES);
         else
-            hipLaunchKernelGGL(k_top<4>, dim3(grid_for(SAS_TOP_NODES)), dim3(256), 0, 0, x->text_w, SaView<4>{x->sa},
-                               sa_n, k.as<uint64_t>(), s.as<uint64_t>(), (uint32_t)SAS_TOP_NODES);
+            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(),
+                               (uint32_t)SAS_TOP2_NODES);
         HIP_TRY(hipGetLastError());
-        x->top_key = static_cast<uint64_t*>(k.release());
-        x->top_sa = static_cast<uint64_t*>(s.release());
+        x->top2 = static_cast<uint4*>(t2.release());
     }
     HIP_TRY(hipMalloc(&x->scratch, 64));
     HIP_TRY(hipMemset(x->scratch, 0, 64));
@@ -1076,6 +1073,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.quad_lds_layers = x->quad_lds_layers;
     st.quad_entry_bytes = x->quad_leaves ? (x->quad_compact ? 8 : 16) : 0;
     st.quad_fan = x->quad_leaves ? x->quad_fan : 0;
+    st.top2_levels = x->top2_levels;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -36,9 +36,9 @@ struct SearchArgs {
     uint64_t next_pos;   // answer when the lower bound is sa_n (n for a whole index)
     uint64_t rank_lo;    // global rank of sa[0]
     const uint8_t* sa;       // SaView<W> (u32 or packed 40-bit)
-    const uint64_t* top_key;
-    const uint64_t* top_sa;
+    const uint4* top2;
     uint32_t top_levels;
+    uint32_t top2_levels;
     uint32_t iters;
     const uint32_t* stree;
     uint64_t stree_off[SAS_STREE_MAX_LAYERS];
@@ -96,8 +96,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         D = a.top_levels;
         uint32_t nodes = 1u << D;
         for (uint32_t k = threadIdx.x; k < nodes; k += blockDim.x) {
-            s_key[k] = a.top_key[k];
-            s_sa[k] = (sa_val_t<W>)a.top_sa[k];
+            const uint4 e = a.top2[k];
+            s_key[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
+            s_sa[k] = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
         }
         __syncthreads();
     }
@@ -124,6 +125,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                 if (TOP && it < D) {
                     p = s_sa[k];
                     lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
+                    k = 2 * k + (lt ? 1u : 0u);
+                } else if (TOP && it < a.top2_levels) {
+                    // the next levels' pivots from the L2-resident top2 array: one 16-B read
+                    // instead of an SA word and a text window
+                    const uint4 e = a.top2[k];
+                    p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
+                    lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
                     k = 2 * k + (lt ? 1u : 0u);
                 } else {
                     p = (sa_val_t<W>)sa[mid];
@@ -1015,8 +1023,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
     if (TOP) {
         D = a.top_levels;
         for (uint32_t k = threadIdx.x; k < (1u << D); k += blockDim.x) {
-            s_key[k] = a.top_key[k];
-            s_sa[k] = a.top_sa[k];
+            const uint4 e = a.top2[k];
+            s_key[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
+            s_sa[k] = (uint64_t)e.z | ((uint64_t)e.w << 32);
         }
         __syncthreads();
     }
@@ -1038,6 +1047,10 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                 if (TOP && it < D) {
                     key = s_key[k];
                     p = s_sa[k];
+                } else if (TOP && it < a.top2_levels) {
+                    const uint4 e = a.top2[k];
+                    key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                    p = (uint64_t)e.z | ((uint64_t)e.w << 32);
                 } else if (KO) {
                     key = quad_entry_key<true>(a, mid);
                     p = key == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
@@ -1047,7 +1060,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                     p = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
                 }
                 const bool ge = sector_ge<QW>(key, p, K64, a, q);
-                if (TOP && it < D) k = 2 * k + (ge ? 0u : 1u);
+                if (TOP && it < a.top2_levels) k = 2 * k + (ge ? 0u : 1u);
                 probes++;
                 if (ge) {
                     r = mid;
@@ -1156,9 +1169,9 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.next_pos = x->next_pos;
     a.rank_lo = x->rank_lo;
     a.sa = x->sa;
-    a.top_key = x->top_key;
-    a.top_sa = x->top_sa;
+    a.top2 = x->top2;
     a.top_levels = x->top_levels;
+    a.top2_levels = x->top2_levels;
     a.iters = x->iters;
     a.stree = x->stree;
     for (int h = 0; h < SAS_STREE_MAX_LAYERS; h++) a.stree_off[h] = x->stree_off[h];

@@ -49,7 +49,7 @@ class SasStats(C.Structure):
         ("sector_bytes", C.c_uint64), ("sector_layers", C.c_uint32), ("sector_lds_layers", C.c_uint32),
         ("quad_bytes", C.c_uint64), ("quad_layers", C.c_uint32), ("quad_lds_layers", C.c_uint32),
         ("quad_entry_bytes", C.c_uint32),
-        ("quad_fan", C.c_uint32),
+        ("quad_fan", C.c_uint32), ("top2_levels", C.c_uint32),
     ]
 
     def as_dict(self):
