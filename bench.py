@@ -80,6 +80,25 @@ def rank_query_offsets(n: int, nq: int, m: int, rank: int) -> np.ndarray:
     return off
 
 
+# The one JSON line goes to the original stdout; everything else that writes to fd 1
+# (RCCL prints its version banner there when a communicator comes up) is sent to
+# stderr, so stdout carries exactly the result line.
+_RESULT_OUT = None
+
+
+def emit(obj) -> None:
+    out = _RESULT_OUT or sys.stdout
+    print(json.dumps(obj), file=out, flush=True)
+
+
+def keep_stdout_for_result() -> None:
+    global _RESULT_OUT
+    if _RESULT_OUT is None:
+        sys.stdout.flush()
+        _RESULT_OUT = os.fdopen(os.dup(1), "w")
+        os.dup2(2, 1)
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -217,7 +236,7 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
     one = s1 / (time.perf_counter() - t1)
     cpu_ok = bool(np.array_equal(cpu_out, ref[:sample]))
     best = max(res, key=lambda k: res[k]["lookups_per_s"])
-    print(json.dumps({
+    emit({
         "metric": "u32 static-search-tree lookups/s (2^28 keys = 1 GiB, 10^7 uniform queries)",
         "value": res[best]["lookups_per_s"], "unit": "lookups/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "higher_is_better": True, "dtype": "u32", "vs_baseline": None,
@@ -229,8 +248,7 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         "cpu_baseline": {"value": sample / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
                          "single_thread_value": one, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
                          "sample": f"oracle STree16 left_max + batch_final::<128> restatement (sst/s_tree.rs:303-326) "
-                                   f"on all {sample} queries, {threads} threads, {dt:.2f} s", "agrees": cpu_ok}}),
-          flush=True)
+                                   f"on all {sample} queries, {threads} threads, {dt:.2f} s", "agrees": cpu_ok}})
 
 
 def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
@@ -323,7 +341,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     if rank == 0:
         h = results[main_algo]
         traffic, tsrc = load_traffic(f"c3_{main_algo}", n, nq, "8-256")
-        print(json.dumps({
+        emit({
             "metric": "pattern lookups/s (configs[3] shape)", "value": h["lookups_per_s"], "unit": "lookups/s",
             "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": nq / h["lookups_per_s"] * 1e3,
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
@@ -341,7 +359,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
                                             "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
                                             "stree_bytes", "sector_bytes", "quad_bytes", "quad_fan",
-                                            "quad_entry_bytes")}}), flush=True)
+                                            "quad_entry_bytes")}})
 
 
 def main():
@@ -367,6 +385,7 @@ def main():
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
     args = ap.parse_args()
+    keep_stdout_for_result()
 
     import torch
     import sas_amd
@@ -540,7 +559,7 @@ def main():
                                             "sa_rounds", "build_sa_ns", "build_total_ns")},
             "setup_s": build_s, "verified": ok,
         }
-        print(json.dumps(line), flush=True)
+        emit(line)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
