@@ -2,6 +2,7 @@
 include/*.h declares, and its host-only entry points agree with the oracle.
 (No kernel is launched here: this container has no GPU.)"""
 import ctypes as C
+import os
 
 import numpy as np
 import pytest
@@ -79,3 +80,29 @@ def test_read_fasta(tmp_path):
         sas_amd.read_fasta_file(str(g))
     with pytest.raises(sas_amd.SasError):
         sas_amd.read_fasta_file(str(tmp_path / "missing.fa"))
+
+
+def test_quad_layout_flags():
+    """Python mirror of the quad build flags (include/sas.h): leaves and inner layout."""
+    from sas_amd.sa import _quad_flags
+    assert _quad_flags(False) == 0
+    assert _quad_flags(True) == _lib.SAS_BUILD_QUAD
+    assert _quad_flags("compact") == _lib.SAS_BUILD_QUAD_COMPACT
+    assert _quad_flags("abs") == _lib.SAS_BUILD_QUAD | _lib.SAS_BUILD_QUAD_ABS
+    assert _quad_flags("rel") == _lib.SAS_BUILD_QUAD | _lib.SAS_BUILD_QUAD_REL
+    assert _quad_flags("compact-rel") == _lib.SAS_BUILD_QUAD_COMPACT | _lib.SAS_BUILD_QUAD_REL
+    for bad in ("wide", "compact-x", 1, None):
+        with pytest.raises(ValueError):
+            _quad_flags(bad)
+    hdr = open(os.path.join(os.path.dirname(_lib.LIB_PATH), "..", "include", "sas.h")).read()
+    for name in ("SAS_BUILD_QUAD_ABS", "SAS_BUILD_QUAD_REL"):
+        assert f"#define {name} (1u << {getattr(_lib, name).bit_length() - 1})" in hdr
+
+
+def test_stats_struct_matches_header():
+    """ctypes SasStats lists the fields of sas_stats in include/sas.h, in order."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(_lib.LIB_PATH), "..", "include", "sas.h")).read()
+    body = hdr[hdr.index("typedef struct sas_stats {"):hdr.index("} sas_stats;")]
+    fields = re.findall(r"^\s*uint(?:32|64)_t\s+(\w+);", body, re.M)
+    assert fields == [f for f, _ in _lib.SasStats._fields_]
