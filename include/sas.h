@@ -155,6 +155,11 @@ int sas_route(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsp
               const uint8_t* qbytes, uint32_t m, uint64_t nq, uint32_t* out_shard,
               void* stream, uint32_t flags);
 
+/* sas_route for ragged queries: query k = qbytes[qoff[k] .. qoff[k] + qlen[k]). */
+int sas_route_batch(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsplit,
+                    const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen, uint64_t nq,
+                    uint32_t* out_shard, void* stream, uint32_t flags);
+
 /* One sharded step's send side, fused on the GPU (device pointers only,
  * SAS_DEVICE_PTRS): route each fixed-length query (as sas_route), group the
  * queries by destination shard (counting sort) and copy their bytes into
@@ -225,6 +230,28 @@ int sas_gen_text(uint64_t seed, uint64_t n, uint8_t* out, uint32_t flags);
 int sas_gen_queries(uint64_t seed, uint64_t word_pos, uint64_t n, uint64_t nq, uint64_t margin,
                     uint32_t len_lo, uint32_t len_hi, uint64_t* off, uint32_t* len,
                     uint64_t* next_word);
+
+/* One process, several GPUs (SURVEY §8b sas_build_multi).  mode
+ * SAS_MULTI_REPLICATE: every device builds the whole index (sas_build) and a
+ * batch is cut into contiguous query chunks, one per device, run concurrently.
+ * SAS_MULTI_SHARD: device g builds only part g of the SA rank space
+ * (sas_build_part, balanced to 7-char-prefix bins); queries are routed on the
+ * first device against the parts' first suffixes (sas_route_batch) and each part
+ * answers its own.  Results are identical to one sas_build index.  `devices`
+ * lists ngpu device ordinals (repeats allowed: several parts on one GPU).  Host
+ * pointers only; the text stays with the caller.  The one-process-per-GPU path
+ * over RCCL is bench.py --mode shard / sas_amd.shard. */
+typedef struct sas_multi sas_multi;
+#define SAS_MULTI_REPLICATE 0
+#define SAS_MULTI_SHARD     1
+int sas_build_multi(const uint8_t* text, uint64_t n, const int* devices, int ngpu, int mode,
+                    uint32_t flags, sas_multi** out);
+int sas_multi_free(sas_multi* multi);
+int sas_multi_parts(const sas_multi* multi);
+int sas_multi_get_stats(const sas_multi* multi, int part, sas_stats* out);
+/* Ragged batch as sas_search_batch (synchronous, host pointers). */
+int sas_search_multi(const sas_multi* multi, const uint8_t* qbytes, const uint64_t* qoff,
+                     const uint32_t* qlen, uint64_t nq, int algo, uint64_t* out_pos, uint32_t flags);
 
 /* Real-data inputs.
  * sas_read_fasta: read_fasta_file (sas/util.rs:144-169) -- records concatenated,

@@ -44,6 +44,7 @@
 #define SAS_QUAD_FAN 17               // quad tree, absolute nodes: 16 u32 separators, 17 children
 #define SAS_QUAD_RFAN 31              // quad tree, prefix-relative nodes: 30 u16 separators, 31 children
 #define SAS_QUAD_RMAXD 13             // relative nodes: at most 13 shared chars in the 27-bit header
+#define SAS_MAX_SPLIT 1024            // sharded mode: at most 1025 parts
 #define SAS_QUAD_MAX_INNER 10         // inner layers the (unrolled) descent supports; leaf index < 2^32
 #define SAS_QUAD_MAX_LDS 4            // of which at most this many LDS-staged
 #define SAS_QUAD_MAX_LAYERS 16

@@ -1351,15 +1351,16 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
 }
 
 // ------------------------------------------------------------------ sharded-mode routing
-#define SAS_MAX_SPLIT 1024
 __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ tw, uint64_t n,
                                                const uint64_t* __restrict__ sp, uint32_t nsplit,
-                                               const uint8_t* __restrict__ qbytes, uint32_t m, uint64_t nq,
-                                               uint32_t* __restrict__ out, uint32_t* bad) {
+                                               const uint8_t* __restrict__ qbytes, uint32_t m,
+                                               const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qlen,
+                                               uint64_t nq, uint32_t* __restrict__ out, uint32_t* bad) {
     uint32_t b = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
         QueryRegs<4> q;
-        q.load(qbytes + i * (uint64_t)m, m, &b);
+        if (qoff) q.load(qbytes + qoff[i], qlen[i], &b);  // ragged (sas_route_batch)
+        else q.load(qbytes + i * (uint64_t)m, m, &b);
         uint32_t lo = 0, hi = nsplit, lcp;
         while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
             uint32_t mid = (lo + hi) >> 1;
@@ -1371,24 +1372,42 @@ __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ tw, 
     if (b) atomicOr(bad, 1u);
 }
 
-extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit, const uint8_t* qbytes,
-                         uint32_t m, uint64_t nq, uint32_t* out_shard, void* stream, uint32_t flags) {
+// Fixed-length (qoff == nullptr) or ragged routing, host or device pointers.
+static int route_impl(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit, const uint8_t* qbytes,
+                      uint32_t m, const uint64_t* qoff, const uint32_t* qlen, uint64_t nq, uint32_t* out_shard,
+                      void* stream, uint32_t flags) {
     if (!x || (nsplit && !splitter_pos) || (nq && (!qbytes || !out_shard))) SAS_FAIL(EINVAL, "sas_route: null argument");
+    if (qoff && !qlen) SAS_FAIL(EINVAL, "sas_route_batch: qoff without qlen");
     if (nsplit > SAS_MAX_SPLIT) SAS_FAIL(EINVAL, "sas_route: too many splitters");
     if (nq == 0) return 0;
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     bool dev = flags & SAS_DEVICE_PTRS;
-    DeviceBuf bsp, bq, bout;
+    DeviceBuf bsp, bq, bout, boff, blen;
     const uint64_t* dsp = splitter_pos;
     const uint8_t* dq = qbytes;
+    const uint64_t* doff = qoff;
+    const uint32_t* dlen = qlen;
     uint32_t* dout = out_shard;
     if (!dev) {
+        uint64_t span = nq * (uint64_t)m;
+        if (qoff) {
+            span = 0;
+            for (uint64_t k = 0; k < nq; k++) span = qoff[k] + qlen[k] > span ? qoff[k] + qlen[k] : span;
+        }
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMalloc(&bsp.p, nsplit * 8 + 8));
         if (nsplit) HIP_TRY(hipMemcpy(bsp.p, splitter_pos, nsplit * 8, hipMemcpyHostToDevice));
-        HIP_TRY(hipMalloc(&bq.p, nq * (uint64_t)m + 64));
-        HIP_TRY(hipMemcpy(bq.p, qbytes, nq * (uint64_t)m, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&bq.p, span + 64));
+        if (span) HIP_TRY(hipMemcpy(bq.p, qbytes, span, hipMemcpyHostToDevice));
+        if (qoff) {
+            HIP_TRY(hipMalloc(&boff.p, nq * 8));
+            HIP_TRY(hipMalloc(&blen.p, nq * 4));
+            HIP_TRY(hipMemcpy(boff.p, qoff, nq * 8, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(blen.p, qlen, nq * 4, hipMemcpyHostToDevice));
+            doff = static_cast<const uint64_t*>(boff.p);
+            dlen = static_cast<const uint32_t*>(blen.p);
+        }
         HIP_TRY(hipMalloc(&bout.p, nq * 4));
         dsp = static_cast<const uint64_t*>(bsp.p);
         dq = static_cast<const uint8_t*>(bq.p);
@@ -1396,14 +1415,26 @@ extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint3
     }
     uint64_t blocks = (nq + 255) / 256;
     if (blocks > 65536) blocks = 65536;
-    hipLaunchKernelGGL(k_route, dim3((unsigned)blocks), dim3(256), 0, st, x->text_w, x->n, dsp, nsplit, dq, m, nq,
-                       dout, x->scratch);
+    hipLaunchKernelGGL(k_route, dim3((unsigned)blocks), dim3(256), 0, st, x->text_w, x->n, dsp, nsplit, dq, m, doff,
+                       dlen, nq, dout, x->scratch);
     HIP_TRY(hipGetLastError());
     if (!dev) {
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMemcpy(out_shard, dout, nq * 4, hipMemcpyDeviceToHost));
     }
     return 0;
+}
+
+extern "C" int sas_route(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit, const uint8_t* qbytes,
+                         uint32_t m, uint64_t nq, uint32_t* out_shard, void* stream, uint32_t flags) {
+    return route_impl(x, splitter_pos, nsplit, qbytes, m, nullptr, nullptr, nq, out_shard, stream, flags);
+}
+
+extern "C" int sas_route_batch(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
+                               const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen, uint64_t nq,
+                               uint32_t* out_shard, void* stream, uint32_t flags) {
+    if (nq && (!qoff || !qlen)) SAS_FAIL(EINVAL, "sas_route_batch: null qoff/qlen");
+    return route_impl(x, splitter_pos, nsplit, qbytes, 0, qoff, qlen, nq, out_shard, stream, flags);
 }
 
 // ------------------------------------------------------------------ route + pack (sharded step)
@@ -1498,7 +1529,8 @@ extern "C" int sas_route_pack(const sas_index* x, const uint64_t* splitter_pos, 
     uint64_t rb = (nq + 255) / 256;
     if (rb > 65536) rb = 65536;
     hipLaunchKernelGGL(k_route, dim3((unsigned)rb), dim3(256), 0, st, x->text_w, x->n, splitter_pos, nsplit, qbytes,
-                       m, nq, static_cast<uint32_t*>(dest), x->scratch);
+                       m, (const uint64_t*)nullptr, (const uint32_t*)nullptr, nq, static_cast<uint32_t*>(dest),
+                       x->scratch);
     hipLaunchKernelGGL(k_pack_count, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest), nq,
                        W, nblk, static_cast<uint64_t*>(cnt));
     HIP_TRY(rocprim::exclusive_scan(tmp, tbytes, static_cast<uint64_t*>(cnt), static_cast<uint64_t*>(cnt),

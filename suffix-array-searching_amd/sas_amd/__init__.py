@@ -6,4 +6,5 @@ over the C ABI of libsas_amd.so (include/sas.h, include/sst.h).
 from ._lib import SasError, lib, build_library, declared_symbols, LIB_PATH  # noqa: F401
 from .sa import (SaNaive, Counter, binary_search, binary_search_batch,  # noqa: F401
                  random_string, random_queries, read_fasta_file, kmer_keys)
+from .multi import SaMulti  # noqa: F401
 from .sst import SortedVec, Eytzinger, STree16, STree15, PartitionedSTree16M, MAX  # noqa: F401

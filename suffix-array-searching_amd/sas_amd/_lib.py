@@ -29,6 +29,7 @@ SAS_BUILD_QUAD = 1 << 9
 SAS_BUILD_QUAD_COMPACT = 1 << 10
 SAS_BUILD_QUAD_ABS = 1 << 11
 SAS_BUILD_QUAD_REL = 1 << 12
+SAS_MULTI_REPLICATE, SAS_MULTI_SHARD = 0, 1
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
@@ -105,6 +106,12 @@ def lib():
     L.sas_build_part.argtypes = [vp, u64, u32, u32, u32, C.POINTER(vp)]
     L.sas_route.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, u32]
     L.sas_route_pack.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, vp, vp, u32]
+    L.sas_route_batch.argtypes = [vp, vp, u32, vp, vp, vp, u64, vp, vp, u32]
+    L.sas_build_multi.argtypes = [vp, u64, vp, i32, i32, u32, C.POINTER(vp)]
+    L.sas_multi_free.argtypes = [vp]
+    L.sas_multi_parts.argtypes = [vp]
+    L.sas_multi_get_stats.argtypes = [vp, i32, C.POINTER(SasStats)]
+    L.sas_search_multi.argtypes = [vp, vp, vp, vp, u64, i32, vp, u32]
     L.sas_get_stats.argtypes = [vp, C.POINTER(SasStats)]
     L.sas_copy_sa.argtypes = [vp, vp, u64, u32]
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]

@@ -762,3 +762,33 @@ def test_full_size_algorithms_agree_and_are_lower_bounds(sas):
         if r > 0:
             prev = int(idx.suffix_array(count=1, start=r - 1)[0])
             assert bytes(ht[prev:prev + len(q)]) < q
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_multi_device_handle(sas, devices):
+    """sas_build_multi / sas_search_multi, REPLICATE and SHARD, with the
+    one GPU listed several times: positions equal one whole index / the oracle on a
+    random and a repeat-rich text, ragged mixed queries incl. misses and text ends."""
+    rng = np.random.default_rng(len(devices))
+    blk = rng.integers(0, 4, 4000, dtype=np.uint8)
+    for t in (sas.random_string(300_017, seed=3), np.concatenate([blk, blk, rng.integers(0, 4, 777, dtype=np.uint8),
+                                                                    blk, blk[:1500]])):
+        n = len(t)
+        whole = sas.SaNaive.build(t, lcp=False, stree=False, sector=False)
+        sa = whole.suffix_array()
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 300, 1500), rng.integers(1, 300, 1500))]
+        qs += [rng.integers(0, 4, rng.integers(0, 40), dtype=np.uint8) for _ in range(500)]
+        qs += [np.full(k, 3, np.uint8) for k in (1, 32, 100)] + [t[n - k:] for k in (1, 7, 40)]
+        buf, off, lens = pack(qs)
+        expect = oracle_positions(t, sa, buf, off, lens)
+        for mode in ("replicate", "shard"):
+            M = sas.SaMulti.build(t, devices, mode=mode)
+            assert M.parts() == len(devices)
+            if mode == "shard":
+                st = [M.stats(g) for g in range(len(devices))]
+                assert sum(s["sa_entries"] for s in st) == n
+                assert [s["rank_lo"] for s in st] == sorted(s["rank_lo"] for s in st)
+            for algo in ("quad", "plain"):
+                got = M.search_batch(buf, off, lens, algo=algo)
+                assert np.array_equal(got, expect), (mode, algo, len(devices), n)
+            M.free()
