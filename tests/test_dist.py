@@ -6,6 +6,7 @@ import os
 import socket
 
 import numpy as np
+import pytest
 import torch.multiprocessing as mp
 
 import bench
@@ -51,20 +52,22 @@ def worker(rank, ws, port, res):
     dist.destroy_process_group()
 
 
-def test_two_rank_harness():
-    ws = 2
+@pytest.mark.parametrize("ws", [2, 8])
+def test_rank_harness(ws):
+    """world_size 2, and 8 (the driver's largest scaling run) rehearsed with gloo."""
     mgr = mp.Manager()
     res = mgr.dict()
     mp.spawn(worker, args=(ws, free_port(), res), nprocs=ws, join=True)
-    (e0, off0, p0), (e1, off1, p1) = res[0], res[1]
-    assert e0 == e1 and e0 >= 3 * 0.02  # both ranks report the same MAX
-    assert off0 != off1  # disjoint query streams per rank
+    els = [res[r][0] for r in range(ws)]
+    assert len(set(els)) == 1 and els[0] >= 3 * 0.02  # every rank reports the same MAX
+    offs = [tuple(res[r][1]) for r in range(ws)]
+    assert len(set(offs)) == ws  # disjoint query streams per rank
     # replicated index: each shard's answers equal a single-process search of those queries
     n, m = 1 << 14, 24
     t = O.random_string(n)
     sa = O.build_sa(t)
     tp = O.padded(t)
-    for off, pos in ((off0, p0), (off1, p1)):
+    for off, pos in ((res[r][1], res[r][2]) for r in range(ws)):
         for o, p in zip(off[:50], pos[:50]):
             assert O.search_one(tp, n, sa, t[o:o + m])[0] == p
             assert list(t[p:p + m]) == list(t[o:o + m])
@@ -127,8 +130,8 @@ def shard_worker(rank, ws, port, res):
     dist.destroy_process_group()
 
 
-def test_sharded_exchange_three_ranks():
-    ws = 3
+@pytest.mark.parametrize("ws", [3, 8])
+def test_sharded_exchange(ws):
     mgr = mp.Manager()
     res = mgr.dict()
     mp.spawn(shard_worker, args=(ws, free_port(), res), nprocs=ws, join=True)
