@@ -268,7 +268,7 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     text = sas_amd.random_string(n, seed=SEED, device=dev)
     # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
     idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
-                                quad=quad_mode, verify=True)
+                                quad=quad_mode, verify=True, llcp=False)
     stats = idx.stats()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
@@ -370,8 +370,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default="quad", choices=["stree", "plain", "lcp", "sector", "quad", "inline"])
-    ap.add_argument("--variants", default="plain,lcp,stree,sector,quad,inline",
+    ap.add_argument("--algo", default="quad", choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp"])
+    ap.add_argument("--variants", default="plain,lcp,llcp,stree,sector,quad,inline",
                     help="other algos timed beside the headline one")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -524,6 +524,8 @@ def main():
                              "S-tree of 16-char SA keys (top layers LDS-staged)",
                     "plain": "configs[1]: 2^30 text in HBM, 10^7 len-32 queries, plain binary search over SA",
                     "lcp": "configs[1] + mlr LCP skipping",
+                    "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (one 8-B {SA, Llcp, Rlcp} "
+                            "entry per probe, text only on lcp ties), 2^30 text in HBM, 10^7 len-32 queries",
                     "sector": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, sector S-tree (32-B nodes, "
                               "fused 32-char key + SA leaves, top layers LDS-staged)",
                     "inline": "configs[1] probe sequence (binary_search_batch) over fused 32-char key + SA "

@@ -67,6 +67,12 @@ typedef struct sas_index sas_index;
                                         layout with fewer levels larger than the 256 MiB
                                         Infinity Cache (absolute on a tie; n = 2^30 builds
                                         absolute, n = 2^34 compact builds relative)        */
+#define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
+                                        SAS_ALGO_LLCP: per SA rank m, one 16-B entry
+                                        {SA[m] 40 bits, Llcp 12 bits, Rlcp 12 bits, 16 chars
+                                        of SA[m] after each} of the binary-search interval
+                                        whose mid is m, derived from the LCP array (built
+                                        too).  16 B per suffix                           */
 
 /* search algorithms; all return bit-identical positions */
 enum sas_algo {
@@ -79,9 +85,14 @@ enum sas_algo {
                            31-ary on the 8 chars after each node's shared prefix (17-ary on
                            16-char keys with SAS_BUILD_QUAD_ABS), leaves = 4 fused (32-char
                            key, SA) entries                                                  */
-    SAS_ALGO_INLINE = 5 /* PLAIN's probe sequence (binary_search_batch) over the quad tree's
+    SAS_ALGO_INLINE = 5, /* PLAIN's probe sequence (binary_search_batch) over the quad tree's
                            fused (32-char key, SA) entries: one 16-B read per probe instead of
                            an SA word + text words ("inlining values", todo.org:18-19)     */
+    SAS_ALGO_LLCP = 6   /* PLAIN's probe sequence with Manber-Myers LLCP/RLCP skipping: a probe
+                           reads one 16-B {SA, Llcp, Rlcp, chars} entry and decides from the
+                           lcp values alone unless they tie llcp/rlcp; a tie compares the
+                           entry's 16 chars before any text (needs SAS_BUILD_LLCP; the LCP
+                           array at work, A21)                                              */
 };
 
 typedef struct sas_stats {
@@ -113,6 +124,7 @@ typedef struct sas_stats {
                                 17 (SAS_BUILD_QUAD_ABS), 0 if not built              */
     uint32_t top2_levels;    /* binary-search levels whose pivots come from LDS or the
                                 cache-resident pivot array (PLAIN/LCP/INLINE)        */
+    uint64_t llcp_bytes;     /* SAS_BUILD_LLCP entries (16 B per suffix), 0 if not built */
 } sas_stats;
 
 const char* sas_last_error(void);

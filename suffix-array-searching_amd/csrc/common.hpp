@@ -83,6 +83,7 @@ struct sas_index {
     uint8_t* sa = nullptr;        // sa_w bytes per entry (SaView<4> / SaView<5>)
     uint32_t sa_w = 4;
     uint32_t* lcp = nullptr;
+    uint4* llcp = nullptr;        // SAS_BUILD_LLCP: {SA[m], Llcp, Rlcp, 2 x 16 chars} per rank m (sas_build.hip)
     uint32_t* stree = nullptr;   // all nodes, 16 u32 each
     uint64_t stree_nodes = 0;
     uint32_t stree_height = 0;
@@ -143,6 +144,8 @@ struct sst_index {
 // ---------------------------------------------------------------- suffix-array element access
 #define SAS_SA40_PAD 8           // bytes after a packed 40-bit SA (aligned 8-B reads)
 #define SAS_SA40_MAX (1ull << 40)
+// SAS_BUILD_LLCP entries: SA (40 bits) | Llcp << 40 | Rlcp << 52 + 16 chars after each lcp
+#define SAS_LLCP_CAP 4095u
 
 template <int W>
 struct SaView {

@@ -423,6 +423,62 @@ __global__ void k_lcp(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa,
     }
 }
 
+// ------------------------------------------------------------------ LLCP / RLCP
+// The Manber-Myers accelerant behind SAS_ALGO_LLCP.  binary_search's loop over
+// [0, sa_n) (sas/sa_search.rs:98-112) probes rank m in exactly one interval [l, r):
+// the one whose mid (l + r) / 2 is m.  Entry m (16 B) holds, for that interval,
+//   .x, .y  SA[m] (40 bits) | Llcp << 40 | Rlcp << 52 (12 bits each, capped at
+//           SAS_LLCP_CAP): Llcp = lcp(SA[l-1], SA[m]) = min LCP[l..m],
+//           Rlcp = lcp(SA[m], SA[r]) = min LCP[m+1..r], LCP[0] = LCP[sa_n] = 0
+//           standing for the virtual bounds (no inference there);
+//   .z      16 chars of suffix SA[m] from char Llcp,  .w  16 chars from char Rlcp
+//           (2-bit packed, first char high, zero past the text end): the chars a
+//           tie compares first, so a tie rarely reads text.
+// Built bottom-up over the implicit tree, one launch per depth: min LCP[l..m] is the
+// smaller of the left child's two values (LCP[m] when that child is empty), and
+// likewise on the right; a min of capped values is the capped min.
+// Depth of rank m's interval, or maxd + 1 when it is deeper than maxd.
+__device__ __forceinline__ uint32_t bs_node(uint64_t sa_n, uint64_t m, uint32_t maxd, uint64_t* l, uint64_t* r) {
+    uint64_t lo = 0, hi = sa_n;
+    uint32_t d = 0;
+    for (;;) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (mid == m) break;
+        if (d == maxd) return maxd + 1;
+        if (m < mid) hi = mid;
+        else lo = mid + 1;
+        d++;
+    }
+    *l = lo;
+    *r = hi;
+    return d;
+}
+
+template <int W>
+__global__ void k_llcp_level(const uint64_t* __restrict__ tw, SaView<W> sa, const uint32_t* __restrict__ lcp,
+                             uint64_t sa_n, uint32_t depth, uint4* __restrict__ e) {
+    GRID_STRIDE(m, sa_n) {
+        uint64_t l = 0, r = 0;
+        if (bs_node(sa_n, m, depth, &l, &r) != depth) continue;
+        auto lcp_at = [&](uint64_t i) -> uint64_t {
+            return (i == 0 || i >= sa_n) ? 0ull : (lcp[i] < SAS_LLCP_CAP ? lcp[i] : SAS_LLCP_CAP);
+        };
+        auto child_min = [&](uint64_t c) -> uint64_t {
+            const uint4 v = e[c];
+            const uint64_t a = (v.y >> 8) & SAS_LLCP_CAP, b = v.y >> 20;
+            return a < b ? a : b;
+        };
+        const uint64_t L = l < m ? child_min((l + m) >> 1) : lcp_at(m);
+        const uint64_t R = m + 1 < r ? child_min((m + 1 + r) >> 1) : lcp_at(r);
+        const uint64_t p = sa[m];
+        const uint64_t lo = p | (L << 40) | (R << 52);
+        // L, R <= n - p (an lcp never exceeds the suffix), so these reads stay inside
+        // the padded text
+        e[m] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)(text_chars32(tw, p + L) >> 32),
+                          (uint32_t)(text_chars32(tw, p + R) >> 32));
+    }
+}
+
 template <int W>
 __global__ void k_verify_adj(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa,
                              uint64_t sa_n, uint32_t* __restrict__ bitmap, uint32_t* __restrict__ bad) {
@@ -783,7 +839,7 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
-    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->stree, x->top2, x->scratch, x->sec_inner,
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->stree, x->top2, x->scratch, x->sec_inner,
                      x->sec_leaves, x->quad_inner, x->quad_leaves};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete x;
@@ -1013,7 +1069,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     const uint64_t sa_n = x->sa_n;
     rank_lo = x->rank_lo;
 
-    if (flags & SAS_BUILD_LCP) {
+    if (flags & (SAS_BUILD_LCP | SAS_BUILD_LLCP)) {
         DevBuf l;
         TRY(l.alloc(sa_n * 4, "lcp"));
         if (W == 5)
@@ -1024,6 +1080,22 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
                                l.as<uint32_t>());
         HIP_TRY(hipGetLastError());
         x->lcp = static_cast<uint32_t*>(l.release());
+    }
+    if (flags & SAS_BUILD_LLCP) {
+        DevBuf e;
+        TRY(e.alloc(sa_n * 16, "llcp entries"));
+        const uint32_t depths = 64 - __builtin_clzll(sa_n);  // binary_search iterations
+        for (int d = (int)depths - 1; d >= 0; d--) {
+            if (W == 5)
+                hipLaunchKernelGGL(k_llcp_level<5>, dim3(grid_for(sa_n)), dim3(256), 0, 0, x->text_w, SaView<5>{x->sa},
+                                   x->lcp, sa_n, (uint32_t)d, e.as<uint4>());
+            else
+                hipLaunchKernelGGL(k_llcp_level<4>, dim3(grid_for(sa_n)), dim3(256), 0, 0, x->text_w, SaView<4>{x->sa},
+                                   x->lcp, sa_n, (uint32_t)d, e.as<uint4>());
+        }
+        HIP_TRY(hipGetLastError());
+        x->llcp = e.as<uint4>();
+        e.release();
     }
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
     if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
@@ -1057,6 +1129,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.sa_bytes = sa_n * W;
     st.sa_width = W;
     st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
+    st.llcp_bytes = x->llcp ? sa_n * 16 : 0;
     st.stree_bytes = x->stree_nodes * 64;
     st.stree_layers = x->stree_height;
     st.stree_lds_layers = x->stree_lds_layers;

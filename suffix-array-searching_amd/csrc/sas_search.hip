@@ -12,6 +12,10 @@
 //          `sa[l]` (:195) needs no extra load.
 //   LCP    PLAIN + Manber-Myers mlr skipping: chars [0, min(llcp, rlcp)) are known
 //          equal and are not compared again (sas/sa_search.rs:344-345 TODO).
+//   LLCP   PLAIN's probes with Manber-Myers' Llcp/Rlcp accelerant (SAS_BUILD_LLCP):
+//          below the cached top levels a probe reads one 16-B {SA, Llcp, Rlcp,
+//          16 chars after each} entry; it decides from the lcps alone unless they
+//          tie, and a tie compares the inlined chars before any text.
 //   STREE  descend an STree<16,16> over the 16-char keys of the SA (top layers in
 //          LDS), giving the key range [r0, r1) of suffixes whose padded 16-char
 //          prefix equals the query's; the lower bound lies in [r0, r1] and is
@@ -36,6 +40,7 @@ struct SearchArgs {
     uint64_t next_pos;   // answer when the lower bound is sa_n (n for a whole index)
     uint64_t rank_lo;    // global rank of sa[0]
     const uint8_t* sa;       // SaView<W> (u32 or packed 40-bit)
+    const uint4* llcp;       // SAS_BUILD_LLCP entries (k_sa_binary<.., BS_LLCP, ..>)
     const uint4* top2;
     uint32_t top_levels;
     uint32_t top2_levels;
@@ -86,7 +91,33 @@ __device__ __forceinline__ void query_ptr(const SearchArgs& a, uint64_t i, const
 template <int W>
 using sa_val_t = typename std::conditional<W == 4, uint32_t, uint64_t>::type;
 
-template <int QW, bool LCP, bool TOP, int W>
+// LLCP tie: the first h chars of suffix p are known equal to q's; inl = the suffix's
+// chars [h, h + 16) from its LLCP entry.  Same result as suffix_less_from(.., h, ..),
+// which only runs when those 16 chars match and both strings go on.
+template <int QW>
+__device__ __forceinline__ bool llcp_tie_less(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
+                                              const QueryRegs<QW>& q, uint32_t h, uint32_t inl, uint32_t* lcp) {
+    const uint64_t lenS = n - p;
+    const uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
+    if (h < L) {
+        const uint32_t c = L - h < 16 ? L - h : 16;
+        const uint32_t mk = ~0u << (32 - 2 * c);  // c >= 1
+        const uint32_t av = inl & mk, bv = (uint32_t)(q.chars32(h) >> 32) & mk;
+        if (av != bv) {
+            *lcp = h + (uint32_t)(__clz(av ^ bv) >> 1);
+            return av < bv;
+        }
+        if (h + 16 < L) return suffix_less_from<QW>(tw, n, p, q, h + 16, lcp);
+    }
+    *lcp = L;
+    return lenS < (uint64_t)q.m;
+}
+
+// MODE 0: PLAIN, 1: LCP (mlr), 2: LLCP (Manber-Myers with the Llcp/Rlcp entries)
+#define BS_PLAIN 0
+#define BS_MLR 1
+#define BS_LLCP 2
+template <int QW, int MODE, bool TOP, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
     __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
     __shared__ sa_val_t<W> s_sa[TOP ? SAS_TOP_NODES : 1];
@@ -118,7 +149,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         for (uint32_t it = 0; it < a.iters; ++it) {
             if (l < r) {
                 uint64_t mid = (l + r) >> 1;
-                uint32_t h = LCP ? (llcp < rlcp ? llcp : rlcp) : 0u;
+                uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
                 sa_val_t<W> p;
                 uint32_t lcp;
                 bool lt;
@@ -133,6 +164,30 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
                     lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
                     k = 2 * k + (lt ? 1u : 0u);
+                } else if (MODE == BS_LLCP) {
+                    // one 16-B read: SA[mid], the lcps of the pivot with the interval's
+                    // bounds L = SA[l-1] (< q) and R = SA[r] (>= q), and 16 pivot chars
+                    // after each.  Manber-Myers: with llcp >= rlcp, Llcp > llcp puts the
+                    // pivot on L's side of q (< q, same lcp), Llcp < llcp on R's side
+                    // (> q, lcp = Llcp); symmetric with Rlcp.  A tie (or a capped value)
+                    // compares from the known lcp, first against the inlined chars.
+                    const uint4 e = a.llcp[mid];
+                    p = (sa_val_t<W>)((uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32));
+                    const uint32_t x = (e.y >> 8) & SAS_LLCP_CAP, y = e.y >> 20;
+                    uint32_t hh = 0, inl = 0;
+                    bool decided = true;
+                    if (llcp >= rlcp) {
+                        if (x > llcp) { lt = true; lcp = llcp; }
+                        else if (x < llcp && x < SAS_LLCP_CAP) { lt = false; lcp = x; }
+                        else { decided = false; hh = x; inl = e.z; }
+                    } else {
+                        if (y > rlcp) { lt = false; lcp = rlcp; }
+                        else if (y < rlcp && y < SAS_LLCP_CAP) { lt = true; lcp = y; }
+                        else { decided = false; hh = y; inl = e.w; }
+                    }
+                    if (!decided) {
+                        lt = llcp_tie_less<QW>(a.tw, n, p, q, hh, inl, &lcp);
+                    }
                 } else {
                     p = (sa_val_t<W>)sa[mid];
                     lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
@@ -1088,10 +1143,12 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
         case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
         default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
     }
-#define K_PLAIN_TOP(Q) (k_sa_binary<Q, false, true, W>)
-#define K_PLAIN(Q) (k_sa_binary<Q, false, false, W>)
-#define K_LCP_TOP(Q) (k_sa_binary<Q, true, true, W>)
-#define K_LCP(Q) (k_sa_binary<Q, true, false, W>)
+#define K_PLAIN_TOP(Q) (k_sa_binary<Q, BS_PLAIN, true, W>)
+#define K_PLAIN(Q) (k_sa_binary<Q, BS_PLAIN, false, W>)
+#define K_LCP_TOP(Q) (k_sa_binary<Q, BS_MLR, true, W>)
+#define K_LCP(Q) (k_sa_binary<Q, BS_MLR, false, W>)
+#define K_LLCP_TOP(Q) (k_sa_binary<Q, BS_LLCP, true, W>)
+#define K_LLCP(Q) (k_sa_binary<Q, BS_LLCP, false, W>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_STREE4X(Q) (k_sa_stree4x<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
@@ -1099,6 +1156,8 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
+    } else if (algo == SAS_ALGO_LLCP) {
+        if (top) { QW_CASE(K_LLCP_TOP) } else { QW_CASE(K_LLCP) }
     } else if (algo == SAS_ALGO_STREE) {
         // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
         if (qw == 1) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
@@ -1169,6 +1228,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.next_pos = x->next_pos;
     a.rank_lo = x->rank_lo;
     a.sa = x->sa;
+    a.llcp = x->llcp;
     a.top2 = x->top2;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;
@@ -1218,7 +1278,8 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_INLINE) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_LLCP) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "search: SAS_ALGO_LLCP needs SAS_BUILD_LLCP");
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
         SAS_FAIL(EINVAL, "search: SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "search: SAS_ALGO_STREE needs SAS_BUILD_STREE");
@@ -1316,7 +1377,8 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_INLINE) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_LLCP) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "sas_time_fixed: index has no LLCP entries");
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
         SAS_FAIL(EINVAL, "sas_time_fixed: index has no quad tree");
     HIP_TRY(hipSetDevice(x->device));

@@ -19,7 +19,7 @@ from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline")
+ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp")
 
 
 @pytest.fixture(scope="module")
@@ -74,7 +74,7 @@ def test_no_lds_top_same(sas, sadef):
     idx = sas.SaNaive.build(t)
     buf, off, lens = pack([q["q"] for q in c["queries"]])
     expect = np.array([q["pos"] for q in c["queries"]], np.uint64)
-    for algo in ("plain", "lcp"):
+    for algo in ("plain", "lcp", "llcp"):
         got = idx.search_batch(buf, off, lens, algo=algo, flags=_lib.SAS_NO_LDS_TOP)
         assert np.array_equal(got, expect)
 
@@ -151,6 +151,46 @@ def test_repetitive_texts(sas):
         for algo in ALGOS:
             got = idx.search_batch(buf, qo, ql, algo=algo)
             assert np.array_equal(got, expect), (name, algo)
+
+
+def test_llcp_capped_lcps(sas):
+    """SAS_ALGO_LLCP stores Llcp/Rlcp capped at 12 bits (SAS_LLCP_CAP = 4095).  Texts
+    whose adjacent suffixes share far more than 4095 chars, with queries longer than
+    the cap (exact matches, one-char mutations deep inside, text-end suffixes), take
+    the capped branches; with and without the LDS / pivot-array top levels, every
+    position equals the oracle's binary_search (sas/sa_search.rs:98-112)."""
+    from sas_amd import _lib
+    rng = np.random.default_rng(11)
+    blk = rng.integers(0, 4, 6000, dtype=np.uint8)
+    texts = {
+        "all_A": np.zeros(20_000, np.uint8),
+        "period_3": np.tile(np.array([0, 2, 1], np.uint8), 7000),
+        "repeats": np.concatenate([blk, rng.integers(0, 4, 50, dtype=np.uint8), blk, blk[:5000], blk]),
+    }
+    for name, t in texts.items():
+        n = len(t)
+        idx = sas.SaNaive.build(t, verify=True, stree=False, sector=False, quad=False)
+        assert idx.stats()["llcp_bytes"] == 16 * n
+        sa = O.build_sa(t)
+        qs = []
+        for m in (1, 31, 33, 300, 4094, 4095, 4096, 4200, 6500):
+            if m >= n:
+                continue
+            for o in rng.integers(0, n - m, 12):
+                q = t[o:o + m].copy()
+                qs.append(q)
+                if m > 2:
+                    for k in (m // 2, m - 1, min(m - 1, 4100)):
+                        mq = q.copy()
+                        mq[k] = (mq[k] + 1 + rng.integers(0, 3)) % 4
+                        qs.append(mq)
+        qs += [np.concatenate([t[n - k:], np.zeros(j, np.uint8)]) for k in (1, 4096, 5000) for j in (0, 3)]
+        buf, qo, ql = pack(qs)
+        expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+        for flags in (0, _lib.SAS_NO_LDS_TOP):
+            for algo in ("plain", "llcp"):
+                got, probes = idx.search_batch(buf, qo, ql, algo=algo, probes=True, flags=flags)
+                assert np.array_equal(got, expect), (name, algo, flags, np.nonzero(got != expect)[0][:5])
 
 
 def test_invalid_codes_rejected(sas):
@@ -523,9 +563,10 @@ def test_sa_beyond_u32(sas):
     import torch
     n = (1 << 32) + 12345
     t = sas.random_string(n, seed=321, device="cuda")
-    idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True)
+    idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True, llcp=False)  # LLCP: the second index below
     st = idx.stats()
     assert st["sa_width"] == 5 and st["n"] == n
+    algos = [a for a in ALGOS if a != "llcp"]
     ht = t.cpu().numpy()
     del t
     torch.cuda.empty_cache()
@@ -536,7 +577,7 @@ def test_sa_beyond_u32(sas):
     qs += [rng.integers(0, 4, rng.integers(1, 30), dtype=np.uint8) for _ in range(500)]
     buf, off, lens = pack(qs)
     lo, hi = idx.search_range(buf, off, lens)
-    got = {algo: idx.search_batch(buf, off, lens, algo=algo) for algo in ALGOS}
+    got = {algo: idx.search_batch(buf, off, lens, algo=algo) for algo in algos}
     big = 0
     for k, q in enumerate(qs):
         qb = bytes(q)
@@ -548,7 +589,7 @@ def test_sa_beyond_u32(sas):
             assert bytes(ht[cur:cur + len(q)]) >= qb, k
         if prev is not None:
             assert bytes(ht[prev:prev + len(q)]) < qb, k
-        for algo in ALGOS:
+        for algo in algos:
             assert int(got[algo][k]) == cur, (k, algo)
         big += cur >= (1 << 32)
         if k < 600:
@@ -557,14 +598,15 @@ def test_sa_beyond_u32(sas):
                 last = int(idx.suffix_array(count=1, start=occ_hi - 1)[0])
                 assert bytes(ht[last:last + len(q)]) == qb
     assert big > 0  # positions above 2^32 were returned
-    # compact quad leaves at the same n: SA values (above 2^32) come from the 40-bit array
+    # compact quad leaves at the same n: SA values (above 2^32) come from the 40-bit array;
+    # the LLCP entries carry 40-bit SA values too
     del idx
     torch.cuda.empty_cache()
     tc = torch.from_numpy(ht).cuda()
     cidx = sas.SaNaive.build(tc, lcp=False, stree=False, sector=False, quad="compact")
     del tc
-    assert cidx.stats()["quad_entry_bytes"] == 8
-    for algo in ("quad", "inline"):
+    assert cidx.stats()["quad_entry_bytes"] == 8 and cidx.stats()["llcp_bytes"] == 16 * n
+    for algo in ("quad", "inline", "llcp"):
         assert np.array_equal(cidx.search_batch(buf, off, lens, algo=algo), got["plain"]), algo
     clo, chi = cidx.search_range(buf, off, lens)
     assert np.array_equal(clo, lo) and np.array_equal(chi, hi)
@@ -680,7 +722,7 @@ def test_part_builds_at_scale(sas):
 
 
 def test_probe_counts_match_reference_counter(sas):
-    """out_probes of PLAIN / LCP = the reference's `cnt` of binary_search
+    """out_probes of PLAIN / LCP / LLCP = the reference's `cnt` of binary_search
     (sas/sa_search.rs:104: one per loop iteration while l < r), query by query,
     on the oracle's restatement; the Counter mirror sums them."""
     n = 200_003
@@ -694,7 +736,7 @@ def test_probe_counts_match_reference_counter(sas):
     qs += [np.full(40, 3, np.uint8), np.zeros(0, np.uint8), t[n - 5:]]
     buf, off, lens = pack(qs)
     expect = [O.search_one(tp, n, sa, np.asarray(q, np.uint8), "binary_search") for q in qs]
-    for algo in ("plain", "lcp"):
+    for algo in ("plain", "lcp", "llcp"):
         pos, probes = idx.search_batch(buf, off, lens, algo=algo, probes=True)
         assert pos.tolist() == [e[0] for e in expect], algo
         assert probes.tolist() == [e[1] for e in expect], algo
