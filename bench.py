@@ -30,6 +30,9 @@ for _p in (REPO, PKG):
 
 METRIC = "pattern lookups/s + achieved HBM GB/s, 2^30-byte text, 10^7 len-32 queries"
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+# independent random 4-B loads over a 4 GiB buffer, one 128-B line each: the chip's
+# random-request ceiling (tools/randbench.hip, profiles/r1/randbench_calibration.jsonl)
+RANDOM_REQ_CEILING = 5.084e10
 SEED = 31415  # sas/main.rs:38
 
 
@@ -46,6 +49,8 @@ def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes:
         return sector_layers * 32 + tail_probes * 12 + m + 8
     if algo == "quad":
         return quad_layers * 64 + tail_probes * 64 + m + 8
+    if algo == "prefix":  # the table pair (two u32) + probes of 16-B fused entries
+        return 8 + max(0.0, tail_probes - 1) * 16 + m + 8  # probes count the table read once
     if algo == "inline":  # P probes of one 16-B fused (key, SA) entry
         P = int(np.log2(n)) + 1
         return P * 16 + m + 8
@@ -370,9 +375,13 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default="quad", choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp"])
-    ap.add_argument("--variants", default="plain,lcp,llcp,stree,sector,quad,inline",
+    ap.add_argument("--algo", default="prefix", choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
+                                                         "prefix"])
+    ap.add_argument("--variants", default="plain,lcp,llcp,stree,sector,quad,inline,prefix",
                     help="other algos timed beside the headline one")
+    ap.add_argument("--prefix-chars", type=int, default=17,
+                    help="p of the prefix table (the reference's main.rs default is -p 20; 4^17 u32 entries "
+                         "= 64 GiB is the largest that sits beside the other indexes in HBM)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
@@ -410,7 +419,7 @@ def main():
     if args.mode == "shard":
         from sas_amd.shard import ShardedSearch
         # each rank builds ONLY its own SA rank range (sas_build_part: no whole-SA step)
-        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True)
+        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True, prefix=args.prefix_chars)
         if dist is None:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -418,7 +427,7 @@ def main():
             dist.init_process_group("nccl", rank=0, world_size=1)
         engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo)
     else:
-        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True)
+        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, prefix=args.prefix_chars)
     stats = idx.stats()
     off = rank_query_offsets(n, nq, m, rank)
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
@@ -512,7 +521,8 @@ def main():
                        "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
                        "mean_probes": float(vp.double().mean().item()), "verified": vok}
 
-    traffic, traffic_src = load_traffic(args.algo, n, nq, m)
+    traffic, traffic_src = load_traffic(args.algo + (str(stats["prefix_chars"]) if args.algo == "prefix" else ""),
+                                        n, nq, m)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu and args.mode == "replicated":
         cpu = cpu_baseline(text, idx, qbytes, m, nq, args.cpu_seconds)
@@ -524,6 +534,9 @@ def main():
                              "S-tree of 16-char SA keys (top layers LDS-staged)",
                     "plain": "configs[1]: 2^30 text in HBM, 10^7 len-32 queries, plain binary search over SA",
                     "lcp": "configs[1] + mlr LCP skipping",
+                    "prefix": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, the reference's prefix table "
+                              "(sas/sa_search.rs:59-95, p = config.prefix_chars: one 8-B read gives the rank range) + binary "
+                              "search over the fused 32-char key + SA entries of that range",
                     "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (one 8-B {SA, Llcp, Rlcp} "
                             "entry per probe, text only on lcp ties), 2^30 text in HBM, 10^7 len-32 queries",
                     "sector": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, sector S-tree (32-B nodes, "
@@ -540,6 +553,7 @@ def main():
             "data": f"synthetic: random_string(ChaCha8Rng::seed_from_u64({SEED})) text + positive len-{m} "
                     f"substrings (sas/util.rs:9-26), per-rank query stream",
             "config": {"workload": workload, "algo": args.algo, "n": n, "queries_per_gpu": nq, "m": m,
+                       "prefix_chars": stats["prefix_chars"],
                        "mode": args.mode,
                        "parallelism": (f"replicated index x{ws}, query shards (no data-path collective)"
                                        if args.mode == "replicated" else
@@ -550,14 +564,20 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad",
-                                    "inline": "k_sa_inline"}.get(args.algo, "k_sa_binary"),
+                                    "inline": "k_sa_inline", "prefix": "k_sa_prefix"}.get(args.algo, "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
-                         "mean_probes": mean_probes},
+                         "mean_probes": mean_probes,
+                         # what bounds this path: dependent random requests (each a 128-B line),
+                         # against the measured random-request ceiling; query/result streams excluded
+                         "requests": None if args.algo != "prefix" else {
+                             "per_lookup": mean_probes, "achieved_per_s": mean_probes * nq / (kernel_ms * 1e-3),
+                             "ceiling_per_s": RANDOM_REQ_CEILING,
+                             "frac": mean_probes * nq / (kernel_ms * 1e-3) / RANDOM_REQ_CEILING}},
             "cpu_baseline": cpu,
             "e2e_host": e2e,
             "variants": variants,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
-                                            "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "iterations",
+                                            "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "iterations", "prefix_chars",
                                             "sa_rounds", "build_sa_ns", "build_total_ns")},
             "setup_s": build_s, "verified": ok,
         }

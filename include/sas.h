@@ -67,6 +67,13 @@ typedef struct sas_index sas_index;
                                         layout with fewer levels larger than the 256 MiB
                                         Infinity Cache (absolute on a tie; n = 2^30 builds
                                         absolute, n = 2^34 compact builds relative)        */
+#define SAS_BUILD_PREFIX  (1u << 14) /* also build the prefix table for SAS_ALGO_PREFIX (the
+                                        reference's fill_prefix_table, sas/sa_search.rs:59-95):
+                                        u32[4^p + 1], entry x = first SA rank whose p-char
+                                        key is >= x.  p = SAS_BUILD_PREFIX_P(p) (1..17) or,
+                                        if 0, ceil(log4(n)) + 1 capped at 16 (16 at n = 2^30:
+                                        16 GiB).  Needs SAS_BUILD_QUAD and < 2^32 SA entries */
+#define SAS_BUILD_PREFIX_P(p) ((uint32_t)(p) << 16)  /* bits 16..20: prefix chars       */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry
                                         {SA[m] 40 bits, Llcp 12 bits, Rlcp 12 bits, 16 chars
@@ -88,11 +95,15 @@ enum sas_algo {
     SAS_ALGO_INLINE = 5, /* PLAIN's probe sequence (binary_search_batch) over the quad tree's
                            fused (32-char key, SA) entries: one 16-B read per probe instead of
                            an SA word + text words ("inlining values", todo.org:18-19)     */
-    SAS_ALGO_LLCP = 6   /* PLAIN's probe sequence with Manber-Myers LLCP/RLCP skipping: a probe
+    SAS_ALGO_LLCP = 6,  /* PLAIN's probe sequence with Manber-Myers LLCP/RLCP skipping: a probe
                            reads one 16-B {SA, Llcp, Rlcp, chars} entry and decides from the
                            lcp values alone unless they tie llcp/rlcp; a tie compares the
                            entry's 16 chars before any text (needs SAS_BUILD_LLCP; the LCP
                            array at work, A21)                                              */
+    SAS_ALGO_PREFIX = 7 /* prefix table lookup (the rank range of q's first p chars, one 8-B
+                           read; sas/sa_search.rs:59-95) + binary search over that range on
+                           the quad tree's leaf entries: ~2 memory requests per lookup
+                           (needs SAS_BUILD_PREFIX)                                          */
 };
 
 typedef struct sas_stats {
@@ -125,6 +136,8 @@ typedef struct sas_stats {
     uint32_t top2_levels;    /* binary-search levels whose pivots come from LDS or the
                                 cache-resident pivot array (PLAIN/LCP/INLINE)        */
     uint64_t llcp_bytes;     /* SAS_BUILD_LLCP entries (16 B per suffix), 0 if not built */
+    uint64_t prefix_bytes;   /* SAS_BUILD_PREFIX table, 0 if not built                */
+    uint32_t prefix_chars;   /* its p (chars per table key)                           */
 } sas_stats;
 
 const char* sas_last_error(void);

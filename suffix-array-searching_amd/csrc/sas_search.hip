@@ -41,6 +41,8 @@ struct SearchArgs {
     uint64_t rank_lo;    // global rank of sa[0]
     const uint8_t* sa;       // SaView<W> (u32 or packed 40-bit)
     const uint4* llcp;       // SAS_BUILD_LLCP entries (k_sa_binary<.., BS_LLCP, ..>)
+    const uint32_t* prefix;  // SAS_BUILD_PREFIX table (k_sa_prefix)
+    uint32_t prefix_chars;
     const uint4* top2;
     uint32_t top_levels;
     uint32_t top2_levels;
@@ -1133,6 +1135,82 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// ------------------------------------------------------------------ PREFIX
+// The reference's prefix table, live (fill_prefix_table / prefix_range,
+// sas/sa_search.rs:59-95; p = 0 there, :31).  One lane per query: K = q's first p
+// chars zero padded; every suffix whose p-char key is < K is < q and every one whose
+// key is > K is > q (zero padding keeps key order = slice order), so
+// the lower bound lies in [table[K], table[K+1]], found by a binary search over the
+// quad leaf entries of that range with the sector predicate.  At p = ceil(log4 n) + 1
+// a random lookup is two memory requests: the table pair, then one leaf entry.
+#ifndef SAS_PREFIX_NT
+#define SAS_PREFIX_NT 1  // non-temporal table / entry loads (-3%, tools/ab_prefix.py)
+#endif
+#ifndef SAS_PREFIX_PAIR
+#define SAS_PREFIX_PAIR 0  // table[K], table[K+1] as one dword-aligned 8-B load
+#endif
+template <int QW, bool KO, int W>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
+    uint32_t bad = 0;
+    const uint32_t sh = 64 - 2 * a.prefix_chars;
+    const uint64_t sa_n = a.sa_n;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint64_t K = K64 >> sh;
+        uint64_t lo, hi;
+        if (SAS_PREFIX_PAIR) {
+            typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
+            const u32x2_a4* pp2 = reinterpret_cast<const u32x2_a4*>(a.prefix + K);
+            const u32x2_a4 v = SAS_PREFIX_NT ? __builtin_nontemporal_load(pp2) : *pp2;
+            lo = v.x;
+            hi = v.y;
+        } else if (SAS_PREFIX_NT) {
+            lo = __builtin_nontemporal_load(a.prefix + K);
+            hi = __builtin_nontemporal_load(a.prefix + K + 1);
+        } else {
+            lo = a.prefix[K];
+            hi = a.prefix[K + 1];
+        }
+        uint32_t probes = 1;
+        uint64_t pr = QUAD_NO_SA;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            uint64_t key, pp;
+            if (KO) {
+                key = quad_entry_key<true>(a, mid);
+                pp = key == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
+            } else {
+                const uint4 e = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
+                key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+            }
+            probes++;
+            if (sector_ge<QW>(key, pp, K64, a, q)) {
+                hi = mid;
+                pr = pp;  // SA at rank hi (QUAD_NO_SA: not read); lo ends at hi
+            } else {
+                lo = mid + 1;
+            }
+        }
+        uint64_t pos;
+        if (lo >= sa_n) pos = a.next_pos;
+        else if (pr != QUAD_NO_SA) pos = pr;
+        else {
+            pos = quad_entry_sa<KO, W>(a, lo);
+            probes++;
+        }
+        a.out_pos[i] = pos;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // ------------------------------------------------------------------ host dispatch
 template <int W>
 static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
@@ -1182,10 +1260,13 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_QUAD4X(Q) (k_sa_quad4x<(Q < SAS_QUAD4X_MAXREGS ? Q : SAS_QUAD4X_MAXREGS), KO, W>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true, KO, W>)
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
+#define K_PREFIX(Q) (k_sa_prefix<Q, KO, W>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
         if (qw == 1) hipLaunchKernelGGL((k_sa_quad<1, KO, W>), grid, block, 0, st, a);
         else { QW_CASE(K_QUAD4X) }
+    } else if (algo == SAS_ALGO_PREFIX) {
+        QW_CASE(K_PREFIX)
     } else {
         if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
     }
@@ -1201,7 +1282,7 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     if (blocks == 0) return 0;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
-    if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) {
+    if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
         if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
         else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);
         else launch_quad<true, 4>(algo, top, qw, grid, block, st, a);
@@ -1229,6 +1310,8 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.rank_lo = x->rank_lo;
     a.sa = x->sa;
     a.llcp = x->llcp;
+    a.prefix = x->prefix;
+    a.prefix_chars = x->prefix_chars;
     a.top2 = x->top2;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;
@@ -1278,7 +1361,8 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_LLCP) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "search: unknown algo");
+    if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
     if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "search: SAS_ALGO_LLCP needs SAS_BUILD_LLCP");
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
         SAS_FAIL(EINVAL, "search: SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
@@ -1377,7 +1461,8 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_LLCP) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
     if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "sas_time_fixed: index has no LLCP entries");
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
         SAS_FAIL(EINVAL, "sas_time_fixed: index has no quad tree");

@@ -30,8 +30,15 @@ SAS_BUILD_QUAD_COMPACT = 1 << 10
 SAS_BUILD_QUAD_ABS = 1 << 11
 SAS_BUILD_QUAD_REL = 1 << 12
 SAS_BUILD_LLCP = 1 << 13
+SAS_BUILD_PREFIX = 1 << 14
+
+
+def SAS_BUILD_PREFIX_P(p: int) -> int:
+    return (int(p) & 31) << 16
+
+
 SAS_MULTI_REPLICATE, SAS_MULTI_SHARD = 0, 1
-ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, "llcp": 6}
+ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, "llcp": 6, "prefix": 7}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
 SST_LEFT_MAX = 1 << 0
@@ -52,6 +59,7 @@ class SasStats(C.Structure):
         ("quad_bytes", C.c_uint64), ("quad_layers", C.c_uint32), ("quad_lds_layers", C.c_uint32),
         ("quad_entry_bytes", C.c_uint32),
         ("quad_fan", C.c_uint32), ("top2_levels", C.c_uint32), ("llcp_bytes", C.c_uint64),
+        ("prefix_bytes", C.c_uint64), ("prefix_chars", C.c_uint32),
     ]
 
     def as_dict(self):

@@ -19,7 +19,7 @@ from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp")
+ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix")
 
 
 @pytest.fixture(scope="module")
@@ -191,6 +191,45 @@ def test_llcp_capped_lcps(sas):
             for algo in ("plain", "llcp"):
                 got, probes = idx.search_batch(buf, qo, ql, algo=algo, probes=True, flags=flags)
                 assert np.array_equal(got, expect), (name, algo, flags, np.nonzero(got != expect)[0][:5])
+
+
+def test_prefix_table(sas, sadef):
+    """SAS_ALGO_PREFIX: the reference's prefix table (sas/sa_search.rs:59-95) for
+    p = 1..16 chars, on fused and compact (u32 / 40-bit SA) quad leaves.  Random and
+    repeat-rich texts give empty, single and very long key ranges and long gaps in
+    the table (the workgroup-filled gap list); queries of every length 0..300,
+    including m < p, positives, negatives and text-end suffixes, equal the oracle."""
+    from sas_amd import _lib
+    rng = np.random.default_rng(5)
+    texts = {c["name"]: np.array(c["text"], np.uint8) for c in sadef["cases"]}
+    texts["random_200k"] = sas.random_string(200_003, seed=77)
+    texts["all_A"] = np.zeros(30_000, np.uint8)
+    texts["period_5"] = np.tile(np.array([3, 1, 0, 2, 2], np.uint8), 8000)
+    for name, t in texts.items():
+        n = len(t)
+        sa = O.build_sa(t)
+        qs = [t[o:o + l] for o, l in zip(rng.integers(0, n, 400), rng.integers(0, 301, 400))]
+        qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(0, 40, 200)]
+        qs += [t[n - k:] for k in (1, 2, 17, min(n, 40))] + [np.zeros(0, np.uint8), np.full(20, 3, np.uint8)]
+        buf, qo, ql = pack(qs)
+        expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+        for p, quad, sa40 in ((0, True, False), (1, True, False), (2, "compact", False), (7, True, False),
+                              (16, "compact", True), (11, "compact", False)):
+            idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=quad, sa40=sa40,
+                                    prefix=p if p else True)
+            st = idx.stats()
+            l4 = next(k for k in range(33) if 4 ** k >= n)  # ceil(log4 n)
+            assert st["prefix_chars"] == (p if p else min(16, l4 + 1)), (name, p)
+            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * 4
+            got, probes = idx.search_batch(buf, qo, ql, algo="prefix", probes=True)
+            assert np.array_equal(got, expect), (name, p, quad, sa40, np.nonzero(got != expect)[0][:5])
+            del idx
+    # built only with a quad tree, and refused without the table
+    with pytest.raises(sas.SasError):
+        sas.SaNaive.build(texts["random_200k"], quad=False, prefix=True)
+    idx = sas.SaNaive.build(texts["random_200k"], prefix=False)
+    with pytest.raises(sas.SasError):
+        idx.search_batch(buf, qo, ql, algo="prefix")
 
 
 def test_invalid_codes_rejected(sas):
@@ -566,7 +605,7 @@ def test_sa_beyond_u32(sas):
     idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True, llcp=False)  # LLCP: the second index below
     st = idx.stats()
     assert st["sa_width"] == 5 and st["n"] == n
-    algos = [a for a in ALGOS if a != "llcp"]
+    algos = [a for a in ALGOS if a not in ("llcp", "prefix")]  # prefix: u32 ranks, n < 2^32 only
     ht = t.cpu().numpy()
     del t
     torch.cuda.empty_cache()

@@ -1,0 +1,30 @@
+"""Kernel times of PREFIX (and QUAD beside it) at the c1 shape (2^30 text, 10^7 len-32
+queries) for same-box A/B of library builds:
+AB_PKG=tools/_var_<name>/suffix-array-searching_amd python3 tools/ab_prefix.py"""
+import os
+import sys
+
+sys.path.insert(0, os.environ.get("AB_PKG") or
+                os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "suffix-array-searching_amd"))
+import numpy as np
+import torch
+
+import sas_amd
+
+n, nq, m = 1 << 30, 10_000_000, 32
+t = sas_amd.random_string(n, seed=31415, device="cuda")
+off, _, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=200, len_lo=m, len_hi=m + 1)
+src = torch.from_numpy(off.astype(np.int64)).cuda()
+qb = t[(src[:, None] + torch.arange(m, device="cuda")[None, :]).reshape(-1)].contiguous()
+out = torch.empty(nq, dtype=torch.int64, device="cuda")
+p = int(os.environ.get("AB_P", "0"))
+idx = sas_amd.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=p if p else True)
+line = {"p": idx.stats()["prefix_chars"]}
+ref = None
+for algo in ("prefix", "quad"):
+    idx.time_fixed(qb, m, nq, out, algo=algo, reps=2)
+    kns, _ = idx.time_fixed(qb, m, nq, out, algo=algo, reps=10)
+    line[algo] = round(kns / 1e6, 4)
+    ref = out.clone() if ref is None else ref
+    line[algo + "_ok"] = bool(torch.equal(out, ref))
+print("ms", line, flush=True)
