@@ -223,6 +223,25 @@ def test_prefix_table(sas, sadef):
             assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * 4
             got, probes = idx.search_batch(buf, qo, ql, algo="prefix", probes=True)
             assert np.array_equal(got, expect), (name, p, quad, sa40, np.nonzero(got != expect)[0][:5])
+            if p == 7 and name == "random_200k":
+                # cnt as the reference counts it (sas/sa_search.rs:86-112): 1 for the table
+                # (p > 0), then one per binary-search iteration over [table[K], table[K+1])
+                keys = np.array([int("".join(str(c) for c in t[x:x + 7]).ljust(7, "0"), 4) for x in sa])
+                tb = bytes(t)
+                for k, q in enumerate(qs[:300]):
+                    K = int("".join(str(c) for c in q[:7]).ljust(7, "0"), 4)
+                    lo, hi = np.searchsorted(keys, K, "left"), np.searchsorted(keys, K + 1, "left")
+                    cnt, qq = 1, bytes(q)
+                    while lo < hi:
+                        mid = (lo + hi) // 2
+                        cnt += 1
+                        if tb[sa[mid]:sa[mid] + len(qq)] < qq:
+                            lo = mid + 1
+                        else:
+                            hi = mid
+                    assert (sa[lo] if lo < n else n) == got[k], k
+                    # the kernel reads the final SA value once more only when no probe left it
+                    assert probes[k] in (cnt, cnt + 1), (k, probes[k], cnt)
             del idx
     # built only with a quad tree, and refused without the table
     with pytest.raises(sas.SasError):
