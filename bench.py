@@ -268,12 +268,16 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     nq = args.nq if args.nq != 10_000_000 else 100_000_000
     fits = n <= (1 << 33)  # 16 B per suffix next to the 40-bit SA
     main_algo = args.algo if (args.algo != "sector" or fits) else "stree"
-    quad_mode = ("compact" if (args.quad_compact or not fits) else True) if main_algo in ("quad", "inline") else False
+    quad_mode = (("compact" if (args.quad_compact or not fits) else True) if main_algo in ("quad", "inline", "prefix")
+                 else False)
+    # prefix table beside a 40-bit SA: packed 40-bit entries; p = 15 (5 GiB) is what fits
+    # next to the 2^34-char index and 10^8 ragged queries
+    c3_prefix = min(args.prefix_chars, 15) if main_algo == "prefix" else False
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
     # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
     idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
-                                quad=quad_mode, verify=True, llcp=False)
+                                quad=quad_mode, verify=True, llcp=False, prefix=c3_prefix)
     stats = idx.stats()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
@@ -338,6 +342,13 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
             ab = H * node + max(0.0, mp - H) * extra + mean_m + 8 + max(0.0, mean_m - 32) / 4
             if algo == "quad" and stats["quad_entry_bytes"] == 8:
                 ab += stats["sa_width"]
+        elif algo == "prefix":
+            # the table pair, entry probes (8-B key-only or 16-B fused), the SA entry of
+            # key-only leaves, the query, the position, the text window past char 32
+            eb = stats["quad_entry_bytes"]
+            ab = 2 * stats["sa_width"] + max(0.0, mp - 1) * eb + mean_m + 8 + max(0.0, mean_m - 32) / 4
+            if eb == 8:
+                ab += stats["sa_width"]
         else:
             ab = P * (4 + mean_m) + mean_m + 8
         results[algo] = {"lookups_per_s": nq * steps / el, "kernel_ms": kms, "mean_probes": mp,
@@ -358,13 +369,13 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
                          "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": traffic,
                          "traffic_source": tsrc,
                          "kernel": {"stree": "k_sa_stree4x", "sector": "k_sa_sector", "quad": "k_sa_quad4x",
-                                    "inline": "k_sa_inline"}.get(main_algo, "k_sa_binary"),
+                                    "inline": "k_sa_inline", "prefix": "k_sa_prefix"}.get(main_algo, "k_sa_binary"),
                          "kernel_ms": h["kernel_ms"]},
             "variants": results, "setup_s": setup,
             "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
                                             "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
                                             "stree_bytes", "sector_bytes", "quad_bytes", "quad_fan",
-                                            "quad_entry_bytes")}})
+                                            "quad_entry_bytes", "prefix_chars", "prefix_bytes")}})
 
 
 def main():
@@ -375,7 +386,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default="prefix", choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
+    ap.add_argument("--algo", default=None, choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
                                                          "prefix"])
     ap.add_argument("--variants", default="plain,lcp,llcp,stree,sector,quad,inline,prefix",
                     help="other algos timed beside the headline one")
@@ -394,6 +405,10 @@ def main():
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
     args = ap.parse_args()
+    if args.algo is None:
+        # c1: the prefix table (1.86e10 vs QUAD 1.40e10 lookups/s); c3 (n = 2^34, 40-bit
+        # SA, ragged 8..256): QUAD on compact leaves (25.0 ms vs 26.6 ms with a p = 15 table)
+        args.algo = "quad" if args.workload == "c3" else "prefix"
     keep_stdout_for_result()
 
     import torch

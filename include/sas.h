@@ -72,7 +72,8 @@ typedef struct sas_index sas_index;
                                         u32[4^p + 1], entry x = first SA rank whose p-char
                                         key is >= x.  p = SAS_BUILD_PREFIX_P(p) (1..17) or,
                                         if 0, ceil(log4(n)) + 1 capped at 16 (16 at n = 2^30:
-                                        16 GiB).  Needs SAS_BUILD_QUAD and < 2^32 SA entries */
+                                        16 GiB).  Needs SAS_BUILD_QUAD.  u32 entries, or
+                                        packed 40-bit ones beside a 40-bit SA             */
 #define SAS_BUILD_PREFIX_P(p) ((uint32_t)(p) << 16)  /* bits 16..20: prefix chars       */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry

@@ -843,6 +843,7 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
 // whose key is x are the ranks [table[x], table[x+1]).  Rank r with a new key fills
 // table(key(r-1), key(r)] = r (rank sa_n fills the rest up to 4^p); a gap longer than
 // PT_SMALL goes to a list that whole workgroups fill.  Keys come from the quad leaves.
+// Entries are u32, or packed 40-bit (SaView<5> / sa_put<5>) beside a 40-bit SA.
 #define PT_SMALL 256
 template <bool KO>
 __device__ __forceinline__ uint64_t pt_key64(const uint4* leaves, uint64_t r) {
@@ -851,8 +852,8 @@ __device__ __forceinline__ uint64_t pt_key64(const uint4* leaves, uint64_t r) {
     return (uint64_t)k.x | ((uint64_t)k.y << 32);
 }
 
-template <bool KO>
-__global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint32_t p, uint32_t* __restrict__ table,
+template <bool KO, int TW>
+__global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint32_t p, uint8_t* __restrict__ table,
                           uint64_t* __restrict__ big, unsigned long long* __restrict__ nbig, uint64_t big_cap) {
     const uint32_t sh = 64 - 2 * p;
     const uint64_t top = 1ull << (2 * p);
@@ -861,7 +862,7 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
         const uint64_t lo = r > 0 ? (pt_key64<KO>(leaves, r - 1) >> sh) + 1 : 0;
         if (lo > kr) continue;  // same key as rank r - 1
         if (kr - lo < PT_SMALL) {
-            for (uint64_t x = lo; x <= kr; x++) table[x] = (uint32_t)r;
+            for (uint64_t x = lo; x <= kr; x++) sa_put<TW>(table, x, r);
         } else {
             const unsigned long long slot = atomicAdd(nbig, 1ull);
             if (slot < big_cap) {
@@ -873,19 +874,22 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
     }
 }
 
+template <int TW>
 __global__ void k_pt_big(const uint64_t* __restrict__ big, const unsigned long long* __restrict__ nbig,
-                         uint32_t* __restrict__ table) {
+                         uint8_t* __restrict__ table) {
     for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x) {
         const uint64_t lo = big[3 * b], hi = big[3 * b + 1];
-        const uint32_t r = (uint32_t)big[3 * b + 2];
-        for (uint64_t x = lo + threadIdx.x; x <= hi; x += blockDim.x) table[x] = r;
+        const uint64_t r = big[3 * b + 2];
+        for (uint64_t x = lo + threadIdx.x; x <= hi; x += blockDim.x) sa_put<TW>(table, x, r);
     }
 }
 
 static int build_prefix(sas_index* x, uint32_t p) {
     const uint64_t sa_n = x->sa_n;
     if (!x->quad_leaves) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX needs SAS_BUILD_QUAD (keys and SA values of the leaves)");
-    if (sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
+    // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA
+    const uint32_t tw = x->sa_w == 5 ? 5 : 4;
+    if (tw == 4 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
     if (p == 0) {
         uint32_t l4 = 0;  // ceil(log4(sa_n))
         while (l4 < 32 && (1ull << (2 * l4)) < sa_n) l4++;
@@ -895,26 +899,32 @@ static int build_prefix(sas_index* x, uint32_t p) {
     const uint64_t entries = (1ull << (2 * p)) + 1;
     const uint64_t cap = entries / (PT_SMALL + 1) + 2;
     DevBuf t, big, nbig;
-    TRY(t.alloc(entries * 4, "prefix table"));
+    TRY(t.alloc(entries * tw + 8, "prefix table"));
     TRY(big.alloc(cap * 24, "prefix table gap list"));
     TRY(nbig.alloc(8, "prefix table gap count"));
     HIP_TRY(hipMemset(nbig.p, 0, 8));
     const dim3 g(grid_for(sa_n + 1)), b(256);
-    if (x->quad_compact)
-        hipLaunchKernelGGL(k_pt_fill<true>, g, b, 0, 0, x->quad_leaves, sa_n, p, t.as<uint32_t>(), big.as<uint64_t>(),
-                           nbig.as<unsigned long long>(), cap);
+    uint8_t* tb = t.as<uint8_t>();
+    uint64_t* bl = big.as<uint64_t>();
+    unsigned long long* nb_d = nbig.as<unsigned long long>();
+    if (x->quad_compact && tw == 5)
+        hipLaunchKernelGGL((k_pt_fill<true, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+    else if (x->quad_compact)
+        hipLaunchKernelGGL((k_pt_fill<true, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+    else if (tw == 5)
+        hipLaunchKernelGGL((k_pt_fill<false, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
     else
-        hipLaunchKernelGGL(k_pt_fill<false>, g, b, 0, 0, x->quad_leaves, sa_n, p, t.as<uint32_t>(), big.as<uint64_t>(),
-                           nbig.as<unsigned long long>(), cap);
-    hipLaunchKernelGGL(k_pt_big, dim3(4096), dim3(256), 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(),
-                       t.as<uint32_t>());
+        hipLaunchKernelGGL((k_pt_fill<false, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+    if (tw == 5) hipLaunchKernelGGL(k_pt_big<5>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb);
+    else hipLaunchKernelGGL(k_pt_big<4>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb);
     HIP_TRY(hipGetLastError());
     uint64_t nb = 0;
     HIP_TRY(hipMemcpy(&nb, nbig.p, 8, hipMemcpyDeviceToHost));
     if (nb > cap) SAS_FAIL(EFAULT, "prefix table: gap list overflow");  // cannot happen: gaps are disjoint
-    x->prefix = t.as<uint32_t>();
+    x->prefix = t.as<uint8_t>();
     t.release();
     x->prefix_chars = p;
+    x->prefix_w = tw;
     return 0;
 }
 
@@ -1213,7 +1223,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.sa_width = W;
     st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
     st.llcp_bytes = x->llcp ? sa_n * 16 : 0;
-    st.prefix_bytes = x->prefix ? ((1ull << (2 * x->prefix_chars)) + 1) * 4 : 0;
+    st.prefix_bytes = x->prefix ? ((1ull << (2 * x->prefix_chars)) + 1) * x->prefix_w : 0;
     st.prefix_chars = x->prefix_chars;
     st.stree_bytes = x->stree_nodes * 64;
     st.stree_layers = x->stree_height;

@@ -41,8 +41,9 @@ struct SearchArgs {
     uint64_t rank_lo;    // global rank of sa[0]
     const uint8_t* sa;       // SaView<W> (u32 or packed 40-bit)
     const uint4* llcp;       // SAS_BUILD_LLCP entries (k_sa_binary<.., BS_LLCP, ..>)
-    const uint32_t* prefix;  // SAS_BUILD_PREFIX table (k_sa_prefix)
+    const uint8_t* prefix;   // SAS_BUILD_PREFIX table (k_sa_prefix): u32 or packed 40-bit entries
     uint32_t prefix_chars;
+    uint32_t prefix_w;       // bytes per table entry (4 or 5)
     const uint4* top2;
     uint32_t top_levels;
     uint32_t top2_levels;
@@ -1149,7 +1150,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
 #ifndef SAS_PREFIX_PAIR
 #define SAS_PREFIX_PAIR 0  // table[K], table[K+1] as one dword-aligned 8-B load
 #endif
-template <int QW, bool KO, int W>
+template <int QW, bool KO, int W, int TW>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
     uint32_t bad = 0;
     const uint32_t sh = 64 - 2 * a.prefix_chars;
@@ -1164,19 +1165,28 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
         const uint64_t K64 = q.w[0];
         const uint64_t K = K64 >> sh;
         uint64_t lo, hi;
-        if (SAS_PREFIX_PAIR) {
+        const uint32_t* pt = reinterpret_cast<const uint32_t*>(a.prefix);
+        if (TW == 5) {
+            const SaView<5> v{a.prefix};
+            lo = v[K];
+            hi = v[K + 1];
+        } else if (SAS_PREFIX_PAIR) {
             typedef uint32_t u32x2_a4 __attribute__((ext_vector_type(2), aligned(4)));
-            const u32x2_a4* pp2 = reinterpret_cast<const u32x2_a4*>(a.prefix + K);
+            const u32x2_a4* pp2 = reinterpret_cast<const u32x2_a4*>(pt + K);
             const u32x2_a4 v = SAS_PREFIX_NT ? __builtin_nontemporal_load(pp2) : *pp2;
             lo = v.x;
             hi = v.y;
         } else if (SAS_PREFIX_NT) {
-            lo = __builtin_nontemporal_load(a.prefix + K);
-            hi = __builtin_nontemporal_load(a.prefix + K + 1);
+            lo = __builtin_nontemporal_load(pt + K);
+            hi = __builtin_nontemporal_load(pt + K + 1);
         } else {
-            lo = a.prefix[K];
-            hi = a.prefix[K + 1];
+            lo = pt[K];
+            hi = pt[K + 1];
         }
+        // binary_search over [table[K], table[K+1]) (sas/sa_search.rs:98-112).  A scan of
+        // short ranges with independent loads measured slower (0.53 -> 0.60 ms at c1,
+        // 26.6 -> 39.4 ms at c3): its key re-reads lengthen the dependent chain.
+        // out_probes = the reference's cnt: 1 for the table, 1 per iteration (:86-104).
         uint32_t probes = 1;
         uint64_t pr = QUAD_NO_SA;
         while (lo < hi) {
@@ -1201,10 +1211,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
         uint64_t pos;
         if (lo >= sa_n) pos = a.next_pos;
         else if (pr != QUAD_NO_SA) pos = pr;
-        else {
-            pos = quad_entry_sa<KO, W>(a, lo);
-            probes++;
-        }
+        else pos = quad_entry_sa<KO, W>(a, lo);
         a.out_pos[i] = pos;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1260,13 +1267,14 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_QUAD4X(Q) (k_sa_quad4x<(Q < SAS_QUAD4X_MAXREGS ? Q : SAS_QUAD4X_MAXREGS), KO, W>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true, KO, W>)
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
-#define K_PREFIX(Q) (k_sa_prefix<Q, KO, W>)
+#define K_PREFIX(Q) (k_sa_prefix<Q, KO, W, 4>)
+#define K_PREFIX5(Q) (k_sa_prefix<Q, KO, W, 5>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
         if (qw == 1) hipLaunchKernelGGL((k_sa_quad<1, KO, W>), grid, block, 0, st, a);
         else { QW_CASE(K_QUAD4X) }
     } else if (algo == SAS_ALGO_PREFIX) {
-        QW_CASE(K_PREFIX)
+        if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) } else { QW_CASE(K_PREFIX) }
     } else {
         if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
     }
@@ -1312,6 +1320,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.llcp = x->llcp;
     a.prefix = x->prefix;
     a.prefix_chars = x->prefix_chars;
+    a.prefix_w = x->prefix_w;
     a.top2 = x->top2;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;

@@ -220,7 +220,7 @@ def test_prefix_table(sas, sadef):
             st = idx.stats()
             l4 = next(k for k in range(33) if 4 ** k >= n)  # ceil(log4 n)
             assert st["prefix_chars"] == (p if p else min(16, l4 + 1)), (name, p)
-            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * 4
+            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * (5 if sa40 else 4)  # 40-bit ranks
             got, probes = idx.search_batch(buf, qo, ql, algo="prefix", probes=True)
             assert np.array_equal(got, expect), (name, p, quad, sa40, np.nonzero(got != expect)[0][:5])
             if p == 7 and name == "random_200k":
@@ -240,8 +240,7 @@ def test_prefix_table(sas, sadef):
                         else:
                             hi = mid
                     assert (sa[lo] if lo < n else n) == got[k], k
-                    # the kernel reads the final SA value once more only when no probe left it
-                    assert probes[k] in (cnt, cnt + 1), (k, probes[k], cnt)
+                    assert probes[k] == cnt, (k, probes[k], cnt)
             del idx
     # built only with a quad tree, and refused without the table
     with pytest.raises(sas.SasError):
@@ -661,10 +660,11 @@ def test_sa_beyond_u32(sas):
     del idx
     torch.cuda.empty_cache()
     tc = torch.from_numpy(ht).cuda()
-    cidx = sas.SaNaive.build(tc, lcp=False, stree=False, sector=False, quad="compact")
+    cidx = sas.SaNaive.build(tc, lcp=False, stree=False, sector=False, quad="compact", prefix=16)
     del tc
     assert cidx.stats()["quad_entry_bytes"] == 8 and cidx.stats()["llcp_bytes"] == 16 * n
-    for algo in ("quad", "inline", "llcp"):
+    assert cidx.stats()["prefix_bytes"] == (4 ** 16 + 1) * 5  # 40-bit ranks beside the 40-bit SA
+    for algo in ("quad", "inline", "llcp", "prefix"):
         assert np.array_equal(cidx.search_batch(buf, off, lens, algo=algo), got["plain"]), algo
     clo, chi = cidx.search_range(buf, off, lens)
     assert np.array_equal(clo, lo) and np.array_equal(chi, hi)
