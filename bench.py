@@ -37,7 +37,7 @@ SEED = 31415  # sas/main.rs:38
 
 
 def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes: float,
-                      sector_layers: int = 0, quad_layers: int = 0) -> float:
+                      sector_layers: int = 0, quad_layers: int = 0, prefix_entry: int = 8) -> float:
     """Bytes a lookup must move: 4 B SA word + m text bytes per
     probe, the query, the 8 B position.  PLAIN/LCP: P = ilog2(n)+1 probes.
     STREE: H 64-B nodes + measured tail probes.  SECTOR: H 32-B nodes (the
@@ -49,8 +49,9 @@ def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes:
         return sector_layers * 32 + tail_probes * 12 + m + 8
     if algo == "quad":
         return quad_layers * 64 + tail_probes * 64 + m + 8
-    if algo == "prefix":  # the table pair (two u32) + probes of 16-B fused entries
-        return 8 + max(0.0, tail_probes - 1) * 16 + m + 8  # probes count the table read once
+    if algo == "prefix":  # the table entry (two u32, or one 16-B inline entry) + probes of
+        # 16-B fused entries; probes = the reference's cnt, which counts the table once
+        return prefix_entry + max(0.0, tail_probes - 1) * 16 + m + 8
     if algo == "inline":  # P probes of one 16-B fused (key, SA) entry
         P = int(np.log2(n)) + 1
         return P * 16 + m + 8
@@ -111,14 +112,17 @@ def dist_env():
     return ws, rank, local
 
 
-def load_traffic(algo: str, n: int, nq: int, m: int):
+def load_traffic(algo: str, n: int, nq: int, m: int, with_requests: bool = False):
     """HBM bytes per launch from a committed rocprofv3 --pmc pass of this exact
     workload (profiles/pmc_<algo>_n<n>_q<nq>_m<m>.json, written by
-    tools/pmc_to_json.py), or None."""
+    tools/pmc_to_json.py), or None; with_requests: also its L2->fabric read
+    requests per launch (TCC_EA0_RDREQ)."""
     path = os.path.join(REPO, "profiles", f"pmc_{algo}_n{n}_q{nq}_m{m}.json")
     if not os.path.exists(path):
-        return None, None
+        return (None, None, None) if with_requests else (None, None)
     d = json.load(open(path))
+    if with_requests:
+        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO), d.get("TCC_EA0_RDREQ")
     return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
 
 
@@ -390,9 +394,11 @@ def main():
                                                          "prefix"])
     ap.add_argument("--variants", default="plain,lcp,llcp,stree,sector,quad,inline,prefix",
                     help="other algos timed beside the headline one")
-    ap.add_argument("--prefix-chars", type=int, default=17,
-                    help="p of the prefix table (the reference's main.rs default is -p 20; 4^17 u32 entries "
-                         "= 64 GiB is the largest that sits beside the other indexes in HBM)")
+    ap.add_argument("--prefix-chars", type=int, default=16,
+                    help="p of the prefix table (the reference's main.rs default is -p 20 key bits)")
+    ap.add_argument("--prefix-table", default="inline", choices=["inline", "ranks"],
+                    help="inline: 16-B entries holding each range's first suffix (4^16 x 16 B = 64 GiB); "
+                         "ranks: u32 ranks only (sas/sa_search.rs:59-75's table)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
@@ -434,7 +440,7 @@ def main():
     if args.mode == "shard":
         from sas_amd.shard import ShardedSearch
         # each rank builds ONLY its own SA rank range (sas_build_part: no whole-SA step)
-        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True, prefix=args.prefix_chars)
+        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True, prefix=args.prefix_chars)  # 40-bit SA
         if dist is None:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -442,7 +448,8 @@ def main():
             dist.init_process_group("nccl", rank=0, world_size=1)
         engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo)
     else:
-        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, prefix=args.prefix_chars)
+        idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, prefix=args.prefix_chars,
+                                    prefix_inline=args.prefix_table == "inline")
     stats = idx.stats()
     off = rank_query_offsets(n, nq, m, rank)
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
@@ -521,8 +528,9 @@ def main():
         mean_probes = float("nan")
     layers_of = {"stree": stats["stree_layers"], "sector": stats["sector_layers"], "quad": stats["quad_layers"]}
     tail = max(0.0, mean_probes - layers_of[args.algo]) if args.algo in layers_of else mean_probes
+    pe = 16 if stats["prefix_bytes"] == (4 ** stats["prefix_chars"] + 1) * 16 else 8
     algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail, stats["sector_layers"],
-                                   stats["quad_layers"])
+                                   stats["quad_layers"], pe)
     achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
 
     variants = {}
@@ -531,13 +539,14 @@ def main():
         _, vp = idx.search_fixed(qbytes, m, algo=v, probes=True)
         vmean = float(vp.double().mean().item())
         vtail = max(0.0, vmean - layers_of[v]) if v in layers_of else vmean
-        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], vtail, stats["sector_layers"], stats["quad_layers"])
+        vb = algorithmic_bytes(v, n, m, stats["stree_layers"], vtail, stats["sector_layers"], stats["quad_layers"], pe)
         variants[v] = {"lookups_per_s": ws * nq * max(3, args.steps // 4) / vel, "kernel_ms": vk,
                        "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
                        "mean_probes": float(vp.double().mean().item()), "verified": vok}
 
-    traffic, traffic_src = load_traffic(args.algo + (str(stats["prefix_chars"]) if args.algo == "prefix" else ""),
-                                        n, nq, m)
+    pkey = str(stats["prefix_chars"]) + ("i" if pe == 16 else "")
+    traffic, traffic_src, rdreq = load_traffic(args.algo + (pkey if args.algo == "prefix" else ""), n, nq, m,
+                                               with_requests=True)
     cpu = None
     if rank == 0 and ws == 1 and not args.no_cpu and args.mode == "replicated":
         cpu = cpu_baseline(text, idx, qbytes, m, nq, args.cpu_seconds)
@@ -582,12 +591,13 @@ def main():
                                     "inline": "k_sa_inline", "prefix": "k_sa_prefix"}.get(args.algo, "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes,
-                         # what bounds this path: dependent random requests (each a 128-B line),
-                         # against the measured random-request ceiling; query/result streams excluded
-                         "requests": None if args.algo != "prefix" else {
-                             "per_lookup": mean_probes, "achieved_per_s": mean_probes * nq / (kernel_ms * 1e-3),
+                         # what bounds this path: random 128-B-line requests (PMC L2->fabric reads
+                         # of this workload, query stream included), against the measured
+                         # random-request ceiling
+                         "requests": None if rdreq is None else {
+                             "per_lookup": rdreq / nq, "achieved_per_s": rdreq / (kernel_ms * 1e-3),
                              "ceiling_per_s": RANDOM_REQ_CEILING,
-                             "frac": mean_probes * nq / (kernel_ms * 1e-3) / RANDOM_REQ_CEILING}},
+                             "frac": rdreq / (kernel_ms * 1e-3) / RANDOM_REQ_CEILING, "source": traffic_src}},
             "cpu_baseline": cpu,
             "e2e_host": e2e,
             "variants": variants,

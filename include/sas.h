@@ -74,6 +74,10 @@ typedef struct sas_index sas_index;
                                         if 0, ceil(log4(n)) + 1 capped at 16 (16 at n = 2^30:
                                         16 GiB).  Needs SAS_BUILD_QUAD.  u32 entries, or
                                         packed 40-bit ones beside a 40-bit SA             */
+#define SAS_BUILD_PREFIX_INLINE (1u << 15) /* the prefix table with 16-B entries: the first
+                                        suffix of each key's range inlined as {32-char key,
+                                        rank, SA}, so a lookup answered by that suffix is
+                                        one read.  Fused quad leaves, u32 SA only         */
 #define SAS_BUILD_PREFIX_P(p) ((uint32_t)(p) << 16)  /* bits 16..20: prefix chars       */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry

@@ -843,13 +843,28 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
 // whose key is x are the ranks [table[x], table[x+1]).  Rank r with a new key fills
 // table(key(r-1), key(r)] = r (rank sa_n fills the rest up to 4^p); a gap longer than
 // PT_SMALL goes to a list that whole workgroups fill.  Keys come from the quad leaves.
-// Entries are u32, or packed 40-bit (SaView<5> / sa_put<5>) beside a 40-bit SA.
+// Entries are u32, or packed 40-bit (SaView<5> / sa_put<5>) beside a 40-bit SA, or
+// (SAS_BUILD_PREFIX_INLINE, TW = 16) {key64, rank, SA} of that first suffix, so a lookup
+// whose answer is the first suffix of its range needs this one read.
 #define PT_SMALL 256
 template <bool KO>
 __device__ __forceinline__ uint64_t pt_key64(const uint4* leaves, uint64_t r) {
     if (KO) return reinterpret_cast<const uint64_t*>(leaves)[r];
     const uint2 k = reinterpret_cast<const uint2*>(leaves)[2 * r];
     return (uint64_t)k.x | ((uint64_t)k.y << 32);
+}
+
+template <int TW>
+__device__ __forceinline__ void pt_put(uint8_t* t, uint64_t x, uint64_t r, uint4 ev) {
+    if (TW == 16) reinterpret_cast<uint4*>(t)[x] = ev;
+    else sa_put<TW>(t, x, r);
+}
+// inline entry for rank r (fused leaves: entry r = {key lo, key hi, SA lo32, SA hi8});
+// r = sa_n (nothing >= the key): key MAX, and the kernel answers next_pos
+__device__ __forceinline__ uint4 pt_inline_entry(const uint4* leaves, uint64_t sa_n, uint64_t r) {
+    if (r >= sa_n) return make_uint4(~0u, ~0u, (uint32_t)sa_n, 0u);
+    const uint4 e = leaves[r];
+    return make_uint4(e.x, e.y, (uint32_t)r, e.z);
 }
 
 template <bool KO, int TW>
@@ -862,7 +877,8 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
         const uint64_t lo = r > 0 ? (pt_key64<KO>(leaves, r - 1) >> sh) + 1 : 0;
         if (lo > kr) continue;  // same key as rank r - 1
         if (kr - lo < PT_SMALL) {
-            for (uint64_t x = lo; x <= kr; x++) sa_put<TW>(table, x, r);
+            const uint4 ev = TW == 16 ? pt_inline_entry(leaves, sa_n, r) : make_uint4(0, 0, 0, 0);
+            for (uint64_t x = lo; x <= kr; x++) pt_put<TW>(table, x, r, ev);
         } else {
             const unsigned long long slot = atomicAdd(nbig, 1ull);
             if (slot < big_cap) {
@@ -876,20 +892,23 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
 
 template <int TW>
 __global__ void k_pt_big(const uint64_t* __restrict__ big, const unsigned long long* __restrict__ nbig,
-                         uint8_t* __restrict__ table) {
+                         uint8_t* __restrict__ table, const uint4* __restrict__ leaves, uint64_t sa_n) {
     for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x) {
         const uint64_t lo = big[3 * b], hi = big[3 * b + 1];
         const uint64_t r = big[3 * b + 2];
-        for (uint64_t x = lo + threadIdx.x; x <= hi; x += blockDim.x) sa_put<TW>(table, x, r);
+        const uint4 ev = TW == 16 ? pt_inline_entry(leaves, sa_n, r) : make_uint4(0, 0, 0, 0);
+        for (uint64_t x = lo + threadIdx.x; x <= hi; x += blockDim.x) pt_put<TW>(table, x, r, ev);
     }
 }
 
-static int build_prefix(sas_index* x, uint32_t p) {
+static int build_prefix(sas_index* x, uint32_t p, bool inl) {
     const uint64_t sa_n = x->sa_n;
     if (!x->quad_leaves) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX needs SAS_BUILD_QUAD (keys and SA values of the leaves)");
-    // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA
-    const uint32_t tw = x->sa_w == 5 ? 5 : 4;
-    if (tw == 4 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
+    if (inl && (x->quad_compact || x->sa_w != 4))
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE needs fused quad leaves and a u32 SA");
+    // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA, 16-B inline ones
+    const uint32_t tw = inl ? 16 : (x->sa_w == 5 ? 5 : 4);
+    if (tw != 5 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
     if (p == 0) {
         uint32_t l4 = 0;  // ceil(log4(sa_n))
         while (l4 < 32 && (1ull << (2 * l4)) < sa_n) l4++;
@@ -907,7 +926,9 @@ static int build_prefix(sas_index* x, uint32_t p) {
     uint8_t* tb = t.as<uint8_t>();
     uint64_t* bl = big.as<uint64_t>();
     unsigned long long* nb_d = nbig.as<unsigned long long>();
-    if (x->quad_compact && tw == 5)
+    if (tw == 16)
+        hipLaunchKernelGGL((k_pt_fill<false, 16>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+    else if (x->quad_compact && tw == 5)
         hipLaunchKernelGGL((k_pt_fill<true, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
     else if (x->quad_compact)
         hipLaunchKernelGGL((k_pt_fill<true, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
@@ -915,8 +936,9 @@ static int build_prefix(sas_index* x, uint32_t p) {
         hipLaunchKernelGGL((k_pt_fill<false, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
     else
         hipLaunchKernelGGL((k_pt_fill<false, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
-    if (tw == 5) hipLaunchKernelGGL(k_pt_big<5>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb);
-    else hipLaunchKernelGGL(k_pt_big<4>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb);
+    if (tw == 16) hipLaunchKernelGGL(k_pt_big<16>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
+    else if (tw == 5) hipLaunchKernelGGL(k_pt_big<5>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
+    else hipLaunchKernelGGL(k_pt_big<4>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
     HIP_TRY(hipGetLastError());
     uint64_t nb = 0;
     HIP_TRY(hipMemcpy(&nb, nbig.p, 8, hipMemcpyDeviceToHost));
@@ -1192,7 +1214,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
     if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
     if (flags & (SAS_BUILD_QUAD | SAS_BUILD_QUAD_COMPACT)) TRY(build_quad(x, (flags & SAS_BUILD_QUAD_COMPACT) != 0, flags & (SAS_BUILD_QUAD_ABS | SAS_BUILD_QUAD_REL)));
-    if (flags & SAS_BUILD_PREFIX) TRY(build_prefix(x, (flags >> 16) & 31));
+    if (flags & (SAS_BUILD_PREFIX | SAS_BUILD_PREFIX_INLINE))
+        TRY(build_prefix(x, (flags >> 16) & 31, (flags & SAS_BUILD_PREFIX_INLINE) != 0));
 
     // binary-search top in LDS
     {

@@ -1164,9 +1164,25 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
         const uint64_t K = K64 >> sh;
-        uint64_t lo, hi;
+        uint64_t lo, hi = 0, pos = QUAD_NO_SA;
         const uint32_t* pt = reinterpret_cast<const uint32_t*>(a.prefix);
-        if (TW == 5) {
+        const uint4* pt16 = reinterpret_cast<const uint4*>(a.prefix);
+        bool have_hi = true;
+        if (TW == 16) {
+            // inline entry: the range's first suffix {key, rank, SA}; if it is >= q it is
+            // the answer, and this was the only read
+            const uint4 e0 = SAS_PREFIX_NT ? nt_load4(pt16 + K) : pt16[K];
+            lo = e0.z;
+            have_hi = false;
+            if (lo >= sa_n) {
+                pos = a.next_pos;
+            } else if (sector_ge<QW>((uint64_t)e0.x | ((uint64_t)e0.y << 32), e0.w, K64, a, q)) {
+                pos = e0.w;
+            } else {
+                hi = pt16[K + 1].z;
+                have_hi = true;
+            }
+        } else if (TW == 5) {
             const SaView<5> v{a.prefix};
             lo = v[K];
             hi = v[K + 1];
@@ -1183,35 +1199,48 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
             lo = pt[K];
             hi = pt[K + 1];
         }
-        // binary_search over [table[K], table[K+1]) (sas/sa_search.rs:98-112).  A scan of
-        // short ranges with independent loads measured slower (0.53 -> 0.60 ms at c1,
-        // 26.6 -> 39.4 ms at c3): its key re-reads lengthen the dependent chain.
-        // out_probes = the reference's cnt: 1 for the table, 1 per iteration (:86-104).
-        uint32_t probes = 1;
-        uint64_t pr = QUAD_NO_SA;
-        while (lo < hi) {
-            const uint64_t mid = (lo + hi) >> 1;
-            uint64_t key, pp;
-            if (KO) {
-                key = quad_entry_key<true>(a, mid);
-                pp = key == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
-            } else {
-                const uint4 e = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
-                key = (uint64_t)e.x | ((uint64_t)e.y << 32);
-                pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+        const uint64_t lo0 = lo;
+        uint64_t hi0 = hi;
+        // binary_search over [table[K], table[K+1]) (sas/sa_search.rs:98-112); with inline
+        // entries rank lo is already known to be < q.  A scan of short ranges with
+        // independent loads measured slower (0.53 -> 0.60 ms at c1, 26.6 -> 39.4 ms at c3):
+        // its key re-reads lengthen the dependent chain.
+        if (pos == QUAD_NO_SA) {
+            uint64_t pr = QUAD_NO_SA;
+            if (TW == 16) lo++;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                uint64_t key, pp;
+                if (KO) {
+                    key = quad_entry_key<true>(a, mid);
+                    pp = key == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
+                } else {
+                    const uint4 e = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
+                    key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                    pp = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+                }
+                if (sector_ge<QW>(key, pp, K64, a, q)) {
+                    hi = mid;
+                    pr = pp;  // SA at rank hi (QUAD_NO_SA: not read); lo ends at hi
+                } else {
+                    lo = mid + 1;
+                }
             }
-            probes++;
-            if (sector_ge<QW>(key, pp, K64, a, q)) {
-                hi = mid;
-                pr = pp;  // SA at rank hi (QUAD_NO_SA: not read); lo ends at hi
-            } else {
-                lo = mid + 1;
+            if (lo >= sa_n) pos = a.next_pos;
+            else if (pr != QUAD_NO_SA) pos = pr;
+            else pos = quad_entry_sa<KO, W>(a, lo);
+        }
+        // out_probes = the reference's cnt (sas/sa_search.rs:86-112): 1 for the table, then
+        // binary_search's iterations over [table[K], table[K+1]), which end at rank lo
+        uint32_t probes = 1;
+        if (a.out_probes) {
+            if (!have_hi) hi0 = pt16[K + 1].z;
+            for (uint64_t l2 = lo0, h2 = hi0; l2 < h2; probes++) {
+                const uint64_t mid = (l2 + h2) >> 1;
+                if (mid < lo) l2 = mid + 1;
+                else h2 = mid;
             }
         }
-        uint64_t pos;
-        if (lo >= sa_n) pos = a.next_pos;
-        else if (pr != QUAD_NO_SA) pos = pr;
-        else pos = quad_entry_sa<KO, W>(a, lo);
         a.out_pos[i] = pos;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1269,12 +1298,15 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
 #define K_PREFIX(Q) (k_sa_prefix<Q, KO, W, 4>)
 #define K_PREFIX5(Q) (k_sa_prefix<Q, KO, W, 5>)
+#define K_PREFIX16(Q) (k_sa_prefix<Q, KO, W, 16>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
         if (qw == 1) hipLaunchKernelGGL((k_sa_quad<1, KO, W>), grid, block, 0, st, a);
         else { QW_CASE(K_QUAD4X) }
     } else if (algo == SAS_ALGO_PREFIX) {
-        if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) } else { QW_CASE(K_PREFIX) }
+        if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) }
+        else if (a.prefix_w == 16 && !KO) { QW_CASE(K_PREFIX16) }
+        else { QW_CASE(K_PREFIX) }
     } else {
         if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
     }

@@ -31,6 +31,7 @@ SAS_BUILD_QUAD_ABS = 1 << 11
 SAS_BUILD_QUAD_REL = 1 << 12
 SAS_BUILD_LLCP = 1 << 13
 SAS_BUILD_PREFIX = 1 << 14
+SAS_BUILD_PREFIX_INLINE = 1 << 15
 
 
 def SAS_BUILD_PREFIX_P(p: int) -> int:

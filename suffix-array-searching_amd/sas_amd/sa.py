@@ -45,16 +45,18 @@ def _as_u8(x):
     return np.ascontiguousarray(np.frombuffer(x, np.uint8) if isinstance(x, (bytes, bytearray)) else x, np.uint8)
 
 
-def _prefix_flags(prefix, quad, n: int) -> int:
+def _prefix_flags(prefix, quad, n: int, inline: bool = False) -> int:
     """prefix=None: build the prefix table (SAS_BUILD_PREFIX, p chosen by the library)
-    whenever a quad tree is built and n < 2^32 - 1; False: never; an int: that p."""
+    whenever a quad tree is built and n < 2^32 - 1; False: never; an int: that p.
+    inline: 16-B entries inlining each range's first suffix (SAS_BUILD_PREFIX_INLINE)."""
     if prefix is None:
         prefix = bool(quad) and n < 0xFFFFFFFF
     if prefix is False:
         return 0
+    f = _lib.SAS_BUILD_PREFIX | (_lib.SAS_BUILD_PREFIX_INLINE if inline else 0)
     if prefix is True:
-        return _lib.SAS_BUILD_PREFIX
-    return _lib.SAS_BUILD_PREFIX | _lib.SAS_BUILD_PREFIX_P(int(prefix))
+        return f
+    return f | _lib.SAS_BUILD_PREFIX_P(int(prefix))
 
 
 def _quad_flags(quad) -> int:
@@ -92,7 +94,7 @@ class SaNaive:
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
               sa40: bool = False, quad: bool | str = True, llcp: bool = True,
-              prefix: bool | int | None = None) -> "SaNaive":
+              prefix: bool | int | None = None, prefix_inline: bool = False) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
@@ -101,14 +103,16 @@ class SaNaive:
         llcp: the Manber-Myers Llcp/Rlcp entries for algo="llcp" (SAS_BUILD_LLCP, 16 B
         per suffix, implies the LCP array).  prefix: the prefix table for algo="prefix"
         (SAS_BUILD_PREFIX; None = whenever quad is built and n < 2^32 - 1, an int = its
-        p chars)."""
+        p chars); prefix_inline: 16-B entries that inline each range's first suffix
+        (SAS_BUILD_PREFIX_INLINE: fused quad leaves, u32 SA)."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= _lib.SAS_BUILD_LLCP if llcp else 0
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         flags |= _lib.SAS_BUILD_SA40 if sa40 else 0
-        flags |= _quad_flags(quad) | _prefix_flags(prefix, quad, n if rank_range is None else rank_range[1] - rank_range[0])
+        flags |= _quad_flags(quad) | _prefix_flags(prefix, quad, n if rank_range is None else rank_range[1] - rank_range[0],
+                                                   prefix_inline)
         sa_ptr, sa_w = None, 4
         if sa is not None:
             if _is_cuda(t) != _is_cuda(sa):
@@ -133,7 +137,7 @@ class SaNaive:
     @classmethod
     def build_part(cls, t, part: int, parts: int, lcp: bool = True, stree: bool = True, verify: bool = False,
                    flags: int = 0, sector: bool = True, quad: bool | str = True, llcp: bool = True,
-                   prefix: bool | int | None = None) -> "SaNaive":
+                   prefix: bool | int | None = None, prefix_inline: bool = False) -> "SaNaive":
         """Sharded-text index that builds ONLY its own SA rank range (sas_build_part):
         part `part` of `parts` contiguous 7-char-prefix bin ranges.  The range is
         chosen by the library (stats: rank_lo, sa_entries, next_pos)."""
@@ -141,7 +145,7 @@ class SaNaive:
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
-        flags |= _quad_flags(quad) | (_lib.SAS_BUILD_LLCP if llcp else 0) | _prefix_flags(prefix, quad, n)
+        flags |= _quad_flags(quad) | (_lib.SAS_BUILD_LLCP if llcp else 0) | _prefix_flags(prefix, quad, n, prefix_inline)
         if _is_cuda(t):
             flags |= _lib.SAS_DEVICE_PTRS
         h = C.c_void_p()

@@ -213,16 +213,18 @@ def test_prefix_table(sas, sadef):
         qs += [t[n - k:] for k in (1, 2, 17, min(n, 40))] + [np.zeros(0, np.uint8), np.full(20, 3, np.uint8)]
         buf, qo, ql = pack(qs)
         expect = oracle_positions(t, sa, buf[:-64], qo, ql)
-        for p, quad, sa40 in ((0, True, False), (1, True, False), (2, "compact", False), (7, True, False),
-                              (16, "compact", True), (11, "compact", False)):
+        for p, quad, sa40, inl in ((0, True, False, False), (1, True, False, False), (2, "compact", False, False),
+                                   (7, True, False, False), (16, "compact", True, False), (11, "compact", False, False),
+                                   (0, True, False, True), (1, True, False, True), (7, True, False, True),
+                                   (13, True, False, True)):
             idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=quad, sa40=sa40,
-                                    prefix=p if p else True)
+                                    prefix=p if p else True, prefix_inline=inl)
             st = idx.stats()
             l4 = next(k for k in range(33) if 4 ** k >= n)  # ceil(log4 n)
             assert st["prefix_chars"] == (p if p else min(16, l4 + 1)), (name, p)
-            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * (5 if sa40 else 4)  # 40-bit ranks
+            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * (16 if inl else 5 if sa40 else 4)
             got, probes = idx.search_batch(buf, qo, ql, algo="prefix", probes=True)
-            assert np.array_equal(got, expect), (name, p, quad, sa40, np.nonzero(got != expect)[0][:5])
+            assert np.array_equal(got, expect), (name, p, quad, sa40, inl, np.nonzero(got != expect)[0][:5])
             if p == 7 and name == "random_200k":
                 # cnt as the reference counts it (sas/sa_search.rs:86-112): 1 for the table
                 # (p > 0), then one per binary-search iteration over [table[K], table[K+1])
@@ -245,6 +247,8 @@ def test_prefix_table(sas, sadef):
     # built only with a quad tree, and refused without the table
     with pytest.raises(sas.SasError):
         sas.SaNaive.build(texts["random_200k"], quad=False, prefix=True)
+    with pytest.raises(sas.SasError):  # inline entries need fused leaves
+        sas.SaNaive.build(texts["random_200k"], quad="compact", prefix=True, prefix_inline=True)
     idx = sas.SaNaive.build(texts["random_200k"], prefix=False)
     with pytest.raises(sas.SasError):
         idx.search_batch(buf, qo, ql, algo="prefix")

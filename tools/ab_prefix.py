@@ -17,14 +17,19 @@ off, _, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=200, le
 src = torch.from_numpy(off.astype(np.int64)).cuda()
 qb = t[(src[:, None] + torch.arange(m, device="cuda")[None, :]).reshape(-1)].contiguous()
 out = torch.empty(nq, dtype=torch.int64, device="cuda")
-p = int(os.environ.get("AB_P", "0"))
-idx = sas_amd.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=p if p else True)
-line = {"p": idx.stats()["prefix_chars"]}
-ref = None
-for algo in ("prefix", "quad"):
-    idx.time_fixed(qb, m, nq, out, algo=algo, reps=2)
-    kns, _ = idx.time_fixed(qb, m, nq, out, algo=algo, reps=10)
-    line[algo] = round(kns / 1e6, 4)
-    ref = out.clone() if ref is None else ref
-    line[algo + "_ok"] = bool(torch.equal(out, ref))
-print("ms", line, flush=True)
+# AB_MODES: comma list of <p><r|i>: ranks-only (u32) or inline (16-B) table entries
+for mode in os.environ.get("AB_MODES", "16r").split(","):
+    p, inl = int(mode[:-1]), mode[-1] == "i"
+    idx = sas_amd.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=p,
+                                prefix_inline=inl)
+    line = {"mode": mode, "p": idx.stats()["prefix_chars"]}
+    ref = None
+    for algo in ("prefix", "quad"):
+        idx.time_fixed(qb, m, nq, out, algo=algo, reps=2)
+        kns, _ = idx.time_fixed(qb, m, nq, out, algo=algo, reps=10)
+        line[algo] = round(kns / 1e6, 4)
+        ref = out.clone() if ref is None else ref
+        line[algo + "_ok"] = bool(torch.equal(out, ref))
+    print("ms", line, flush=True)
+    idx.free()
+    torch.cuda.empty_cache()
