@@ -47,6 +47,10 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_VERIFY  (1u << 3)  /* run the adjacency + permutation check on the SA  */
 #define SAS_NO_LDS_TOP    (1u << 4)  /* search: do not serve the top levels from LDS     */
 #define SAS_VALIDATE      (1u << 5)  /* search: reject query bytes > 3 (synchronises)    */
+#define SAS_PREFIX_RANGE  (1u << 24) /* search, PLAIN / LCP: start binary_search from the
+                                        prefix table's range of q's first p chars, as the
+                                        reference's binary_search does (sas/sa_search.rs:
+                                        98-101); needs SAS_BUILD_PREFIX                    */
 #define SAS_BUILD_WIDE    (1u << 6)  /* build: use the n >= 2^31 two-pass doubling rounds
                                         at any n (test hook for that path)               */
 #define SAS_BUILD_SECTOR  (1u << 7)  /* also build the sector tree (SAS_ALGO_SECTOR)     */

@@ -116,11 +116,32 @@ __device__ __forceinline__ bool llcp_tie_less(const uint64_t* __restrict__ tw, u
     return lenS < (uint64_t)q.m;
 }
 
+// prefix_range (sas/sa_search.rs:86-95): the SA ranks [lo, hi) whose p-char key is K,
+// from the prefix table in any of its entry formats
+__device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, uint64_t* lo, uint64_t* hi) {
+    if (a.prefix_w == 16) {
+        const uint4* t = reinterpret_cast<const uint4*>(a.prefix);
+        *lo = t[K].z;
+        *hi = t[K + 1].z;
+    } else if (a.prefix_w == 5) {
+        const SaView<5> v{a.prefix};
+        *lo = v[K];
+        *hi = v[K + 1];
+    } else {
+        const uint32_t* t = reinterpret_cast<const uint32_t*>(a.prefix);
+        *lo = t[K];
+        *hi = t[K + 1];
+    }
+}
+
 // MODE 0: PLAIN, 1: LCP (mlr), 2: LLCP (Manber-Myers with the Llcp/Rlcp entries)
+// RANGE (SAS_PREFIX_RANGE, PLAIN / LCP without the LDS top): start from the prefix
+// table's range for q's first p chars instead of [0, sa_n), exactly as the reference's
+// binary_search does (sas/sa_search.rs:98-101) once its p is not 0
 #define BS_PLAIN 0
 #define BS_MLR 1
 #define BS_LLCP 2
-template <int QW, int MODE, bool TOP, int W>
+template <int QW, int MODE, bool TOP, int W, bool RANGE = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
     __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
     __shared__ sa_val_t<W> s_sa[TOP ? SAS_TOP_NODES : 1];
@@ -149,6 +170,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         uint64_t l = 0, r = a.sa_n;
         uint32_t k = 1, probes = 0, llcp = 0, rlcp = 0;
         sa_val_t<W> pr = 0;  // SA[r] once r has moved
+        bool rmoved = false;
+        if (RANGE) {
+            prefix_range(a, q.w[0] >> (64 - 2 * a.prefix_chars), &l, &r);
+            probes = 1;  // the reference's cnt counts the table read (:87-89)
+        }
         for (uint32_t it = 0; it < a.iters; ++it) {
             if (l < r) {
                 uint64_t mid = (l + r) >> 1;
@@ -203,9 +229,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     r = mid;
                     rlcp = lcp;
                     pr = p;
+                    rmoved = true;
                 }
             }
         }
+        if (RANGE && !rmoved && r < a.sa_n) pr = (sa_val_t<W>)sa[r];
         a.out_pos[i] = (r >= a.sa_n) ? a.next_pos : (uint64_t)pr;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1249,7 +1277,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
 
 // ------------------------------------------------------------------ host dispatch
 template <int W>
-static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
+static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 block, hipStream_t st,
+                     const SearchArgs& a) {
 #define QW_CASE(KERNEL_T)                                                           \
     switch (qw) {                                                                   \
         case 1: hipLaunchKernelGGL(KERNEL_T(1), grid, block, 0, st, a); break;      \
@@ -1263,10 +1292,16 @@ static void launch_w(int algo, bool top, int qw, dim3 grid, dim3 block, hipStrea
 #define K_LCP(Q) (k_sa_binary<Q, BS_MLR, false, W>)
 #define K_LLCP_TOP(Q) (k_sa_binary<Q, BS_LLCP, true, W>)
 #define K_LLCP(Q) (k_sa_binary<Q, BS_LLCP, false, W>)
+#define K_PLAIN_RANGE(Q) (k_sa_binary<Q, BS_PLAIN, false, W, true>)
+#define K_LCP_RANGE(Q) (k_sa_binary<Q, BS_MLR, false, W, true>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_STREE4X(Q) (k_sa_stree4x<Q, W>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
-    if (algo == SAS_ALGO_PLAIN) {
+    if (algo == SAS_ALGO_PLAIN && range) {
+        QW_CASE(K_PLAIN_RANGE)
+    } else if (algo == SAS_ALGO_LCP && range) {
+        QW_CASE(K_LCP_RANGE)
+    } else if (algo == SAS_ALGO_PLAIN) {
         if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
         if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
@@ -1322,14 +1357,15 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     if (blocks == 0) return 0;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
+    const bool range = (flags & SAS_PREFIX_RANGE) != 0;
     if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
         if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
         else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);
         else launch_quad<true, 4>(algo, top, qw, grid, block, st, a);
     } else if (x->sa_w == 5 && algo != SAS_ALGO_SECTOR) {
-        launch_w<5>(algo, top, qw, grid, block, st, a);
+        launch_w<5>(algo, top, range, qw, grid, block, st, a);
     } else {
-        launch_w<4>(algo, top, qw, grid, block, st, a);
+        launch_w<4>(algo, top, range, qw, grid, block, st, a);
     }
     HIP_TRY(hipGetLastError());
     return 0;
@@ -1403,6 +1439,8 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
     if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "search: unknown algo");
+    if ((flags & SAS_PREFIX_RANGE) && (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP)))
+        SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP on an index with SAS_BUILD_PREFIX");
     if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
     if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "search: SAS_ALGO_LLCP needs SAS_BUILD_LLCP");
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
@@ -1503,6 +1541,8 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
     if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
+    if ((flags & SAS_PREFIX_RANGE) && (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP)))
+        SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP on an index with SAS_BUILD_PREFIX");
     if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
     if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "sas_time_fixed: index has no LLCP entries");
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)

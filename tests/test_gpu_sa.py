@@ -225,6 +225,13 @@ def test_prefix_table(sas, sadef):
             assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * (16 if inl else 5 if sa40 else 4)
             got, probes = idx.search_batch(buf, qo, ql, algo="prefix", probes=True)
             assert np.array_equal(got, expect), (name, p, quad, sa40, inl, np.nonzero(got != expect)[0][:5])
+            # the reference's own binary_search over SA + text, started from the table's range
+            rng_probes = {}
+            for base in ("plain", "lcp"):
+                g2, rng_probes[base] = idx.search_batch(buf, qo, ql, algo=base, probes=True,
+                                                        flags=_lib.SAS_PREFIX_RANGE)
+                assert np.array_equal(g2, expect), (name, p, base, "range")
+            assert np.array_equal(rng_probes["plain"], probes)  # same cnt as PREFIX
             if p == 7 and name == "random_200k":
                 # cnt as the reference counts it (sas/sa_search.rs:86-112): 1 for the table
                 # (p > 0), then one per binary-search iteration over [table[K], table[K+1])
@@ -252,6 +259,11 @@ def test_prefix_table(sas, sadef):
     idx = sas.SaNaive.build(texts["random_200k"], prefix=False)
     with pytest.raises(sas.SasError):
         idx.search_batch(buf, qo, ql, algo="prefix")
+    with pytest.raises(sas.SasError):
+        idx.search_batch(buf, qo, ql, algo="plain", flags=_lib.SAS_PREFIX_RANGE)
+    idx = sas.SaNaive.build(texts["random_200k"], prefix=True)
+    with pytest.raises(sas.SasError):  # LLCP's entries belong to the intervals from [0, n)
+        idx.search_batch(buf, qo, ql, algo="llcp", flags=_lib.SAS_PREFIX_RANGE)
 
 
 def test_invalid_codes_rejected(sas):
