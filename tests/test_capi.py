@@ -99,6 +99,20 @@ def test_quad_layout_flags():
         assert f"#define {name} (1u << {getattr(_lib, name).bit_length() - 1})" in hdr
 
 
+def test_flag_and_algo_mirror_matches_header():
+    """Every single-bit #define in include/sas.h has its _lib mirror with the same value,
+    and the algorithm names map to the sas_algo enum."""
+    import re
+    hdr = open(os.path.join(os.path.dirname(_lib.LIB_PATH), "..", "include", "sas.h")).read()
+    defs = dict(re.findall(r"^#define (SAS_[A-Z0-9_]+)\s+\(1u << (\d+)\)", hdr, re.M))
+    assert len(defs) >= 15
+    for name, bit in defs.items():
+        assert getattr(_lib, name) == 1 << int(bit), name
+    enum = dict(re.findall(r"SAS_ALGO_([A-Z]+)\s*=\s*(\d+)", hdr))
+    assert {k.lower(): int(v) for k, v in enum.items()} == _lib.ALGOS
+    assert _lib.SAS_BUILD_PREFIX_P(17) == 17 << 16
+
+
 def test_stats_struct_matches_header():
     """ctypes SasStats lists the fields of sas_stats in include/sas.h, in order."""
     import re
