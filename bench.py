@@ -274,32 +274,30 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
     main_algo = args.algo if (args.algo != "sector" or fits) else "stree"
     quad_mode = (("compact" if (args.quad_compact or not fits) else True) if main_algo in ("quad", "inline", "prefix")
                  else False)
-    # prefix table beside a 40-bit SA: packed 40-bit entries; p = 15 (5 GiB) is what fits
-    # next to the 2^34-char index and 10^8 ragged queries
-    c3_prefix = min(args.prefix_chars, 15) if main_algo == "prefix" else False
+    # prefix table beside a 40-bit SA: packed 40-bit entries, p = 16 (20 GiB); it fits
+    # because the 16 GiB byte copy of the text is dropped after the build (queries are
+    # cut from, and answers checked against, the index's packed text: sas_extract)
+    c3_prefix = min(args.prefix_chars, 16) if main_algo == "prefix" else False
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
     # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
     idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
                                 quad=quad_mode, verify=True, llcp=False, prefix=c3_prefix)
     stats = idx.stats()
+    del text
+    torch.cuda.empty_cache()
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
     lens = torch.from_numpy(ln.astype(np.int64)).to(dev)
     qoff = torch.zeros(nq, dtype=torch.int64, device=dev)
     qoff[1:] = torch.cumsum(lens, 0)[:-1]
     total = int(lens.sum().item())
-    qbytes = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    qbytes = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
     src = torch.from_numpy(off.astype(np.int64)).to(dev)
-    chunk = 1 << 18  # bounds the gather temporaries (HBM is nearly full at n = 2^34)
-    for s in range(0, nq, chunk):
-        e = min(nq, s + chunk)
-        L = lens[s:e]
-        start = qoff[s:e]
-        rep = torch.repeat_interleave(torch.arange(e - s, device=dev), L)
-        within = torch.arange(rep.numel(), device=dev) - (start - start[0])[rep]
-        qbytes[start[0]:start[0] + rep.numel()] = text[src[s:e][rep] + within]
     qlen = lens.to(torch.int32)
+    idx.extract(src, qlen, qoff, qbytes)  # t[off .. off + len) from the packed text
+    del src
+    chunk = 1 << 20
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
@@ -326,11 +324,10 @@ def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
         okc = True
         for s in range(0, nq, chunk):
             e = min(nq, s + chunk)
-            L = lens[s:e]
-            rep = torch.repeat_interleave(torch.arange(e - s, device=dev), L)
-            within = torch.arange(rep.numel(), device=dev) - (qoff[s:e] - qoff[s])[rep]
-            got = text[(out[s:e][rep] + within).clamp_(max=n - 1)]
-            okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + rep.numel()]))
+            span = int((qoff[e - 1] + lens[e - 1] - qoff[s]).item())
+            got = torch.empty(span, dtype=torch.uint8, device=dev)
+            idx.extract(out[s:e].contiguous(), qlen[s:e].contiguous(), (qoff[s:e] - qoff[s]).contiguous(), got)
+            okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + span]))
         _, pr = idx.search_batch(qbytes, qoff, qlen, algo=algo, probes=True)
         mp = float(pr.double().mean().item())
         mean_m = total / nq
@@ -412,9 +409,9 @@ def main():
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
     args = ap.parse_args()
     if args.algo is None:
-        # c1: the prefix table (1.86e10 vs QUAD 1.40e10 lookups/s); c3 (n = 2^34, 40-bit
-        # SA, ragged 8..256): QUAD on compact leaves (25.0 ms vs 26.6 ms with a p = 15 table)
-        args.algo = "quad" if args.workload == "c3" else "prefix"
+        # the prefix table: c1 2.77e10 vs QUAD 1.40e10 lookups/s; c3 (n = 2^34, 40-bit SA,
+        # ragged 8..256, p = 16 rank table) 24.5 vs 24.9 ms per 10^8 (tools/ab_c3.py: -7%)
+        args.algo = "prefix"
     keep_stdout_for_result()
 
     import torch

@@ -215,6 +215,13 @@ int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t 
 int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t count, uint64_t* dst, uint32_t flags);
 int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags);
 
+/* Substrings of the indexed text as byte codes 0..3: out[out_off[i] .. out_off[i] + len[i])
+ * = text[pos[i] .. pos[i] + len[i]) (0 past the text end), from the index's packed copy,
+ * so a caller can drop its own byte copy of a large text after sas_build.  Device
+ * pointers only (SAS_DEVICE_PTRS), stream-ordered on `stream`. */
+int sas_extract(const sas_index* index, const uint64_t* pos, const uint32_t* len, const uint64_t* out_off,
+                uint64_t count, uint8_t* out, void* stream, uint32_t flags);
+
 /* GPU check of the SA: strictly increasing adjacent suffixes (the
  * reference's build assertion, sas/sa_search.rs:36-38) + permutation.
  * Returns 0 if valid, EINVAL (with message) if not. */

@@ -1315,6 +1315,35 @@ extern "C" int sas_copy_sa_range(const sas_index* index, uint64_t start, uint64_
     return copy_out(index->sa + (start - index->rank_lo) * 4, dst, count * 4, flags);
 }
 
+// Substrings of the indexed text as byte codes: out[out_off[i] .. + len[i]) = text[pos[i] ..
+// + len[i]), read from the packed copy, so a caller may drop its own byte copy of a large
+// text after sas_build and still cut queries from it or check answers (the c3 bench).
+// One thread per substring; bytes past the text end read 0 (the padding).
+__global__ void k_extract(const uint64_t* __restrict__ tw, uint64_t n, const uint64_t* __restrict__ pos,
+                          const uint32_t* __restrict__ len, const uint64_t* __restrict__ out_off, uint64_t count,
+                          uint8_t* __restrict__ out) {
+    GRID_STRIDE(i, count) {
+        const uint64_t p = pos[i], o = out_off[i];
+        const uint32_t L = len[i];
+        for (uint32_t j = 0; j < L; j++) {
+            const uint64_t c = p + j;
+            out[o + j] = c < n ? (uint8_t)((tw[c >> 5] >> (62 - 2 * (c & 31))) & 3u) : (uint8_t)0;
+        }
+    }
+}
+
+extern "C" int sas_extract(const sas_index* index, const uint64_t* pos, const uint32_t* len, const uint64_t* out_off,
+                           uint64_t count, uint8_t* out, void* stream, uint32_t flags) {
+    if (!index || (count && (!pos || !len || !out_off || !out))) SAS_FAIL(EINVAL, "sas_extract: null argument");
+    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_extract: device pointers only (SAS_DEVICE_PTRS)");
+    if (count == 0) return 0;
+    HIP_TRY(hipSetDevice(index->device));
+    hipLaunchKernelGGL(k_extract, dim3(grid_for(count)), dim3(256), 0, static_cast<hipStream_t>(stream),
+                       index->text_w, index->n, pos, len, out_off, count, out);
+    HIP_TRY(hipGetLastError());
+    return 0;
+}
+
 template <int W>
 __global__ void k_widen_sa(SaView<W> sa, uint64_t start, uint64_t count, uint64_t* __restrict__ out) {
     GRID_STRIDE(i, count) out[i] = sa[start + i];

@@ -1175,6 +1175,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
 #ifndef SAS_PREFIX_NT
 #define SAS_PREFIX_NT 1  // non-temporal table / entry loads (-3%, tools/ab_prefix.py)
 #endif
+#ifndef SAS_PREFIX_QWMAX
+#define SAS_PREFIX_QWMAX 8  // register-resident query words (later ones repacked from the bytes)
+#endif
 #ifndef SAS_PREFIX_PAIR
 #define SAS_PREFIX_PAIR 0  // table[K], table[K+1] as one dword-aligned 8-B load
 #endif
@@ -1331,9 +1334,9 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_QUAD4X(Q) (k_sa_quad4x<(Q < SAS_QUAD4X_MAXREGS ? Q : SAS_QUAD4X_MAXREGS), KO, W>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true, KO, W>)
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
-#define K_PREFIX(Q) (k_sa_prefix<Q, KO, W, 4>)
-#define K_PREFIX5(Q) (k_sa_prefix<Q, KO, W, 5>)
-#define K_PREFIX16(Q) (k_sa_prefix<Q, KO, W, 16>)
+#define K_PREFIX(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 4>)
+#define K_PREFIX5(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 5>)
+#define K_PREFIX16(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 16>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
         if (qw == 1) hipLaunchKernelGGL((k_sa_quad<1, KO, W>), grid, block, 0, st, a);

@@ -185,6 +185,16 @@ class SaNaive:
         check(lib().sas_copy_lcp(self._h, out.ctypes.data, self.sa_n, 0))
         return out
 
+    def extract(self, pos, lens, out_off, out, stream=None):
+        """Text substrings as byte codes from the index's packed text (sas_extract):
+        out[out_off[i] : out_off[i] + lens[i]] = text[pos[i] : pos[i] + lens[i]].
+        torch CUDA tensors (int64 pos / out_off, int32 lens, uint8 out), async."""
+        import torch
+        st = stream if stream is not None else torch.cuda.current_stream(out.device).cuda_stream
+        check(lib().sas_extract(self._h, _ptr(pos), _ptr(lens), _ptr(out_off), int(pos.numel()), _ptr(out), st,
+                                _lib.SAS_DEVICE_PTRS))
+        return out
+
     def route(self, splitter_pos, qbytes, m: int, stream=None):
         """Sharded mode: shard id of each fixed-length query = number of splitter
         suffixes < q (sas_route).  numpy in -> numpy out; CUDA in -> CUDA out."""

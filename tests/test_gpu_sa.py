@@ -266,6 +266,26 @@ def test_prefix_table(sas, sadef):
         idx.search_batch(buf, qo, ql, algo="llcp", flags=_lib.SAS_PREFIX_RANGE)
 
 
+def test_extract_substrings(sas):
+    """sas_extract: substrings of the indexed text from its packed copy (what the c3
+    bench cuts its queries from after dropping the byte text), 0 past the end."""
+    import torch
+    n = 100_003
+    t = sas.random_string(n, seed=23)
+    idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=False, llcp=False)
+    rng = np.random.default_rng(4)
+    pos = np.concatenate([rng.integers(0, n, 500), [0, n - 1, n - 5, n]]).astype(np.int64)
+    lens = np.concatenate([rng.integers(0, 300, 500), [40, 1, 12, 3]]).astype(np.int32)
+    off = np.zeros(len(pos), np.int64)
+    off[1:] = np.cumsum(lens[:-1])
+    out = torch.full((int(lens.sum()),), 9, dtype=torch.uint8, device="cuda")
+    idx.extract(torch.from_numpy(pos).cuda(), torch.from_numpy(lens).cuda(), torch.from_numpy(off).cuda(), out)
+    got = out.cpu().numpy()
+    tp = np.concatenate([t, np.zeros(400, np.uint8)])
+    for p_, l_, o_ in zip(pos, lens, off):
+        assert np.array_equal(got[o_:o_ + l_], tp[p_:p_ + l_]), (p_, l_)
+
+
 def test_invalid_codes_rejected(sas):
     with pytest.raises(sas.SasError):
         sas.SaNaive.build(np.array([0, 1, 4, 2], np.uint8))
