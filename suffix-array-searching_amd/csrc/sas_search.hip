@@ -119,10 +119,11 @@ __device__ __forceinline__ bool llcp_tie_less(const uint64_t* __restrict__ tw, u
 // prefix_range (sas/sa_search.rs:86-95): the SA ranks [lo, hi) whose p-char key is K,
 // from the prefix table in any of its entry formats
 __device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, uint64_t* lo, uint64_t* hi) {
-    if (a.prefix_w == 16) {
+    if (a.prefix_w >= 16) {  // inline entries: rank in the first slot's .z
         const uint4* t = reinterpret_cast<const uint4*>(a.prefix);
-        *lo = t[K].z;
-        *hi = t[K + 1].z;
+        const uint64_t st = a.prefix_w / 16;
+        *lo = t[st * K].z;
+        *hi = t[st * (K + 1)].z;
     } else if (a.prefix_w == 5) {
         const SaView<5> v{a.prefix};
         *lo = v[K];
@@ -1278,6 +1279,72 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// SAS_BUILD_PREFIX_INLINE2: 32-B entries, the first two suffixes (ranks r, r + 1) of
+// the range of q's p-char key.  A lane pair reads the entry as one 32-B request, each
+// lane evaluates one suffix, and the pair ballot takes the first that is >= q; only if
+// both are < q does the search go on in [r + 2, table[K+1]).
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
+    uint32_t bad = 0;
+    const uint32_t sh = 64 - 2 * a.prefix_chars;
+    const uint64_t sa_n = a.sa_n;
+    const uint32_t sub = threadIdx.x & 1;
+    const int lane0 = (int)((threadIdx.x & 63) & ~1u);
+    const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / 2;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 2; i < a.nq; i += stride) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);  // both lanes: the same addresses, one request
+        const uint64_t K64 = q.w[0];
+        const uint64_t K = K64 >> sh;
+        const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + 2 * K + sub) : pt[2 * K + sub];
+        const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
+        const uint64_t rank = r0 + sub;
+        // rank sa_n stands for "past every suffix": it is the answer if reached
+        const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), e.w, K64, a, q);
+        const uint32_t pair = (uint32_t)(__ballot(ok) >> lane0) & 3u;
+        const uint32_t pw = (uint32_t)__shfl((int)e.w, lane0 + (pair & 1u ? 0 : 1), 64);
+        uint64_t ans, pos;
+        if (pair) {
+            ans = r0 + ((pair & 1u) ? 0u : 1u);
+            pos = ans >= sa_n ? a.next_pos : pw;
+        } else {
+            uint64_t lo = r0 + 2, hi = pt[2 * (K + 1)].z, pr = QUAD_NO_SA;
+            while (lo < hi) {
+                const uint64_t mid = (lo + hi) >> 1;
+                const uint4 f = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
+                const uint64_t pp = (uint64_t)f.z | ((uint64_t)(f.w & 0xFFu) << 32);
+                if (sector_ge<QW>((uint64_t)f.x | ((uint64_t)f.y << 32), pp, K64, a, q)) {
+                    hi = mid;
+                    pr = pp;
+                } else {
+                    lo = mid + 1;
+                }
+            }
+            ans = lo;
+            if (lo >= sa_n) pos = a.next_pos;
+            else if (pr != QUAD_NO_SA) pos = pr;
+            else pos = quad_entry_sa<false, 4>(a, lo);
+        }
+        if (sub == 0) {
+            a.out_pos[i] = pos;
+            if (a.out_probes) {  // the reference's cnt over [table[K], table[K+1])
+                uint32_t probes = 1;
+                for (uint64_t l2 = r0, h2 = pt[2 * (K + 1)].z; l2 < h2; probes++) {
+                    const uint64_t mid = (l2 + h2) >> 1;
+                    if (mid < ans) l2 = mid + 1;
+                    else h2 = mid;
+                }
+                a.out_probes[i] = probes;
+            }
+        }
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // ------------------------------------------------------------------ host dispatch
 template <int W>
 static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 block, hipStream_t st,
@@ -1336,6 +1403,7 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
 #define K_PREFIX(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 4>)
 #define K_PREFIX5(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 5>)
+#define K_PREFIX2(Q) (k_sa_prefix2<Q>)
 #define K_PREFIX16(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 16>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
@@ -1344,6 +1412,7 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
     } else if (algo == SAS_ALGO_PREFIX) {
         if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) }
         else if (a.prefix_w == 16 && !KO) { QW_CASE(K_PREFIX16) }
+        else if (a.prefix_w == 32 && !KO) { QW_CASE(K_PREFIX2) }
         else { QW_CASE(K_PREFIX) }
     } else {
         if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
@@ -1353,7 +1422,8 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
-    const uint64_t lanes = a.nq * (coop ? QUAD_G : 1);
+    const bool pair = algo == SAS_ALGO_PREFIX && x->prefix_w == 32;
+    const uint64_t lanes = a.nq * (coop ? QUAD_G : pair ? 2 : 1);
     uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;

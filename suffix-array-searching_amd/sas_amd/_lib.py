@@ -33,6 +33,7 @@ SAS_BUILD_QUAD_REL = 1 << 12
 SAS_BUILD_LLCP = 1 << 13
 SAS_BUILD_PREFIX = 1 << 14
 SAS_BUILD_PREFIX_INLINE = 1 << 15
+SAS_BUILD_PREFIX_INLINE2 = 1 << 21
 
 
 def SAS_BUILD_PREFIX_P(p: int) -> int:

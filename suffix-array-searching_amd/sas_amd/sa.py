@@ -48,12 +48,13 @@ def _as_u8(x):
 def _prefix_flags(prefix, quad, n: int, inline: bool = False) -> int:
     """prefix=None: build the prefix table (SAS_BUILD_PREFIX, p chosen by the library)
     whenever a quad tree is built and n < 2^32 - 1; False: never; an int: that p.
-    inline: 16-B entries inlining each range's first suffix (SAS_BUILD_PREFIX_INLINE)."""
+    inline: 1 (or True): 16-B entries inlining each range's first suffix
+    (SAS_BUILD_PREFIX_INLINE); 2: 32-B entries with its first two (_INLINE2)."""
     if prefix is None:
         prefix = bool(quad) and n < 0xFFFFFFFF
     if prefix is False:
         return 0
-    f = _lib.SAS_BUILD_PREFIX | (_lib.SAS_BUILD_PREFIX_INLINE if inline else 0)
+    f = _lib.SAS_BUILD_PREFIX | ({1: _lib.SAS_BUILD_PREFIX_INLINE, 2: _lib.SAS_BUILD_PREFIX_INLINE2}.get(int(inline), 0))
     if prefix is True:
         return f
     return f | _lib.SAS_BUILD_PREFIX_P(int(prefix))
@@ -94,7 +95,7 @@ class SaNaive:
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
               sa40: bool = False, quad: bool | str = True, llcp: bool = True,
-              prefix: bool | int | None = None, prefix_inline: bool = False) -> "SaNaive":
+              prefix: bool | int | None = None, prefix_inline: bool | int = False) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
@@ -104,7 +105,8 @@ class SaNaive:
         per suffix, implies the LCP array).  prefix: the prefix table for algo="prefix"
         (SAS_BUILD_PREFIX; None = whenever quad is built and n < 2^32 - 1, an int = its
         p chars); prefix_inline: 16-B entries that inline each range's first suffix
-        (SAS_BUILD_PREFIX_INLINE: fused quad leaves, u32 SA)."""
+        (True / 1: SAS_BUILD_PREFIX_INLINE) or 32-B ones with its first two (2:
+        SAS_BUILD_PREFIX_INLINE2); fused quad leaves, u32 SA."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)

@@ -213,16 +213,17 @@ def test_prefix_table(sas, sadef):
         qs += [t[n - k:] for k in (1, 2, 17, min(n, 40))] + [np.zeros(0, np.uint8), np.full(20, 3, np.uint8)]
         buf, qo, ql = pack(qs)
         expect = oracle_positions(t, sa, buf[:-64], qo, ql)
-        for p, quad, sa40, inl in ((0, True, False, False), (1, True, False, False), (2, "compact", False, False),
-                                   (7, True, False, False), (16, "compact", True, False), (11, "compact", False, False),
-                                   (0, True, False, True), (1, True, False, True), (7, True, False, True),
-                                   (13, True, False, True)):
+        for p, quad, sa40, inl in ((0, True, False, 0), (1, True, False, 0), (2, "compact", False, 0),
+                                   (7, True, False, 0), (16, "compact", True, 0), (11, "compact", False, 0),
+                                   (0, True, False, 1), (1, True, False, 1), (7, True, False, 1),
+                                   (13, True, False, 1), (0, True, False, 2), (1, True, False, 2),
+                                   (7, True, False, 2), (12, True, False, 2)):
             idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=quad, sa40=sa40,
                                     prefix=p if p else True, prefix_inline=inl)
             st = idx.stats()
             l4 = next(k for k in range(33) if 4 ** k >= n)  # ceil(log4 n)
             assert st["prefix_chars"] == (p if p else min(16, l4 + 1)), (name, p)
-            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * (16 if inl else 5 if sa40 else 4)
+            assert st["prefix_bytes"] == (4 ** st["prefix_chars"] + 1) * (16 * inl if inl else 5 if sa40 else 4)
             got, probes = idx.search_batch(buf, qo, ql, algo="prefix", probes=True)
             assert np.array_equal(got, expect), (name, p, quad, sa40, inl, np.nonzero(got != expect)[0][:5])
             # the reference's own binary_search over SA + text, started from the table's range
