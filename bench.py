@@ -598,7 +598,9 @@ def main():
                          "frac": achieved / HBM_PEAK_GBPS,
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad",
-                                    "inline": "k_sa_inline", "prefix": "k_sa_prefix"}.get(args.algo, "k_sa_binary"),
+                                    "inline": "k_sa_inline",
+                                    "prefix": "k_sa_prefix2" if pe == 32 else "k_sa_prefix"}.get(args.algo,
+                                                                                                 "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes,
                          # what bounds this path: random 128-B-line requests (PMC L2->fabric reads
