@@ -393,7 +393,7 @@ def main():
                     help="other algos timed beside the headline one")
     ap.add_argument("--prefix-chars", type=int, default=16,
                     help="p of the prefix table (the reference's main.rs default is -p 20 key bits)")
-    ap.add_argument("--prefix-table", default="inline2", choices=["inline2", "inline", "ranks"],
+    ap.add_argument("--prefix-table", default="inline2", choices=["inline2", "inline4", "inline", "ranks"],
                     help="inline2: 32-B entries holding each range's first two suffixes, read by lane pairs "
                          "(4^16 x 32 B = 128 GiB); inline: 16-B entries with the first suffix (64 GiB); "
                          "ranks: u32 ranks only (sas/sa_search.rs:59-75's table)")
@@ -447,7 +447,8 @@ def main():
         engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo)
     else:
         idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, prefix=args.prefix_chars,
-                                    prefix_inline={"ranks": 0, "inline": 1, "inline2": 2}[args.prefix_table])
+                                    prefix_inline={"ranks": 0, "inline": 1, "inline2": 2,
+                                                   "inline4": 4}[args.prefix_table])
     stats = idx.stats()
     off = rank_query_offsets(n, nq, m, rank)
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
@@ -533,7 +534,7 @@ def main():
         mean_probes = float("nan")
     layers_of = {"stree": stats["stree_layers"], "sector": stats["sector_layers"], "quad": stats["quad_layers"]}
     tail = max(0.0, mean_probes - layers_of[args.algo]) if args.algo in layers_of else mean_probes
-    pe = {16: 16, 32: 32}.get(stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1), 8)
+    pe = {16: 16, 32: 32, 64: 64}.get(stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1), 8)
     algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail, stats["sector_layers"],
                                    stats["quad_layers"], pe)
     achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
@@ -554,7 +555,7 @@ def main():
                        "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
                        "mean_probes": float(vp.double().mean().item()), "verified": vok}
 
-    pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d"}.get(pe, "")
+    pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d", 64: "q"}.get(pe, "")
     traffic, traffic_src, rdreq = load_traffic(args.algo + (pkey if args.algo == "prefix" else ""), n, nq, m,
                                                with_requests=True)
     cpu = None
@@ -599,7 +600,7 @@ def main():
                          "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad",
                                     "inline": "k_sa_inline",
-                                    "prefix": "k_sa_prefix2" if pe == 32 else "k_sa_prefix"}.get(args.algo,
+                                    "prefix": "k_sa_prefix2" if pe >= 32 else "k_sa_prefix"}.get(args.algo,
                                                                                                  "k_sa_binary"),
                          "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
                          "mean_probes": mean_probes,

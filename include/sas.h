@@ -85,6 +85,8 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_PREFIX_INLINE2 (1u << 21) /* the prefix table with 32-B entries: the first
                                         TWO suffixes of each key's range (ranks r, r + 1)
                                         inlined, read by a lane pair as one request       */
+#define SAS_BUILD_PREFIX_INLINE4 (1u << 22) /* 64-B entries: the first FOUR suffixes of each
+                                        range, read by a 4-lane group as one request      */
 #define SAS_BUILD_PREFIX_P(p) ((uint32_t)(p) << 16)  /* bits 16..20: prefix chars       */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry

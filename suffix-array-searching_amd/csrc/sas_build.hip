@@ -854,23 +854,30 @@ __device__ __forceinline__ uint64_t pt_key64(const uint4* leaves, uint64_t r) {
     return (uint64_t)k.x | ((uint64_t)k.y << 32);
 }
 
-template <int TW>
-__device__ __forceinline__ void pt_put(uint8_t* t, uint64_t x, uint64_t r, uint4 ev, uint4 ev2) {
-    if (TW == 32) {
-        reinterpret_cast<uint4*>(t)[2 * x] = ev;
-        reinterpret_cast<uint4*>(t)[2 * x + 1] = ev2;
-    } else if (TW == 16) {
-        reinterpret_cast<uint4*>(t)[x] = ev;
-    } else {
-        sa_put<TW>(t, x, r);
-    }
-}
 // inline entry for rank r (fused leaves: entry r = {key lo, key hi, SA lo32, SA hi8});
 // r = sa_n (nothing >= the key): key MAX, and the kernel answers next_pos
 __device__ __forceinline__ uint4 pt_inline_entry(const uint4* leaves, uint64_t sa_n, uint64_t r) {
     if (r >= sa_n) return make_uint4(~0u, ~0u, (uint32_t)sa_n, 0u);
     const uint4 e = leaves[r];
     return make_uint4(e.x, e.y, (uint32_t)r, e.z);
+}
+
+// Entry x <- rank r: TW = 4 / 5 bytes of rank, or TW / 16 inline slots (ranks r, r+1, ..)
+template <int TW>
+__device__ __forceinline__ void pt_fill_range(uint8_t* t, uint64_t lo, uint64_t hi, uint64_t step, uint64_t r,
+                                              const uint4* leaves, uint64_t sa_n) {
+    if (TW >= 16) {
+        constexpr int G = TW >= 16 ? TW / 16 : 1;
+        uint4 ev[G];
+#pragma unroll
+        for (int j = 0; j < G; j++) ev[j] = pt_inline_entry(leaves, sa_n, r + j);
+        for (uint64_t x = lo; x <= hi; x += step) {
+#pragma unroll
+            for (int j = 0; j < G; j++) reinterpret_cast<uint4*>(t)[G * x + j] = ev[j];
+        }
+    } else {
+        for (uint64_t x = lo; x <= hi; x += step) sa_put<TW>(t, x, r);
+    }
 }
 
 template <bool KO, int TW>
@@ -883,9 +890,7 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
         const uint64_t lo = r > 0 ? (pt_key64<KO>(leaves, r - 1) >> sh) + 1 : 0;
         if (lo > kr) continue;  // same key as rank r - 1
         if (kr - lo < PT_SMALL) {
-            const uint4 ev = TW >= 16 ? pt_inline_entry(leaves, sa_n, r) : make_uint4(0, 0, 0, 0);
-            const uint4 ev2 = TW == 32 ? pt_inline_entry(leaves, sa_n, r + 1) : make_uint4(0, 0, 0, 0);
-            for (uint64_t x = lo; x <= kr; x++) pt_put<TW>(table, x, r, ev, ev2);
+            pt_fill_range<TW>(table, lo, kr, 1, r, leaves, sa_n);
         } else {
             const unsigned long long slot = atomicAdd(nbig, 1ull);
             if (slot < big_cap) {
@@ -900,20 +905,15 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
 template <int TW>
 __global__ void k_pt_big(const uint64_t* __restrict__ big, const unsigned long long* __restrict__ nbig,
                          uint8_t* __restrict__ table, const uint4* __restrict__ leaves, uint64_t sa_n) {
-    for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x) {
-        const uint64_t lo = big[3 * b], hi = big[3 * b + 1];
-        const uint64_t r = big[3 * b + 2];
-        const uint4 ev = TW >= 16 ? pt_inline_entry(leaves, sa_n, r) : make_uint4(0, 0, 0, 0);
-        const uint4 ev2 = TW == 32 ? pt_inline_entry(leaves, sa_n, r + 1) : make_uint4(0, 0, 0, 0);
-        for (uint64_t x = lo + threadIdx.x; x <= hi; x += blockDim.x) pt_put<TW>(table, x, r, ev, ev2);
-    }
+    for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x)
+        pt_fill_range<TW>(table, big[3 * b] + threadIdx.x, big[3 * b + 1], blockDim.x, big[3 * b + 2], leaves, sa_n);
 }
 
 static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     const uint64_t sa_n = x->sa_n;
     if (!x->quad_leaves) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX needs SAS_BUILD_QUAD (keys and SA values of the leaves)");
     if (inl && (x->quad_compact || x->sa_w != 4))
-        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 need fused quad leaves and a u32 SA");
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 / _INLINE4 need fused quad leaves and a u32 SA");
     // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA, 16-B inline ones
     const uint32_t tw = inl ? 16 * inl : (x->sa_w == 5 ? 5 : 4);
     if (tw != 5 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
@@ -934,7 +934,9 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     uint8_t* tb = t.as<uint8_t>();
     uint64_t* bl = big.as<uint64_t>();
     unsigned long long* nb_d = nbig.as<unsigned long long>();
-    if (tw == 32)
+    if (tw == 64)
+        hipLaunchKernelGGL((k_pt_fill<false, 64>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+    else if (tw == 32)
         hipLaunchKernelGGL((k_pt_fill<false, 32>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
     else if (tw == 16)
         hipLaunchKernelGGL((k_pt_fill<false, 16>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
@@ -946,7 +948,8 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
         hipLaunchKernelGGL((k_pt_fill<false, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
     else
         hipLaunchKernelGGL((k_pt_fill<false, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
-    if (tw == 32) hipLaunchKernelGGL(k_pt_big<32>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
+    if (tw == 64) hipLaunchKernelGGL(k_pt_big<64>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
+    else if (tw == 32) hipLaunchKernelGGL(k_pt_big<32>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
     else if (tw == 16) hipLaunchKernelGGL(k_pt_big<16>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
     else if (tw == 5) hipLaunchKernelGGL(k_pt_big<5>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
     else hipLaunchKernelGGL(k_pt_big<4>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
@@ -1225,9 +1228,11 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     if (flags & SAS_BUILD_STREE) TRY(build_stree(x));
     if (flags & SAS_BUILD_SECTOR) TRY(build_sector(x));
     if (flags & (SAS_BUILD_QUAD | SAS_BUILD_QUAD_COMPACT)) TRY(build_quad(x, (flags & SAS_BUILD_QUAD_COMPACT) != 0, flags & (SAS_BUILD_QUAD_ABS | SAS_BUILD_QUAD_REL)));
-    if (flags & (SAS_BUILD_PREFIX | SAS_BUILD_PREFIX_INLINE | SAS_BUILD_PREFIX_INLINE2))
+    if (flags & (SAS_BUILD_PREFIX | SAS_BUILD_PREFIX_INLINE | SAS_BUILD_PREFIX_INLINE2 | SAS_BUILD_PREFIX_INLINE4))
         TRY(build_prefix(x, (flags >> 16) & 31,
-                         (flags & SAS_BUILD_PREFIX_INLINE2) ? 2u : (flags & SAS_BUILD_PREFIX_INLINE) ? 1u : 0u));
+                         (flags & SAS_BUILD_PREFIX_INLINE4)   ? 4u
+                         : (flags & SAS_BUILD_PREFIX_INLINE2) ? 2u
+                         : (flags & SAS_BUILD_PREFIX_INLINE)  ? 1u : 0u));
 
     // binary-search top in LDS
     {

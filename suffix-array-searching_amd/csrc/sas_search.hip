@@ -1279,40 +1279,41 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
-// SAS_BUILD_PREFIX_INLINE2: 32-B entries, the first two suffixes (ranks r, r + 1) of
-// the range of q's p-char key.  A lane pair reads the entry as one 32-B request, each
-// lane evaluates one suffix, and the pair ballot takes the first that is >= q; only if
-// both are < q does the search go on in [r + 2, table[K+1]).
-template <int QW>
+// SAS_BUILD_PREFIX_INLINE2 / _INLINE4: 16·G-byte entries, the first G suffixes (ranks
+// r .. r + G - 1) of the range of q's p-char key.  A G-lane group reads the entry as one
+// request (16 B per lane), each lane tests one suffix, and the group ballot takes the
+// first that is >= q; only if all are < q does the search go on in [r + G, table[K+1]).
+template <int QW, int G>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     uint32_t bad = 0;
     const uint32_t sh = 64 - 2 * a.prefix_chars;
     const uint64_t sa_n = a.sa_n;
-    const uint32_t sub = threadIdx.x & 1;
-    const int lane0 = (int)((threadIdx.x & 63) & ~1u);
+    const uint32_t sub = threadIdx.x & (G - 1);
+    const int lane0 = (int)((threadIdx.x & 63) & ~(uint32_t)(G - 1));
     const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
-    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / 2;
-    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 2; i < a.nq; i += stride) {
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; i < a.nq; i += stride) {
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
-        q.load(qb, m, &bad);  // both lanes: the same addresses, one request
+        q.load(qb, m, &bad);  // every lane of the group: the same addresses, one request
         const uint64_t K64 = q.w[0];
         const uint64_t K = K64 >> sh;
-        const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + 2 * K + sub) : pt[2 * K + sub];
+        const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + G * K + sub) : pt[G * K + sub];
         const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
         const uint64_t rank = r0 + sub;
         // rank sa_n stands for "past every suffix": it is the answer if reached
         const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), e.w, K64, a, q);
-        const uint32_t pair = (uint32_t)(__ballot(ok) >> lane0) & 3u;
-        const uint32_t pw = (uint32_t)__shfl((int)e.w, lane0 + (pair & 1u ? 0 : 1), 64);
+        const uint32_t grp = (uint32_t)(__ballot(ok) >> lane0) & ((1u << G) - 1u);
+        const uint32_t j = grp ? (uint32_t)__builtin_ctz(grp) : 0u;
+        const uint32_t pw = (uint32_t)__shfl((int)e.w, lane0 + (int)j, 64);
         uint64_t ans, pos;
-        if (pair) {
-            ans = r0 + ((pair & 1u) ? 0u : 1u);
+        if (grp) {
+            ans = r0 + j;
             pos = ans >= sa_n ? a.next_pos : pw;
         } else {
-            uint64_t lo = r0 + 2, hi = pt[2 * (K + 1)].z, pr = QUAD_NO_SA;
+            uint64_t lo = r0 + G, hi = pt[G * (K + 1)].z, pr = QUAD_NO_SA;
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
                 const uint4 f = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
@@ -1333,7 +1334,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
             a.out_pos[i] = pos;
             if (a.out_probes) {  // the reference's cnt over [table[K], table[K+1])
                 uint32_t probes = 1;
-                for (uint64_t l2 = r0, h2 = pt[2 * (K + 1)].z; l2 < h2; probes++) {
+                for (uint64_t l2 = r0, h2 = pt[G * (K + 1)].z; l2 < h2; probes++) {
                     const uint64_t mid = (l2 + h2) >> 1;
                     if (mid < ans) l2 = mid + 1;
                     else h2 = mid;
@@ -1403,7 +1404,8 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
 #define K_PREFIX(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 4>)
 #define K_PREFIX5(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 5>)
-#define K_PREFIX2(Q) (k_sa_prefix2<Q>)
+#define K_PREFIX2(Q) (k_sa_prefix2<Q, 2>)
+#define K_PREFIX4(Q) (k_sa_prefix2<Q, 4>)
 #define K_PREFIX16(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 16>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
@@ -1413,6 +1415,7 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
         if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) }
         else if (a.prefix_w == 16 && !KO) { QW_CASE(K_PREFIX16) }
         else if (a.prefix_w == 32 && !KO) { QW_CASE(K_PREFIX2) }
+        else if (a.prefix_w == 64 && !KO) { QW_CASE(K_PREFIX4) }
         else { QW_CASE(K_PREFIX) }
     } else {
         if (top) { QW_CASE(K_INLINE_TOP) } else { QW_CASE(K_INLINE) }
@@ -1422,8 +1425,9 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
-    const bool pair = algo == SAS_ALGO_PREFIX && x->prefix_w == 32;
-    const uint64_t lanes = a.nq * (coop ? QUAD_G : pair ? 2 : 1);
+    // inline prefix tables with G slots: G lanes per query
+    const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
+    const uint64_t lanes = a.nq * (coop ? QUAD_G : g);
     uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;

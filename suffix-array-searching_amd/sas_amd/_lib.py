@@ -34,6 +34,7 @@ SAS_BUILD_LLCP = 1 << 13
 SAS_BUILD_PREFIX = 1 << 14
 SAS_BUILD_PREFIX_INLINE = 1 << 15
 SAS_BUILD_PREFIX_INLINE2 = 1 << 21
+SAS_BUILD_PREFIX_INLINE4 = 1 << 22
 
 
 def SAS_BUILD_PREFIX_P(p: int) -> int:

@@ -49,12 +49,14 @@ def _prefix_flags(prefix, quad, n: int, inline: bool = False) -> int:
     """prefix=None: build the prefix table (SAS_BUILD_PREFIX, p chosen by the library)
     whenever a quad tree is built and n < 2^32 - 1; False: never; an int: that p.
     inline: 1 (or True): 16-B entries inlining each range's first suffix
-    (SAS_BUILD_PREFIX_INLINE); 2: 32-B entries with its first two (_INLINE2)."""
+    (SAS_BUILD_PREFIX_INLINE); 2 / 4: 32-B / 64-B entries with its first two / four
+    (_INLINE2 / _INLINE4)."""
     if prefix is None:
         prefix = bool(quad) and n < 0xFFFFFFFF
     if prefix is False:
         return 0
-    f = _lib.SAS_BUILD_PREFIX | ({1: _lib.SAS_BUILD_PREFIX_INLINE, 2: _lib.SAS_BUILD_PREFIX_INLINE2}.get(int(inline), 0))
+    f = _lib.SAS_BUILD_PREFIX | ({1: _lib.SAS_BUILD_PREFIX_INLINE, 2: _lib.SAS_BUILD_PREFIX_INLINE2,
+                                    4: _lib.SAS_BUILD_PREFIX_INLINE4}.get(int(inline), 0))
     if prefix is True:
         return f
     return f | _lib.SAS_BUILD_PREFIX_P(int(prefix))

@@ -217,7 +217,8 @@ def test_prefix_table(sas, sadef):
                                    (7, True, False, 0), (16, "compact", True, 0), (11, "compact", False, 0),
                                    (0, True, False, 1), (1, True, False, 1), (7, True, False, 1),
                                    (13, True, False, 1), (0, True, False, 2), (1, True, False, 2),
-                                   (7, True, False, 2), (12, True, False, 2)):
+                                   (7, True, False, 2), (12, True, False, 2), (0, True, False, 4),
+                                   (1, True, False, 4), (7, True, False, 4), (12, True, False, 4)):
             idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=quad, sa40=sa40,
                                     prefix=p if p else True, prefix_inline=inl)
             st = idx.stats()

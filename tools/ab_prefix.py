@@ -17,10 +17,10 @@ off, _, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=200, le
 src = torch.from_numpy(off.astype(np.int64)).cuda()
 qb = t[(src[:, None] + torch.arange(m, device="cuda")[None, :]).reshape(-1)].contiguous()
 out = torch.empty(nq, dtype=torch.int64, device="cuda")
-# AB_MODES: comma list of <p><r|i|d>: ranks-only (u32), inline (16-B) or two-suffix inline
-# (32-B) table entries
+# AB_MODES: comma list of <p><r|i|d|q>: ranks-only (u32), or inline entries holding the
+# first 1 / 2 / 4 suffixes of each range (16 / 32 / 64 B)
 for mode in os.environ.get("AB_MODES", "16r").split(","):
-    p, inl = int(mode[:-1]), {"r": 0, "i": 1, "d": 2}[mode[-1]]
+    p, inl = int(mode[:-1]), {"r": 0, "i": 1, "d": 2, "q": 4}[mode[-1]]
     idx = sas_amd.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=p,
                                 prefix_inline=inl)
     line = {"mode": mode, "p": idx.stats()["prefix_chars"]}
