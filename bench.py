@@ -201,6 +201,7 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         "STree15": lambda: sas_amd.STree15.new(vals),
         "PartitionedSTree16M_b16": lambda: sas_amd.PartitionedSTree16M.new(vals, 16),
         "PartitionedSTree16M_b20": lambda: sas_amd.PartitionedSTree16M.new(vals, 20),
+        "DirectMap": lambda: sas_amd.DirectMap.new(vals),
     }
     res, ref = {}, None
     for name, mk in layouts.items():

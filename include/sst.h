@@ -42,9 +42,15 @@ enum sst_layout {
     SST_EYTZINGER = 1, /* Eytzinger BFS layout, vals[0] = u32::MAX                  */
     SST_STREE16   = 2, /* STree<16,16>: B+ tree, 64-B nodes                          */
     SST_STREE15   = 3, /* STree<15,16>: 15 keys + copy of the next node's first key */
-    SST_PARTITIONED_MAP = 4 /* PartitionedSTree16M: prefix map on the top b key bits
+    SST_PARTITIONED_MAP = 4, /* PartitionedSTree16M: prefix map on the top b key bits
                                + S-tree (sst/partitioned_s_tree.rs:111-190,364-648);
                                b = SST_PART_BITS(b) in flags                         */
+    SST_DIRECT_MAP = 5 /* the prefix map taken to its limit: a direct-address table on
+                          the top b of the 31 key bits (b = SST_PART_BITS(b), 0 = ceil(
+                          log2 n) + 1, at most 30), 16-B entries {first index whose key
+                          is >= the bucket start, that key and the next two}: a lookup
+                          is one read unless three keys of its bucket are < q (then a
+                          binary search over the sorted keys of the bucket)          */
 };
 
 /* layout flags (STree::new_params arguments) */

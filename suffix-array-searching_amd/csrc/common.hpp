@@ -139,6 +139,7 @@ struct sst_index {
     uint32_t lds_nodes = 0;
     int num_cus = 256;
     uint32_t* prefix_map = nullptr;  // PartitionedSTree16M
+    uint4* direct = nullptr;         // SST_DIRECT_MAP entries [2^shift... see sst.hip]
     uint64_t pmap_words = 0;
     uint32_t shift = 0;
     uint32_t parts = 0;

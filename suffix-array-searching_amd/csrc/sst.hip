@@ -35,6 +35,7 @@ struct SstArgs {
     uint32_t shift;
     uint32_t parts;
     uint32_t leaf_nt;  // leaf layer read non-temporal (> SAS_NT_BYTES)
+    const uint4* direct;  // SST_DIRECT_MAP: [2^b + 1] entries {index, key, next key, next-but-one}
 };
 
 // count of keys < q under SIGNED compare (find_popcnt, sst/node.rs:93-109)
@@ -234,6 +235,78 @@ __global__ __launch_bounds__(SST_BLOCK) void k_sst_sorted(SstArgs a) {
         }
         a.out[i] = l < a.n ? a.nodes[l] : 0xFFFFFFFFu;
         if (a.rank) a.rank[i] = l;
+    }
+}
+
+// ------------------------------------------------------------------ SST_DIRECT_MAP
+// Bucket x = the keys whose top b of 31 bits are x (key >> (31 - b)); entry x holds the
+// first index r whose key is >= x's start and keys r, r+1, r+2 (MAX past the end), so
+// the answer to q is one of them unless three keys of q's bucket are < q.  A query
+// above i32::MAX takes the last entry (index n, MAX): no key is >= it.
+__device__ __forceinline__ uint4 direct_entry(const uint32_t* vals, uint64_t n, uint64_t r) {
+    auto v = [&](uint64_t i) -> uint32_t { return i < n ? vals[i] : 0xFFFFFFFFu; };
+    return make_uint4((uint32_t)r, v(r), v(r + 1), v(r + 2));
+}
+
+// index r starting a new bucket fills entries (bucket(r-1), bucket(r)] (r = n: up to 2^b);
+// gaps over 256 entries go to a list that whole workgroups fill
+__global__ void k_direct_fill(const uint32_t* __restrict__ vals, uint64_t n, uint32_t b, uint4* __restrict__ t,
+                              uint64_t* __restrict__ big, unsigned long long* __restrict__ nbig, uint64_t cap) {
+    const uint32_t sh = 31 - b;
+    for (uint64_t r = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; r <= n; r += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t kr = r < n ? (vals[r] >> sh) : (1ull << b);
+        const uint64_t lo = r > 0 ? (vals[r - 1] >> sh) + 1 : 0;
+        if (lo > kr) continue;
+        if (kr - lo < 256) {
+            const uint4 e = direct_entry(vals, n, r);
+            for (uint64_t x = lo; x <= kr; x++) t[x] = e;
+        } else {
+            const unsigned long long s = atomicAdd(nbig, 1ull);
+            if (s < cap) {
+                big[3 * s] = lo;
+                big[3 * s + 1] = kr;
+                big[3 * s + 2] = r;
+            }
+        }
+    }
+}
+
+__global__ void k_direct_big(const uint32_t* __restrict__ vals, uint64_t n, const uint64_t* __restrict__ big,
+                             const unsigned long long* __restrict__ nbig, uint4* __restrict__ t) {
+    for (uint64_t g = blockIdx.x; g < *nbig; g += gridDim.x) {
+        const uint4 e = direct_entry(vals, n, big[3 * g + 2]);
+        for (uint64_t x = big[3 * g] + threadIdx.x; x <= big[3 * g + 1]; x += blockDim.x) t[x] = e;
+    }
+}
+
+// one lane per query: one 16-B read, the first of its three keys >= q; else a binary
+// search over the bucket's remaining keys [r + 3, entry(x + 1).index)
+__global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_direct(SstArgs a) {
+    const uint32_t sh = 31 - a.shift;  // a.shift holds b here
+    const uint64_t top = 1ull << a.shift;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint32_t q = a.qs[i];
+        uint64_t x = q >> sh;
+        x = x < top ? x : top;
+        const uint4 e = nt_load4(a.direct + x);
+        uint64_t r;
+        uint32_t v;
+        if (e.y >= q) { r = e.x; v = e.y; }
+        else if (e.z >= q) { r = (uint64_t)e.x + 1; v = e.z; }
+        else if (e.w >= q) { r = (uint64_t)e.x + 2; v = e.w; }
+        else {
+            uint64_t l = (uint64_t)e.x + 3, h = a.direct[x + 1].x;
+            while (l < h) {
+                const uint64_t m = (l + h) >> 1;
+                if (a.nodes[m] < q) l = m + 1;
+                else h = m;
+            }
+            r = l;
+            v = l < a.n ? a.nodes[l] : 0xFFFFFFFFu;
+        }
+        a.out[i] = v;
+        if (a.rank) a.rank[i] = r < a.n ? r : a.n;
     }
 }
 
@@ -458,6 +531,24 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
         case SST_PARTITIONED_MAP:
             rc = build_pmap_host(sorted_vals, n, SST_PART_BITS_OF(flags), host, pmap, x);
             break;
+        case SST_DIRECT_MAP:
+            host.assign(sorted_vals, sorted_vals + n);  // the sorted keys (the fallback search)
+            if (sorted_vals[n - 1] > SST_MAX) {  // buckets cover the 31-bit key space
+                rc = EINVAL;
+                sas_set_error(EINVAL, "sst_build: SST_DIRECT_MAP keys must be <= i32::MAX");
+                break;
+            }
+            {
+                uint32_t b = SST_PART_BITS_OF(flags);
+                if (b == 0) {
+                    b = 1;
+                    while ((1ull << b) < n && b < 30) b++;
+                    b = b + 1 < 30 ? b + 1 : 30;  // ceil(log2 n) + 1
+                }
+                if (b > 30) { rc = EINVAL; sas_set_error(EINVAL, "sst_build: SST_DIRECT_MAP needs b <= 30"); }
+                x->shift = b;
+            }
+            break;
         default:
             rc = EINVAL;
             sas_set_error(EINVAL, "sst_build: unknown layout");
@@ -471,6 +562,31 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
     if (e != hipSuccess) { delete x; SAS_FAIL(ENOMEM, "sst_build: hipMalloc failed"); }
     e = hipMemcpy(x->nodes, host.data(), host.size() * 4, hipMemcpyHostToDevice);
     if (e != hipSuccess) { (void)hipFree(x->nodes); delete x; SAS_FAIL(EIO, "sst_build: upload failed"); }
+    if (layout == SST_DIRECT_MAP) {
+        const uint32_t b = x->shift;
+        const uint64_t entries = (1ull << b) + 1, cap = entries / 257 + 2;
+        void *big = nullptr, *nb = nullptr;
+        e = hipMalloc(&x->direct, entries * 16);
+        if (e == hipSuccess) e = hipMalloc(&big, cap * 24);
+        if (e == hipSuccess) e = hipMalloc(&nb, 8);
+        if (e == hipSuccess) e = hipMemset(nb, 0, 8);
+        if (e == hipSuccess) {
+            const unsigned g = (unsigned)((n + 1 + 255) / 256 < 262144 ? (n + 1 + 255) / 256 : 262144);
+            hipLaunchKernelGGL(k_direct_fill, dim3(g), dim3(256), 0, 0, x->nodes, n, b, x->direct,
+                               static_cast<uint64_t*>(big), static_cast<unsigned long long*>(nb), cap);
+            hipLaunchKernelGGL(k_direct_big, dim3(4096), dim3(256), 0, 0, x->nodes, n, static_cast<uint64_t*>(big),
+                               static_cast<unsigned long long*>(nb), x->direct);
+            e = hipDeviceSynchronize();
+        }
+        if (big) (void)hipFree(big);
+        if (nb) (void)hipFree(nb);
+        if (e != hipSuccess) {
+            if (x->direct) (void)hipFree(x->direct);
+            (void)hipFree(x->nodes);
+            delete x;
+            SAS_FAIL(ENOMEM, "sst_build: direct map build failed");
+        }
+    }
     if (!pmap.empty()) {
         x->pmap_words = pmap.size();
         e = hipMalloc(&x->prefix_map, pmap.size() * 4);
@@ -485,6 +601,7 @@ extern "C" int sst_free(sst_index* x) {
     if (x) {
         if (x->nodes) (void)hipFree(x->nodes);
         if (x->prefix_map) (void)hipFree(x->prefix_map);
+        if (x->direct) (void)hipFree(x->direct);
         delete x;
     }
     return 0;
@@ -493,7 +610,7 @@ extern "C" int sst_free(sst_index* x) {
 extern "C" uint64_t sst_size(const sst_index* x) {
     // SearchIndex::size(): bytes of the node / value array (sst/lib.rs:35-36), plus
     // the prefix map for PartitionedSTree16M (sst/partitioned_s_tree.rs:100-102)
-    return x ? (x->words + x->pmap_words) * 4 : 0;
+    return x ? (x->words + x->pmap_words) * 4 + (x->direct ? ((1ull << x->shift) + 1) * 16 : 0) : 0;
 }
 
 extern "C" uint64_t sst_layers(const sst_index* x) {
@@ -502,6 +619,7 @@ extern "C" uint64_t sst_layers(const sst_index* x) {
         case SST_SORTED: return 64 - __builtin_clzll(x->n);              // ilog2(len)+1 (binary_search.rs:29-31)
         case SST_EYTZINGER: return 64 - __builtin_clzll(x->n + 1);       // ilog2(len)+1 (eytzinger.rs:72-74)
         case SST_PARTITIONED_MAP: return x->height + 1;                  // offsets.len() + MAP (partitioned_s_tree.rs:104-106)
+        case SST_DIRECT_MAP: return 1;                                   // the table (the sorted keys are a fallback)
         default: return x->height;                                       // offsets.len() (s_tree.rs:52-54)
     }
 }
@@ -522,6 +640,8 @@ static int sst_launch(const sst_index* x, SstArgs& a, uint32_t flags, hipStream_
         hipLaunchKernelGGL(k_sst_sorted, grid, block, 0, st, a);
     } else if (x->layout == SST_EYTZINGER) {
         hipLaunchKernelGGL(k_sst_eytzinger, grid, block, 0, st, a);
+    } else if (x->layout == SST_DIRECT_MAP) {
+        hipLaunchKernelGGL(k_sst_direct, grid, block, 0, st, a);
     } else {
         // S-tree layouts: the 4-lane cooperative kernels (one request per node)
         uint64_t b4 = (a.nq * QUAD_G + SST_BLOCK - 1) / SST_BLOCK;
@@ -552,6 +672,7 @@ static void sst_fill(const sst_index* x, SstArgs& a) {
     a.shift = x->shift;
     a.parts = x->parts;
     a.leaf_nt = x->height > 0 && x->layer_nodes[x->height - 1] * 64 > SAS_NT_BYTES;
+    a.direct = x->direct;
 }
 
 extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, uint32_t* out_val, uint64_t* out_rank,

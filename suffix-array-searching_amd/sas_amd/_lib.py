@@ -44,7 +44,7 @@ def SAS_BUILD_PREFIX_P(p: int) -> int:
 SAS_MULTI_REPLICATE, SAS_MULTI_SHARD = 0, 1
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, "llcp": 6, "prefix": 7}
 
-SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP = 0, 1, 2, 3, 4
+SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP, SST_DIRECT_MAP = 0, 1, 2, 3, 4, 5
 SST_LEFT_MAX = 1 << 0
 SST_REVERSE = 1 << 1
 SST_FULL = 1 << 2

@@ -126,3 +126,15 @@ class PartitionedSTree16M(_Index):
     @classmethod
     def new(cls, vals, b: int = 16):
         return cls._build(vals, cls.LAYOUT, (b & 0xFF) << 16)
+
+
+class DirectMap(_Index):
+    """SST_DIRECT_MAP: the prefix map of PartitionedSTree16M taken to its limit, a
+    direct-address table on the top b of the 31 key bits whose 16-B entries inline
+    the first three keys at or after each bucket start (b = 0: ceil(log2 n) + 1).
+    Same answers as every other layout: the first key >= q and its index."""
+    LAYOUT = _lib.SST_DIRECT_MAP
+
+    @classmethod
+    def new(cls, vals, b: int = 0):
+        return cls._build(vals, cls.LAYOUT, (b & 0xFF) << 16)

@@ -76,6 +76,29 @@ def test_differential(sas, size):
         assert np.array_equal(v, ref), (size, b)
         assert np.array_equal(vals[np.minimum(r, len(vals) - 1)], ref)
         assert pm.layers() >= 1 and pm.size() >= len(vals) * 4
+    # SST_DIRECT_MAP: same values and ranks as SortedVec, for the automatic and forced b
+    for b in (0, 1, 5, 12, 24):
+        dm = sas.DirectMap.new(vals, b)
+        v, r = dm.query(qs, want_rank=True)
+        assert np.array_equal(v, ref) and np.array_equal(r, ref_rank), (size, b)
+
+
+def test_direct_map_edges(sas):
+    """SST_DIRECT_MAP on clustered keys (huge empty bucket runs: the gap list), runs of
+    equal keys longer than the three inlined ones (the fallback search), queries above
+    every key and above i32::MAX, against SortedVec."""
+    rng = np.random.default_rng(9)
+    vals = np.sort(np.concatenate([np.full(50, 7), np.full(9, 1 << 30), rng.integers(0, 1000, 300),
+                                   rng.integers((1 << 31) - 5000, (1 << 31) - 1, 300)]).astype(np.uint32))
+    qs = np.concatenate([rng.integers(0, 1 << 32, 3000, dtype=np.uint64),
+                         np.array([0, 6, 7, 8, 999, 1000, (1 << 30) - 1, 1 << 30, (1 << 30) + 1,
+                                   (1 << 31) - 1, 1 << 31, (1 << 32) - 1], np.uint64)]).astype(np.uint32)
+    ref, ref_rank = O.SortedVec(vals).query(qs, want_rank=True)
+    for b in (0, 2, 16, 30):
+        v, r = sas.DirectMap.new(vals, b).query(qs, want_rank=True)
+        assert np.array_equal(v, ref) and np.array_equal(r, ref_rank), b
+    with pytest.raises(sas.SasError):
+        sas.DirectMap.new([1, 2, 0x80000000])
 
 
 def test_no_lds_and_device_path(sas):
