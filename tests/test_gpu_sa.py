@@ -867,12 +867,13 @@ def test_route_pack(sas):
 
 def test_full_size_algorithms_agree_and_are_lower_bounds(sas):
     """BASELINE size (n = 2^30, 10^6 mixed queries: positive len 32 as in the bench,
-    random negatives, other lengths): all algorithms return identical positions; a
+    random negatives, other lengths), index as the bench builds it (p = 16 two-suffix
+    inline prefix table): all algorithms return identical positions; a
     sample is proven exact on the host text (SA[lo-1] < q <= SA[lo], pos = SA[lo])."""
     import torch
     n = 1 << 30
     t = sas.random_string(n, seed=31415, device="cuda")
-    idx = sas.SaNaive.build(t)
+    idx = sas.SaNaive.build(t, prefix=16, prefix_inline=2)  # the bench's two-suffix inline table
     ht = t.cpu().numpy()
     rng = np.random.default_rng(30)
     offs = rng.integers(0, n - 200, 700_000)
@@ -888,6 +889,10 @@ def test_full_size_algorithms_agree_and_are_lower_bounds(sas):
         res[algo] = idx.search_batch(dbuf, doff, dlen, algo=algo).cpu().numpy()
     for algo in ALGOS:
         assert np.array_equal(res[algo], res["plain"]), algo
+    from sas_amd import _lib
+    for base in ("plain", "lcp"):  # the reference's binary_search from the table's range
+        got = idx.search_batch(dbuf, doff, dlen, algo=base, flags=_lib.SAS_PREFIX_RANGE).cpu().numpy()
+        assert np.array_equal(got, res["plain"]), base
     lo, hi = idx.search_range(dbuf, doff, dlen)
     lo = lo.cpu().numpy()
     for k in rng.choice(len(qs), 3000, replace=False):
