@@ -1176,6 +1176,12 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
 #ifndef SAS_PREFIX_NT
 #define SAS_PREFIX_NT 1  // non-temporal table / entry loads (-3%, tools/ab_prefix.py)
 #endif
+#ifndef SAS_PREFIX_SPLITQ
+#define SAS_PREFIX_SPLITQ 1  // lane pairs split a 32-B query load (k_sa_prefix2; -4%)
+#endif
+#ifndef SAS_PREFIX_NT_OUT
+#define SAS_PREFIX_NT_OUT 0  // non-temporal position stores (k_sa_prefix2)
+#endif
 #ifndef SAS_PREFIX_QWMAX
 #define SAS_PREFIX_QWMAX 8  // register-resident query words (later ones repacked from the bytes)
 #endif
@@ -1297,7 +1303,20 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
-        q.load(qb, m, &bad);  // every lane of the group: the same addresses, one request
+        if (SAS_PREFIX_SPLITQ && G == 2 && QW == 1 && a.qoff == nullptr && m == 32 && (((uintptr_t)qb) & 15) == 0) {
+            // the pair splits the 32-B query: lane j packs bytes 16j..16j+15 to 32 bits,
+            // then the halves are swapped within the pair (DPP quad_perm [1,0,3,2])
+            const uint4 v = SAS_QUAD_NT_IO ? nt_load4(reinterpret_cast<const uint4*>(qb) + sub)
+                                           : reinterpret_cast<const uint4*>(qb)[sub];
+            bad |= (v.x | v.y | v.z | v.w) & 0xFCFCFCFCu;
+            const uint32_t part = (pack4(v.x) << 24) | (pack4(v.y) << 16) | (pack4(v.z) << 8) | pack4(v.w);
+            const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)part, 0xB1, 0xF, 0xF, false);
+            q.bytes = qb;
+            q.m = m;
+            q.w[0] = sub ? (((uint64_t)other << 32) | part) : (((uint64_t)part << 32) | other);
+        } else {
+            q.load(qb, m, &bad);  // every lane of the group: the same addresses, one request
+        }
         const uint64_t K64 = q.w[0];
         const uint64_t K = K64 >> sh;
         const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + G * K + sub) : pt[G * K + sub];
@@ -1331,7 +1350,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
             else pos = quad_entry_sa<false, 4>(a, lo);
         }
         if (sub == 0) {
-            a.out_pos[i] = pos;
+            if (SAS_PREFIX_NT_OUT) __builtin_nontemporal_store(pos, a.out_pos + i);
+            else a.out_pos[i] = pos;
             if (a.out_probes) {  // the reference's cnt over [table[K], table[K+1])
                 uint32_t probes = 1;
                 for (uint64_t l2 = r0, h2 = pt[G * (K + 1)].z; l2 < h2; probes++) {
