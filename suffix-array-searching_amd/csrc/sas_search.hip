@@ -1179,6 +1179,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
 #ifndef SAS_PREFIX_SPLITQ
 #define SAS_PREFIX_SPLITQ 1  // lane pairs split a 32-B query load (k_sa_prefix2; -4%)
 #endif
+#ifndef SAS_PREFIX_QPREFETCH
+#define SAS_PREFIX_QPREFETCH 1  // load the next query while this one's entry is in flight (-1%)
+#endif
 #ifndef SAS_PREFIX_NT_OUT
 #define SAS_PREFIX_NT_OUT 0  // non-temporal position stores (k_sa_prefix2)
 #endif
@@ -1298,16 +1301,31 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     const int lane0 = (int)((threadIdx.x & 63) & ~(uint32_t)(G - 1));
     const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / G;
-    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; i < a.nq; i += stride) {
+    // fixed 32-char queries at 16-B aligned addresses: the pair splits each query load
+    const bool split = SAS_PREFIX_SPLITQ && G == 2 && QW == 1 && a.qoff == nullptr && a.m_fixed == 32 &&
+                       (((uintptr_t)a.qbytes) & 15) == 0;
+    auto qload = [&](uint64_t k) -> uint4 {
+        const uint4* p = reinterpret_cast<const uint4*>(a.qbytes + k * 32) + sub;
+        return SAS_QUAD_NT_IO ? nt_load4(p) : *p;
+    };
+    const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
+    uint4 vnext = make_uint4(0, 0, 0, 0);
+    if (SAS_PREFIX_QPREFETCH && split && i0 < a.nq) vnext = qload(i0);
+    for (uint64_t i = i0; i < a.nq; i += stride) {
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
-        if (SAS_PREFIX_SPLITQ && G == 2 && QW == 1 && a.qoff == nullptr && m == 32 && (((uintptr_t)qb) & 15) == 0) {
+        if (split) {
             // the pair splits the 32-B query: lane j packs bytes 16j..16j+15 to 32 bits,
             // then the halves are swapped within the pair (DPP quad_perm [1,0,3,2])
-            const uint4 v = SAS_QUAD_NT_IO ? nt_load4(reinterpret_cast<const uint4*>(qb) + sub)
-                                           : reinterpret_cast<const uint4*>(qb)[sub];
+            uint4 v;
+            if (SAS_PREFIX_QPREFETCH) {  // the next query's load overlaps this lookup
+                v = vnext;
+                if (i + stride < a.nq) vnext = qload(i + stride);
+            } else {
+                v = qload(i);
+            }
             bad |= (v.x | v.y | v.z | v.w) & 0xFCFCFCFCu;
             const uint32_t part = (pack4(v.x) << 24) | (pack4(v.y) << 16) | (pack4(v.z) << 8) | pack4(v.w);
             const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)part, 0xB1, 0xF, 0xF, false);
