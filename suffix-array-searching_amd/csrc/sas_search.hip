@@ -1575,9 +1575,17 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
     fill_args(x, a);
     a.nq = nq;
     a.m_fixed = m_fixed;
+    // invalid-code flag: a per-call word when it is read back, so that concurrent calls
+    // on other streams (allowed: the index is immutable) never see each other's flags;
+    // otherwise the index's write-only sink
     a.bad = x->scratch;
     bool check_bad = !dev || (flags & SAS_VALIDATE);
-    if (check_bad) HIP_TRY(hipMemsetAsync(x->scratch, 0, 4, st));
+    DeviceBuf bflag;
+    if (check_bad) {
+        HIP_TRY(hipMalloc(&bflag.p, 4));
+        HIP_TRY(hipMemsetAsync(bflag.p, 0, 4, st));
+        a.bad = static_cast<uint32_t*>(bflag.p);
+    }
 
     int qw = 4;
     DeviceBuf bqb, bqoff, bqlen, bout, bprobes;
@@ -1627,7 +1635,7 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
     if (check_bad || !dev) {
         HIP_TRY(hipStreamSynchronize(st));
         uint32_t hbad = 0;
-        HIP_TRY(hipMemcpy(&hbad, x->scratch, 4, hipMemcpyDeviceToHost));
+        if (check_bad) HIP_TRY(hipMemcpy(&hbad, a.bad, 4, hipMemcpyDeviceToHost));
         if (!dev) {
             HIP_TRY(hipMemcpy(out_pos, a.out_pos, nq * 8, hipMemcpyDeviceToHost));
             if (out_probes) HIP_TRY(hipMemcpy(out_probes, a.out_probes, nq * 4, hipMemcpyDeviceToHost));
@@ -1913,9 +1921,14 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
     SearchArgs a{};
     fill_args(x, a);
     a.nq = nq;
-    a.bad = x->scratch;
+    a.bad = x->scratch;  // per-call flag when read back (see search_impl)
     bool check_bad = !dev || (flags & SAS_VALIDATE);
-    if (check_bad) HIP_TRY(hipMemsetAsync(x->scratch, 0, 4, st));
+    DeviceBuf bflag;
+    if (check_bad) {
+        HIP_TRY(hipMalloc(&bflag.p, 4));
+        HIP_TRY(hipMemsetAsync(bflag.p, 0, 4, st));
+        a.bad = static_cast<uint32_t*>(bflag.p);
+    }
     DeviceBuf bqb, bqoff, bqlen, blo, bhi;
     uint64_t* dhi = out_hi;
     int qw = 4;
@@ -1968,7 +1981,7 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
     if (check_bad || !dev) {
         HIP_TRY(hipStreamSynchronize(st));
         uint32_t hbad = 0;
-        HIP_TRY(hipMemcpy(&hbad, x->scratch, 4, hipMemcpyDeviceToHost));
+        if (check_bad) HIP_TRY(hipMemcpy(&hbad, a.bad, 4, hipMemcpyDeviceToHost));
         if (!dev) {
             HIP_TRY(hipMemcpy(out_lo, a.out_pos, nq * 8, hipMemcpyDeviceToHost));
             HIP_TRY(hipMemcpy(out_hi, dhi, nq * 8, hipMemcpyDeviceToHost));

@@ -288,6 +288,40 @@ def test_extract_substrings(sas):
         assert np.array_equal(got[o_:o_ + l_], tp[p_:p_ + l_]), (p_, l_)
 
 
+def test_concurrent_calls_keep_their_error_flags(sas):
+    """The index is immutable and may be searched from several threads at once
+    (SearchIndex: Sync, sst/lib.rs:30): a call with invalid query codes
+    fails, a concurrent valid call on the same index does not, and its answers hold."""
+    from concurrent.futures import ThreadPoolExecutor
+    n = 50_000
+    t = sas.random_string(n, seed=41)
+    idx = sas.SaNaive.build(t, stree=False, sector=False, llcp=False)
+    sa = O.build_sa(t)
+    rng = np.random.default_rng(6)
+    qs = [t[o:o + 32] for o in rng.integers(0, n - 40, 4000)]
+    buf, off, lens = pack(qs)
+    expect = oracle_positions(t, sa, buf[:-64], off, lens)
+    bad = buf.copy()
+    bad[5] = 7
+
+    def good_call(_):
+        return idx.search_batch(buf, off, lens, algo="prefix")
+
+    def bad_call(_):
+        try:
+            idx.search_batch(bad, off, lens, algo="prefix")
+        except sas.SasError:
+            return True
+        return False
+
+    with ThreadPoolExecutor(8) as ex:
+        goods = [ex.submit(good_call, k) for k in range(24)]
+        bads = [ex.submit(bad_call, k) for k in range(24)]
+        for f in goods:
+            assert np.array_equal(f.result(), expect)
+        assert all(f.result() for f in bads)
+
+
 def test_invalid_codes_rejected(sas):
     with pytest.raises(sas.SasError):
         sas.SaNaive.build(np.array([0, 1, 4, 2], np.uint8))
