@@ -11,7 +11,7 @@ import numpy as np
 
 from . import _lib
 from ._lib import check, lib
-from .sa import _as_u8, _ptr, _quad_flags
+from .sa import _as_u8, _prefix_flags, _ptr, _quad_flags
 
 MODES = {"replicate": _lib.SAS_MULTI_REPLICATE, "shard": _lib.SAS_MULTI_SHARD}
 
@@ -25,12 +25,14 @@ class SaMulti:
 
     @classmethod
     def build(cls, t, devices, mode: str = "replicate", lcp: bool = False, stree: bool = False,
-              sector: bool = False, quad: bool | str = True, flags: int = 0) -> "SaMulti":
-        """t: host text (codes 0..3).  devices: device ordinals, repeats allowed."""
+              sector: bool = False, quad: bool | str = True, flags: int = 0,
+              prefix: bool | int | None = None) -> "SaMulti":
+        """t: host text (codes 0..3).  devices: device ordinals, repeats allowed.
+        prefix: the prefix table for algo="prefix" (as SaNaive.build)."""
         t = np.ascontiguousarray(_as_u8(t))
         dv = np.ascontiguousarray(devices, np.int32)
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
-        flags |= (_lib.SAS_BUILD_SECTOR if sector else 0) | _quad_flags(quad)
+        flags |= (_lib.SAS_BUILD_SECTOR if sector else 0) | _quad_flags(quad) | _prefix_flags(prefix, quad, len(t))
         h = C.c_void_p()
         check(lib().sas_build_multi(_ptr(t), len(t), _ptr(dv), len(dv), MODES[mode], flags, C.byref(h)))
         return cls(h, len(t), dv.tolist(), mode)

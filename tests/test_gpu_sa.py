@@ -965,7 +965,7 @@ def test_multi_device_handle(sas, devices):
                 st = [M.stats(g) for g in range(len(devices))]
                 assert sum(s["sa_entries"] for s in st) == n
                 assert [s["rank_lo"] for s in st] == sorted(s["rank_lo"] for s in st)
-            for algo in ("quad", "plain"):
+            for algo in ("quad", "plain", "prefix"):
                 got = M.search_batch(buf, off, lens, algo=algo)
                 assert np.array_equal(got, expect), (mode, algo, len(devices), n)
             M.free()
