@@ -16,6 +16,11 @@
 //          below the cached top levels a probe reads one 16-B {SA, Llcp, Rlcp,
 //          16 chars after each} entry; it decides from the lcps alone unless they
 //          tie, and a tie compares the inlined chars before any text.
+//   SECTOR / QUAD  B-trees over the fused (32-char key, SA) leaf entries.
+//   PREFIX the reference's prefix table made live (sas/sa_search.rs:59-95): the
+//          rank range of q's first p chars, then binary_search over it on the
+//          fused leaf entries; with inline tables one G-lane group reads the first
+//          G suffixes of the range as one request (the headline, k_sa_prefix2).
 //   STREE  descend an STree<16,16> over the 16-char keys of the SA (top layers in
 //          LDS), giving the key range [r0, r1) of suffixes whose padded 16-char
 //          prefix equals the query's; the lower bound lies in [r0, r1] and is
