@@ -390,7 +390,7 @@ def main():
     ap.add_argument("--m", type=int, default=32, help="query length")
     ap.add_argument("--algo", default=None, choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
                                                          "prefix"])
-    ap.add_argument("--variants", default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,prefix",
+    ap.add_argument("--variants", default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,prefix,prefix_packed",
                     help="other algos timed beside the headline one")
     ap.add_argument("--prefix-chars", type=int, default=16,
                     help="p of the prefix table (the reference's main.rs default is -p 20 key bits)")
@@ -478,12 +478,19 @@ def main():
         # reference's binary_search with its prefix table live (sas/sa_search.rs:86-112)
         return (name[:-6], sas_amd._lib.SAS_PREFIX_RANGE) if name.endswith("_range") else (name, 0)
 
+    packed = {}
+
     def run_algo(algo, steps, warmup):
         base, fl = algo_flags(algo)
+        if algo == "prefix_packed" and "w" not in packed:
+            # queries handed over 2-bit packed (sas_pack_queries, untimed: the caller's format)
+            packed["w"] = sas_amd.SaNaive.pack_queries(qbytes, m)
 
         def step():
             if args.mode == "shard":
                 out.copy_(engine.search_fixed(qbytes, m))
+            elif algo == "prefix_packed":
+                idx.search_packed(packed["w"], m, out=out)
             else:
                 idx.search_fixed(qbytes, m, algo=base, out=out, flags=fl)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -544,14 +551,18 @@ def main():
     for v in [x for x in args.variants.split(",") if x and x != args.algo and args.mode == "replicated"]:
         vel, vk, vok = run_algo(v, max(3, args.steps // 4), 1)
         vbase, vfl = algo_flags(v)
-        _, vp = idx.search_fixed(qbytes, m, algo=vbase, probes=True, flags=vfl)
+        if v == "prefix_packed":
+            vbase = "prefix"
+            _, vp = idx.search_packed(packed["w"], m, probes=True)
+        else:
+            _, vp = idx.search_fixed(qbytes, m, algo=vbase, probes=True, flags=vfl)
         vmean = float(vp.double().mean().item())
         vtail = max(0.0, vmean - layers_of[v]) if v in layers_of else vmean
         if vfl:  # the table entry + the reference's per-iteration SA word and text window
             vb = pe + max(0.0, vmean - 1) * (4 + m) + m + 8
         else:
-            vb = algorithmic_bytes(v, n, m, stats["stree_layers"], vtail, stats["sector_layers"], stats["quad_layers"],
-                                   pe)
+            vb = algorithmic_bytes(vbase, n, 8 if v == "prefix_packed" else m, stats["stree_layers"], vtail,
+                                   stats["sector_layers"], stats["quad_layers"], pe)
         variants[v] = {"lookups_per_s": ws * nq * max(3, args.steps // 4) / vel, "kernel_ms": vk,
                        "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
                        "mean_probes": float(vp.double().mean().item()), "verified": vok}

@@ -220,6 +220,16 @@ int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t 
 int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t count, uint64_t* dst, uint32_t flags);
 int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags);
 
+/* 2-bit packed fixed-length queries, m <= 32: word i holds query i's chars, the first in
+ * bits 63..62, zero padded (how the reference packs DNA for its interpolation search,
+ * string_value<K>, sas/util.rs:76-117).  A lookup then reads 8 B of query instead of m.
+ * sas_pack_queries: device pointers only (SAS_DEVICE_PTRS); EINVAL on codes > 3.
+ * sas_search_packed: SAS_ALGO_PREFIX only; host or device pointers per flags. */
+int sas_pack_queries(const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_words, void* stream,
+                     uint32_t flags);
+int sas_search_packed(const sas_index* index, const uint64_t* qwords, uint32_t m, uint64_t nq, int algo,
+                      uint64_t* out_pos, uint32_t* out_probes, void* stream, uint32_t flags);
+
 /* Substrings of the indexed text as byte codes 0..3: out[out_off[i] .. out_off[i] + len[i])
  * = text[pos[i] .. pos[i] + len[i]) (0 past the text end), from the index's packed copy,
  * so a caller can drop its own byte copy of a large text after sas_build.  Device

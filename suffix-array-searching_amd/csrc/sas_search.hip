@@ -76,6 +76,7 @@ struct SearchArgs {
     uint32_t quad_lds_layers;
     uint32_t quad_lds_nodes;
     const uint8_t* qbytes;
+    const uint64_t* qwords;  // sas_search_packed: 2-bit packed fixed-length queries (PREFIX)
     const uint64_t* qoff;
     const uint32_t* qlen;
     uint32_t m_fixed;
@@ -1207,7 +1208,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
-        q.load(qb, m, &bad);
+        if (a.qwords) {  // packed fixed-length query: the key word itself
+            q.bytes = nullptr;
+            q.m = m;
+            q.w[0] = a.qwords[i];
+        } else {
+            q.load(qb, m, &bad);
+        }
         const uint64_t K64 = q.w[0];
         const uint64_t K = K64 >> sh;
         uint64_t lo, hi = 0, pos = QUAD_NO_SA;
@@ -1307,7 +1314,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / G;
     // fixed 32-char queries at 16-B aligned addresses: the pair splits each query load
-    const bool split = SAS_PREFIX_SPLITQ && G == 2 && QW == 1 && a.qoff == nullptr && a.m_fixed == 32 &&
+    const bool split = SAS_PREFIX_SPLITQ && G == 2 && QW == 1 && a.qoff == nullptr && a.qwords == nullptr &&
+                       a.m_fixed == 32 &&
                        (((uintptr_t)a.qbytes) & 15) == 0;
     auto qload = [&](uint64_t k) -> uint4 {
         const uint4* p = reinterpret_cast<const uint4*>(a.qbytes + k * 32) + sub;
@@ -1321,7 +1329,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
         uint32_t m;
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
-        if (split) {
+        if (a.qwords) {  // packed: the key word itself (both lanes, one 8-B request)
+            q.bytes = nullptr;
+            q.m = m;
+            q.w[0] = a.qwords[i];
+        } else if (split) {
             // the pair splits the 32-B query: lane j packs bytes 16j..16j+15 to 32 bits,
             // then the halves are swapped within the pair (DPP quad_perm [1,0,3,2])
             uint4 v;
@@ -1660,6 +1672,79 @@ extern "C" int sas_search_batch(const sas_index* index, const uint8_t* qbytes, c
 extern "C" int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, uint64_t nq, int algo,
                                 uint64_t* out_pos, uint32_t* out_probes, void* stream, uint32_t flags) {
     return search_impl(index, qbytes, nullptr, nullptr, m, nq, algo, out_pos, out_probes, stream, flags);
+}
+
+__global__ void k_pack_queries(const uint8_t* __restrict__ qb, uint32_t m, uint64_t nq, uint64_t* __restrict__ out,
+                               uint32_t* __restrict__ bad) {
+    uint32_t b = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = pack_query_word(qb + i * (uint64_t)m, m, 0, &b);
+    if (b) atomicOr(bad, 1u);
+}
+
+extern "C" int sas_pack_queries(const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_words, void* stream,
+                                uint32_t flags) {
+    if (m > 32) SAS_FAIL(EINVAL, "sas_pack_queries: m must be <= 32");
+    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_pack_queries: device pointers only (SAS_DEVICE_PTRS)");
+    if (nq == 0) return 0;
+    if (!qbytes || !out_words) SAS_FAIL(EINVAL, "sas_pack_queries: null argument");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    DeviceBuf bflag;
+    HIP_TRY(hipMalloc(&bflag.p, 4));
+    HIP_TRY(hipMemsetAsync(bflag.p, 0, 4, st));
+    uint64_t blocks = (nq + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    hipLaunchKernelGGL(k_pack_queries, dim3((unsigned)blocks), dim3(256), 0, st, qbytes, m, nq, out_words,
+                       static_cast<uint32_t*>(bflag.p));
+    HIP_TRY(hipGetLastError());
+    uint32_t hbad = 0;
+    HIP_TRY(hipMemcpyAsync(&hbad, bflag.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hbad) SAS_FAIL(EINVAL, "sas_pack_queries: query bytes must be DNA codes 0..3");
+    return 0;
+}
+
+extern "C" int sas_search_packed(const sas_index* x, const uint64_t* qwords, uint32_t m, uint64_t nq, int algo,
+                                 uint64_t* out_pos, uint32_t* out_probes, void* stream, uint32_t flags) {
+    if (!x) SAS_FAIL(EINVAL, "sas_search_packed: null index");
+    if (algo != SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "sas_search_packed: SAS_ALGO_PREFIX only");
+    if (!x->prefix) SAS_FAIL(EINVAL, "sas_search_packed: needs SAS_BUILD_PREFIX");
+    if (m > 32) SAS_FAIL(EINVAL, "sas_search_packed: m must be <= 32");
+    if (nq == 0) return 0;
+    if (!qwords || !out_pos) SAS_FAIL(EINVAL, "sas_search_packed: null argument");
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const bool dev = flags & SAS_DEVICE_PTRS;
+    SearchArgs a{};
+    fill_args(x, a);
+    a.nq = nq;
+    a.m_fixed = m;
+    a.bad = x->scratch;  // packed words hold no invalid codes
+    DeviceBuf bw, bout, bprobes;
+    if (dev) {
+        a.qwords = qwords;
+        a.out_pos = out_pos;
+        a.out_probes = out_probes;
+    } else {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMalloc(&bw.p, nq * 8));
+        HIP_TRY(hipMemcpy(bw.p, qwords, nq * 8, hipMemcpyHostToDevice));
+        HIP_TRY(hipMalloc(&bout.p, nq * 8));
+        a.qwords = static_cast<const uint64_t*>(bw.p);
+        a.out_pos = static_cast<uint64_t*>(bout.p);
+        if (out_probes) {
+            HIP_TRY(hipMalloc(&bprobes.p, nq * 4));
+            a.out_probes = static_cast<uint32_t*>(bprobes.p);
+        }
+    }
+    int rc = launch_search(x, a, algo, 1, flags | SAS_DEVICE_PTRS, st);
+    if (rc) return rc;
+    if (!dev) {
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemcpy(out_pos, a.out_pos, nq * 8, hipMemcpyDeviceToHost));
+        if (out_probes) HIP_TRY(hipMemcpy(out_probes, a.out_probes, nq * 4, hipMemcpyDeviceToHost));
+    }
+    return 0;
 }
 
 extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint32_t m, uint64_t nq, int algo,

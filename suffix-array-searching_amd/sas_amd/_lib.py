@@ -122,6 +122,8 @@ def lib():
     L.sas_route_batch.argtypes = [vp, vp, u32, vp, vp, vp, u64, vp, vp, u32]
     L.sas_build_multi.argtypes = [vp, u64, vp, i32, i32, u32, C.POINTER(vp)]
     L.sas_extract.argtypes = [vp, vp, vp, vp, u64, vp, vp, u32]
+    L.sas_pack_queries.argtypes = [vp, u32, u64, vp, vp, u32]
+    L.sas_search_packed.argtypes = [vp, vp, u32, u64, i32, vp, vp, vp, u32]
     L.sas_multi_free.argtypes = [vp]
     L.sas_multi_parts.argtypes = [vp]
     L.sas_multi_get_stats.argtypes = [vp, i32, C.POINTER(SasStats)]

@@ -199,6 +199,37 @@ class SaNaive:
                                 _lib.SAS_DEVICE_PTRS))
         return out
 
+    @staticmethod
+    def pack_queries(qbytes, m: int, stream=None):
+        """2-bit packed fixed-length queries (sas_pack_queries; m <= 32): torch CUDA
+        uint8 in -> torch CUDA int64 words out (first char in bits 63..62)."""
+        import torch
+        nq = qbytes.numel() // m if m else 0
+        out = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+        st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
+        check(lib().sas_pack_queries(_ptr(qbytes), m, nq, _ptr(out), st, _lib.SAS_DEVICE_PTRS))
+        return out
+
+    def search_packed(self, qwords, m: int, algo: str = "prefix", probes: bool = False, out=None, stream=None):
+        """Lookups of packed fixed-length queries (sas_search_packed): numpy uint64 in ->
+        numpy out; torch CUDA in -> torch CUDA out (async)."""
+        if _is_cuda(qwords):
+            import torch
+            nq = qwords.numel()
+            out = torch.empty(nq, dtype=torch.int64, device=qwords.device) if out is None else out
+            pr = torch.empty(nq, dtype=torch.int32, device=qwords.device) if probes else None
+            st = stream if stream is not None else torch.cuda.current_stream(qwords.device).cuda_stream
+            check(lib().sas_search_packed(self._h, _ptr(qwords), m, nq, _lib.ALGOS[algo], _ptr(out),
+                                          _ptr(pr) if probes else None, st, _lib.SAS_DEVICE_PTRS))
+            return (out, pr) if probes else out
+        qwords = np.ascontiguousarray(qwords, np.uint64)
+        nq = len(qwords)
+        out = np.zeros(max(nq, 1), np.uint64)
+        pr = np.zeros(max(nq, 1), np.uint32) if probes else None
+        check(lib().sas_search_packed(self._h, qwords.ctypes.data, m, nq, _lib.ALGOS[algo], out.ctypes.data,
+                                      pr.ctypes.data if probes else None, None, 0))
+        return (out[:nq], pr[:nq]) if probes else out[:nq]
+
     def route(self, splitter_pos, qbytes, m: int, stream=None):
         """Sharded mode: shard id of each fixed-length query = number of splitter
         suffixes < q (sas_route).  numpy in -> numpy out; CUDA in -> CUDA out."""

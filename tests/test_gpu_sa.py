@@ -288,6 +288,39 @@ def test_extract_substrings(sas):
         assert np.array_equal(got[o_:o_ + l_], tp[p_:p_ + l_]), (p_, l_)
 
 
+def test_packed_queries(sas):
+    """sas_pack_queries / sas_search_packed: 2-bit packed fixed-length queries (first char
+    high, as string_value<K> packs them, sas/util.rs:76-117) give the byte queries'
+    positions, on rank and inline prefix tables, host and device pointers."""
+    import torch
+    n = 300_007
+    t = sas.random_string(n, seed=52)
+    sa = O.build_sa(t)
+    rng = np.random.default_rng(8)
+    for inl in (0, 2):
+        idx = sas.SaNaive.build(t, stree=False, sector=False, llcp=False, lcp=False, prefix=True, prefix_inline=inl)
+        for m in (1, 7, 16, 31, 32):
+            offs = rng.integers(0, n - m, 3000)
+            qb = np.concatenate([np.concatenate([t[o:o + m] for o in offs]),
+                                 rng.integers(0, 4, 500 * m, dtype=np.uint8)])
+            nq = len(qb) // m
+            expect = oracle_positions(t, sa, qb, np.arange(nq, dtype=np.uint64) * m, np.full(nq, m, np.uint32))
+            words = sas.SaNaive.pack_queries(torch.from_numpy(qb).cuda(), m)
+            ref = np.array([int("".join(str(c) for c in qb[k * m:(k + 1) * m]).ljust(32, "0"), 4) for k in range(nq)],
+                           np.uint64)
+            assert np.array_equal(words.cpu().numpy().view(np.uint64), ref), m
+            got = idx.search_packed(words, m).cpu().numpy().view(np.uint64)
+            assert np.array_equal(got, expect), (inl, m)
+            got_h, pr = idx.search_packed(ref, m, probes=True)
+            assert np.array_equal(got_h, expect), (inl, m)
+            _, pr_b = idx.search_fixed(qb, m, algo="prefix", probes=True)
+            assert np.array_equal(pr, pr_b), (inl, m)
+    with pytest.raises(sas.SasError):
+        sas.SaNaive.pack_queries(torch.full((64,), 5, dtype=torch.uint8, device="cuda"), 32)
+    with pytest.raises(sas.SasError):
+        idx.search_packed(ref, 32, algo="quad")
+
+
 def test_concurrent_calls_keep_their_error_flags(sas):
     """The index is immutable and may be searched from several threads at once
     (SearchIndex: Sync, sst/lib.rs:30): a call with invalid query codes
