@@ -35,6 +35,17 @@ struct DevBuf {
         }
         return 0;
     }
+    // hipExtMallocWithFlags (e.g. hipDeviceMallocContiguous) when mflags != 0, plain
+    // hipMalloc if that fails or mflags == 0
+    int alloc_flags(size_t bytes, const char* what, unsigned mflags) {
+        if (mflags) {
+            if (p) { (void)hipFree(p); p = nullptr; }
+            if (hipExtMallocWithFlags(&p, bytes ? bytes : 1, mflags) == hipSuccess) return 0;
+            p = nullptr;
+            (void)hipGetLastError();
+        }
+        return alloc(bytes, what);
+    }
     void* release() { void* q = p; p = nullptr; return q; }
 };
 

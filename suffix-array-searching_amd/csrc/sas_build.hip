@@ -847,6 +847,9 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
 // (SAS_BUILD_PREFIX_INLINE, TW = 16) {key64, rank, SA} of that first suffix, so a lookup
 // whose answer is the first suffix of its range needs this one read.
 #define PT_SMALL 256
+#ifndef SAS_PREFIX_ALLOC_FLAGS
+#define SAS_PREFIX_ALLOC_FLAGS 0  // hipExtMallocWithFlags flags for the table (A/B: contiguous, uncached)
+#endif
 template <bool KO>
 __device__ __forceinline__ uint64_t pt_key64(const uint4* leaves, uint64_t r) {
     if (KO) return reinterpret_cast<const uint64_t*>(leaves)[r];
@@ -926,7 +929,7 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     const uint64_t entries = (1ull << (2 * p)) + 1;
     const uint64_t cap = entries / (PT_SMALL + 1) + 2;
     DevBuf t, big, nbig;
-    TRY(t.alloc(entries * tw + 8, "prefix table"));
+    TRY(t.alloc_flags(entries * tw + 8, "prefix table", SAS_PREFIX_ALLOC_FLAGS));
     TRY(big.alloc(cap * 24, "prefix table gap list"));
     TRY(nbig.alloc(8, "prefix table gap count"));
     HIP_TRY(hipMemset(nbig.p, 0, 8));
