@@ -96,7 +96,7 @@ class SaNaive:
     @classmethod
     def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
-              sa40: bool = False, quad: bool | str = True, llcp: bool = True,
+              sa40: bool = False, quad: bool | str = True, llcp: bool | None = None,
               prefix: bool | int | None = None, prefix_inline: bool | int = False) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
@@ -104,7 +104,7 @@ class SaNaive:
         builder even when n < 2^32 (automatic above).  quad="compact": key-only quad
         leaves (8 B per suffix, SA values read from the SA array; SAS_BUILD_QUAD_COMPACT).
         llcp: the Manber-Myers Llcp/Rlcp entries for algo="llcp" (SAS_BUILD_LLCP, 16 B
-        per suffix, implies the LCP array).  prefix: the prefix table for algo="prefix"
+        per suffix, implies the LCP array); None = only while n < 2^31 (<= 32 GiB).  prefix: the prefix table for algo="prefix"
         (SAS_BUILD_PREFIX; None = whenever quad is built and n < 2^32 - 1, an int = its
         p chars); prefix_inline: 16-B entries that inline each range's first suffix
         (True / 1: SAS_BUILD_PREFIX_INLINE) or 32-B ones with its first two (2:
@@ -112,6 +112,8 @@ class SaNaive:
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
+        if llcp is None:
+            llcp = n < (1 << 31)
         flags |= _lib.SAS_BUILD_LLCP if llcp else 0
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         flags |= _lib.SAS_BUILD_SA40 if sa40 else 0
@@ -140,7 +142,7 @@ class SaNaive:
 
     @classmethod
     def build_part(cls, t, part: int, parts: int, lcp: bool = True, stree: bool = True, verify: bool = False,
-                   flags: int = 0, sector: bool = True, quad: bool | str = True, llcp: bool = True,
+                   flags: int = 0, sector: bool = True, quad: bool | str = True, llcp: bool | None = None,
                    prefix: bool | int | None = None, prefix_inline: bool = False) -> "SaNaive":
         """Sharded-text index that builds ONLY its own SA rank range (sas_build_part):
         part `part` of `parts` contiguous 7-char-prefix bin ranges.  The range is
@@ -149,6 +151,7 @@ class SaNaive:
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
+        llcp = (n < (1 << 31)) if llcp is None else llcp
         flags |= _quad_flags(quad) | (_lib.SAS_BUILD_LLCP if llcp else 0) | _prefix_flags(prefix, quad, n, prefix_inline)
         if _is_cuda(t):
             flags |= _lib.SAS_DEVICE_PTRS

@@ -765,7 +765,7 @@ def test_sa_beyond_u32(sas):
     del idx
     torch.cuda.empty_cache()
     tc = torch.from_numpy(ht).cuda()
-    cidx = sas.SaNaive.build(tc, lcp=False, stree=False, sector=False, quad="compact", prefix=16)
+    cidx = sas.SaNaive.build(tc, lcp=False, stree=False, sector=False, quad="compact", prefix=16, llcp=True)
     del tc
     assert cidx.stats()["quad_entry_bytes"] == 8 and cidx.stats()["llcp_bytes"] == 16 * n
     assert cidx.stats()["prefix_bytes"] == (4 ** 16 + 1) * 5  # 40-bit ranks beside the 40-bit SA
