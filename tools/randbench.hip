@@ -6,6 +6,8 @@
 //   rand8x2  : random 8-B + the next 8-B word (text_chars32 shape)
 //   rand64   : random 64-B node, 4 x 16-B loads by one lane (S-tree node shape)
 //   rand128  : random 128-B line, 8 x 16-B loads by one lane
+//   rand16   : one random 16-B slot per lane
+//   rand32pair: one random 32-B slot per lane pair, 16 B per lane (the PREFIX entry read)
 //
 // Prints one JSON line per kernel: accesses/s and bytes moved per the access shape.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/randbench tools/randbench.hip
@@ -36,7 +38,7 @@ __global__ __launch_bounds__(1024) void k_rand(const uint8_t* __restrict__ p, ui
                                                uint32_t seed, uint32_t* out) {
     uint32_t acc = 0;
     uint64_t lines = bytes / 128;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < accesses;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; SHAPE != 5 && i < accesses;
          i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
         uint64_t line = h % lines;
@@ -51,10 +53,23 @@ __global__ __launch_bounds__(1024) void k_rand(const uint8_t* __restrict__ p, ui
             const uint4* v = reinterpret_cast<const uint4*>(b + ((h >> 40) & 1) * 64);
 #pragma unroll
             for (int k = 0; k < 4; k++) { uint4 t = v[k]; acc ^= t.x ^ t.y ^ t.z ^ t.w; }
-        } else {
+        } else if (SHAPE == 3) {
             const uint4* v = reinterpret_cast<const uint4*>(b);
 #pragma unroll
             for (int k = 0; k < 8; k++) { uint4 t = v[k]; acc ^= t.x ^ t.y ^ t.z ^ t.w; }
+        } else if (SHAPE == 4) {  // one lane, one random 16-B slot (one-suffix inline entry)
+            const uint4 t = reinterpret_cast<const uint4*>(b)[(h >> 40) & 7];
+            acc ^= t.x ^ t.y ^ t.z ^ t.w;
+        }
+    }
+    if (SHAPE == 5) {  // lane pairs share one random 32-B slot, 16 B each (k_sa_prefix2's entry read)
+        const uint32_t sub = threadIdx.x & 1;
+        for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 2; i < accesses;
+             i += (uint64_t)gridDim.x * blockDim.x / 2) {
+            uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
+            const uint8_t* b = p + (h % lines) * 128 + ((h >> 40) & 3) * 32;
+            const uint4 t = reinterpret_cast<const uint4*>(b)[sub];
+            acc ^= t.x ^ t.y ^ t.z ^ t.w;
         }
     }
     if (acc == 0x12345678u) out[0] = acc;
@@ -108,5 +123,7 @@ int main(int argc, char** argv) {
     RUN(1, "rand8x2", 16)
     RUN(2, "rand64", 64)
     RUN(3, "rand128", 128)
+    RUN(4, "rand16", 16)
+    RUN(5, "rand32pair", 32)
     return 0;
 }
