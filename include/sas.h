@@ -47,6 +47,8 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_VERIFY  (1u << 3)  /* run the adjacency + permutation check on the SA  */
 #define SAS_NO_LDS_TOP    (1u << 4)  /* search: do not serve the top levels from LDS     */
 #define SAS_VALIDATE      (1u << 5)  /* search: reject query bytes > 3 (synchronises)    */
+#define SAS_NO_PREFIX_TABLE (1u << 25) /* sas_search_range: use the tree descents even when
+                                        the index has a prefix table                      */
 #define SAS_PREFIX_RANGE  (1u << 24) /* search, PLAIN / LCP: start binary_search from the
                                         prefix table's range of q's first p chars, as the
                                         reference's binary_search does (sas/sa_search.rs:

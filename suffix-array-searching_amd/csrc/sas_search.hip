@@ -1401,6 +1401,61 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// Occurrence ranges from the prefix table (any entry format; Search::search_prefix,
+// sas/util.rs:36-46): lo = the lower bound, bisected in [table[K], table[K+1]]; hi = the
+// first suffix whose first min(m, len) chars are > q, bisected in the range of the
+// routing key (q padded with 3s for m <= 32, its own key above), with the predicates of
+// k_sa_quad_range over the quad leaves' entries.
+template <int QW, bool KO, int W, bool UPPER>
+__device__ __forceinline__ uint64_t prefix_bound(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64,
+                                                 uint64_t Q3, uint32_t sh) {
+    uint64_t lo, hi;
+    prefix_range(a, ((UPPER && q.m <= 32) ? Q3 : K64) >> sh, &lo, &hi);
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        const uint64_t key = quad_entry_key<KO>(a, mid);
+        const uint64_t tie = UPPER ? (q.m > 32 && key == K64) : (key == K64);
+        const uint64_t pp = tie ? quad_entry_sa<KO, W>(a, mid) : QUAD_NO_SA;
+        const bool pr = UPPER ? sector_gt_prefix<QW>(key, pp, K64, Q3, a, q) : sector_ge<QW>(key, pp, K64, a, q);
+        if (pr) hi = mid;
+        else lo = mid + 1;
+    }
+    return lo;
+}
+
+template <int QW, bool KO, int W>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix_range(SearchArgs a, uint64_t* out_hi) {
+    uint32_t bad = 0;
+    const uint32_t sh = 64 - 2 * a.prefix_chars;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
+        const uint64_t lo = prefix_bound<QW, KO, W, false>(a, q, K64, Q3, sh);
+        uint64_t hi = prefix_bound<QW, KO, W, true>(a, q, K64, Q3, sh);
+        if (hi < lo) hi = lo;
+        a.out_pos[i] = a.rank_lo + lo;
+        out_hi[i] = a.rank_lo + hi;
+        if (a.out_probes) a.out_probes[i] = 2;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+template <bool KO, int W>
+static void launch_prefix_range(int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a, uint64_t* dhi) {
+    switch (qw) {
+        case 1: hipLaunchKernelGGL((k_sa_prefix_range<1, KO, W>), grid, block, 0, st, a, dhi); break;
+        case 2: hipLaunchKernelGGL((k_sa_prefix_range<2, KO, W>), grid, block, 0, st, a, dhi); break;
+        case 4: hipLaunchKernelGGL((k_sa_prefix_range<4, KO, W>), grid, block, 0, st, a, dhi); break;
+        default: hipLaunchKernelGGL((k_sa_prefix_range<8, KO, W>), grid, block, 0, st, a, dhi); break;
+    }
+}
+
 // ------------------------------------------------------------------ host dispatch
 template <int W>
 static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 block, hipStream_t st,
@@ -2050,11 +2105,17 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
         a.out_pos = static_cast<uint64_t*>(blo.p);
         dhi = static_cast<uint64_t*>(bhi.p);
     }
-    uint64_t blocks = (nq * (quad ? QUAD_G : 1) + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    // the prefix table, when built, replaces the two tree descents (one lane per query)
+    const bool ptab = quad && x->prefix && !(flags & SAS_NO_PREFIX_TABLE);
+    uint64_t blocks = (nq * ((quad && !ptab) ? QUAD_G : 1) + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    if (quad && !x->quad_compact) {
+    if (ptab) {
+        if (!x->quad_compact) launch_prefix_range<false, 4>(qw, grid, block, st, a, dhi);
+        else if (x->sa_w == 5) launch_prefix_range<true, 5>(qw, grid, block, st, a, dhi);
+        else launch_prefix_range<true, 4>(qw, grid, block, st, a, dhi);
+    } else if (quad && !x->quad_compact) {
         launch_quad_range<false, 4>(qw, grid, block, st, a, dhi);
     } else if (quad) {
         if (x->sa_w == 5) launch_quad_range<true, 5>(qw, grid, block, st, a, dhi);

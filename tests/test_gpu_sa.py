@@ -532,9 +532,11 @@ def test_occurrence_ranges(sas, sadef):
 
 
 def test_occurrence_ranges_both_trees(sas, sadef):
-    """sas_search_range runs on the quad tree when it is built (k_sa_quad_range) and on
-    the sector tree otherwise (k_sa_sector_range): both give identical ranges, including
+    """sas_search_range runs on the prefix table when it is built (k_sa_prefix_range, any
+    entry format), on the quad tree otherwise (k_sa_quad_range) and on the sector tree
+    without one (k_sa_sector_range): all give identical ranges, including
     above-every-suffix, empty and long queries, and a quad-only index searches."""
+    from sas_amd import _lib
     rng = np.random.default_rng(21)
     cases = [np.array(c["text"], np.uint8) for c in sadef["cases"]]
     cases += [sas.random_string(300_000, seed=5), np.zeros(20_000, np.uint8),
@@ -547,9 +549,16 @@ def test_occurrence_ranges_both_trees(sas, sadef):
         qs += [np.full(l, 3, np.uint8) for l in (1, 16, 31, 32, 33, 64, 200)]  # above every suffix
         qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(0, 70, 200)]
         buf, off, lens = pack(qs)
-        lq, hq = q_only.search_range(buf, off, lens)
+        lq, hq = q_only.search_range(buf, off, lens)  # prefix table (built with the quad tree)
         ls, hs = s_only.search_range(buf, off, lens)
         assert np.array_equal(lq, ls) and np.array_equal(hq, hs), n
+        lt, ht = q_only.search_range(buf, off, lens, flags=_lib.SAS_NO_PREFIX_TABLE)  # quad descents
+        assert np.array_equal(lq, lt) and np.array_equal(hq, ht), n
+        for inl in (1, 2):
+            qi = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=True,
+                                   prefix_inline=inl)
+            li, hi = qi.search_range(buf, off, lens)
+            assert np.array_equal(lq, li) and np.array_equal(hq, hi), (n, inl)
         assert np.array_equal(q_only.search_batch(buf, off, lens, algo="quad"),
                               s_only.search_batch(buf, off, lens, algo="sector")), n
 
