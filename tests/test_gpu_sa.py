@@ -456,7 +456,7 @@ def test_large_text_sampled(sas):
     import torch
     n = (1 << 31) + 12345
     t = sas.random_string(n, seed=123, device="cuda")
-    idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True)
+    idx = sas.SaNaive.build(t, lcp=False, stree=True, llcp=True, verify=True)
     ht = t.cpu().numpy()
     del t
     torch.cuda.empty_cache()
