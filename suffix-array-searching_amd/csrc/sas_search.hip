@@ -1436,8 +1436,26 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix_range(SearchArgs 
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
         const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
-        const uint64_t lo = prefix_bound<QW, KO, W, false>(a, q, K64, Q3, sh);
-        uint64_t hi = prefix_bound<QW, KO, W, true>(a, q, K64, Q3, sh);
+        // both bisections advance in lock step: two independent entry reads in flight per lane
+        uint64_t lo, l1, hi, h1;
+        prefix_range(a, K64 >> sh, &lo, &l1);
+        prefix_range(a, (q.m <= 32 ? Q3 : K64) >> sh, &hi, &h1);
+        while (lo < l1 || hi < h1) {
+            const bool g0 = lo < l1, g1 = hi < h1;
+            const uint64_t m0 = (lo + l1) >> 1, m1 = (hi + h1) >> 1;
+            const uint64_t k0 = g0 ? quad_entry_key<KO>(a, m0) : 0;
+            const uint64_t k1 = g1 ? quad_entry_key<KO>(a, m1) : 0;
+            const uint64_t p0 = (g0 && k0 == K64) ? quad_entry_sa<KO, W>(a, m0) : QUAD_NO_SA;
+            const uint64_t p1 = (g1 && q.m > 32 && k1 == K64) ? quad_entry_sa<KO, W>(a, m1) : QUAD_NO_SA;
+            if (g0) {
+                if (sector_ge<QW>(k0, p0, K64, a, q)) l1 = m0;
+                else lo = m0 + 1;
+            }
+            if (g1) {
+                if (sector_gt_prefix<QW>(k1, p1, K64, Q3, a, q)) h1 = m1;
+                else hi = m1 + 1;
+            }
+        }
         if (hi < lo) hi = lo;
         a.out_pos[i] = a.rank_lo + lo;
         out_hi[i] = a.rank_lo + hi;
