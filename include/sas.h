@@ -90,6 +90,19 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_PREFIX_INLINE4 (1u << 22) /* 64-B entries: the first FOUR suffixes of each
                                         range, read by a 4-lane group as one request      */
 #define SAS_BUILD_PREFIX_P(p) ((uint32_t)(p) << 16)  /* bits 16..20: prefix chars       */
+#define SAS_BUILD_TAGGED  (1u << 23) /* store the SA as 8-B tagged entries {SA 40 bits | the
+                                        suffix's chars [p, p+12) in the high 24 bits} plus a
+                                        u64 bucket table over the first p chars {first rank
+                                        40 bits | rank count 24 bits} (the reference's prefix
+                                        table, sas/sa_search.rs:59-95, live) for
+                                        SAS_ALGO_TAGGED: an entry holds a suffix's (p+12)-char
+                                        key AND its position, so a lookup is the bucket
+                                        entry, one window of consecutive entries and (for
+                                        m > p + 12) one text window.  p = SAS_BUILD_PREFIX_P
+                                        or ceil(log4 n) capped at 16 (16 at n = 2^34: 32 GiB
+                                        table beside 128 GiB of entries).  The entries
+                                        replace the SA (sa_width 8).  Combines with LCP;
+                                        not with the trees, LLCP or SAS_BUILD_PREFIX*  */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry
                                         {SA[m] 40 bits, Llcp 12 bits, Rlcp 12 bits, 16 chars
@@ -116,10 +129,20 @@ enum sas_algo {
                            lcp values alone unless they tie llcp/rlcp; a tie compares the
                            entry's 16 chars before any text (needs SAS_BUILD_LLCP; the LCP
                            array at work, A21)                                              */
-    SAS_ALGO_PREFIX = 7 /* prefix table lookup (the rank range of q's first p chars, one 8-B
+    SAS_ALGO_PREFIX = 7, /* prefix table lookup (the rank range of q's first p chars, one 8-B
                            read; sas/sa_search.rs:59-95) + binary search over that range on
                            the quad tree's leaf entries: ~2 memory requests per lookup
                            (needs SAS_BUILD_PREFIX)                                          */
+    SAS_ALGO_INTERP = 8, /* interpolation_search<16> (sas/sa_search.rs:376-421): the mid is
+                           interpolated from string_value<16> of the bounds and the query
+                           (sas/util.rs:76-117), clamped to [1/16, 15/16] of the range, exact
+                           compares; out_probes = its cnt.  Reads the fused quad leaves'
+                           {32-char key, SA} entries when built (one request per probe),
+                           else SA + text.  With SAS_PREFIX_RANGE it starts from the prefix
+                           table's range.  n < 2^32 (the reference asserts r_val * r fits a
+                           usize, :389-392); ENOTSUP above                                   */
+    SAS_ALGO_TAGGED = 9 /* bucket table + tagged SA entries (needs SAS_BUILD_TAGGED): the
+                           configs[3] shape's lookup, ~4-5 memory requests for a long query  */
 };
 
 typedef struct sas_stats {
@@ -154,6 +177,11 @@ typedef struct sas_stats {
     uint64_t llcp_bytes;     /* SAS_BUILD_LLCP entries (16 B per suffix), 0 if not built */
     uint64_t prefix_bytes;   /* SAS_BUILD_PREFIX table, 0 if not built                */
     uint32_t prefix_chars;   /* its p (chars per table key)                           */
+    uint32_t tag_chars;      /* SAS_BUILD_TAGGED: p of the bucket table (0 if not built);
+                                sa_width is then 8 (tagged entries)                   */
+    uint64_t tag_table_bytes; /* SAS_BUILD_TAGGED bucket table, (4^p + 1) x 8 B       */
+    uint64_t index_bytes;    /* every HBM array of the index together (text, SA or tagged
+                                entries, LCP, LLCP, trees, tables, top2)              */
 } sas_stats;
 
 const char* sas_last_error(void);

@@ -46,6 +46,9 @@ def lib():
         for f in ("orc_binary_search", "orc_binary_search_cmp", "orc_branchy_search", "orc_branchfree_search"):
             getattr(L, f).argtypes = [C.c_void_p, C.c_uint64, u32p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint64)]
             getattr(L, f).restype = C.c_uint64
+        L.orc_interpolation_search.argtypes = [C.c_void_p, C.c_uint64, u32p, C.c_void_p, C.c_uint64, C.c_int,
+                                               C.POINTER(C.c_uint64)]
+        L.orc_interpolation_search.restype = C.c_uint64
         L.orc_lower_bound_rank.argtypes = [C.c_void_p, C.c_uint64, u32p, C.c_void_p, C.c_uint64]
         L.orc_lower_bound_rank.restype = C.c_uint64
         L.orc_prefix_range.argtypes = [C.c_void_p, C.c_uint64, u32p, C.c_void_p, C.c_uint64,
@@ -151,7 +154,17 @@ def prefix_range(tpad, n, sa, q):
     return lo.value, hi.value
 
 
-SEARCH_ALGOS = {"binary_search": 0, "binary_search_cmp": 1, "batch_c16": 2, "batch16": 3}
+SEARCH_ALGOS = {"binary_search": 0, "binary_search_cmp": 1, "batch_c16": 2, "batch16": 3, "interpolation16": 4}
+
+
+def interpolation_search(tpad, n, sa, q, K: int = 16):
+    """sas/sa_search.rs:376-421 interpolation_search<K> -> (pos, cnt); q zero padded."""
+    qb = np.zeros(len(q) + 64, np.uint8)
+    qb[: len(q)] = q
+    cnt = C.c_uint64(0)
+    pos = lib().orc_interpolation_search(tpad.ctypes.data, n, np.ascontiguousarray(sa, np.uint32), qb.ctypes.data,
+                                         len(q), K, C.byref(cnt))
+    return int(pos), int(cnt.value)
 
 
 def search_many(tpad, n, sa, qbytes, qoff, qlen, algo="binary_search", threads=1):

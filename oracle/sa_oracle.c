@@ -327,6 +327,49 @@ EXPORT uint64_t orc_branchfree_search(const uint8_t* t, uint64_t n, const uint32
     return l < n ? sa[l] : n;
 }
 
+/* sas/util.rs:76-117 `string_value<K>`: the first K chars as a base-4 number.
+ * The K = 16 path (the one main.rs:97 runs) reads 16 bytes with two unaligned
+ * u64 loads + pext of each byte's low 2 bits, i.e. it reads past a slice shorter
+ * than K: with the zero padding after the text (sas/main.rs:56-58) and after
+ * each query (the callers here pad queries with zeros) that is "zero padded". */
+static inline uint64_t string_value(const uint8_t* s, int K) {
+    uint64_t v = 0;
+    for (int i = 0; i < K; i++) v = v * 4 + (s[i] & 3u);
+    return v;
+}
+
+/* sas/sa_search.rs:376-421 `interpolation_search<K>` (A12).  prefix_range() is
+ * [0, n) with no cnt increment (p = 0, :86-95).  Mid = the interpolated rank
+ * l + (r-l)(q_val - l_val + 1) / (r_val - l_val + 2) clamped to the
+ * [1/16, 15/16] interior (:406-409), exact slice compare (:411).  usize
+ * arithmetic wraps in the release profile (Cargo.toml: no overflow-checks), so
+ * q_val < l_val - 1 (q below the first suffix) wraps here too: the clamp keeps
+ * l <= mid < r, and the result is binary_search's.  The reference asserts
+ * r_val * r does not overflow (:389-392): n < 2^32 at K = 16. */
+EXPORT uint64_t orc_interpolation_search(const uint8_t* t, uint64_t n, const uint32_t* sa,
+                                         const uint8_t* q, uint64_t m, int K, uint64_t* cnt) {
+    uint64_t l = 0, r = n;
+    uint64_t l_val = string_value(t + sa[l], K);
+    uint64_t r_val = r < n ? string_value(t + sa[r], K) : (1ull << (2 * K));
+    const uint64_t q_val = string_value(q, K);
+    while (l < r) {
+        (*cnt)++;
+        uint64_t mid = l + ((r - l) * (q_val - l_val + 1)) / (r_val - l_val + 2);
+        const uint64_t low = l + (r - l) / 16, high = l + 15 * (r - l) / 16;
+        mid = mid < low ? low : (mid > high ? high : mid);
+        const uint32_t p = sa[mid];
+        const uint64_t m_val = string_value(t + p, K);
+        if (suffix_lt(t, n, p, q, m)) {
+            l = mid + 1;
+            l_val = m_val;
+        } else {
+            r = mid;
+            r_val = m_val;
+        }
+    }
+    return l < n ? sa[l] : n;
+}
+
 /* sas/sa_search.rs:157-239 `binary_search_batch<B>` / `_batch_c<B>` (A9):
  * B queries in lockstep for ilog2(n)+1 iterations (:171-172), three passes
  * per iteration (mids + prefetch sa, load sa + prefetch text, compare).
@@ -365,7 +408,8 @@ EXPORT void orc_binary_search_batch(const uint8_t* t, uint64_t n, const uint32_t
 /* Multi-threaded driver, same shape as the reference benches: contiguous
  * query chunks per thread (sst/bin/bench.rs:558-573), one wall clock.
  * algo: 0 binary_search (A6), 1 binary_search_cmp (A8),
- *       2 binary_search_batch_c<16> (A9), 3 binary_search_batch<16>.
+ *       2 binary_search_batch_c<16> (A9), 3 binary_search_batch<16>,
+ *       4 interpolation_search<16> (A12).
  * Queries are qbytes[qoff[k] .. qoff[k]+qlen[k]]. */
 typedef struct {
     const uint8_t* t; uint64_t n; const uint32_t* sa;
@@ -386,6 +430,9 @@ static void* search_worker(void* arg) {
         }
         for (; k < j->hi; k++)  /* remainder: the reference drops it (:441); we don't */
             j->out[k] = orc_binary_search_cmp(j->t, j->n, j->sa, j->qb + j->qoff[k], j->qlen[k], &cnt);
+    } else if (j->algo == 4) {
+        for (uint64_t k = j->lo; k < j->hi; k++)
+            j->out[k] = orc_interpolation_search(j->t, j->n, j->sa, j->qb + j->qoff[k], j->qlen[k], 16, &cnt);
     } else {
         for (uint64_t k = j->lo; k < j->hi; k++) {
             const uint8_t* q = j->qb + j->qoff[k];

@@ -122,6 +122,11 @@ struct sas_index {
     uint32_t quad_lds_layers = 0;
     uint32_t quad_lds_nodes = 0;
     uint64_t quad_inner_nodes = 0;
+    // SAS_BUILD_TAGGED: `sa` holds u64 entries {SA 40 bits | chars [tag_p, tag_p + 12) << 40}
+    // (sa_w = 8) and tag_table[x] = {first rank whose tag_p-char key is >= x (40 bits) |
+    // min(rank count of key x, 2^24 - 1) << 40} for x in [0, 4^tag_p]
+    uint64_t* tag_table = nullptr;
+    uint32_t tag_p = 0;
     sas_stats stats = {};
 };
 
@@ -151,11 +156,15 @@ struct sst_index {
 // SAS_BUILD_LLCP entries: SA (40 bits) | Llcp << 40 | Rlcp << 52 + 16 chars after each lcp
 #define SAS_LLCP_CAP 4095u
 
+// W = 8: the tagged SA of SAS_BUILD_TAGGED, u64 entries {SA 40 bits | 12 chars << 40}
+// (sas_build.hip, build_tagged): the SA value is the low 40 bits.
+#define SAS_TAG_CHARS 12
 template <int W>
 struct SaView {
     const uint8_t* p;
     __device__ __forceinline__ uint64_t operator[](uint64_t i) const {
         if (W == 4) return reinterpret_cast<const uint32_t*>(p)[i];
+        if (W == 8) return reinterpret_cast<const uint64_t*>(p)[i] & (SAS_SA40_MAX - 1);
         // 5-byte entry at byte 5i: two aligned u32 loads (same 128-B line except
         // when straddling one) and a funnel shift
         uint64_t o = 5 * i;
@@ -168,6 +177,10 @@ struct SaView {
 // Writes: byte stores, so neighbouring entries written by other lanes never race.
 template <int W>
 __device__ __forceinline__ void sa_put(uint8_t* p, uint64_t i, uint64_t v) {
+    if (W == 8) {
+        reinterpret_cast<uint64_t*>(p)[i] = v;
+        return;
+    }
     if (W == 4) {
         reinterpret_cast<uint32_t*>(p)[i] = (uint32_t)v;
         return;

@@ -967,11 +967,116 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     return 0;
 }
 
+// ------------------------------------------------------------------ tagged SA + bucket table
+// SAS_BUILD_TAGGED: entry r = SA[r] | chars [p, p+12) of suffix SA[r] << 40
+// (zero padded past the text end), so the entries of a p-char bucket carry the suffixes'
+// (p+12)-char keys next to their positions.  The bucket table is the reference's prefix
+// table (sas/sa_search.rs:59-75) with p live, u64 entries {first rank with key >= x |
+// min(count, 2^24 - 1) << 40}: one aligned 8-B read gives a bucket's whole rank range.
+template <int W>
+__global__ void k_tag_entries(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p,
+                              uint64_t* __restrict__ out) {
+    GRID_STRIDE(r, sa_n) {
+        const uint64_t s = sa[r];
+        const uint64_t tag = (text_chars32(tw, s) << (2 * p)) >> 40;
+        out[r] = s | (tag << 40);
+    }
+}
+
+__device__ __forceinline__ uint64_t tag_key(const uint64_t* tw, const uint64_t* ent, uint64_t r, uint32_t p) {
+    return text_chars32(tw, ent[r] & (SAS_SA40_MAX - 1)) >> (64 - 2 * p);
+}
+
+// Rank r with a new p-char key fills table(key(r-1), key(r)] = r (rank sa_n fills the rest
+// up to 4^p); gaps longer than PT_SMALL go to a list that whole workgroups fill.
+__global__ void k_tt_fill(const uint64_t* __restrict__ tw, const uint64_t* __restrict__ ent, uint64_t sa_n,
+                          uint32_t p, uint64_t* __restrict__ table, uint64_t* __restrict__ big,
+                          unsigned long long* __restrict__ nbig, uint64_t big_cap) {
+    const uint64_t top = 1ull << (2 * p);
+    GRID_STRIDE(r, sa_n + 1) {
+        const uint64_t kr = r < sa_n ? tag_key(tw, ent, r, p) : top;
+        const uint64_t lo = r > 0 ? tag_key(tw, ent, r - 1, p) + 1 : 0;
+        if (lo > kr) continue;
+        if (kr - lo < PT_SMALL) {
+            for (uint64_t x = lo; x <= kr; x++) table[x] = r;
+        } else {
+            const unsigned long long slot = atomicAdd(nbig, 1ull);
+            if (slot < big_cap) {
+                big[3 * slot] = lo;
+                big[3 * slot + 1] = kr;
+                big[3 * slot + 2] = r;
+            }
+        }
+    }
+}
+
+__global__ void k_tt_big(const uint64_t* __restrict__ big, const unsigned long long* __restrict__ nbig,
+                         uint64_t* __restrict__ table) {
+    for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x)
+        for (uint64_t x = big[3 * b] + threadIdx.x; x <= big[3 * b + 1]; x += blockDim.x) table[x] = big[3 * b + 2];
+}
+
+// count field: entry x gets min(table[x+1] - table[x], 2^24 - 1) in bits 40..63.  Thread
+// x+1 only ever changes the high bits of entry x+1, so the rank read here is stable.
+__global__ void k_tt_count(uint64_t* __restrict__ table, uint64_t keys) {
+    GRID_STRIDE(x, keys) {
+        const uint64_t a = table[x] & (SAS_SA40_MAX - 1), b = table[x + 1] & (SAS_SA40_MAX - 1);
+        const uint64_t c = b - a < 0xFFFFFFull ? b - a : 0xFFFFFFull;
+        table[x] = a | (c << 40);
+    }
+}
+
+static int build_tagged(sas_index* x, uint32_t p) {
+    const uint64_t sa_n = x->sa_n;
+    if (p == 0) {
+        uint32_t l4 = 0;  // ceil(log4(sa_n)): ~1-4 suffixes per bucket
+        while (l4 < 32 && (1ull << (2 * l4)) < sa_n) l4++;
+        p = l4 < 1 ? 1 : (l4 > 16 ? 16 : l4);
+    }
+    if (p > 17) SAS_FAIL(EINVAL, "SAS_BUILD_TAGGED: p must be 1..17");
+    DevBuf ent;
+    TRY(ent.alloc(sa_n * 8 + 16, "tagged SA entries"));
+    HIP_TRY(hipMemset(ent.as<uint8_t>() + sa_n * 8, 0, 16));
+    const dim3 g(grid_for(sa_n)), b(256);
+    if (x->sa_w == 5)
+        hipLaunchKernelGGL(k_tag_entries<5>, g, b, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, p, ent.as<uint64_t>());
+    else
+        hipLaunchKernelGGL(k_tag_entries<4>, g, b, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, p, ent.as<uint64_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    // the entries hold every SA value: the plain SA goes (80 GiB at n = 2^34)
+    (void)hipFree(x->sa);
+    x->sa = ent.as<uint8_t>();
+    x->sa_w = 8;
+    ent.release();
+    const uint64_t keys = 1ull << (2 * p);
+    const uint64_t cap = (keys + 1) / (PT_SMALL + 1) + 2;
+    DevBuf t, big, nbig;
+    TRY(t.alloc((keys + 1) * 8 + 8, "tagged bucket table"));
+    TRY(big.alloc(cap * 24, "bucket table gap list"));
+    TRY(nbig.alloc(8, "bucket table gap count"));
+    HIP_TRY(hipMemset(nbig.p, 0, 8));
+    const uint64_t* ep = reinterpret_cast<const uint64_t*>(x->sa);
+    hipLaunchKernelGGL(k_tt_fill, dim3(grid_for(sa_n + 1)), b, 0, 0, x->text_w, ep, sa_n, p, t.as<uint64_t>(),
+                       big.as<uint64_t>(), nbig.as<unsigned long long>(), cap);
+    hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(),
+                       t.as<uint64_t>());
+    hipLaunchKernelGGL(k_tt_count, dim3(grid_for(keys)), b, 0, 0, t.as<uint64_t>(), keys);
+    HIP_TRY(hipGetLastError());
+    uint64_t nb = 0;
+    HIP_TRY(hipMemcpy(&nb, nbig.p, 8, hipMemcpyDeviceToHost));
+    if (nb > cap) SAS_FAIL(EFAULT, "bucket table: gap list overflow");  // cannot happen: gaps are disjoint
+    x->tag_table = t.as<uint64_t>();
+    t.release();
+    x->tag_p = p;
+    return 0;
+}
+
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
     void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->scratch, x->sec_inner,
-                     x->sec_leaves, x->quad_inner, x->quad_leaves};
+                     x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     delete x;
 }
@@ -996,7 +1101,10 @@ static int verify_sa(const uint64_t* tw, uint64_t n, const uint8_t* sa, uint32_t
     }
     TRY(bad.alloc(16, "verify flags"));
     HIP_TRY(hipMemset(bad.p, 0, 16));
-    if (w == 5)
+    if (w == 8)
+        hipLaunchKernelGGL(k_verify_adj<8>, dim3(grid_for(sa_n)), dim3(256), 0, 0, tw, n, SaView<8>{sa}, sa_n,
+                           full ? bitmap.as<uint32_t>() : nullptr, bad.as<uint32_t>());
+    else if (w == 5)
         hipLaunchKernelGGL(k_verify_adj<5>, dim3(grid_for(sa_n)), dim3(256), 0, 0, tw, n, SaView<5>{sa}, sa_n,
                            full ? bitmap.as<uint32_t>() : nullptr, bad.as<uint32_t>());
     else
@@ -1110,6 +1218,11 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         SAS_FAIL(EINVAL, "sas_build: sa_width must be 4 (u32), 5 (packed 40-bit) or 8 (u64)");
     if (sa_or_null && sa_width == 4 && n > 0xFFFFFFFFull) SAS_FAIL(EINVAL, "sas_build: a u32 SA cannot index n >= 2^32");
     if (rank_lo >= rank_hi || rank_hi > n) SAS_FAIL(EINVAL, "sas_build_shard: empty or out-of-range rank range");
+    if ((flags & SAS_BUILD_TAGGED) &&
+        (flags & (SAS_BUILD_STREE | SAS_BUILD_SECTOR | SAS_BUILD_QUAD | SAS_BUILD_QUAD_COMPACT | SAS_BUILD_LLCP |
+                  SAS_BUILD_PREFIX | SAS_BUILD_PREFIX_INLINE | SAS_BUILD_PREFIX_INLINE2 | SAS_BUILD_PREFIX_INLINE4)))
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_TAGGED replaces the SA: it combines with SAS_BUILD_LCP only, not with the "
+                          "trees, LLCP or the prefix tables");
     uint64_t t0 = now_ns();
     sas_index* x = new sas_index();
     x->n = n;
@@ -1255,6 +1368,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         HIP_TRY(hipGetLastError());
         x->top2 = static_cast<uint4*>(t2.release());
     }
+    if (flags & SAS_BUILD_TAGGED) TRY(build_tagged(x, (flags >> 16) & 31));
     HIP_TRY(hipMalloc(&x->scratch, 64));
     HIP_TRY(hipMemset(x->scratch, 0, 64));
     HIP_TRY(hipDeviceSynchronize());
@@ -1262,8 +1376,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     sas_stats& st = x->stats;
     st.n = n;
     st.text_bytes = x->text_words * 8;
-    st.sa_bytes = sa_n * W;
-    st.sa_width = W;
+    st.sa_bytes = sa_n * x->sa_w;
+    st.sa_width = x->sa_w;
     st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
     st.llcp_bytes = x->llcp ? sa_n * 16 : 0;
     st.prefix_bytes = x->prefix ? ((1ull << (2 * x->prefix_chars)) + 1) * x->prefix_w : 0;
@@ -1285,6 +1399,10 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.quad_entry_bytes = x->quad_leaves ? (x->quad_compact ? 8 : 16) : 0;
     st.quad_fan = x->quad_leaves ? x->quad_fan : 0;
     st.top2_levels = x->top2_levels;
+    st.tag_chars = x->tag_p;
+    st.tag_table_bytes = x->tag_table ? ((1ull << (2 * x->tag_p)) + 1) * 8 : 0;
+    st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
+                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + (uint64_t)SAS_TOP2_NODES * 16;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard
@@ -1320,7 +1438,7 @@ static int copy_out(const void* src, void* dst, uint64_t bytes, uint32_t flags) 
 
 extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t flags) {
     if (!index || !dst) SAS_FAIL(EINVAL, "sas_copy_sa: null argument");
-    if (index->sa_w != 4) SAS_FAIL(EINVAL, "sas_copy_sa: the SA is 40-bit (n >= 2^32 or SAS_BUILD_SA40): use sas_copy_sa64");
+    if (index->sa_w != 4) SAS_FAIL(EINVAL, "sas_copy_sa: the SA is not u32 (40-bit for n >= 2^32 or SAS_BUILD_SA40, or tagged): use sas_copy_sa64");
     if (count > index->sa_n) SAS_FAIL(EINVAL, "sas_copy_sa: count > number of SA entries");
     return copy_out(index->sa, dst, count * 4, flags);
 }
@@ -1328,7 +1446,7 @@ extern "C" int sas_copy_sa(const sas_index* index, uint32_t* dst, uint64_t count
 extern "C" int sas_copy_sa_range(const sas_index* index, uint64_t start, uint64_t count, uint32_t* dst,
                                  uint32_t flags) {
     if (!index || (count && !dst)) SAS_FAIL(EINVAL, "sas_copy_sa_range: null argument");
-    if (index->sa_w != 4) SAS_FAIL(EINVAL, "sas_copy_sa_range: the SA is 40-bit: use sas_copy_sa64");
+    if (index->sa_w != 4) SAS_FAIL(EINVAL, "sas_copy_sa_range: the SA is not u32 (40-bit or tagged): use sas_copy_sa64");
     if (start < index->rank_lo || start - index->rank_lo + count > index->sa_n)
         SAS_FAIL(EINVAL, "sas_copy_sa_range: ranks outside this index");
     if (count == 0) return 0;
@@ -1382,7 +1500,9 @@ extern "C" int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t co
         out = tmp.as<uint64_t>();
     }
     uint64_t s0 = start - index->rank_lo;
-    if (index->sa_w == 5)
+    if (index->sa_w == 8)
+        hipLaunchKernelGGL(k_widen_sa<8>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<8>{index->sa}, s0, count, out);
+    else if (index->sa_w == 5)
         hipLaunchKernelGGL(k_widen_sa<5>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<5>{index->sa}, s0, count, out);
     else
         hipLaunchKernelGGL(k_widen_sa<4>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<4>{index->sa}, s0, count, out);

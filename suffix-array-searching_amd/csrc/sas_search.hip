@@ -36,6 +36,7 @@
 #include <vector>
 
 #define SEARCH_BLOCK 1024
+#define TRY_RC(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
 #define BLOCKS_PER_CU 2
 
 struct SearchArgs {
@@ -75,6 +76,8 @@ struct SearchArgs {
     uint32_t quad_inner_layers;
     uint32_t quad_lds_layers;
     uint32_t quad_lds_nodes;
+    const uint64_t* tag_table;  // SAS_BUILD_TAGGED bucket table (sa = tagged entries, W = 8)
+    uint32_t tag_p;
     const uint8_t* qbytes;
     const uint64_t* qwords;  // sas_search_packed: 2-bit packed fixed-length queries (PREFIX)
     const uint64_t* qoff;
@@ -1211,7 +1214,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
         if (a.qwords) {  // packed fixed-length query: the key word itself
             q.bytes = nullptr;
             q.m = m;
-            q.w[0] = a.qwords[i];
+            q.w[0] = a.qwords[i] & chars_mask(m);
         } else {
             q.load(qb, m, &bad);
         }
@@ -1332,7 +1335,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
         if (a.qwords) {  // packed: the key word itself (both lanes, one 8-B request)
             q.bytes = nullptr;
             q.m = m;
-            q.w[0] = a.qwords[i];
+            q.w[0] = a.qwords[i] & chars_mask(m);
         } else if (split) {
             // the pair splits the 32-B query: lane j packs bytes 16j..16j+15 to 32 bits,
             // then the halves are swapped within the pair (DPP quad_perm [1,0,3,2])
@@ -1406,23 +1409,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
 // first suffix whose first min(m, len) chars are > q, bisected in the range of the
 // routing key (q padded with 3s for m <= 32, its own key above), with the predicates of
 // k_sa_quad_range over the quad leaves' entries.
-template <int QW, bool KO, int W, bool UPPER>
-__device__ __forceinline__ uint64_t prefix_bound(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64,
-                                                 uint64_t Q3, uint32_t sh) {
-    uint64_t lo, hi;
-    prefix_range(a, ((UPPER && q.m <= 32) ? Q3 : K64) >> sh, &lo, &hi);
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) >> 1;
-        const uint64_t key = quad_entry_key<KO>(a, mid);
-        const uint64_t tie = UPPER ? (q.m > 32 && key == K64) : (key == K64);
-        const uint64_t pp = tie ? quad_entry_sa<KO, W>(a, mid) : QUAD_NO_SA;
-        const bool pr = UPPER ? sector_gt_prefix<QW>(key, pp, K64, Q3, a, q) : sector_ge<QW>(key, pp, K64, a, q);
-        if (pr) hi = mid;
-        else lo = mid + 1;
-    }
-    return lo;
-}
-
 template <int QW, bool KO, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix_range(SearchArgs a, uint64_t* out_hi) {
     uint32_t bad = 0;
@@ -1459,7 +1445,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix_range(SearchArgs 
         if (hi < lo) hi = lo;
         a.out_pos[i] = a.rank_lo + lo;
         out_hi[i] = a.rank_lo + hi;
-        if (a.out_probes) a.out_probes[i] = 2;
     }
     if (bad) atomicOr(a.bad, 1u);
 }
@@ -1472,6 +1457,269 @@ static void launch_prefix_range(int qw, dim3 grid, dim3 block, hipStream_t st, c
         case 4: hipLaunchKernelGGL((k_sa_prefix_range<4, KO, W>), grid, block, 0, st, a, dhi); break;
         default: hipLaunchKernelGGL((k_sa_prefix_range<8, KO, W>), grid, block, 0, st, a, dhi); break;
     }
+}
+
+// ------------------------------------------------------------------ INTERP
+// interpolation_search<16> (sas/sa_search.rs:376-421), one lane per query.  string_value<16>
+// (sas/util.rs:76-117) of a suffix is the high half of its 32-char packed key; of the query,
+// the high half of its first packed word (zero padded past m).  The mid is the
+// reference's l + (r-l)(q_val - l_val + 1) / (r_val - l_val + 2) in wrapping u64 arithmetic
+// (its release build), clamped to [l + (r-l)/16, l + 15(r-l)/16] (:406-409), so l <= mid < r
+// and every probe is an exact compare: the result is binary_search's, the probe count the
+// reference's cnt.  FUSED: a probe reads the fused quad leaf entry {key64, SA} (one 16-B
+// request); otherwise SA[mid], then the text window (two dependent requests), as the
+// reference does.  range: start from the prefix table's range of q's first p chars (cnt + 1,
+// sas/sa_search.rs:86-89).
+template <int QW, int W, bool FUSED>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uint32_t range) {
+    uint32_t bad = 0;
+    const SaView<W> sa{a.sa};
+    const uint64_t sa_n = a.sa_n;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        uint64_t l = 0, r = sa_n;
+        uint32_t cnt = 0;
+        if (range) {
+            prefix_range(a, K64 >> (64 - 2 * a.prefix_chars), &l, &r);
+            cnt = 1;
+        }
+        auto probe = [&](uint64_t x, uint64_t* key) -> uint64_t {
+            if (FUSED) {
+                const uint4 e = nt_load4(a.quad_leaves + x);
+                *key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                return (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+            }
+            const uint64_t p = sa[x];
+            *key = text_chars32(a.tw, p);
+            return p;
+        };
+        uint64_t key = 0, l_val = 0, r_val = 1ull << 32, pr = QUAD_NO_SA;
+        if (l < sa_n) {  // sa.suffix(l) (:378)
+            (void)probe(l, &key);
+            l_val = key >> 32;
+        }
+        if (r < sa_n) {  // sa.suffix(r) when r < len, else 4^K (:379-383)
+            pr = probe(r, &key);
+            r_val = key >> 32;
+        }
+        const uint64_t q_val = K64 >> 32;
+        while (l < r) {
+            cnt++;
+            uint64_t mid = l + ((r - l) * (q_val - l_val + 1)) / (r_val - l_val + 2);
+            const uint64_t low = l + (r - l) / 16, high = l + 15 * (r - l) / 16;
+            mid = mid < low ? low : (mid > high ? high : mid);
+            const uint64_t p = probe(mid, &key);
+            if (sector_ge<QW>(key, p, K64, a, q)) {  // !(t < q)
+                r = mid;
+                r_val = key >> 32;
+                pr = p;
+            } else {
+                l = mid + 1;
+                l_val = key >> 32;
+            }
+        }
+        a.out_pos[i] = l >= sa_n ? a.next_pos : pr;  // pr = SA[r] (read or moved), l == r
+        if (a.out_probes) a.out_probes[i] = cnt;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// ------------------------------------------------------------------ TAGGED
+// SAS_BUILD_TAGGED (the configs[3] path): entries e[r] = {SA[r] 40 bits |
+// chars [p, p+12) of that suffix << 40} in rank order, and the bucket table of the
+// reference's prefix_range (sas/sa_search.rs:86-95) with p live: {first rank 40 bits |
+// count 24 bits} per p-char key.  Every entry of q's bucket shares q's (zero-padded) first p
+// chars, so the entry's tag extends that to a (p+12)-char key: "tag < q's tag" proves
+// suffix < q, "tag > q's tag" proves suffix > q, and only a tie needs the length (m <= p+12)
+// or an exact compare from char p+12 (the sector predicate with L = p + 12).  A lookup is:
+// the bucket word (one aligned 8-B read), the first SAS_TAG_WIN entries of the bucket as
+// independent loads (one or two 128-B lines: a bucket holds ~4 suffixes at n = 4^p), the
+// text past char p+12 of the single candidate whose tag ties q's (a positive query's own
+// suffix), and its position straight from the entry.  Larger buckets continue with a binary
+// search over the rest.
+#ifndef SAS_TAG_WIN
+#define SAS_TAG_WIN 8
+#endif
+#define TAG_M40 (SAS_SA40_MAX - 1)
+
+// chars [p, p+12) of a packed 32-char key (p + 12 <= 32)
+__device__ __forceinline__ uint32_t tag_of_key(uint64_t k64, uint32_t p) { return (uint32_t)((k64 << (2 * p)) >> 40); }
+
+// suffix(e) >= q, for an entry of q's bucket
+template <int QW>
+__device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArgs& a, const QueryRegs<QW>& q) {
+    const uint32_t T = (uint32_t)(e >> 40);
+    if (T != Q12) return T > Q12;
+    const uint64_t p = e & TAG_M40;
+    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+    if (q.m <= L) return (a.n - p) >= (uint64_t)q.m;  // equal padded keys: a shorter suffix is a prefix of q
+    uint32_t lcp;
+    return !suffix_less_from<QW>(a.tw, a.n, p, q, L, &lcp);
+}
+
+// the first min(m, len) chars of suffix(e) are > q, for an entry of the bucket of q's routing
+// key (Q3 = q padded with 3s when m <= p + 12, else q's own; as sector_gt_prefix)
+template <int QW>
+__device__ __forceinline__ bool tag_gt_prefix(uint64_t e, uint32_t Q12, uint32_t Q3t, const SearchArgs& a,
+                                              const QueryRegs<QW>& q) {
+    const uint32_t T = (uint32_t)(e >> 40);
+    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+    if (q.m <= L) return T > Q3t;
+    if (T != Q12) return T > Q12;
+    uint32_t lcp;
+    const bool lt = suffix_less_from<QW>(a.tw, a.n, e & TAG_M40, q, L, &lcp);
+    return !lt && lcp < q.m;
+}
+
+// ranks [lo, hi) of p-char key x (a saturated count reads the next bucket word)
+__device__ __forceinline__ void tag_bucket(const SearchArgs& a, uint64_t x, uint64_t* lo, uint64_t* hi) {
+    const uint64_t t = __builtin_nontemporal_load(a.tag_table + x);
+    *lo = t & TAG_M40;
+    const uint64_t c = t >> 40;
+    *hi = c == 0xFFFFFFull ? (a.tag_table[x + 1] & TAG_M40) : *lo + c;
+}
+
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged(SearchArgs a) {
+    uint32_t bad = 0;
+    const uint64_t* ent = reinterpret_cast<const uint64_t*>(a.sa);
+    const uint64_t sa_n = a.sa_n;
+    const uint32_t sh = 64 - 2 * a.tag_p;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint32_t Q12 = tag_of_key(K64, a.tag_p);
+        uint64_t lo, hi;
+        tag_bucket(a, K64 >> sh, &lo, &hi);
+        // candidates are ranks lo .. hi (rank hi = the next bucket's first suffix, > q: the
+        // answer when every suffix of the bucket is < q); the window holds the first nw
+        const uint64_t span = hi - lo + 1;
+        const uint32_t nw = span < SAS_TAG_WIN ? (uint32_t)span : (uint32_t)SAS_TAG_WIN;
+        uint64_t e[SAS_TAG_WIN];
+#pragma unroll
+        for (int j = 0; j < SAS_TAG_WIN; j++)
+            e[j] = ((uint32_t)j < nw && lo + j < sa_n) ? __builtin_nontemporal_load(ent + lo + j) : 0ull;
+        // first slot whose tag is >= q's (or rank hi): every slot before it is < q (tags are
+        // sorted within a bucket)
+        uint32_t j0 = nw;
+#pragma unroll
+        for (int j = SAS_TAG_WIN - 1; j >= 0; j--)
+            if ((uint32_t)j < nw && (lo + j == hi || (uint32_t)(e[j] >> 40) >= Q12)) j0 = (uint32_t)j;
+        uint64_t ej = e[0];
+#pragma unroll
+        for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
+        uint64_t ans = 0, pos = 0, start;
+        bool done = false;
+        if (j0 < nw) {
+            const uint64_t r = lo + j0;
+            if (r >= sa_n) {
+                ans = r;
+                pos = a.next_pos;
+                done = true;
+            } else if (r == hi || tag_ge<QW>(ej, Q12, a, q)) {
+                ans = r;
+                pos = ej & TAG_M40;
+                done = true;
+            }
+            start = r + 1;  // a tag tie whose suffix is < q
+        } else {
+            start = lo + nw;  // the whole window is < q
+        }
+        if (!done) {  // binary search over the rest of the bucket (rank hi if nothing qualifies)
+            uint64_t l2 = start, h2 = hi, pr = QUAD_NO_SA;
+            while (l2 < h2) {
+                const uint64_t mid = (l2 + h2) >> 1;
+                const uint64_t f = __builtin_nontemporal_load(ent + mid);
+                if (tag_ge<QW>(f, Q12, a, q)) {
+                    h2 = mid;
+                    pr = f & TAG_M40;
+                } else {
+                    l2 = mid + 1;
+                }
+            }
+            ans = l2;
+            pos = l2 >= sa_n ? a.next_pos : (pr != QUAD_NO_SA ? pr : (ent[l2] & TAG_M40));
+        }
+        a.out_pos[i] = pos;
+        if (a.out_probes) {  // the reference's cnt: the table, then binary_search over [lo, hi)
+            uint32_t probes = 1;
+            for (uint64_t l2 = lo, h2 = hi; l2 < h2; probes++) {
+                const uint64_t mid = (l2 + h2) >> 1;
+                if (mid < ans) l2 = mid + 1;
+                else h2 = mid;
+            }
+            a.out_probes[i] = probes;
+        }
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// Occurrence ranges on the tagged index: lo = the lower bound in q's bucket, hi = the first
+// suffix whose first min(m, len) chars are > q, in the bucket of the routing key; both
+// bisections advance in lock step (two entry reads in flight).
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_range(SearchArgs a, uint64_t* out_hi) {
+    uint32_t bad = 0;
+    const uint64_t* ent = reinterpret_cast<const uint64_t*>(a.sa);
+    const uint32_t sh = 64 - 2 * a.tag_p;
+    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
+        const uint32_t Q12 = tag_of_key(K64, a.tag_p), Q3t = tag_of_key(Q3, a.tag_p);
+        uint64_t lo, l1, hi, h1;
+        tag_bucket(a, K64 >> sh, &lo, &l1);
+        tag_bucket(a, (m <= L ? Q3 : K64) >> sh, &hi, &h1);
+        while (lo < l1 || hi < h1) {
+            const bool g0 = lo < l1, g1 = hi < h1;
+            const uint64_t m0 = (lo + l1) >> 1, m1 = (hi + h1) >> 1;
+            const uint64_t e0 = g0 ? __builtin_nontemporal_load(ent + m0) : 0;
+            const uint64_t e1 = g1 ? __builtin_nontemporal_load(ent + m1) : 0;
+            if (g0) {
+                if (tag_ge<QW>(e0, Q12, a, q)) l1 = m0;
+                else lo = m0 + 1;
+            }
+            if (g1) {
+                if (tag_gt_prefix<QW>(e1, Q12, Q3t, a, q)) h1 = m1;
+                else hi = m1 + 1;
+            }
+        }
+        if (hi < lo) hi = lo;
+        a.out_pos[i] = a.rank_lo + lo;
+        out_hi[i] = a.rank_lo + hi;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// Validation pass (SAS_VALIDATE, host-pointer calls): every byte of every query must be a
+// DNA code 0..3, including those past the words a search kernel holds in registers.
+__global__ void k_validate_queries(const uint8_t* __restrict__ qb, const uint64_t* __restrict__ qoff,
+                                   const uint32_t* __restrict__ qlen, uint32_t m_fixed, uint64_t nq,
+                                   uint32_t* __restrict__ bad) {
+    uint32_t b = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* q = qoff ? qb + qoff[i] : qb + i * (uint64_t)m_fixed;
+        const uint32_t m = qoff ? qlen[i] : m_fixed;
+        for (uint32_t k = 0; k < m; k++) b |= q[k];
+    }
+    if (b & 0xFCu) atomicOr(bad, 1u);
 }
 
 // ------------------------------------------------------------------ host dispatch
@@ -1551,6 +1799,41 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #undef QW_CASE
 }
 
+// INTERP: fused quad leaves (W = 4 instantiation, no SA reads) or SA + text at any width
+template <int W, bool FUSED>
+static void launch_interp(int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a, uint32_t range) {
+    switch (qw) {
+        case 1: hipLaunchKernelGGL((k_sa_interp<1, W, FUSED>), grid, block, 0, st, a, range); break;
+        case 2: hipLaunchKernelGGL((k_sa_interp<2, W, FUSED>), grid, block, 0, st, a, range); break;
+        case 4: hipLaunchKernelGGL((k_sa_interp<4, W, FUSED>), grid, block, 0, st, a, range); break;
+        default: hipLaunchKernelGGL((k_sa_interp<8, W, FUSED>), grid, block, 0, st, a, range); break;
+    }
+}
+
+// Tagged indexes (sa_w = 8): TAGGED, and PLAIN / LCP reading the SA values from the entries
+static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a) {
+#define QW_CASE(KERNEL_T)                                                           \
+    switch (qw) {                                                                   \
+        case 1: hipLaunchKernelGGL(KERNEL_T(1), grid, block, 0, st, a); break;      \
+        case 2: hipLaunchKernelGGL(KERNEL_T(2), grid, block, 0, st, a); break;      \
+        case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
+        default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
+    }
+#define K_TAGGED(Q) (k_sa_tagged<Q>)
+#define K8_PLAIN_TOP(Q) (k_sa_binary<Q, BS_PLAIN, true, 8>)
+#define K8_PLAIN(Q) (k_sa_binary<Q, BS_PLAIN, false, 8>)
+#define K8_LCP_TOP(Q) (k_sa_binary<Q, BS_MLR, true, 8>)
+#define K8_LCP(Q) (k_sa_binary<Q, BS_MLR, false, 8>)
+    if (algo == SAS_ALGO_TAGGED) {
+        QW_CASE(K_TAGGED)
+    } else if (algo == SAS_ALGO_PLAIN) {
+        if (top) { QW_CASE(K8_PLAIN_TOP) } else { QW_CASE(K8_PLAIN) }
+    } else {
+        if (top) { QW_CASE(K8_LCP_TOP) } else { QW_CASE(K8_LCP) }
+    }
+#undef QW_CASE
+}
+
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
     // inline prefix tables with G slots: G lanes per query
@@ -1563,7 +1846,14 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
     const bool range = (flags & SAS_PREFIX_RANGE) != 0;
-    if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
+    if (algo == SAS_ALGO_INTERP) {
+        if (x->quad_leaves && !x->quad_compact) launch_interp<4, true>(qw, grid, block, st, a, range);
+        else if (x->sa_w == 8) launch_interp<8, false>(qw, grid, block, st, a, range);
+        else if (x->sa_w == 5) launch_interp<5, false>(qw, grid, block, st, a, range);
+        else launch_interp<4, false>(qw, grid, block, st, a, range);
+    } else if (x->sa_w == 8) {
+        launch_w8(algo, top, qw, grid, block, st, a);
+    } else if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
         if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
         else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);
         else launch_quad<true, 4>(algo, top, qw, grid, block, st, a);
@@ -1630,6 +1920,31 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.quad_inner_layers = x->quad_inner_layers;
     a.quad_lds_layers = x->quad_lds_layers;
     a.quad_lds_nodes = x->quad_lds_nodes;
+    a.tag_table = x->tag_table;
+    a.tag_p = x->tag_p;
+}
+
+// Algorithm / index / flag compatibility, shared by the search entry points.
+static int check_algo(const sas_index* x, int algo, uint32_t flags, const char* where) {
+    const std::string w(where);
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_TAGGED) SAS_FAIL(EINVAL, w + ": unknown algo");
+    if ((flags & SAS_PREFIX_RANGE) &&
+        (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP && algo != SAS_ALGO_INTERP)))
+        SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP / INTERP on an index with SAS_BUILD_PREFIX");
+    if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
+    if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, w + ": SAS_ALGO_LLCP needs SAS_BUILD_LLCP");
+    if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
+        SAS_FAIL(EINVAL, w + ": SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
+    if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, w + ": SAS_ALGO_STREE needs SAS_BUILD_STREE");
+    if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, w + ": SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
+    if (algo == SAS_ALGO_TAGGED && !x->tag_table) SAS_FAIL(EINVAL, w + ": SAS_ALGO_TAGGED needs SAS_BUILD_TAGGED");
+    if (x->sa_w == 8 && algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP && algo != SAS_ALGO_INTERP &&
+        algo != SAS_ALGO_TAGGED)
+        SAS_FAIL(EINVAL, w + ": a tagged index (SAS_BUILD_TAGGED) serves TAGGED, PLAIN, LCP and INTERP");
+    if (algo == SAS_ALGO_INTERP && x->n >= (1ull << 32))
+        SAS_FAIL(ENOTSUP, w + ": interpolation_search<16> needs n < 2^32 (the reference asserts r_val * r "
+                              "fits a usize, sas/sa_search.rs:389-392)");
+    return 0;
 }
 
 struct DeviceBuf {
@@ -1643,15 +1958,7 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "search: null index");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "search: unknown algo");
-    if ((flags & SAS_PREFIX_RANGE) && (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP)))
-        SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP on an index with SAS_BUILD_PREFIX");
-    if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
-    if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "search: SAS_ALGO_LLCP needs SAS_BUILD_LLCP");
-    if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
-        SAS_FAIL(EINVAL, "search: SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
-    if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "search: SAS_ALGO_STREE needs SAS_BUILD_STREE");
-    if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "search: SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
+    TRY_RC(check_algo(x, algo, flags, "search"));
     if (nq == 0) return 0;
     if (!out_pos) SAS_FAIL(EINVAL, "search: null out_pos");
     if (!qbytes) SAS_FAIL(EINVAL, "search: null qbytes");
@@ -1719,6 +2026,12 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
             HIP_TRY(hipMalloc(&bprobes.p, nq * 4));
             a.out_probes = static_cast<uint32_t*>(bprobes.p);
         }
+    }
+    if (check_bad) {  // every query byte, not only those the search kernel packs
+        uint64_t vb = (nq + 255) / 256;
+        if (vb > 65536) vb = 65536;
+        hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, st, a.qbytes, a.qoff, a.qlen,
+                           a.m_fixed, nq, a.bad);
     }
     int rc = launch_search(x, a, algo, qw, flags, st);
     if (rc) return rc;
@@ -1824,15 +2137,7 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
                               uint64_t* d_out_pos, int reps, void* stream, uint32_t flags, double* kernel_ns,
                               double* call_ns) {
     if (!x || !d_qbytes || !d_out_pos || reps < 1) SAS_FAIL(EINVAL, "sas_time_fixed: bad argument");
-    if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, "sas_time_fixed: index has no S-tree");
-    if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, "sas_time_fixed: index has no sector tree");
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_PREFIX) SAS_FAIL(EINVAL, "sas_time_fixed: unknown algo");
-    if ((flags & SAS_PREFIX_RANGE) && (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP)))
-        SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP on an index with SAS_BUILD_PREFIX");
-    if (algo == SAS_ALGO_PREFIX && !x->prefix) SAS_FAIL(EINVAL, "SAS_ALGO_PREFIX needs SAS_BUILD_PREFIX");
-    if (algo == SAS_ALGO_LLCP && !x->llcp) SAS_FAIL(EINVAL, "sas_time_fixed: index has no LLCP entries");
-    if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
-        SAS_FAIL(EINVAL, "sas_time_fixed: index has no quad tree");
+    TRY_RC(check_algo(x, algo, flags, "sas_time_fixed"));
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     SearchArgs a{};
@@ -2073,8 +2378,8 @@ static void launch_quad_range(int qw, dim3 grid, dim3 block, hipStream_t st, con
 extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
                                 uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
-    if (!x->sec_leaves && !x->quad_leaves)
-        SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_QUAD or SAS_BUILD_SECTOR");
+    if (!x->sec_leaves && !x->quad_leaves && !x->tag_table)
+        SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_QUAD, SAS_BUILD_SECTOR or SAS_BUILD_TAGGED");
     const bool quad = x->quad_leaves != nullptr;
     if (nq == 0) return 0;
     if (!qbytes || !qoff || !qlen || !out_lo || !out_hi) SAS_FAIL(EINVAL, "sas_search_range: null argument");
@@ -2123,13 +2428,26 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
         a.out_pos = static_cast<uint64_t*>(blo.p);
         dhi = static_cast<uint64_t*>(bhi.p);
     }
+    if (check_bad) {
+        uint64_t vb = (nq + 255) / 256;
+        if (vb > 65536) vb = 65536;
+        hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, st, a.qbytes, a.qoff, a.qlen, 0u,
+                           nq, a.bad);
+    }
     // the prefix table, when built, replaces the two tree descents (one lane per query)
     const bool ptab = quad && x->prefix && !(flags & SAS_NO_PREFIX_TABLE);
     uint64_t blocks = (nq * ((quad && !ptab) ? QUAD_G : 1) + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    if (ptab) {
+    if (x->tag_table) {
+        switch (qw) {
+            case 1: hipLaunchKernelGGL(k_sa_tagged_range<1>, grid, block, 0, st, a, dhi); break;
+            case 2: hipLaunchKernelGGL(k_sa_tagged_range<2>, grid, block, 0, st, a, dhi); break;
+            case 4: hipLaunchKernelGGL(k_sa_tagged_range<4>, grid, block, 0, st, a, dhi); break;
+            default: hipLaunchKernelGGL(k_sa_tagged_range<8>, grid, block, 0, st, a, dhi); break;
+        }
+    } else if (ptab) {
         if (!x->quad_compact) launch_prefix_range<false, 4>(qw, grid, block, st, a, dhi);
         else if (x->sa_w == 5) launch_prefix_range<true, 5>(qw, grid, block, st, a, dhi);
         else launch_prefix_range<true, 4>(qw, grid, block, st, a, dhi);

@@ -36,6 +36,7 @@ SAS_BUILD_PREFIX = 1 << 14
 SAS_BUILD_PREFIX_INLINE = 1 << 15
 SAS_BUILD_PREFIX_INLINE2 = 1 << 21
 SAS_BUILD_PREFIX_INLINE4 = 1 << 22
+SAS_BUILD_TAGGED = 1 << 23
 
 
 def SAS_BUILD_PREFIX_P(p: int) -> int:
@@ -43,7 +44,8 @@ def SAS_BUILD_PREFIX_P(p: int) -> int:
 
 
 SAS_MULTI_REPLICATE, SAS_MULTI_SHARD = 0, 1
-ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, "llcp": 6, "prefix": 7}
+ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, "llcp": 6, "prefix": 7,
+         "interp": 8, "tagged": 9}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP, SST_DIRECT_MAP = 0, 1, 2, 3, 4, 5
 SST_LEFT_MAX = 1 << 0
@@ -64,7 +66,8 @@ class SasStats(C.Structure):
         ("quad_bytes", C.c_uint64), ("quad_layers", C.c_uint32), ("quad_lds_layers", C.c_uint32),
         ("quad_entry_bytes", C.c_uint32),
         ("quad_fan", C.c_uint32), ("top2_levels", C.c_uint32), ("llcp_bytes", C.c_uint64),
-        ("prefix_bytes", C.c_uint64), ("prefix_chars", C.c_uint32),
+        ("prefix_bytes", C.c_uint64), ("prefix_chars", C.c_uint32), ("tag_chars", C.c_uint32),
+        ("tag_table_bytes", C.c_uint64), ("index_bytes", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -94,10 +94,11 @@ class SaNaive:
         self.rank_lo = self.stats()["rank_lo"]
 
     @classmethod
-    def build(cls, t, sa=None, lcp: bool = True, stree: bool = True, verify: bool = False,
-              rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool = True,
-              sa40: bool = False, quad: bool | str = True, llcp: bool | None = None,
-              prefix: bool | int | None = None, prefix_inline: bool | int = False) -> "SaNaive":
+    def build(cls, t, sa=None, lcp: bool = True, stree: bool | None = None, verify: bool = False,
+              rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool | None = None,
+              sa40: bool = False, quad: bool | str | None = None, llcp: bool | None = None,
+              prefix: bool | int | None = None, prefix_inline: bool | int = False,
+              tagged: bool | int = False) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
@@ -108,9 +109,19 @@ class SaNaive:
         (SAS_BUILD_PREFIX; None = whenever quad is built and n < 2^32 - 1, an int = its
         p chars); prefix_inline: 16-B entries that inline each range's first suffix
         (True / 1: SAS_BUILD_PREFIX_INLINE) or 32-B ones with its first two (2:
-        SAS_BUILD_PREFIX_INLINE2); fused quad leaves, u32 SA."""
+        SAS_BUILD_PREFIX_INLINE2); fused quad leaves, u32 SA.  tagged: the SA as 8-B tagged
+        entries + a bucket table over the first p chars (SAS_BUILD_TAGGED; True = p chosen by
+        the library, an int = that p) for algo="tagged"; it replaces the SA and leaves out the
+        trees, LLCP and the prefix tables (their defaults turn off)."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
+        if tagged is not False:
+            stree, sector, quad, prefix = bool(stree), bool(sector), quad or False, prefix or False
+            llcp = bool(llcp)
+            flags |= _lib.SAS_BUILD_TAGGED | (0 if tagged is True else _lib.SAS_BUILD_PREFIX_P(int(tagged)))
+        stree = True if stree is None else stree
+        sector = True if sector is None else sector
+        quad = True if quad is None else quad
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
         if llcp is None:
             llcp = n < (1 << 31)
@@ -356,7 +367,7 @@ class SaNaive:
         buf = np.concatenate([q, np.zeros(64, np.uint8)])
         lo, hi = self.search_range(buf, np.zeros(1, np.uint64), np.array([len(q)], np.uint32))
         cnt = int(hi[0] - lo[0])
-        if self.stats()["sa_width"] == 5:
+        if self.stats()["sa_width"] != 4:
             out = np.zeros(max(cnt, 1), np.uint64)
             check(lib().sas_copy_sa64(self._h, int(lo[0]), cnt, out.ctypes.data, 0))
             return out[:cnt]

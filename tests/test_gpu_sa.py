@@ -19,7 +19,7 @@ from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix")
+ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix", "interp")
 
 
 @pytest.fixture(scope="module")
@@ -737,7 +737,7 @@ def test_sa_beyond_u32(sas):
     idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True, llcp=False)  # LLCP: the second index below
     st = idx.stats()
     assert st["sa_width"] == 5 and st["n"] == n
-    algos = [a for a in ALGOS if a not in ("llcp", "prefix")]  # prefix: u32 ranks, n < 2^32 only
+    algos = [a for a in ALGOS if a not in ("llcp", "prefix", "interp")]  # prefix: u32 ranks; interp: n < 2^32
     ht = t.cpu().numpy()
     del t
     torch.cuda.empty_cache()

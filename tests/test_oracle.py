@@ -131,6 +131,28 @@ def test_binary_search_matches_definition(sadef):
             assert cnt <= int(np.log2(max(n, 1))) + 1
 
 
+def test_interpolation_search_matches_definition(sadef):
+    """interpolation_search<16> (sas/sa_search.rs:376-421) returns binary_search's position
+    on every definition-fixture query (its mids are clamped inside (l, r), so only the
+    probe count differs); the count is at least 1 for a non-empty range.  The count
+    itself has no reference-held vector (parity unpinned beyond this restatement)."""
+    for c in sadef["cases"]:
+        t = np.array(c["text"], np.uint8)
+        n = len(t)
+        sa = np.array(c["sa"], np.uint32)
+        tp = O.padded(t)
+        for qd in c["queries"]:
+            pos, cnt = O.interpolation_search(tp, n, sa, np.array(qd["q"], np.uint8))
+            assert pos == qd["pos"], (c["name"], qd)
+            assert 1 <= cnt <= n
+    t = O.random_string(1 << 16)
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    off, _, _ = O.random_queries(1 << 16, 500, len_lo=16, len_hi=17)
+    cnts = [O.interpolation_search(tp, 1 << 16, sa, t[o:o + 16])[1] for o in off.astype(np.int64)]
+    assert np.mean(cnts) < 17  # fewer probes than binary search's 17 on uniform keys
+
+
 def test_batch_and_threads_match_canonical(sadef):
     c = [c for c in sadef["cases"] if c["name"] == "random_4096"][0]
     t = np.array(c["text"], np.uint8)
