@@ -4,17 +4,31 @@ BASELINE.json metric: "pattern lookups/s + achieved HBM GB/s, 2^30-byte text,
 10^7 len-32 queries".  One step = one batched lookup of all queries of this
 GPU (inputs already resident in HBM), through the C ABI (sas_search_fixed).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--algo stree|plain|lcp]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--algo prefix|plain|quad|...]
     torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
 
-Multi-GPU: the index is replicated (the text is generated and indexed on every
-GPU), each rank searches its own 10^7 queries -> weak scaling, no collective on
-the data path; only the timing barrier and a MAX all-reduce of elapsed times.
+One JSON line.  `value` is the headline algorithm (PREFIX: a p = 16-char bucket table with
+32-B inline entries over fused quad leaves) on the configs[1]/[2] workload; `configs` holds
+one sub-record per BASELINE config, each with its own algorithm, index size, bytes per
+lookup split by where they are served (HBM / Infinity-Cache-resident arrays / LDS), PMC
+traffic where a committed --pmc pass exists, and ns per lookup:
+    c0: the reference's CPU plumbing case (1 MiB text, 10^4 x len-16) timed on the host
+        (oracle restatement, 1 thread and all cores), and the GPU on the same queries;
+    c1: PLAIN binary search (sas/sa_search.rs:98-112) on the same 2^30 index;
+    c2: the fastest LCP / S-tree layout with LDS-staged top layers;
+    c3: n = 2^34 text (the configs[3] deviation), 10^8 ragged 8..256 queries
+        on the tagged index (run after the 2^30 index is freed; N = 1 only).
+Every variant's positions must equal the headline's bit for bit, and a sample of each
+batch is proven an exact lower bound (SA[lo-1] < q <= SA[lo], SA[lo] = answer) on the GPU
+index's own SA; any mismatch exits non-zero.
+
+Multi-GPU: the index is replicated (the text is generated and indexed on every GPU), each
+rank searches its own 10^7 queries -> weak scaling, no collective on the data path; only
+the timing barrier and a MAX all-reduce of elapsed times.
 """
 from __future__ import annotations
 
 import argparse
-import glob
 import json
 import os
 import sys
@@ -33,32 +47,92 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # independent random 4-B loads over a 4 GiB buffer, one 128-B line each: the chip's
 # random-request ceiling (tools/randbench.hip, profiles/r1/randbench_calibration.jsonl)
 RANDOM_REQ_CEILING = 5.084e10
+CACHE_BYTES = 256 << 20  # Infinity Cache (MALL): arrays at most this large count as cache-served
 SEED = 31415  # sas/main.rs:38
+TOP_LDS_LEVELS, TOP2_LEVELS = 12, 21  # binary-search levels served from LDS / the 32 MiB top2 array
+
+KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
+           "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
+           "tagged": "k_sa_tagged"}
 
 
-def algorithmic_bytes(algo: str, n: int, m: int, stree_layers: int, tail_probes: float,
-                      sector_layers: int = 0, quad_layers: int = 0, prefix_entry: int = 8) -> float:
-    """Bytes a lookup must move: 4 B SA word + m text bytes per
-    probe, the query, the 8 B position.  PLAIN/LCP: P = ilog2(n)+1 probes.
-    STREE: H 64-B nodes + measured tail probes.  SECTOR: H 32-B nodes (the
-    leaf holds the keys and the SA values) + measured extra leaf probes x 12 B.
-    QUAD: H 64-B nodes (4-entry leaves) + measured extra leaf probes x 64 B."""
-    if algo == "stree":
-        return stree_layers * 64 + tail_probes * (4 + m) + m + 8
-    if algo == "sector":
-        return sector_layers * 32 + tail_probes * 12 + m + 8
-    if algo == "quad":
-        return quad_layers * 64 + tail_probes * 64 + m + 8
-    if algo == "prefix":  # the table entry (two u32, or one 16-B inline entry) + probes of
-        # 16-B fused entries; probes = the reference's cnt, which counts the table once
-        return prefix_entry + max(0.0, tail_probes - 1) * 16 + m + 8
-    if algo == "inline":  # P probes of one 16-B fused (key, SA) entry
-        P = int(np.log2(n)) + 1
-        return P * 16 + m + 8
+# ---------------------------------------------------------------- bytes per lookup
+def _tree_layers(n: int, leaf_entries: int, leaf_bytes: int, fan: int, node_bytes: int, layers: int):
+    """Footprint in bytes of each layer of a tree over n entries, root first (layers counts
+    the leaf layer)."""
+    cnt = -(-n // leaf_entries)
+    sizes = [cnt * leaf_bytes]
+    for _ in range(layers - 1):
+        cnt = -(-cnt // fan)
+        sizes.append(cnt * node_bytes)
+    return sizes[::-1]
+
+
+def _classify(sizes, node_bytes, lds_layers):
+    """(hbm, cache, lds) bytes of one node read per layer"""
+    hbm = cache = lds = 0.0
+    for h, sz in enumerate(sizes):
+        if h < lds_layers:
+            lds += node_bytes
+        elif sz <= CACHE_BYTES:
+            cache += node_bytes
+        else:
+            hbm += node_bytes
+    return hbm, cache, lds
+
+
+def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range_flag: bool = False,
+                     packed: bool = False) -> dict:
+    """Algorithmic bytes one lookup moves on this index's layout (2-bit packed text: a
+    compare window of m chars is m/4 bytes), split by where they are served: `hbm`
+    (arrays larger than the 256 MiB Infinity Cache, and the query/position streams),
+    `cache` (arrays that fit it) and `lds` (top levels staged per workgroup).  `probes` is
+    the measured mean of out_probes (the reference's cnt where it applies).  Also returns
+    SURVEY §8(d)'s reference-layout figure for PLAIN (byte text)."""
+    io = (8.0 if packed else m) + 8  # query in, position out
+    win = m / 4.0  # packed text window of a full compare
     P = int(np.log2(n)) + 1
-    return P * (4 + m) + m + 8
+    hbm = cache = lds = 0.0
+    sa_w = st["sa_width"]
+    if algo == "prefix" and not range_flag:
+        entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)
+        hbm += entry  # the table entry (inline entries hold the range's first suffixes)
+        leaf = 16 if st["quad_entry_bytes"] == 16 else 8 + sa_w
+        hbm += max(0.0, probes - 1) * leaf
+    elif algo == "tagged":
+        hbm += 8 + min(n / 4 ** st["tag_chars"] + 1, 8) * 8 + max(0.0, m - st["tag_chars"] - 12) / 4
+    elif range_flag:  # PLAIN / LCP from the prefix table's range: table entry + SA word + window per probe
+        entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)
+        hbm += entry + max(0.0, probes - 1) * (sa_w + win)
+    elif algo in ("plain", "lcp", "inline", "llcp", "interp"):
+        per = {"plain": sa_w + win, "lcp": sa_w + win, "inline": 16, "llcp": 16, "interp": 16}[algo]
+        if algo in ("plain", "lcp", "inline", "llcp"):
+            lds += min(probes, TOP_LDS_LEVELS) * 12
+            cache += max(0.0, min(probes, TOP2_LEVELS) - TOP_LDS_LEVELS) * 16
+            hbm += max(0.0, probes - TOP2_LEVELS) * per
+        else:
+            hbm += probes * per
+    elif algo in ("stree", "quad", "sector"):
+        if algo == "stree":
+            H, node, lds_l = st["stree_layers"], 64, st["stree_lds_layers"]
+            sizes = _tree_layers(n, 16, 64, 17, 64, H)
+            tail = sa_w + win
+        elif algo == "sector":
+            H, node, lds_l = st["sector_layers"], 32, st["sector_lds_layers"]
+            sizes = _tree_layers(n, 2, 32, 9, 32, H)
+            tail = 12
+        else:
+            H, node, lds_l = st["quad_layers"], 64, st["quad_lds_layers"]
+            leaf_entries = 4 if st["quad_entry_bytes"] == 16 else 8
+            sizes = _tree_layers(n, leaf_entries, 64, st["quad_fan"], 64, H)
+            tail = 64
+        h, c, l = _classify(sizes, node, lds_l)
+        hbm, cache, lds = h + max(0.0, probes - H) * tail + (max(0.0, m - 32) / 4 if algo != "stree" else 0), c, l
+    hbm += io
+    return {"hbm": hbm, "cache": cache, "lds": lds, "section_8d_plain": P * (4 + m) + m + 8}
 
 
+# ---------------------------------------------------------------- harness
 def timed_loop(step, steps: int, warmup: int, sync, barrier, reduce_max):
     """W untimed steps, then K steps bracketed by barrier + device sync on both
     sides; returns the MAX over ranks of the elapsed seconds."""
@@ -105,6 +179,10 @@ def keep_stdout_for_result() -> None:
         os.dup2(2, 1)
 
 
+def log(msg: str) -> None:
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def dist_env():
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -112,18 +190,16 @@ def dist_env():
     return ws, rank, local
 
 
-def load_traffic(algo: str, n: int, nq: int, m: int, with_requests: bool = False):
-    """HBM bytes per launch from a committed rocprofv3 --pmc pass of this exact
-    workload (profiles/pmc_<algo>_n<n>_q<nq>_m<m>.json, written by
-    tools/pmc_to_json.py), or None; with_requests: also its L2->fabric read
-    requests per launch (TCC_EA0_RDREQ)."""
-    path = os.path.join(REPO, "profiles", f"pmc_{algo}_n{n}_q{nq}_m{m}.json")
+def load_pmc(key: str):
+    """The committed rocprofv3 --pmc summary of this exact workload
+    (profiles/pmc_<key>.json, written by tools/pmc_to_json.py): HBM bytes and L2->fabric
+    read requests per launch, or None."""
+    path = os.path.join(REPO, "profiles", f"pmc_{key}.json")
     if not os.path.exists(path):
-        return (None, None, None) if with_requests else (None, None)
+        return None
     d = json.load(open(path))
-    if with_requests:
-        return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO), d.get("TCC_EA0_RDREQ")
-    return d.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+    return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"), "rdreq_per_launch": d.get("TCC_EA0_RDREQ"),
+            "source": os.path.relpath(path, REPO)}
 
 
 def host_cpu() -> str:
@@ -136,33 +212,104 @@ def host_cpu() -> str:
     return "unknown"
 
 
+def host_threads() -> int:
+    """Every core this process may run on (its affinity mask)."""
+    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+
+
+def record(name, lookups, kernel_ms, wall_s, bpl, idx_bytes, pmc, probes, extra=None):
+    """One sub-record for one launch of `lookups` queries: throughput, ns per lookup, bytes
+    per lookup split by where they are served, achieved HBM GB/s (HBM bytes only), PMC
+    traffic if a pass exists.  wall_s: the host clock over the timed steps (for
+    lookups_per_s the caller sets)."""
+    r = {"algo": name, "kernel_ms": kernel_ms,
+         "kernel_lookups_per_s": lookups / (kernel_ms * 1e-3), "ns_per_lookup": kernel_ms * 1e6 / lookups,
+         "mean_probes": probes, "bytes_per_lookup": bpl,
+         "achieved_hbm_GBps": bpl["hbm"] * lookups / (kernel_ms * 1e-3) / 1e9,
+         "achieved_cache_GBps": bpl["cache"] * lookups / (kernel_ms * 1e-3) / 1e9,
+         "index_bytes": idx_bytes}
+    if pmc and pmc.get("hbm_bytes_per_launch"):
+        r["pmc"] = {"fabric_bytes_per_lookup": pmc["hbm_bytes_per_launch"] / lookups,
+                    "fabric_GBps": pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9,
+                    "requests_per_lookup": (pmc["rdreq_per_launch"] or 0) / lookups,
+                    "requests_frac_of_ceiling": (pmc["rdreq_per_launch"] or 0) / (kernel_ms * 1e-3) /
+                    RANDOM_REQ_CEILING,
+                    "source": pmc["source"]}
+    if extra:
+        r.update(extra)
+    return r
+
+
+# ---------------------------------------------------------------- correctness guard
+def lower_bound_proof(idx, window, qwin, out, sample_ids) -> int:
+    """For each sampled query i: lo = its occurrence range's first rank (sas_search_range),
+    and the proof that lo is the lower bound on the index's own (verified) SA:
+    SA[lo] == out[i], suffix(SA[lo-1]) < q <= suffix(SA[lo]) in Rust slice order.
+    window(p, L) -> the text chars [p, min(p+L, n)); qwin(i) -> query i; out[j] = the
+    answer of sample_ids[j].  Returns the count of failures."""
+    n = idx.n
+    bad = 0
+    qs = [np.asarray(qwin(int(i)), np.uint8) for i in sample_ids]
+    lens = np.array([len(q) for q in qs], np.uint32)
+    off = np.zeros(len(qs), np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    buf = np.concatenate(qs + [np.zeros(64, np.uint8)])
+    lo, _ = idx.search_range(buf, off, lens)
+
+    def less(a, q):  # Rust slice order a < q
+        k = min(len(a), len(q))
+        d = np.nonzero(a[:k] != q[:k])[0]
+        if len(d):
+            return a[d[0]] < q[d[0]]
+        return len(a) < len(q)
+
+    for j in range(len(sample_ids)):
+        q, r = qs[j], int(lo[j]) - idx.rank_lo
+        if r < idx.sa_n:
+            sa2 = idx.suffix_array(count=2 if r > 0 else 1, start=r - 1 if r > 0 else 0).astype(np.int64)
+            p0, prev = int(sa2[-1]), (int(sa2[0]) if r > 0 else None)
+        else:
+            p0 = n
+            prev = int(idx.suffix_array(count=1, start=r - 1)[0]) if r > 0 else None
+        if p0 != int(out[j]):
+            bad += 1
+            continue
+        if p0 < n and less(window(p0, len(q)), q):
+            bad += 1
+        if prev is not None and not less(window(prev, len(q)), q):
+            bad += 1
+    return bad
+
+
+# ---------------------------------------------------------------- CPU baselines
 def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
-    """The oracle's restatement of the reference CPU search, timed on this host's
-    cores on a bounded sample of the same queries (rank 0, N=1 only)."""
+    """The oracle's restatement of the reference CPU search, timed on all of this host's
+    cores (its affinity mask) and on 1 thread, on a bounded sample of the same queries
+    (rank 0, N = 1 only).  Its answers are returned for comparison with the GPU's."""
     from oracle import pyoracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()))
+    threads = host_threads()
     n = idx.n
     t = O.padded(text_dev.cpu().numpy())
     sa = idx.suffix_array()
     best = None
     for algo in ("binary_search", "batch_c16"):
-        sample = min(nq, 50_000)
+        sample = min(nq, 100_000)
         while True:
             qb = np.concatenate([qbytes_dev[: sample * m].cpu().numpy(), np.zeros(64, np.uint8)])
             off = np.arange(sample, dtype=np.uint64) * m
             ln = np.full(sample, m, np.uint32)
             t0 = time.perf_counter()
-            O.search_many(t, n, sa, qb, off, ln, algo, threads)
+            pos, _ = O.search_many(t, n, sa, qb, off, ln, algo, threads)
             dt = time.perf_counter() - t0
             if dt * 2 > seconds / 2 or sample >= nq:
                 break
             sample = min(nq, int(sample * max(2.0, (seconds / 2) / max(dt, 1e-3))))
         rate = sample / dt
         if best is None or rate > best[0]:
-            best = (rate, algo, sample, dt)
-    rate, algo, sample, dt = best
+            best = (rate, algo, sample, dt, pos)
+    rate, algo, sample, dt, pos = best
     # one thread on a smaller sample of the same queries (SURVEY §8d: 1 thread and all cores)
-    s1 = min(nq, max(1000, int(sample * (seconds / 8) / max(dt * threads, 1e-3))))
+    s1 = min(nq, max(1000, int(rate / threads * seconds / 8)))
     qb = np.concatenate([qbytes_dev[: s1 * m].cpu().numpy(), np.zeros(64, np.uint8)])
     t0 = time.perf_counter()
     O.search_many(t, n, sa, qb, np.arange(s1, dtype=np.uint64) * m, np.full(s1, m, np.uint32), algo, 1)
@@ -172,9 +319,193 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
             "sample": f"oracle/{algo} (restates sas/sa_search.rs "
                       f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
                       f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA, {dt:.1f} s, "
-                      f"{threads} threads, contiguous chunks (sst/bin/bench.rs:558-573)"}
+                      f"{threads} threads (every core of this process's affinity mask), contiguous chunks "
+                      f"(sst/bin/bench.rs:558-573)", "_pos": pos}
 
 
+def c0_record(torch, sas_amd, dev, seconds: float):
+    """configs[0]: the reference's CPU run shape (1 MiB ChaCha8 text, 10^4 len-16 queries,
+    sas/main.rs:38-61) timed through the oracle restatement on 1 thread and all cores,
+    repeated to ~seconds, and the GPU on the same queries; answers compared."""
+    from oracle import pyoracle as O
+    n, nq, m = 1 << 20, 10_000, 16
+    t = O.random_string(n, SEED)
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    off, _, _ = sas_amd.random_queries(n, nq, seed=SEED, len_lo=m, len_hi=m + 1)
+    qb = np.concatenate([t[o:o + m] for o in off.astype(np.int64)] + [np.zeros(64, np.uint8)])
+    qoff = np.arange(nq, dtype=np.uint64) * m
+    ln = np.full(nq, m, np.uint32)
+    res = {}
+    allc = host_threads()
+    for threads in sorted({1, allc}):
+        reps, dt = 0, 0.0
+        t0 = time.perf_counter()
+        while dt < seconds / 2:
+            pos, _ = O.search_many(tp, n, sa, qb, qoff, ln, "binary_search", threads)
+            reps += 1
+            dt = time.perf_counter() - t0
+        res[threads] = (reps * nq / dt, pos)
+    idx = sas_amd.SaNaive.build(torch.from_numpy(t).to(dev), lcp=True, prefix=8)
+    dq = torch.from_numpy(qb[: nq * m]).to(dev)
+    out = idx.search_fixed(dq, m, algo="plain")
+    torch.cuda.synchronize()
+    gpu_ok = bool(np.array_equal(out.cpu().numpy().astype(np.uint64), res[1][1]))
+    if not gpu_ok:
+        raise SystemExit("bench c0: GPU positions differ from the CPU restatement")
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        idx.search_fixed(dq, m, algo="plain", out=out)
+    e1.record()
+    torch.cuda.synchronize()
+    gms = e0.elapsed_time(e1) / 20
+    idx.free()
+    return {"workload": "configs[0]: 1 MiB random ACGT text (ChaCha8Rng(31415)), 10^4 len-16 positive queries",
+            "cpu_1thread_lookups_per_s": res[1][0], "cpu_all_cores_lookups_per_s": res[allc][0],
+            "cpu_cores": allc, "cpu_kind": "port: oracle/binary_search (restates sas/sa_search.rs:98-112)",
+            "cpu_ns_per_lookup_1thread": 1e9 / res[1][0], "host_cpu": host_cpu(),
+            "gpu_plain_kernel_ms": gms, "gpu_lookups_per_s": nq / (gms * 1e-3),
+            "gpu_matches_cpu": gpu_ok,
+            "note": "10^4 queries are ~0.1 ms of GPU work: launch-bound, a plumbing check, not a GPU benchmark"}
+
+
+# ---------------------------------------------------------------- configs[3]
+def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plain",)):
+    """configs[3]-shaped run: n = 2^34 chars (16 GiB of byte-coded text; BASELINE's
+    "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and 10^8 positive
+    queries of mixed length 8..256 (random_queries with len in [8, 257), sas/util.rs:18-26),
+    ragged, through sas_search_batch on device buffers.  TAGGED: 8-B tagged SA entries + a
+    p = 16 bucket table (SAS_BUILD_TAGGED); PREFIX / QUAD: compact key-only quad leaves
+    beside the 40-bit SA (+ a p = 16 40-bit rank table for PREFIX)."""
+    n = args.c3_n
+    nq = args.c3_nq
+    t0 = time.perf_counter()
+    text = sas_amd.random_string(n, seed=SEED, device=dev)
+    # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
+    if algo == "tagged":
+        idx = sas_amd.SaNaive.build(text, lcp=False, verify=True, tagged=True)
+    else:
+        idx = sas_amd.SaNaive.build(text, lcp=False, stree=algo == "stree", sector=False,
+                                    quad="compact" if algo in ("quad", "prefix") else False, verify=True,
+                                    llcp=False, prefix=16 if algo == "prefix" else False)
+    st = idx.stats()
+    del text  # queries are cut from, and answers checked against, the index's packed text
+    torch.cuda.empty_cache()
+    off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
+                                        len_hi=257)
+    lens = torch.from_numpy(ln.astype(np.int64)).to(dev)
+    qoff = torch.zeros(nq, dtype=torch.int64, device=dev)
+    qoff[1:] = torch.cumsum(lens, 0)[:-1]
+    total = int(lens.sum().item())
+    qbytes = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
+    src = torch.from_numpy(off.astype(np.int64)).to(dev)
+    qlen = lens.to(torch.int32)
+    idx.extract(src, qlen, qoff, qbytes)  # t[off .. off + len) from the packed text
+    del src
+    out = torch.empty(nq, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    setup = time.perf_counter() - t0
+    log(f"c3 setup {setup:.1f} s ({algo}, n={n}, nq={nq})")
+    mean_m = total / nq
+    res, ref = {}, None
+    for a in (algo,) + tuple(x for x in extra_algos if x != algo):
+        def step():
+            idx.search_batch(qbytes, qoff, qlen, algo=a, out=out)
+        steps = args.c3_steps if a == algo else max(2, args.c3_steps // 2)
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tt = time.perf_counter()
+        ev0.record()
+        for _ in range(steps):
+            step()
+        ev1.record()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - tt
+        kms = ev0.elapsed_time(ev1) / steps
+        if ref is None:
+            ref = out.clone()
+            # guard 1: each answer is an occurrence of its query (positive queries)
+            okc = True
+            chunk = 1 << 20
+            for s in range(0, nq, chunk):
+                e = min(nq, s + chunk)
+                span = int((qoff[e - 1] + lens[e - 1] - qoff[s]).item())
+                got = torch.empty(span, dtype=torch.uint8, device=dev)
+                idx.extract(out[s:e].contiguous(), qlen[s:e].contiguous(), (qoff[s:e] - qoff[s]).contiguous(), got)
+                okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + span]))
+            if not okc:
+                raise SystemExit(f"bench c3: {a} returned a non-occurrence position")
+            # guard 2: exact lower bounds on a sample
+            rng = np.random.default_rng(7)
+            ids = np.sort(rng.choice(nq, size=min(nq, args.proof_sample), replace=False))
+            dids = torch.from_numpy(ids).to(dev)
+            qo_h = qoff[dids].cpu().numpy()
+            hq = {}
+            for j, i in enumerate(ids):
+                hq[int(i)] = qbytes[int(qo_h[j]):int(qo_h[j]) + int(ln[i])].cpu().numpy()
+
+            def window(p, L):
+                L = min(L, n - p)
+                if L <= 0:
+                    return np.zeros(0, np.uint8)
+                o = torch.empty(L, dtype=torch.uint8, device=dev)
+                idx.extract(torch.tensor([p], dtype=torch.int64, device=dev),
+                            torch.tensor([L], dtype=torch.int32, device=dev),
+                            torch.zeros(1, dtype=torch.int64, device=dev), o)
+                return o.cpu().numpy()
+            nbad = lower_bound_proof(idx, window, lambda i: hq[i], out[dids].cpu().numpy(), ids)
+            if nbad:
+                raise SystemExit(f"bench c3: {nbad} of {len(ids)} sampled answers are not exact lower bounds")
+            agrees = True
+        else:
+            agrees = bool(torch.equal(out, ref))
+            if not agrees:
+                raise SystemExit(f"bench c3: {a} differs from {algo}")
+        _, pr = idx.search_batch(qbytes, qoff, qlen, algo=a, probes=True)
+        mp = float(pr.double().mean().item())
+        bpl = bytes_per_lookup(a, st, n, mean_m, mp)
+        res[a] = record(a, nq, kms, el, bpl, st["index_bytes"],
+                        load_pmc(f"c3_{a}_n{n}_q{nq}") if a == algo else None, mp,
+                        {"identical_to_" + algo: agrees, "lookups_per_s": nq * steps / el})
+        log(f"c3 {a}: {kms:.3f} ms per {nq}")
+    h = res[algo]
+    idx.free()
+    del qbytes, qoff, qlen, lens, out, ref
+    torch.cuda.empty_cache()
+    return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({st['sa_width'] * 8}-bit "
+                        f"{'tagged entries' if algo == 'tagged' else 'SA'}), {nq} positive queries of length "
+                        f"8..256 (mean {mean_m:.1f}), ragged",
+            "algo": algo, "lookups_per_s": h["lookups_per_s"], "kernel_ms": h["kernel_ms"],
+            "ns_per_lookup": h["ns_per_lookup"], "index_bytes": st["index_bytes"], "setup_s": setup,
+            "proof_sample": args.proof_sample, "verified": True,
+            "roofline": {"bound": "hbm", "achieved": h["achieved_hbm_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                         "frac": h["achieved_hbm_GBps"] / HBM_PEAK_GBPS,
+                         "traffic": (h.get("pmc") or {}).get("fabric_bytes_per_lookup"),
+                         "kernel": KERNELS.get(algo, "k_sa_prefix")},
+            "variants": res,
+            "index": {k: st[k] for k in ("sa_width", "sa_bytes", "quad_bytes", "prefix_chars", "prefix_bytes",
+                                         "tag_chars", "tag_table_bytes", "index_bytes", "build_sa_ns",
+                                         "build_total_ns")}}
+
+
+def run_c3(args, torch, sas_amd, dev, ws, rank):
+    """--workload c3: the configs[3] record on its own line."""
+    algo = args.algo or "tagged"
+    rec = c3_record(args, torch, sas_amd, dev, rank, algo=algo, extra_algos=("plain", "lcp"))
+    if rank == 0:
+        emit({"metric": "pattern lookups/s (configs[3] shape)", "value": rec["lookups_per_s"], "unit": "lookups/s",
+              "n_gpus": ws, "steps": args.c3_steps, "warmup": args.warmup,
+              "ms_per_step": args.c3_nq / rec["lookups_per_s"] * 1e3, "higher_is_better": True, "scaling": "weak",
+              "vs_baseline": None, "dtype": "u8",
+              "data": f"synthetic: random_string(ChaCha8Rng({SEED})) text, positive queries len in [8,257)",
+              "config": {"workload": rec["workload"], "n": args.c3_n, "queries_per_gpu": args.c3_nq, "algo": algo},
+              "roofline": rec["roofline"], "c3": rec})
+
+
+# ---------------------------------------------------------------- u32 path
 def run_sst(args, torch, sas_amd, dev, ws, rank):
     """The u32 path (static-search-tree crate): the reference's bench sweeps sizes up to
     2^30 bytes (sst/bin/bench.rs:455-472); this runs the largest, 2^28 keys (gen_vals:
@@ -212,9 +543,11 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         got = dout.cpu().numpy().view(np.uint32).copy()
         if ref is None:
             ref = got
-        res[name] = {"lookups_per_s": nq / (kns * 1e-9), "kernel_ms": kns * 1e-6, "layers": idx.layers(),
-                     "index_bytes": idx.size(), "agrees": bool(np.array_equal(got, ref))}
+        res[name] = {"lookups_per_s": nq / (kns * 1e-9), "kernel_ms": kns * 1e-6, "ns_per_lookup": kns / nq,
+                     "layers": idx.layers(), "index_bytes": idx.size(), "agrees": bool(np.array_equal(got, ref))}
         idx.free()
+    if not all(r["agrees"] for r in res.values()):
+        raise SystemExit("bench sst: layouts disagree")
     # --range mode (sst/bin/bench.rs:84-109): the interleaved [q, q+1] stream through
     # STree16 left_max; rank(q+1) - rank(q) = number of keys equal to q (checked)
     rq = np.stack([qs, np.minimum(qs.astype(np.uint64) + 1, O.MAX).astype(np.uint32)], 1).reshape(-1)
@@ -233,9 +566,9 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
     st16.free()
     # CPU: the oracle's restatement of the reference's bench variant, STree16 left_max
     # + batch_final::<128> (sst/bin/bench.rs:96; sst/s_tree.rs:303-326), contiguous
-    # per-thread chunks (sst/bin/bench.rs:558-573); 16 threads and 1 thread
+    # per-thread chunks (sst/bin/bench.rs:558-573); all cores and 1 thread
     tree = O.STree(vals, left_max=True)
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    threads = host_threads()
     sample = nq
     t0 = time.perf_counter()
     cpu_out = tree.query_batch(qs[:sample], threads)
@@ -261,123 +594,24 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
                                    f"on all {sample} queries, {threads} threads, {dt:.2f} s", "agrees": cpu_ok}})
 
 
-def run_c3(args, torch, sas_amd, dev, ws, rank, dist):
-    """configs[3]-shaped run: n = 2^34 chars (16 GiB of byte-coded text, a 40-bit SA:
-    BASELINE's "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and
-    10^8 positive queries of mixed length 8..256 (random_queries with len in
-    [8, 257)), ragged, through sas_search_batch on device buffers.  The sector tree
-    and the fused quad leaves (16 B per suffix) fit next to the SA only up to n = 2^33;
-    above, QUAD / INLINE run on compact key-only quad leaves (8 B per suffix,
-    SAS_BUILD_QUAD_COMPACT) and SECTOR falls back to STREE."""
-    n = args.n if args.n != 1 << 30 else 1 << 34
-    nq = args.nq if args.nq != 10_000_000 else 100_000_000
-    fits = n <= (1 << 33)  # 16 B per suffix next to the 40-bit SA
-    main_algo = args.algo if (args.algo != "sector" or fits) else "stree"
-    quad_mode = (("compact" if (args.quad_compact or not fits) else True) if main_algo in ("quad", "inline", "prefix")
-                 else False)
-    # prefix table beside a 40-bit SA: packed 40-bit entries, p = 16 (20 GiB); it fits
-    # because the 16 GiB byte copy of the text is dropped after the build (queries are
-    # cut from, and answers checked against, the index's packed text: sas_extract)
-    c3_prefix = min(args.prefix_chars, 16) if main_algo == "prefix" else False
-    t0 = time.perf_counter()
-    text = sas_amd.random_string(n, seed=SEED, device=dev)
-    # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
-    idx = sas_amd.SaNaive.build(text, lcp=False, stree=main_algo == "stree", sector=main_algo == "sector",
-                                quad=quad_mode, verify=True, llcp=False, prefix=c3_prefix)
-    stats = idx.stats()
-    del text
-    torch.cuda.empty_cache()
-    off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
-                                        len_hi=257)
-    lens = torch.from_numpy(ln.astype(np.int64)).to(dev)
-    qoff = torch.zeros(nq, dtype=torch.int64, device=dev)
-    qoff[1:] = torch.cumsum(lens, 0)[:-1]
-    total = int(lens.sum().item())
-    qbytes = torch.zeros(total + 64, dtype=torch.uint8, device=dev)
-    src = torch.from_numpy(off.astype(np.int64)).to(dev)
-    qlen = lens.to(torch.int32)
-    idx.extract(src, qlen, qoff, qbytes)  # t[off .. off + len) from the packed text
-    del src
-    chunk = 1 << 20
-    out = torch.empty(nq, dtype=torch.int64, device=dev)
-    torch.cuda.synchronize()
-    setup = time.perf_counter() - t0
-    results = {}
-    for algo in [a for a in (main_algo, "plain", "lcp") if a]:
-        if algo in results:
-            continue
-        def step():
-            idx.search_batch(qbytes, qoff, qlen, algo=algo, out=out)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        ev0.record()
-        tt = time.perf_counter()
-        steps = args.steps if algo == main_algo else max(2, args.steps // 4)
-        for _ in range(steps):
-            step()
-        ev1.record()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - tt
-        kms = ev0.elapsed_time(ev1) / steps
-        # guard: each answer is an occurrence of its query (positive queries)
-        okc = True
-        for s in range(0, nq, chunk):
-            e = min(nq, s + chunk)
-            span = int((qoff[e - 1] + lens[e - 1] - qoff[s]).item())
-            got = torch.empty(span, dtype=torch.uint8, device=dev)
-            idx.extract(out[s:e].contiguous(), qlen[s:e].contiguous(), (qoff[s:e] - qoff[s]).contiguous(), got)
-            okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + span]))
-        _, pr = idx.search_batch(qbytes, qoff, qlen, algo=algo, probes=True)
-        mp = float(pr.double().mean().item())
-        mean_m = total / nq
-        P = int(np.log2(n)) + 1
-        if algo == "stree":
-            ab = stats["stree_layers"] * 64 + max(0.0, mp - stats["stree_layers"]) * (4 + mean_m) + mean_m + 8
-        elif algo in ("sector", "quad"):
-            # H nodes (leaf = keys + SA), extra leaf probes, the query, the position, and
-            # the packed text window past char 32 for the final compare (+ the 5-B SA
-            # entry for compact key-only quad leaves)
-            H = stats[f"{algo}_layers"]
-            node, extra = (32, 12) if algo == "sector" else (64, 64)
-            ab = H * node + max(0.0, mp - H) * extra + mean_m + 8 + max(0.0, mean_m - 32) / 4
-            if algo == "quad" and stats["quad_entry_bytes"] == 8:
-                ab += stats["sa_width"]
-        elif algo == "prefix":
-            # the table pair, entry probes (8-B key-only or 16-B fused), the SA entry of
-            # key-only leaves, the query, the position, the text window past char 32
-            eb = stats["quad_entry_bytes"]
-            ab = 2 * stats["sa_width"] + max(0.0, mp - 1) * eb + mean_m + 8 + max(0.0, mean_m - 32) / 4
-            if eb == 8:
-                ab += stats["sa_width"]
-        else:
-            ab = P * (4 + mean_m) + mean_m + 8
-        results[algo] = {"lookups_per_s": nq * steps / el, "kernel_ms": kms, "mean_probes": mp,
-                         "algorithmic_bytes_per_lookup": ab, "achieved_GBps": ab * nq / (kms * 1e-3) / 1e9,
-                         "verified": okc}
-    if rank == 0:
-        h = results[main_algo]
-        traffic, tsrc = load_traffic(f"c3_{main_algo}", n, nq, "8-256")
-        emit({
-            "metric": "pattern lookups/s (configs[3] shape)", "value": h["lookups_per_s"], "unit": "lookups/s",
-            "n_gpus": ws, "steps": args.steps, "warmup": args.warmup, "ms_per_step": nq / h["lookups_per_s"] * 1e3,
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
-            "data": f"synthetic: random_string(ChaCha8Rng({SEED})) text, positive queries len in [8,257)",
-            "config": {"workload": f"configs[3]-shaped: n={n} chars, {stats['sa_width'] * 8}-bit SA, "
-                                   f"{nq} mixed-length 8..256 queries, ragged", "n": n, "queries_per_gpu": nq,
-                       "mean_m": total / nq, "algo": main_algo},
-            "roofline": {"bound": "hbm", "achieved": h["achieved_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": h["achieved_GBps"] / HBM_PEAK_GBPS, "traffic": traffic,
-                         "traffic_source": tsrc,
-                         "kernel": {"stree": "k_sa_stree4x", "sector": "k_sa_sector", "quad": "k_sa_quad4x",
-                                    "inline": "k_sa_inline", "prefix": "k_sa_prefix"}.get(main_algo, "k_sa_binary"),
-                         "kernel_ms": h["kernel_ms"]},
-            "variants": results, "setup_s": setup,
-            "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "iterations", "sa_rounds",
-                                            "build_sa_ns", "build_total_ns", "sa_width", "sa_bytes",
-                                            "stree_bytes", "sector_bytes", "quad_bytes", "quad_fan",
-                                            "quad_entry_bytes", "prefix_chars", "prefix_bytes")}})
+# ---------------------------------------------------------------- configs[1] / [2] (headline)
+WORKLOADS = {
+    "prefix": "PREFIX: p = {p}-char bucket table (the reference's prefix table, sas/sa_search.rs:59-95, "
+              "with p live) of {e}-B inline entries holding each bucket's first {k} suffixes "
+              "({tb:.0f} GiB), then binary search over the fused {{32-char key, SA}} quad-leaf entries "
+              "of the bucket; 2^30 text in HBM, 10^7 len-32 queries",
+    "plain": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112), top 12 levels from LDS, "
+             "levels 13-21 from a 32 MiB cache-resident pivot array",
+    "lcp": "configs[1] + mlr LCP skipping",
+    "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (16-B {SA, Llcp, Rlcp, chars} entries)",
+    "inline": "configs[1] probe sequence over fused {32-char key, SA} entries",
+    "stree": "configs[2]: S-tree of 16-char SA keys (17-ary 64-B nodes, top layers LDS-staged) + LCP-skipping tail",
+    "sector": "configs[2]: sector S-tree (9-ary 32-B nodes, fused 32-char key + SA leaves, top layers LDS-staged)",
+    "quad": "configs[2]: quad S-tree (17-ary 64-B nodes read by 4-lane groups, 4-entry fused {32-char key, SA} "
+            "leaves, top layers LDS-staged)",
+    "interp": "interpolation_search<16> (sas/sa_search.rs:376-421) over fused {32-char key, SA} entries",
+    "tagged": "tagged SA entries + bucket table",
+}
 
 
 def main():
@@ -389,31 +623,31 @@ def main():
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
     ap.add_argument("--algo", default=None, choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
-                                                         "prefix"])
-    ap.add_argument("--variants", default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,prefix,prefix_packed",
+                                                     "prefix", "tagged", "interp"])
+    ap.add_argument("--variants", default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,interp,prefix_packed",
                     help="other algos timed beside the headline one")
     ap.add_argument("--prefix-chars", type=int, default=16,
-                    help="p of the prefix table (the reference's main.rs default is -p 20 key bits)")
+                    help="p of the prefix table in chars (the reference's main.rs intends -p 20 key BITS)")
     ap.add_argument("--prefix-table", default="inline2", choices=["inline2", "inline4", "inline", "ranks"],
                     help="inline2: 32-B entries holding each range's first two suffixes, read by lane pairs "
                          "(4^16 x 32 B = 128 GiB); inline: 16-B entries with the first suffix (64 GiB); "
                          "ranks: u32 ranks only (sas/sa_search.rs:59-75's table)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-c3", action="store_true", help="skip the configs[3] sub-record")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-buffer end-to-end pass")
+    ap.add_argument("--c3-n", type=int, default=1 << 34)
+    ap.add_argument("--c3-nq", type=int, default=100_000_000)
+    ap.add_argument("--c3-steps", type=int, default=5)
+    ap.add_argument("--proof-sample", type=int, default=3000, help="queries per batch proven exact lower bounds")
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
-                    help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric); c3: largest u32-SA text "
-                         "(2^32 - 2^20 chars), 10^8 queries of mixed length 8..256")
-    ap.add_argument("--quad-compact", action="store_true",
-                    help="c3: key-only quad leaves even where the fused ones fit (n <= 2^33)")
+                    help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric) + every config's sub-record; "
+                         "c3: the configs[3] record alone; sst: the u32 static-search-tree path")
     ap.add_argument("--positive", action="store_true", help="sst workload: queries drawn from the keys")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
     args = ap.parse_args()
-    if args.algo is None:
-        # the prefix table: c1 2.77e10 vs QUAD 1.40e10 lookups/s; c3 (n = 2^34, 40-bit SA,
-        # ragged 8..256, p = 16 rank table) 24.5 vs 24.9 ms per 10^8 (tools/ab_c3.py: -7%)
-        args.algo = "prefix"
     keep_stdout_for_result()
 
     import torch
@@ -429,9 +663,11 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     if args.workload == "c3":
-        return run_c3(args, torch, sas_amd, dev, ws, rank, dist)
+        return run_c3(args, torch, sas_amd, dev, ws, rank)
     if args.workload == "sst":
         return run_sst(args, torch, sas_amd, dev, ws, rank)
+    if args.algo is None:
+        args.algo = "prefix"
     n, nq, m = args.n, args.nq, args.m
 
     t_build0 = time.perf_counter()
@@ -455,13 +691,14 @@ def main():
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
     qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
     ar = torch.arange(m, device=dev, dtype=torch.int64)
-    chunk = 1 << 18  # bounds the gather temporaries (HBM is nearly full at n = 2^34)
+    chunk = 1 << 18  # bounds the gather temporaries
     for s in range(0, nq, chunk):
         e = min(nq, s + chunk)
         qbytes[s * m:e * m] = text[(off_t[s:e, None] + ar[None, :]).reshape(-1)]
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     build_s = time.perf_counter() - t_build0
+    log(f"c1 index built + queries cut in {build_s:.1f} s")
 
     def reduce_max(x):
         if dist is None:
@@ -480,7 +717,7 @@ def main():
 
     packed = {}
 
-    def run_algo(algo, steps, warmup):
+    def run_algo(algo, steps, warmup, dst):
         base, fl = algo_flags(algo)
         if algo == "prefix_packed" and "w" not in packed:
             # queries handed over 2-bit packed (sas_pack_queries, untimed: the caller's format)
@@ -488,148 +725,184 @@ def main():
 
         def step():
             if args.mode == "shard":
-                out.copy_(engine.search_fixed(qbytes, m))
+                dst.copy_(engine.search_fixed(qbytes, m))
             elif algo == "prefix_packed":
-                idx.search_packed(packed["w"], m, out=out)
+                idx.search_packed(packed["w"], m, out=dst)
             else:
-                idx.search_fixed(qbytes, m, algo=base, out=out, flags=fl)
+                idx.search_fixed(qbytes, m, algo=base, out=dst, flags=fl)
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        holder = {}
+        state = {"i": 0}
 
-        def timed_step_factory():
+        def timed_step():
             # events bracket exactly the K timed launches on the launch stream
-            state = {"i": 0}
+            if state["i"] == warmup:
+                ev0.record(stream)
+            step()
+            state["i"] += 1
+            if state["i"] == warmup + steps:
+                ev1.record(stream)
+        el = timed_loop(timed_step, steps, warmup, torch.cuda.synchronize, barrier, reduce_max)
+        return el, ev0.elapsed_time(ev1) / steps
 
-            def s():
-                if state["i"] == warmup:
-                    ev0.record(stream)
-                step()
-                state["i"] += 1
-                if state["i"] == warmup + steps:
-                    ev1.record(stream)
-            return s
-        el = timed_loop(timed_step_factory(), steps, warmup, torch.cuda.synchronize, barrier, reduce_max)
-        holder["kernel_ms"] = ev0.elapsed_time(ev1) / steps
-        # correctness guard (untimed): every answer must be an occurrence of its query
-        occ = text[(out[:, None] + ar[None, :]).reshape(-1).clamp_(max=n - 1)]
-        ok = bool(torch.equal(occ, qbytes))
-        return el, holder["kernel_ms"], ok
-
-    el, kernel_ms, ok = run_algo(args.algo, args.steps, args.warmup)
-    if not ok:
-        raise SystemExit(f"bench: {args.algo} returned a non-occurrence position")
-    # end to end from host buffers: pageable queries H2D, the search, positions
-    # D2H, as a caller handing host memory through the C ABI would see it.  Never `value`.
-    e2e = None
-    if args.mode == "replicated":
-        hq = qbytes.cpu().numpy()
-        best = None
-        for _ in range(2):
-            t0 = time.perf_counter()
-            hpos = idx.search_fixed(hq, m, algo=args.algo)
-            dt = time.perf_counter() - t0
-            best = dt if best is None else min(best, dt)
-        e2e = {"lookups_per_s": nq / best, "ms": best * 1e3,
-               "matches_device_run": bool(np.array_equal(hpos, out.cpu().numpy().astype(np.uint64))),
-               "path": "host query bytes -> sas_search_fixed (staging hipMalloc + H2D, kernel, D2H)"}
-    # probes -> tail probes for the algorithmic byte count (untimed pass; a shard of a
-    # multi-GPU sharded run only holds part of the SA, so the pass needs the whole index)
-    whole = args.mode == "replicated" or ws == 1
-    if whole:
-        _, probes = idx.search_fixed(qbytes, m, algo=args.algo, probes=True)
-        mean_probes = float(probes.double().mean().item())
-    else:
-        mean_probes = float("nan")
-    layers_of = {"stree": stats["stree_layers"], "sector": stats["sector_layers"], "quad": stats["quad_layers"]}
-    tail = max(0.0, mean_probes - layers_of[args.algo]) if args.algo in layers_of else mean_probes
-    pe = {16: 16, 32: 32, 64: 64}.get(stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1), 8)
-    algo_bytes = algorithmic_bytes(args.algo, n, m, stats["stree_layers"], tail, stats["sector_layers"],
-                                   stats["quad_layers"], pe)
-    achieved = algo_bytes * nq / (kernel_ms * 1e-3) / 1e9
-
-    variants = {}
-    for v in [x for x in args.variants.split(",") if x and x != args.algo and args.mode == "replicated"]:
-        vel, vk, vok = run_algo(v, max(3, args.steps // 4), 1)
-        vbase, vfl = algo_flags(v)
-        if v == "prefix_packed":
-            vbase = "prefix"
+    def probes_of(algo):
+        base, fl = algo_flags(algo)
+        if algo == "prefix_packed":
             _, vp = idx.search_packed(packed["w"], m, probes=True)
         else:
-            _, vp = idx.search_fixed(qbytes, m, algo=vbase, probes=True, flags=vfl)
-        vmean = float(vp.double().mean().item())
-        vtail = max(0.0, vmean - layers_of[v]) if v in layers_of else vmean
-        if vfl:  # the table entry + the reference's per-iteration SA word and text window
-            vb = pe + max(0.0, vmean - 1) * (4 + m) + m + 8
-        else:
-            vb = algorithmic_bytes(vbase, n, 8 if v == "prefix_packed" else m, stats["stree_layers"], vtail,
-                                   stats["sector_layers"], stats["quad_layers"], pe)
-        variants[v] = {"lookups_per_s": ws * nq * max(3, args.steps // 4) / vel, "kernel_ms": vk,
-                       "achieved_GBps": vb * nq / (vk * 1e-3) / 1e9, "algorithmic_bytes_per_lookup": vb,
-                       "mean_probes": float(vp.double().mean().item()), "verified": vok}
+            _, vp = idx.search_fixed(qbytes, m, algo=base, probes=True, flags=fl)
+        return float(vp.double().mean().item())
 
+    el, kernel_ms = run_algo(args.algo, args.steps, args.warmup, out)
+    log(f"headline {args.algo}: {kernel_ms:.3f} ms per {nq}")
+    # correctness guard (untimed): every answer is an occurrence of its query, and a sample
+    # is proven an exact lower bound on the index's own SA
+    occ = text[(out[:, None] + ar[None, :]).reshape(-1).clamp_(max=n - 1)]
+    if not bool(torch.equal(occ, qbytes)):
+        raise SystemExit(f"bench: {args.algo} returned a non-occurrence position")
+    del occ
+    whole = args.mode == "replicated" or ws == 1
+    proven = 0
+    if whole:
+        rng = np.random.default_rng(11 + rank)
+        ids = np.sort(rng.choice(nq, size=min(nq, args.proof_sample), replace=False))
+        dids = torch.from_numpy(ids).to(dev)
+        hq = qbytes.view(nq, m)[dids].cpu().numpy()
+        qmap = {int(i): hq[j] for j, i in enumerate(ids)}
+        htext = text.cpu().numpy()
+        nbad = lower_bound_proof(idx, lambda p, L: htext[p:p + L], lambda i: qmap[i], out[dids].cpu().numpy(), ids)
+        if nbad:
+            raise SystemExit(f"bench: {nbad} of {len(ids)} sampled {args.algo} answers are not exact lower bounds")
+        proven = len(ids)
+        del htext
+    mean_probes = probes_of(args.algo) if whole else float("nan")
+
+    # end to end from host buffers: pageable query bytes in, positions out, as a
+    # caller handing host memory through the C ABI sees it (pinned staging, chunked
+    # H2D / kernel / D2H over 3 streams, csrc/host_stage.hpp).  Never `value`.
+    e2e = None
+    if args.mode == "replicated" and not args.no_e2e:
+        hq = qbytes.cpu().numpy()
+        ref_host = out.cpu().numpy().astype(np.uint64)
+        times = []
+        hpos = None
+        for _ in range(3):
+            t0 = time.perf_counter()
+            hpos = idx.search_fixed(hq, m, algo=args.algo)
+            times.append(time.perf_counter() - t0)
+        e2e = {"lookups_per_s": nq / min(times), "ms": min(times) * 1e3, "ms_first_call": times[0] * 1e3,
+               "matches_device_run": bool(np.array_equal(hpos, ref_host)),
+               "path": "pageable host query bytes -> sas_search_fixed: reusable pinned staging (the index's slot "
+                       "set), 16 MiB chunks, H2D / kernel / D2H overlapped on 3 streams"
+                       + ("; PREFIX with m <= 32 packs the queries 2-bit on the host (8 B per query over PCIe)"
+                          if args.algo == "prefix" and m <= 32 else "")}
+        if not e2e["matches_device_run"]:
+            raise SystemExit("bench: the host-buffer path differs from the device run")
+        del hq
+        log(f"e2e host: {e2e['ms']:.2f} ms")
+
+    headline_pos = out.clone()
+    variants = {}
+    vout = torch.empty_like(out)
+    for v in [x for x in args.variants.split(",") if x and x != args.algo and args.mode == "replicated"]:
+        vsteps = max(3, args.steps // 4)
+        vel, vk = run_algo(v, vsteps, 1, vout)
+        same = bool(torch.equal(vout, headline_pos))
+        if not same:
+            raise SystemExit(f"bench: variant {v} differs from {args.algo}")
+        vmean = probes_of(v)
+        vbase, vfl = algo_flags(v)
+        bpl = bytes_per_lookup("prefix" if v == "prefix_packed" else vbase, stats, n, m, vmean,
+                               range_flag=bool(vfl), packed=v == "prefix_packed")
+        key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector"}.get(v)
+        pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}") if key else None
+        variants[v] = record(v, nq, vk, vel, bpl, stats["index_bytes"], pmc, vmean,
+                             {"identical_to_headline": same, "lookups_per_s": ws * nq * vsteps / vel})
+        log(f"variant {v}: {vk:.3f} ms")
+
+    pe = stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1) if stats["prefix_chars"] else 0
     pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d", 64: "q"}.get(pe, "")
-    traffic, traffic_src, rdreq = load_traffic(args.algo + (pkey if args.algo == "prefix" else ""), n, nq, m,
-                                               with_requests=True)
+    hpmc = load_pmc(f"{args.algo}{pkey if args.algo == 'prefix' else ''}_n{n}_q{nq}_m{m}")
+    hbpl = bytes_per_lookup(args.algo, stats, n, m, mean_probes)
+    head = record(args.algo, nq, kernel_ms, el, hbpl, stats["index_bytes"], hpmc, mean_probes)
+    achieved = head["achieved_hbm_GBps"]
+
     cpu = None
+    configs = {}
     if rank == 0 and ws == 1 and not args.no_cpu and args.mode == "replicated":
         cpu = cpu_baseline(text, idx, qbytes, m, nq, args.cpu_seconds)
+        cpos = cpu.pop("_pos")
+        cpu["agrees_with_gpu"] = bool(np.array_equal(cpos, headline_pos[:len(cpos)].cpu().numpy().astype(np.uint64)))
+        if not cpu["agrees_with_gpu"]:
+            raise SystemExit("bench: the CPU restatement of the reference differs from the GPU positions")
+        log("cpu baseline done")
+        configs["c0"] = c0_record(torch, sas_amd, dev, min(10.0, args.cpu_seconds / 2))
+        log("c0 done")
+    if args.mode == "replicated":
+        if "plain" in variants:
+            configs["c1"] = dict(variants["plain"], workload=WORKLOADS["plain"])
+        best2 = max((v for v in ("quad", "sector", "stree") if v in variants),
+                    key=lambda v: variants[v]["kernel_lookups_per_s"], default=None)
+        if best2:
+            configs["c2"] = dict(variants[best2], workload=WORKLOADS[best2],
+                                 lds_layers={"quad": stats["quad_lds_layers"], "sector": stats["sector_lds_layers"],
+                                             "stree": stats["stree_lds_layers"]}[best2])
+    idx_stats = {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
+                                       "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels",
+                                       "iterations", "prefix_chars", "prefix_bytes", "sa_bytes", "text_bytes",
+                                       "quad_bytes", "stree_bytes", "sector_bytes", "lcp_bytes", "llcp_bytes",
+                                       "index_bytes", "sa_rounds", "build_sa_ns", "build_total_ns")}
+    # configs[3]: free the 2^30 index first (N = 1 only: the scaling runs time the headline)
+    if ws == 1 and not args.no_c3 and args.mode == "replicated":
+        idx.free()
+        del text, qbytes, out, headline_pos, vout, off_t, packed
+        torch.cuda.empty_cache()
+        configs["c3"] = c3_record(args, torch, sas_amd, dev, rank)
+        log("c3 done")
 
     if rank == 0:
         ms = el / args.steps * 1e3
         value = ws * nq * args.steps / el
-        workload = {"stree": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, LCP-skipping search over an "
-                             "S-tree of 16-char SA keys (top layers LDS-staged)",
-                    "plain": "configs[1]: 2^30 text in HBM, 10^7 len-32 queries, plain binary search over SA",
-                    "lcp": "configs[1] + mlr LCP skipping",
-                    "prefix": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, the reference's prefix table "
-                              "(sas/sa_search.rs:59-95, p = config.prefix_chars: one 8-B read gives the rank range) + binary "
-                              "search over the fused 32-char key + SA entries of that range",
-                    "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (one 8-B {SA, Llcp, Rlcp} "
-                            "entry per probe, text only on lcp ties), 2^30 text in HBM, 10^7 len-32 queries",
-                    "sector": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, sector S-tree (32-B nodes, "
-                              "fused 32-char key + SA leaves, top layers LDS-staged)",
-                    "inline": "configs[1] probe sequence (binary_search_batch) over fused 32-char key + SA "
-                              "entries, 2^30 text in HBM, 10^7 len-32 queries",
-                    "quad": "configs[2]: 2^30 text in HBM, 10^7 len-32 queries, quad S-tree (17-ary 64-B nodes "
-                            "loaded by 4-lane groups in one request each, 4-entry fused 32-char key + SA leaves, "
-                            "top layers LDS-staged)"}[args.algo]
+        wl = WORKLOADS[args.algo]
+        if args.algo == "prefix":
+            wl = wl.format(p=stats["prefix_chars"], e=pe, k=max(1, pe // 16), tb=stats["prefix_bytes"] / 2 ** 30)
         line = {
             "metric": METRIC, "value": value, "unit": "lookups/s", "n_gpus": ws, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
             "vs_baseline": None, "dtype": "u8",
             "data": f"synthetic: random_string(ChaCha8Rng::seed_from_u64({SEED})) text + positive len-{m} "
                     f"substrings (sas/util.rs:9-26), per-rank query stream",
-            "config": {"workload": workload, "algo": args.algo, "n": n, "queries_per_gpu": nq, "m": m,
-                       "prefix_chars": stats["prefix_chars"],
-                       "mode": args.mode,
+            "config": {"workload": wl, "algo": args.algo, "n": n, "queries_per_gpu": nq, "m": m,
+                       "prefix_chars": stats["prefix_chars"], "prefix_entry_bytes": pe,
+                       "index_bytes": stats["index_bytes"], "prefix_bytes": stats["prefix_bytes"],
+                       "ns_per_lookup": head["ns_per_lookup"], "mode": args.mode,
                        "parallelism": (f"replicated index x{ws}, query shards (no data-path collective)"
                                        if args.mode == "replicated" else
                                        f"SA rank ranges over {ws} GPUs, sas_route + RCCL all_to_all_single "
                                        f"(queries out, positions back)")},
             # shard mode: the events bracket route + exchanges + search, not one kernel
-            "roofline": None if args.mode != "replicated" else {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBPS,
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad",
-                                    "inline": "k_sa_inline",
-                                    "prefix": "k_sa_prefix2" if pe >= 32 else "k_sa_prefix"}.get(args.algo,
-                                                                                                 "k_sa_binary"),
-                         "kernel_ms": kernel_ms, "algorithmic_bytes_per_lookup": algo_bytes,
-                         "mean_probes": mean_probes,
-                         # what bounds this path: random 128-B-line requests (PMC L2->fabric reads
-                         # of this workload, query stream included), against the measured
-                         # random-request ceiling
-                         "requests": None if rdreq is None else {
-                             "per_lookup": rdreq / nq, "achieved_per_s": rdreq / (kernel_ms * 1e-3),
-                             "ceiling_per_s": RANDOM_REQ_CEILING,
-                             "frac": rdreq / (kernel_ms * 1e-3) / RANDOM_REQ_CEILING, "source": traffic_src}},
+            "roofline": None if args.mode != "replicated" else {
+                "bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBPS,
+                "traffic": (head.get("pmc") or {}).get("fabric_bytes_per_lookup"),
+                "traffic_unit": "bytes per lookup (PMC, L2->fabric, Infinity-Cache hits included)",
+                "traffic_source": (hpmc or {}).get("source"),
+                "kernel": "k_sa_prefix2" if args.algo == "prefix" and pe >= 32 else
+                          ("k_sa_prefix" if args.algo == "prefix" else KERNELS.get(args.algo)),
+                "kernel_ms": kernel_ms, "bytes_per_lookup": hbpl, "mean_probes": mean_probes,
+                # what bounds this path: random 128-B-line requests (PMC L2->fabric reads of this
+                # workload, query stream included), against the measured random-request ceiling
+                "requests": None if not head.get("pmc") else {
+                    "per_lookup": head["pmc"]["requests_per_lookup"],
+                    "ceiling_per_s": RANDOM_REQ_CEILING, "frac": head["pmc"]["requests_frac_of_ceiling"]}},
             "cpu_baseline": cpu,
             "e2e_host": e2e,
+            "configs": configs,
             "variants": variants,
-            "index": {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
-                                            "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "iterations", "prefix_chars",
-                                            "sa_rounds", "build_sa_ns", "build_total_ns")},
-            "setup_s": build_s, "verified": ok,
+            "index": idx_stats,
+            "setup_s": build_s, "verified": True,
+            "verification": f"every answer an occurrence; {proven} sampled answers proven exact lower bounds on the "
+                            f"index's SA; every variant bit-identical to the headline"
+                            + ("; CPU restatement identical on its sample" if cpu else ""),
         }
         emit(line)
     if dist is not None:

@@ -240,6 +240,16 @@ int sas_route_pack(const sas_index* index, const uint64_t* splitter_pos, uint32_
                    const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_counts,
                    uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags);
 
+/* sas_route_pack with fixed-capacity buckets: bucket w owns send slots [w*cap, (w+1)*cap)
+ * (out_send holds (nsplit + 1) * cap * m bytes), so every rank's all-to-all uses equal splits
+ * and needs no host-side counts.  out_counts[w] is the true count; a query past its bucket's
+ * cap is not copied and its out_slot is (nsplit + 1) * cap - 1: the caller checks
+ * out_counts[w] <= cap on the device and redoes an overflowing step exactly.  Send slots a
+ * bucket does not fill keep their old bytes.  EINVAL if cap == 0. */
+int sas_route_pack_cap(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsplit,
+                       const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t cap, uint64_t* out_counts,
+                       uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags);
+
 int sas_get_stats(const sas_index* index, sas_stats* out);
 
 /* Copy the suffix array / LCP array out (dst host or device per flags).

@@ -71,6 +71,8 @@ int sas_errno_of(hipError_t e);
     } while (0)
 
 // ---------------------------------------------------------------- index structs
+struct StagePool;                     // host_stage.hpp: pinned staging of host-pointer calls
+void sas_stage_pool_free(StagePool*);  // sas_search.hip
 struct sas_index {
     uint64_t n = 0;               // text length (chars)
     uint64_t sa_n = 0;            // SA entries held (= n, or a shard's rank range)
@@ -128,6 +130,7 @@ struct sas_index {
     uint64_t* tag_table = nullptr;
     uint32_t tag_p = 0;
     sas_stats stats = {};
+    mutable StagePool* stage = nullptr;  // created by the first host-pointer search
 };
 
 struct sst_index {
@@ -335,9 +338,9 @@ struct QueryRegs {
 
 // Rust slice order `t[p..n] < q`, with the first h chars known equal.
 // Returns lt; *lcp = lcp(t[p..n], q) (capped at min(n-p, m)).
-template <int QW>
+template <int QW, class Q>
 __device__ __forceinline__ bool suffix_less_from(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
-                                                 const QueryRegs<QW>& q, uint32_t h, uint32_t* lcp) {
+                                                 const Q& q, uint32_t h, uint32_t* lcp) {
     uint64_t lenS = n - p;
     uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
     if (h < L) {
@@ -363,9 +366,9 @@ __device__ __forceinline__ bool suffix_less_from(const uint64_t* __restrict__ tw
 }
 
 // Same decision when the first 32 chars of the suffix are already known (key).
-template <int QW>
+template <int QW, class Q>
 __device__ __forceinline__ bool suffix_less_key(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
-                                                uint64_t key, const QueryRegs<QW>& q, uint32_t h,
+                                                uint64_t key, const Q& q, uint32_t h,
                                                 uint32_t* lcp) {
     uint64_t lenS = n - p;
     uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
@@ -385,3 +388,117 @@ __device__ __forceinline__ bool suffix_less_key(const uint64_t* __restrict__ tw,
     }
     return suffix_less_from<QW>(tw, n, p, q, h, lcp);
 }
+
+// ---------------------------------------------------------------- wave-staged queries
+// The 64 queries of a wavefront (consecutive query ids) usually sit in one contiguous span
+// of the caller's buffer.  Loading them lane by lane costs one L1->L2 request per 16-B piece
+// of every query (the configs[3] shape: ~12 of its ~19 requests per lookup); instead the
+// wave reads the span once, coalesced (lane l reads 16-B block l, l+64, ...), packs it 2 bits
+// per char into LDS, and each lane reads its query words from there.  A span longer than
+// SAS_WQ_WORDS words (16K chars) falls back to per-lane loads.
+#define SAS_WQ_WORDS 512
+
+__device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t t = (uint64_t)__shfl_xor((long long)v, o);
+        v = t < v ? t : v;
+    }
+    return v;
+}
+__device__ __forceinline__ uint64_t wave_max_u64(uint64_t v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint64_t t = (uint64_t)__shfl_xor((long long)v, o);
+        v = t > v ? t : v;
+    }
+    return v;
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// 16 byte codes -> 32 bits, first char in bits 31..30
+__device__ __forceinline__ uint32_t pack16(uint4 v) {
+    return (pack4(v.x) << 24) | (pack4(v.y) << 16) | (pack4(v.z) << 8) | pack4(v.w);
+}
+
+// Stage the span of this wave's queries (qo = byte offset of this lane's query in qbytes, m
+// its length, act = the lane holds a query).  Wave-uniform result: true = staged, *lo16 = the
+// byte offset of LDS char 0 (the span's first byte rounded down to 16 B).  Every 16-B block
+// read holds a byte of the span, which lies inside the caller's buffer.
+__device__ __forceinline__ bool wave_stage_queries(const uint8_t* __restrict__ qbytes, uint64_t qo, uint32_t m,
+                                                   bool act, uint32_t* L32, uint64_t* lo16) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t lo = wave_min_u64(act && m ? qo : ~0ull);
+    const uint64_t hi = wave_max_u64(act && m ? qo + m : 0ull);
+    wave_sync_lds();  // the previous batch's reads of L32 are done
+    if (hi == 0) {  // no lane has a char to stage
+        *lo16 = 0;
+        if (lane < 2) L32[lane] = 0;
+        wave_sync_lds();
+        return true;
+    }
+    const uint64_t base = lo & ~15ull;
+    const uint64_t span = hi - base;
+    if (span > (uint64_t)(SAS_WQ_WORDS - 1) * 32) return false;
+    const uint32_t nblk = (uint32_t)((span + 15) >> 4);
+    const uint4* src = reinterpret_cast<const uint4*>(qbytes + base);
+    for (uint32_t b = lane; b < nblk; b += 64) L32[b ^ 1] = pack16(src[b]);
+    // zero the rest of the last word and one guard word after it
+    const uint32_t nw = (nblk + 1) >> 1, z = nblk + lane;
+    if (z < 2 * nw + 2) L32[z ^ 1] = 0;
+    wave_sync_lds();
+    *lo16 = base;
+    return true;
+}
+
+// A query read from the wave's LDS words (same interface as QueryRegs: m, w[0], word,
+// chars32; chars past m read as 0).
+struct WaveQuery {
+    const uint64_t* L;
+    uint32_t qo;  // the query's first char in L
+    uint32_t m;
+    uint64_t w[1];
+    __device__ __forceinline__ void init(const uint32_t* L32, uint32_t off, uint32_t len) {
+        L = reinterpret_cast<const uint64_t*>(L32);
+        qo = off;
+        m = len;
+        w[0] = chars32(0);
+    }
+    __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
+        if (off >= m) return 0;
+        const uint32_t c = qo + off, k = c >> 5, s = (c & 31) << 1;
+        uint64_t v = L[k];
+        if (s) v = (v << s) | (L[k + 1] >> (64 - s));
+        return v & chars_mask(m - off < 32 ? m - off : 32);
+    }
+    __device__ __forceinline__ uint64_t word(uint32_t j) const { return chars32(j << 5); }
+};
+
+// A query read from its bytes on demand (the fallback of spread-out batches): word 0 in a
+// register, later windows packed from global memory when a compare reaches them.
+struct ByteQuery {
+    const uint8_t* bytes;
+    uint32_t m;
+    uint64_t w[1];
+    __device__ __forceinline__ void init(const uint8_t* q, uint32_t len) {
+        bytes = q;
+        m = len;
+        uint32_t dummy = 0;
+        w[0] = pack_query_word(q, len, 0, &dummy);
+    }
+    __device__ __forceinline__ uint64_t word(uint32_t j) const {
+        if (j == 0) return w[0];
+        uint32_t dummy = 0;
+        return pack_query_word(bytes, m, j, &dummy);
+    }
+    __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
+        const uint32_t j = off >> 5, s = (off & 31) << 1;
+        const uint64_t a = word(j);
+        if (s == 0) return a;
+        return (a << s) | (word(j + 1) >> (64 - s));
+    }
+};

@@ -1078,6 +1078,7 @@ static void free_index(sas_index* x) {
     void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->scratch, x->sec_inner,
                      x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table};
     for (void* p : ptrs) if (p) (void)hipFree(p);
+    sas_stage_pool_free(x->stage);
     delete x;
 }
 

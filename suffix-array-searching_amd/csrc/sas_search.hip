@@ -28,6 +28,7 @@
 //
 // Text compares are 2-bit packed: 32 chars per u64 compare.
 #include "common.hpp"
+#include "host_stage.hpp"
 
 #include <rocprim/device/device_scan.hpp>
 
@@ -1547,13 +1548,25 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 #define SAS_TAG_WIN 8
 #endif
 #define TAG_M40 (SAS_SA40_MAX - 1)
+// waves per SIMD the long-query (QW >= SAS_TAG_LB_QW) instances are built for
+#ifndef SAS_TAG_LB
+#define SAS_TAG_LB 5
+#endif
+#ifndef SAS_TAG_LB_QW
+#define SAS_TAG_LB_QW 1
+#endif
+// threads per block of k_sa_tagged (one wave per SIMD per block: the grid is num_cus x
+// SAS_TAG_LB blocks)
+#ifndef SAS_TAG_BLOCK
+#define SAS_TAG_BLOCK 256
+#endif
 
 // chars [p, p+12) of a packed 32-char key (p + 12 <= 32)
 __device__ __forceinline__ uint32_t tag_of_key(uint64_t k64, uint32_t p) { return (uint32_t)((k64 << (2 * p)) >> 40); }
 
 // suffix(e) >= q, for an entry of q's bucket
-template <int QW>
-__device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArgs& a, const QueryRegs<QW>& q) {
+template <int QW, class Q>
+__device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArgs& a, const Q& q) {
     const uint32_t T = (uint32_t)(e >> 40);
     if (T != Q12) return T > Q12;
     const uint64_t p = e & TAG_M40;
@@ -1565,9 +1578,9 @@ __device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArg
 
 // the first min(m, len) chars of suffix(e) are > q, for an entry of the bucket of q's routing
 // key (Q3 = q padded with 3s when m <= p + 12, else q's own; as sector_gt_prefix)
-template <int QW>
+template <int QW, class Q>
 __device__ __forceinline__ bool tag_gt_prefix(uint64_t e, uint32_t Q12, uint32_t Q3t, const SearchArgs& a,
-                                              const QueryRegs<QW>& q) {
+                                              const Q& q) {
     const uint32_t T = (uint32_t)(e >> 40);
     const uint32_t L = a.tag_p + SAS_TAG_CHARS;
     if (q.m <= L) return T > Q3t;
@@ -1585,12 +1598,122 @@ __device__ __forceinline__ void tag_bucket(const SearchArgs& a, uint64_t x, uint
     *hi = c == 0xFFFFFFull ? (a.tag_table[x + 1] & TAG_M40) : *lo + c;
 }
 
-template <int QW>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged(SearchArgs a) {
-    uint32_t bad = 0;
+// One lookup on the tagged index (q: QueryRegs or WaveQuery).
+template <int QW, class Q>
+__device__ __forceinline__ void tagged_lookup(const SearchArgs& a, const Q& q, uint64_t i) {
     const uint64_t* ent = reinterpret_cast<const uint64_t*>(a.sa);
     const uint64_t sa_n = a.sa_n;
     const uint32_t sh = 64 - 2 * a.tag_p;
+    const uint64_t K64 = q.w[0];
+    const uint32_t Q12 = tag_of_key(K64, a.tag_p);
+    uint64_t lo, hi;
+    tag_bucket(a, K64 >> sh, &lo, &hi);
+    // candidates are ranks lo .. hi (rank hi = the next bucket's first suffix, > q: the
+    // answer when every suffix of the bucket is < q); the window holds the first nw
+    const uint64_t span = hi - lo + 1;
+    const uint32_t nw = span < SAS_TAG_WIN ? (uint32_t)span : (uint32_t)SAS_TAG_WIN;
+    uint64_t e[SAS_TAG_WIN];
+#pragma unroll
+    for (int j = 0; j < SAS_TAG_WIN; j++)
+        e[j] = ((uint32_t)j < nw && lo + j < sa_n) ? __builtin_nontemporal_load(ent + lo + j) : 0ull;
+    // first slot whose tag is >= q's (or rank hi): every slot before it is < q (tags are
+    // sorted within a bucket)
+    uint32_t j0 = nw;
+#pragma unroll
+    for (int j = SAS_TAG_WIN - 1; j >= 0; j--)
+        if ((uint32_t)j < nw && (lo + j == hi || (uint32_t)(e[j] >> 40) >= Q12)) j0 = (uint32_t)j;
+    uint64_t ej = e[0];
+#pragma unroll
+    for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
+    uint64_t ans = 0, pos = 0, start;
+    bool done = false;
+    if (j0 < nw) {
+        const uint64_t r = lo + j0;
+        if (r >= sa_n) {
+            ans = r;
+            pos = a.next_pos;
+            done = true;
+        } else if (r == hi || tag_ge<QW>(ej, Q12, a, q)) {
+            ans = r;
+            pos = ej & TAG_M40;
+            done = true;
+        }
+        start = r + 1;  // a tag tie whose suffix is < q
+    } else {
+        start = lo + nw;  // the whole window is < q
+    }
+    if (!done) {  // binary search over the rest of the bucket (rank hi if nothing qualifies)
+        uint64_t l2 = start, h2 = hi, pr = QUAD_NO_SA;
+        while (l2 < h2) {
+            const uint64_t mid = (l2 + h2) >> 1;
+            const uint64_t f = __builtin_nontemporal_load(ent + mid);
+            if (tag_ge<QW>(f, Q12, a, q)) {
+                h2 = mid;
+                pr = f & TAG_M40;
+            } else {
+                l2 = mid + 1;
+            }
+        }
+        ans = l2;
+        pos = l2 >= sa_n ? a.next_pos : (pr != QUAD_NO_SA ? pr : (ent[l2] & TAG_M40));
+    }
+    a.out_pos[i] = pos;
+    if (a.out_probes) {  // the reference's cnt: the table, then binary_search over [lo, hi)
+        uint32_t probes = 1;
+        for (uint64_t l2 = lo, h2 = hi; l2 < h2; probes++) {
+            const uint64_t mid = (l2 + h2) >> 1;
+            if (mid < ans) l2 = mid + 1;
+            else h2 = mid;
+        }
+        a.out_probes[i] = probes;
+    }
+}
+
+// byte offset and length of query i
+__device__ __forceinline__ void query_span(const SearchArgs& a, uint64_t i, uint64_t* off, uint32_t* m) {
+    if (a.qoff) {
+        *off = a.qoff[i];
+        *m = a.qlen[i];
+    } else {
+        *off = i * (uint64_t)a.m_fixed;
+        *m = a.m_fixed;
+    }
+}
+
+#ifndef SAS_TAG_WQ
+#define SAS_TAG_WQ 1
+#endif
+
+template <int QW>
+__global__ __launch_bounds__(SAS_TAG_BLOCK, (QW >= SAS_TAG_LB_QW ? SAS_TAG_LB : 8)) void k_sa_tagged(SearchArgs a) {
+    uint32_t bad = 0;
+#if SAS_TAG_WQ
+    // wave-uniform loop over batches of 64 consecutive queries; the batch's bytes are staged
+    // through LDS (wave_stage_queries) unless they are spread out
+    __shared__ uint32_t wq[SAS_TAG_BLOCK / 64][2 * SAS_WQ_WORDS];
+    uint32_t* L32 = wq[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); b0 < a.nq;
+         b0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = b0 + lane;
+        const bool act = i < a.nq;
+        uint64_t qo = 0;
+        uint32_t m = 0;
+        if (act) query_span(a, i, &qo, &m);
+        uint64_t base;
+        if (wave_stage_queries(a.qbytes, qo, m, act, L32, &base)) {
+            if (act) {
+                WaveQuery q;
+                q.init(L32, (uint32_t)(qo - base), m);
+                tagged_lookup<QW>(a, q, i);
+            }
+        } else if (act) {
+            ByteQuery q;
+            q.init(a.qbytes + qo, m);
+            tagged_lookup<QW>(a, q, i);
+        }
+    }
+#else
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t* qb;
@@ -1598,70 +1721,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged(SearchArgs a) {
         query_ptr(a, i, &qb, &m);
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
-        const uint64_t K64 = q.w[0];
-        const uint32_t Q12 = tag_of_key(K64, a.tag_p);
-        uint64_t lo, hi;
-        tag_bucket(a, K64 >> sh, &lo, &hi);
-        // candidates are ranks lo .. hi (rank hi = the next bucket's first suffix, > q: the
-        // answer when every suffix of the bucket is < q); the window holds the first nw
-        const uint64_t span = hi - lo + 1;
-        const uint32_t nw = span < SAS_TAG_WIN ? (uint32_t)span : (uint32_t)SAS_TAG_WIN;
-        uint64_t e[SAS_TAG_WIN];
-#pragma unroll
-        for (int j = 0; j < SAS_TAG_WIN; j++)
-            e[j] = ((uint32_t)j < nw && lo + j < sa_n) ? __builtin_nontemporal_load(ent + lo + j) : 0ull;
-        // first slot whose tag is >= q's (or rank hi): every slot before it is < q (tags are
-        // sorted within a bucket)
-        uint32_t j0 = nw;
-#pragma unroll
-        for (int j = SAS_TAG_WIN - 1; j >= 0; j--)
-            if ((uint32_t)j < nw && (lo + j == hi || (uint32_t)(e[j] >> 40) >= Q12)) j0 = (uint32_t)j;
-        uint64_t ej = e[0];
-#pragma unroll
-        for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
-        uint64_t ans = 0, pos = 0, start;
-        bool done = false;
-        if (j0 < nw) {
-            const uint64_t r = lo + j0;
-            if (r >= sa_n) {
-                ans = r;
-                pos = a.next_pos;
-                done = true;
-            } else if (r == hi || tag_ge<QW>(ej, Q12, a, q)) {
-                ans = r;
-                pos = ej & TAG_M40;
-                done = true;
-            }
-            start = r + 1;  // a tag tie whose suffix is < q
-        } else {
-            start = lo + nw;  // the whole window is < q
-        }
-        if (!done) {  // binary search over the rest of the bucket (rank hi if nothing qualifies)
-            uint64_t l2 = start, h2 = hi, pr = QUAD_NO_SA;
-            while (l2 < h2) {
-                const uint64_t mid = (l2 + h2) >> 1;
-                const uint64_t f = __builtin_nontemporal_load(ent + mid);
-                if (tag_ge<QW>(f, Q12, a, q)) {
-                    h2 = mid;
-                    pr = f & TAG_M40;
-                } else {
-                    l2 = mid + 1;
-                }
-            }
-            ans = l2;
-            pos = l2 >= sa_n ? a.next_pos : (pr != QUAD_NO_SA ? pr : (ent[l2] & TAG_M40));
-        }
-        a.out_pos[i] = pos;
-        if (a.out_probes) {  // the reference's cnt: the table, then binary_search over [lo, hi)
-            uint32_t probes = 1;
-            for (uint64_t l2 = lo, h2 = hi; l2 < h2; probes++) {
-                const uint64_t mid = (l2 + h2) >> 1;
-                if (mid < ans) l2 = mid + 1;
-                else h2 = mid;
-            }
-            a.out_probes[i] = probes;
-        }
+        tagged_lookup<QW>(a, q, i);
     }
+#endif
     if (bad) atomicOr(a.bad, 1u);
 }
 
@@ -1846,7 +1908,12 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
     bool top = !(flags & SAS_NO_LDS_TOP);
     const bool range = (flags & SAS_PREFIX_RANGE) != 0;
-    if (algo == SAS_ALGO_INTERP) {
+    if (algo == SAS_ALGO_TAGGED) {
+        uint64_t tb = (a.nq + SAS_TAG_BLOCK - 1) / SAS_TAG_BLOCK;
+        const uint64_t tcap = (uint64_t)x->num_cus * (qw >= SAS_TAG_LB_QW ? SAS_TAG_LB : 8);
+        if (tb > tcap) tb = tcap;
+        launch_w8(algo, top, qw, dim3((unsigned)tb), dim3(SAS_TAG_BLOCK), st, a);
+    } else if (algo == SAS_ALGO_INTERP) {
         if (x->quad_leaves && !x->quad_compact) launch_interp<4, true>(qw, grid, block, st, a, range);
         else if (x->sa_w == 8) launch_interp<8, false>(qw, grid, block, st, a, range);
         else if (x->sa_w == 5) launch_interp<5, false>(qw, grid, block, st, a, range);
@@ -1952,6 +2019,139 @@ struct DeviceBuf {
     ~DeviceBuf() { if (p) (void)hipFree(p); }
 };
 
+// ------------------------------------------------------------------ host-pointer pipeline
+void sas_stage_pool_free(StagePool* p) {
+    if (!p) return;
+    for (StageSet* s : p->free_sets) stage_set_free(s);
+    delete p;
+}
+
+enum HostMode {
+    HM_FIXED = 0,   // fixed-length query bytes, staged as bytes
+    HM_RAGGED = 1,  // ragged query bytes, gathered chunk by chunk
+    HM_PACK = 2,    // fixed-length bytes, m <= 32, PREFIX: packed to 2-bit words on the host
+    HM_WORDS = 3,   // the caller's packed words (sas_search_packed)
+};
+
+// Synchronous search of host arrays through the index's pinned staging slots (host_stage.hpp).
+// Returns with out_pos / out_probes filled; EINVAL (after the whole batch) if a query byte
+// is not a DNA code.
+static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, const uint64_t* qoff,
+                         const uint32_t* qlen, const uint64_t* qwords, uint32_t m, uint64_t nq, int algo,
+                         uint64_t* out_pos, uint32_t* out_probes, hipStream_t user_st, uint32_t flags) {
+    StageLease lease;
+    TRY_RC(stage_acquire(x, &lease));
+    StageSet& S = *lease.set;
+    HIP_TRY(hipStreamSynchronize(user_st));  // the caller's earlier work on its stream
+    const bool validate = mode == HM_FIXED || mode == HM_RAGGED;
+    std::atomic<uint32_t> host_bad{0};
+    uint32_t dev_bad = 0;
+    HostPool& pool = HostPool::get();
+    int err = 0;
+    auto finish = [&](StageSlot& sl) -> int {
+        HIP_TRY(hipStreamSynchronize(sl.st));
+        const uint64_t k = sl.e - sl.s;
+        par_memcpy(out_pos + sl.s, sl.h_out, k * 8);
+        if (out_probes) memcpy(out_probes + sl.s, sl.h_pr, k * 4);
+        if (validate) dev_bad |= *sl.h_bad;
+        sl.busy = false;
+        return 0;
+    };
+    auto drain = [&]() {
+        for (auto& sl : S.slot)
+            if (sl.busy) {
+                (void)hipStreamSynchronize(sl.st);
+                sl.busy = false;
+            }
+    };
+    uint64_t s = 0;
+    for (int c = 0; s < nq && !err; c++) {
+        StageSlot& sl = S.slot[c % SAS_STAGE_SLOTS];
+        if (sl.busy && (err = finish(sl))) break;
+        SearchArgs a{};
+        fill_args(x, a);
+        a.m_fixed = m;
+        uint64_t k = 0, in_bytes = 0;
+        int qw = 1;
+        if (mode == HM_FIXED) {
+            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_bytes / std::max(m, 1u), S.cap_q));
+            in_bytes = k * m;
+            par_memcpy(sl.h_in, qbytes + s * m, in_bytes);
+            qw = qw_for(m);
+        } else if (mode == HM_WORDS) {
+            k = std::min<uint64_t>(nq - s, S.cap_q);
+            in_bytes = k * 8;
+            par_memcpy(sl.h_in, qwords + s, in_bytes);
+        } else if (mode == HM_PACK) {
+            k = std::min<uint64_t>(nq - s, S.cap_q);
+            in_bytes = k * 8;
+            const uint64_t per = 16384;
+            const int parts = (int)((k + per - 1) / per);
+            uint64_t* w = reinterpret_cast<uint64_t*>(sl.h_in);
+            const uint8_t* src = qbytes + s * m;
+            pool.run(parts, [&](int pi) {
+                const uint64_t b = pi * per, e = std::min(k, b + per);
+                const uint8_t r = host_pack_words(src + b * m, m, e - b, w + b);
+                if (r & 0xFC) host_bad.fetch_or(1);
+            });
+        } else {  // ragged: consecutive queries up to the byte and count caps (at least one)
+            uint64_t bytes = 0, e = s;
+            uint32_t maxlen = 0;
+            while (e < nq && e - s < S.cap_q && (e == s || bytes + qlen[e] <= S.cap_bytes)) {
+                sl.h_off[e - s] = bytes;
+                sl.h_len[e - s] = qlen[e];
+                bytes += qlen[e];
+                maxlen = std::max(maxlen, qlen[e]);
+                e++;
+            }
+            k = e - s;
+            in_bytes = bytes;
+            const uint64_t per = 4096;
+            const int parts = (int)((k + per - 1) / per);
+            pool.run(parts, [&](int pi) {
+                const uint64_t b = pi * per, ee = std::min(k, b + per);
+                for (uint64_t j = b; j < ee; j++) memcpy(sl.h_in + sl.h_off[j], qbytes + qoff[s + j], sl.h_len[j]);
+            });
+            qw = qw_for(maxlen);
+        }
+        HIP_TRY(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes, hipMemcpyHostToDevice, sl.st));
+        if (mode == HM_RAGGED) {
+            HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, k * 8, hipMemcpyHostToDevice, sl.st));
+            HIP_TRY(hipMemcpyAsync(sl.d_len, sl.h_len, k * 4, hipMemcpyHostToDevice, sl.st));
+            a.qoff = sl.d_off;
+            a.qlen = sl.d_len;
+        }
+        if (mode == HM_WORDS || mode == HM_PACK) a.qwords = reinterpret_cast<const uint64_t*>(sl.d_in);
+        else a.qbytes = sl.d_in;
+        a.nq = k;
+        a.out_pos = sl.d_out;
+        a.out_probes = out_probes ? sl.d_pr : nullptr;
+        a.bad = x->scratch;
+        if (validate) {
+            HIP_TRY(hipMemsetAsync(sl.d_bad, 0, 4, sl.st));
+            a.bad = sl.d_bad;
+            uint64_t vb = (k + 255) / 256;
+            if (vb > 65536) vb = 65536;
+            hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, sl.st, a.qbytes, a.qoff, a.qlen,
+                               a.m_fixed, k, a.bad);
+        }
+        if ((err = launch_search(x, a, algo, qw, flags | SAS_DEVICE_PTRS, sl.st))) break;
+        HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, k * 8, hipMemcpyDeviceToHost, sl.st));
+        if (out_probes) HIP_TRY(hipMemcpyAsync(sl.h_pr, sl.d_pr, k * 4, hipMemcpyDeviceToHost, sl.st));
+        if (validate) HIP_TRY(hipMemcpyAsync(sl.h_bad, sl.d_bad, 4, hipMemcpyDeviceToHost, sl.st));
+        sl.busy = true;
+        sl.s = s;
+        sl.e = s + k;
+        s += k;
+    }
+    for (int c = 0; c < SAS_STAGE_SLOTS && !err; c++)
+        if (S.slot[c].busy) err = finish(S.slot[c]);
+    drain();
+    if (err) return err;
+    if (dev_bad || host_bad.load()) SAS_FAIL(EINVAL, "search: query bytes must be DNA codes 0..3");
+    return 0;
+}
+
 // Host-pointer calls stage through plain hipMalloc + synchronous copies: the
 // stream-ordered allocator + pageable async copies raced on the null stream.
 static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
@@ -1968,6 +2168,19 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
     hipStream_t st = static_cast<hipStream_t>(stream);
     bool dev = flags & SAS_DEVICE_PTRS;
 
+    if (!dev) {
+        // host arrays: the pinned, chunked pipeline (host_pipeline) unless one query alone
+        // exceeds a staging chunk
+        uint64_t maxlen = m_fixed;
+        if (ragged)
+            for (uint64_t k = 0; k < nq; k++) maxlen = qlen[k] > maxlen ? qlen[k] : maxlen;
+        if (maxlen <= SAS_STAGE_BYTES) {
+            const bool pack = !ragged && algo == SAS_ALGO_PREFIX && m_fixed > 0 && m_fixed <= 32 &&
+                              !(flags & SAS_PREFIX_RANGE);
+            return host_pipeline(x, ragged ? HM_RAGGED : (pack ? HM_PACK : HM_FIXED), qbytes, qoff, qlen, nullptr,
+                                 m_fixed, nq, algo, out_pos, out_probes, st, flags);
+        }
+    }
     SearchArgs a{};
     fill_args(x, a);
     a.nq = nq;
@@ -2101,6 +2314,9 @@ extern "C" int sas_search_packed(const sas_index* x, const uint64_t* qwords, uin
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const bool dev = flags & SAS_DEVICE_PTRS;
+    if (!dev)
+        return host_pipeline(x, HM_WORDS, nullptr, nullptr, nullptr, qwords, m, nq, algo, out_pos, out_probes, st,
+                             flags);
     SearchArgs a{};
     fill_args(x, a);
     a.nq = nq;
@@ -2284,12 +2500,15 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_count(const uint32_t* __res
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) cnt[(uint64_t)w * nblk + blockIdx.x] = h[w];
 }
 
+// cap == 0: buckets packed back to back (slot = the exclusive scan); cap > 0: bucket w
+// owns slots [w * cap, (w + 1) * cap) and a query past its bucket's cap is not copied (its
+// slot is clamped to the last one; the caller sees the overflow in out_counts > cap)
 __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __restrict__ dest, uint64_t nq,
                                                              uint32_t W, uint64_t nblk,
                                                              const uint64_t* __restrict__ base_slot,
                                                              const uint8_t* __restrict__ qbytes, uint32_t m,
                                                              uint8_t* __restrict__ send,
-                                                             uint64_t* __restrict__ slot_of) {
+                                                             uint64_t* __restrict__ slot_of, uint64_t cap) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
@@ -2299,7 +2518,15 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
         const uint64_t i = base + (uint64_t)it * PACK_BLOCK + threadIdx.x;
         if (i >= nq) continue;
         const uint32_t w = dest[i];
-        const uint64_t slot = base_slot[(uint64_t)w * nblk + blockIdx.x] + atomicAdd(&h[w], 1u);
+        uint64_t slot = base_slot[(uint64_t)w * nblk + blockIdx.x] + atomicAdd(&h[w], 1u);
+        if (cap) {
+            const uint64_t r = slot - base_slot[(uint64_t)w * nblk];  // rank inside bucket w
+            if (r >= cap) {
+                slot_of[i] = (uint64_t)W * cap - 1;
+                continue;
+            }
+            slot = (uint64_t)w * cap + r;
+        }
         slot_of[i] = slot;
         const uint8_t* src = qbytes + i * (uint64_t)m;
         uint8_t* dst = send + slot * (uint64_t)m;
@@ -2321,9 +2548,9 @@ __global__ void k_pack_totals(const uint64_t* __restrict__ base_slot, uint32_t W
     }
 }
 
-extern "C" int sas_route_pack(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
-                              const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_counts,
-                              uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
+static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
+                           const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t cap, uint64_t* out_counts,
+                           uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
     if (!x || (nsplit && !splitter_pos) || !out_counts || (nq && (!qbytes || !out_send || !out_slot)))
         SAS_FAIL(EINVAL, "sas_route_pack: null argument");
     if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_route_pack: device pointers only (SAS_DEVICE_PTRS)");
@@ -2355,13 +2582,26 @@ extern "C" int sas_route_pack(const sas_index* x, const uint64_t* splitter_pos, 
     HIP_TRY(rocprim::exclusive_scan(tmp, tbytes, static_cast<uint64_t*>(cnt), static_cast<uint64_t*>(cnt),
                                     (uint64_t)0, (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
     hipLaunchKernelGGL(k_pack_scatter, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest),
-                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot);
+                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot, cap);
     hipLaunchKernelGGL(k_pack_totals, dim3(1), dim3(256), 0, st, static_cast<uint64_t*>(cnt), W, nblk, nq, out_counts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFreeAsync(dest, st));
     HIP_TRY(hipFreeAsync(cnt, st));
     HIP_TRY(hipFreeAsync(tmp, st));
     return 0;
+}
+
+extern "C" int sas_route_pack(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
+                              const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_counts,
+                              uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
+    return route_pack_impl(x, splitter_pos, nsplit, qbytes, m, nq, 0, out_counts, out_send, out_slot, stream, flags);
+}
+
+extern "C" int sas_route_pack_cap(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
+                                  const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t cap, uint64_t* out_counts,
+                                  uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
+    if (cap == 0) SAS_FAIL(EINVAL, "sas_route_pack_cap: cap must be > 0");
+    return route_pack_impl(x, splitter_pos, nsplit, qbytes, m, nq, cap, out_counts, out_send, out_slot, stream, flags);
 }
 
 // ------------------------------------------------------------------ occurrence ranges

@@ -222,7 +222,7 @@ def test_tagged_saturated_bucket(sas):
     idx = sas.SaNaive.build(t, tagged=True, lcp=False)
     st = idx.stats()
     p = st["tag_chars"]
-    assert p == 12
+    assert p == 13  # ceil(log4 n): 4^12 = 2^24 < n; one bucket holds all n > 2^24 - 1 suffixes
     sa = idx.suffix_array(count=5)
     assert sa.tolist() == [n - 1 - r for r in range(5)]
     ms = [1, 5, 11, 12, 13, 27, 28, 29, 100, 257, 4000, n, n + 1]
