@@ -213,8 +213,12 @@ def host_cpu() -> str:
 
 
 def host_threads() -> int:
-    """Every core this process may run on (its affinity mask)."""
-    return len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    """The cores this process is allotted: its affinity mask, capped by OMP_NUM_THREADS when
+    the host sets it (the GPU box allots 16 cores per GPU and exports OMP_NUM_THREADS=16,
+    while its affinity mask shows the whole machine)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    share = os.environ.get("OMP_NUM_THREADS", "")
+    return max(1, min(n, int(share))) if share.isdigit() and int(share) > 0 else n
 
 
 def record(name, lookups, kernel_ms, wall_s, bpl, idx_bytes, pmc, probes, extra=None):
@@ -319,7 +323,7 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
             "sample": f"oracle/{algo} (restates sas/sa_search.rs "
                       f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
                       f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA, {dt:.1f} s, "
-                      f"{threads} threads (every core of this process's affinity mask), contiguous chunks "
+                      f"{threads} threads (this process's allotted cores), contiguous chunks "
                       f"(sst/bin/bench.rs:558-573)", "_pos": pos}
 
 
@@ -725,7 +729,9 @@ def main():
 
         def step():
             if args.mode == "shard":
-                dst.copy_(engine.search_fixed(qbytes, m))
+                # fixed-capacity buckets, no host sync inside the step; the overflow flag is
+                # checked once after the timed loop (engine.assert_no_overflow)
+                dst.copy_(engine.search_fixed(qbytes, m, check=False))
             elif algo == "prefix_packed":
                 idx.search_packed(packed["w"], m, out=dst)
             else:
@@ -753,6 +759,8 @@ def main():
         return float(vp.double().mean().item())
 
     el, kernel_ms = run_algo(args.algo, args.steps, args.warmup, out)
+    if args.mode == "shard":
+        engine.assert_no_overflow()
     log(f"headline {args.algo}: {kernel_ms:.3f} ms per {nq}")
     # correctness guard (untimed): every answer is an occurrence of its query, and a sample
     # is proven an exact lower bound on the index's own SA

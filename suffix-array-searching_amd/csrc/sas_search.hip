@@ -2083,7 +2083,9 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
             in_bytes = k * 8;
             par_memcpy(sl.h_in, qwords + s, in_bytes);
         } else if (mode == HM_PACK) {
-            k = std::min<uint64_t>(nq - s, S.cap_q);
+            // smaller chunks than the byte modes: the host packing is the longest stage, and
+            // the pipeline fills and drains faster
+            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_q, SAS_STAGE_PACK_Q));
             in_bytes = k * 8;
             const uint64_t per = 16384;
             const int parts = (int)((k + per - 1) / per);

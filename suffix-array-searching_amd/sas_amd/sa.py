@@ -263,21 +263,29 @@ class SaNaive:
                               out.ctypes.data, stream, 0))
         return out[:nq]
 
-    def route_pack(self, splitter_pos, qbytes, m: int, stream=None):
+    def route_pack(self, splitter_pos, qbytes, m: int, stream=None, cap: int | None = None, send=None):
         """Send side of one sharded step, fused on the GPU (sas_route_pack): CUDA
         tensors in -> (counts int64 [W], send uint8 [nq*m] grouped by shard,
-        slot int64 [nq] = send position of each query)."""
+        slot int64 [nq] = send position of each query).  cap: fixed-capacity buckets
+        (sas_route_pack_cap): send holds W*cap*m bytes, bucket w at [w*cap*m, ...), and
+        counts > cap on the device marks an overflow.  `send` may be passed in (reused)."""
         import torch
         nq = qbytes.numel() // m
         W = splitter_pos.numel() + 1
         counts = torch.empty(W, dtype=torch.int64, device=qbytes.device)
-        send = torch.empty(max(nq * m, 1), dtype=torch.uint8, device=qbytes.device)
+        size = (W * cap if cap else nq) * m
+        if send is None or send.numel() < max(size, 1):
+            send = torch.zeros(max(size, 1), dtype=torch.uint8, device=qbytes.device)
         slot = torch.empty(max(nq, 1), dtype=torch.int64, device=qbytes.device)
         st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
-        check(lib().sas_route_pack(self._h, splitter_pos.data_ptr() if W > 1 else None, W - 1, qbytes.data_ptr(), m,
-                                   nq, counts.data_ptr(), send.data_ptr(), slot.data_ptr(), st,
-                                   _lib.SAS_DEVICE_PTRS))
-        return counts, send[: nq * m], slot[:nq]
+        sp = splitter_pos.data_ptr() if W > 1 else None
+        if cap:
+            check(lib().sas_route_pack_cap(self._h, sp, W - 1, qbytes.data_ptr(), m, nq, int(cap), counts.data_ptr(),
+                                           send.data_ptr(), slot.data_ptr(), st, _lib.SAS_DEVICE_PTRS))
+        else:
+            check(lib().sas_route_pack(self._h, sp, W - 1, qbytes.data_ptr(), m, nq, counts.data_ptr(),
+                                       send.data_ptr(), slot.data_ptr(), st, _lib.SAS_DEVICE_PTRS))
+        return counts, send[:size], slot[:nq]
 
     def verify(self):
         check(lib().sas_verify(self._h))

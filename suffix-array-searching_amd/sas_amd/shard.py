@@ -2,15 +2,24 @@
 one per GPU; queries are routed to the GPU owning their lower bound and the
 positions come back -- the only place this engine uses a collective.
 
-    rank g holds global SA ranks [g*n/W, (g+1)*n/W) (SaNaive.build(rank_range=...)),
-    splitters = text positions of the first suffix of shards 1..W-1 (all-gathered once),
-    step: route (sas_route) -> group by destination -> all_to_all counts, query bytes
-          -> local lookup -> all_to_all positions back -> restore query order.
+    rank g holds global SA ranks [g*n/W, (g+1)*n/W) (SaNaive.build(rank_range=...) or
+    SaNaive.build_part), splitters = text positions of the first suffix of shards 1..W-1
+    (all-gathered once),
+    step: route + group by destination into fixed-capacity buckets (sas_route_pack_cap)
+          -> all_to_all query bytes (equal splits) -> local lookup of every received slot
+          -> all_to_all positions back (equal splits) -> gather by send slot.
 
 Hash-partitioning the SA would break its order (a lower bound would need every
 shard); rank ranges keep each answer on exactly one shard.  The collective is
 `torch.distributed.all_to_all_single` (RCCL over xGMI with backend "nccl";
 gloo in the CPU tests).  Payload per query: m bytes out, 8 bytes back.
+
+Fixed-capacity buckets (cap = nq * slack / W per destination, agreed by all ranks) make
+both exchanges equal-split, so a step issues no host synchronisation: no count exchange,
+no .tolist().  A bucket that overflows its cap is detected on the device; with
+`check=True` (the default) the step reads that one flag and redoes itself with exact
+variable-size exchanges, so results are always exact; `check=False` defers the flag to
+`assert_no_overflow()` (the bench calls it once after its timed loop).
 """
 from __future__ import annotations
 
@@ -23,21 +32,95 @@ def shard_range(n: int, world: int, rank: int) -> tuple[int, int]:
 class ShardedSearch:
     """`index` needs: .route(splitters, qbytes, m) -> dest shard per query,
     .search_fixed(qbytes, m, algo=...) -> positions (int64), .suffix_array(1) ->
-    its first SA value.  The GPU implementation is sas_amd.SaNaive."""
+    its first SA value; the GPU implementation (sas_amd.SaNaive) also has
+    .route_pack(splitters, qbytes, m, cap=None) (the fused send side)."""
 
-    def __init__(self, index, dist, world: int, rank: int, device, algo: str = "stree", group=None):
+    SLACK = 1.125  # bucket capacity over the balanced share
+
+    def __init__(self, index, dist, world: int, rank: int, device, algo: str = "stree", group=None,
+                 slack: float | None = None, min_cap: int = 256):
         import torch
         self.index, self.dist, self.world, self.rank = index, dist, world, rank
         self.device, self.algo, self.group = device, algo, group
+        self.slack = self.SLACK if slack is None else slack
+        self.min_cap = min_cap
         first = torch.tensor([int(index.suffix_array(1)[0])], dtype=torch.int64, device=device)
         firsts = [torch.empty_like(first) for _ in range(world)]
         dist.all_gather(firsts, first, group=group)
         # first suffix of shards 1..W-1, in increasing suffix order
         self.splitters = torch.cat(firsts[1:]).to(torch.int64) if world > 1 else torch.empty(0, dtype=torch.int64,
                                                                                               device=device)
+        self._caps = {}  # nq -> capacity agreed by every rank
+        self._bufs = {}
+        self.overflow = torch.zeros(1, dtype=torch.bool, device=device)
 
-    def search_fixed(self, qbytes, m: int):
+    # ---------------------------------------------------------------- capacity
+    def capacity(self, nq: int) -> int:
+        """Per-destination bucket capacity for a batch of nq queries: every rank must use
+        the same one (equal all-to-all splits), so it is the MAX over ranks, agreed once
+        per batch size."""
+        import torch
+        if nq not in self._caps:
+            if self.world == 1:
+                cap = nq
+            else:
+                cap = min(nq, int(nq * self.slack / self.world) + self.min_cap)
+            t = torch.tensor([max(cap, 1)], dtype=torch.int64, device=self.device)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+            self._caps[nq] = int(t.item())
+        return self._caps[nq]
+
+    def _buffers(self, nq: int, m: int, cap: int):
+        import torch
+        key = (nq, m)
+        if key not in self._bufs:
+            W = self.world
+            self._bufs[key] = {
+                "send": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device),
+                "recv": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device),
+                "back": torch.empty(W * cap, dtype=torch.int64, device=self.device),
+                "local": torch.empty(W * cap, dtype=torch.int64, device=self.device),
+            }
+        return self._bufs[key]
+
+    # ---------------------------------------------------------------- steps
+    def search_fixed(self, qbytes, m: int, check: bool = True):
         """qbytes: uint8 tensor [nq*m] of this rank's queries -> int64 positions."""
+        if not hasattr(self.index, "route_pack"):
+            return self.search_fixed_exact(qbytes, m)
+        import torch
+        nq = qbytes.numel() // m
+        cap = self.capacity(nq)
+        buf = self._buffers(nq, m, cap)
+        counts, send, slot = self.index.route_pack(self.splitters, qbytes, m, cap=cap, send=buf["send"])
+        self.dist.all_to_all_single(buf["recv"], send, group=self.group)
+        self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
+        self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group)
+        over = (counts > cap).any().reshape(1)
+        out = buf["back"].index_select(0, slot)
+        if check:
+            # one flag per rank, agreed by all (an overflow anywhere changes every rank's
+            # exchange): redo the step with exact splits
+            flag = over.to(torch.int32)
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
+            if int(flag.item()):
+                return self.search_fixed_exact(qbytes, m)
+        else:
+            self.overflow |= over
+        return out
+
+    def assert_no_overflow(self):
+        """After steps run with check=False: every bucket fitted its capacity (so every
+        result was exact)."""
+        import torch
+        flag = self.overflow.to(torch.int32)
+        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
+        if int(flag.item()):
+            raise RuntimeError("ShardedSearch: a bucket overflowed its capacity in a check=False step; "
+                               "raise slack or run with check=True")
+
+    def search_fixed_exact(self, qbytes, m: int):
+        """Variable-size exchanges (counts first): exact for any routing, two host syncs."""
         import torch
         dist = self.dist
         if hasattr(self.index, "route_pack"):

@@ -93,7 +93,40 @@ class OracleShard:
         qs = qbytes.view(-1, m).tolist()
         return torch.tensor([sum(self.tb[s:] < bytes(q) for s in sp) for q in qs], dtype=torch.int32)
 
-    def search_fixed(self, qbytes, m, algo=None):
+    def route_pack(self, splitters, qbytes, m, cap=None, send=None):
+        """sas_route_pack / sas_route_pack_cap semantics in torch: queries grouped by
+        destination; with cap, bucket w owns send slots [w*cap, (w+1)*cap) and a query past
+        its bucket's cap is dropped (slot W*cap - 1, counts > cap)."""
+        import torch
+        nq = qbytes.numel() // m
+        W = splitters.numel() + 1
+        dest = self.route(splitters, qbytes, m).to(torch.int64)
+        counts = torch.bincount(dest, minlength=W)
+        order = torch.argsort(dest, stable=True)
+        starts = torch.cumsum(counts, 0) - counts
+        rank_in = torch.empty(nq, dtype=torch.int64)
+        rank_in[order] = torch.arange(nq) - starts[dest[order]]
+        if not cap:
+            slot = starts[dest] + rank_in
+            qsend = torch.zeros(nq * m, dtype=torch.uint8)
+            qsend.view(nq, m)[slot] = qbytes.view(nq, m)
+            return counts, qsend, slot
+        if send is None or send.numel() < W * cap * m:
+            send = torch.zeros(W * cap * m, dtype=torch.uint8)
+        ok = rank_in < cap
+        slot = torch.where(ok, dest * cap + rank_in, torch.full_like(dest, W * cap - 1))
+        send.view(-1, m)[slot[ok]] = qbytes.view(nq, m)[ok]
+        return counts, send[: W * cap * m], slot
+
+    def search_fixed(self, qbytes, m, algo=None, out=None):
+        import torch
+        res = self._search(qbytes, m)
+        if out is not None:
+            out.copy_(res)
+            return out
+        return res
+
+    def _search(self, qbytes, m):
         import torch
         out = []
         for q in qbytes.view(-1, m).tolist():
@@ -125,7 +158,21 @@ def shard_worker(rank, ws, port, res):
     qs = np.stack([t[o:o + m] for o in offs])
     qs[: nq // 4] = rng.integers(0, 4, (nq // 4, m))  # negatives too
     qs[-1] = 3  # above every suffix -> n
-    pos = eng.search_fixed(torch.from_numpy(qs.reshape(-1).copy()), m)
+    dq = torch.from_numpy(qs.reshape(-1).copy())
+    pos = eng.search_fixed(dq, m)  # fixed-capacity buckets, the overflow flag checked
+    pos2 = eng.search_fixed(dq, m, check=False)  # deferred check
+    eng.assert_no_overflow()
+    exact = eng.search_fixed_exact(dq, m)  # variable-size exchanges
+    assert pos.tolist() == pos2.tolist() == exact.tolist()
+    # skewed batch (every query the same) into tiny buckets: the checked step overflows and
+    # redoes itself exactly; the deferred one reports the overflow
+    tight = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", slack=0.5, min_cap=0)
+    skew = torch.from_numpy(np.tile(qs[nq // 2], nq // 4).copy())
+    got = tight.search_fixed(skew, m)
+    assert got.tolist() == eng.search_fixed_exact(skew, m).tolist()
+    tight.search_fixed(skew, m, check=False)
+    with pytest.raises(RuntimeError):
+        tight.assert_no_overflow()
     res[rank] = (qs.tolist(), pos.tolist())
     dist.destroy_process_group()
 

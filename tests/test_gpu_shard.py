@@ -1,0 +1,180 @@
+"""Sharded-text mode on the GPU: ShardedSearch over sas_build_part indexes,
+fixed-capacity buckets from sas_route_pack_cap, against the whole index.
+
+* ws = 1 through a real RCCL ("nccl") process group, initialised in this process;
+* W = 3 parts on one GPU through a loopback exchange (three threads, one per rank, a
+  torch.distributed-shaped object that moves the all-to-all chunks between them), so that
+  the routing, the bucket layout and the slot gather of a multi-part step run on the GPU.
+Bar: positions bit-identical to the whole index's PLAIN search; an overflowing bucket is
+redone exactly (check=True) or reported (check=False -> assert_no_overflow raises).
+"""
+import os
+import socket
+import threading
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def sas():
+    import sas_amd
+    return sas_amd
+
+
+def queries(t, nq, m, seed):
+    rng = np.random.default_rng(seed)
+    n = len(t)
+    offs = rng.integers(0, n - m, nq)
+    qs = np.stack([t[o:o + m] for o in offs])
+    qs[: nq // 5] = rng.integers(0, 4, (nq // 5, m))  # negatives
+    qs[-1] = 3
+    qs[-2] = 0
+    return qs.reshape(-1).copy()
+
+
+def test_sharded_nccl_world1(sas):
+    """RCCL process group of one rank: the whole step (route_pack_cap, two equal-split
+    all_to_all_single, search, slot gather) with no host synchronisation inside."""
+    import torch
+    import torch.distributed as dist
+    from sas_amd.shard import ShardedSearch
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        n, nq, m = 1_000_003, 50_000, 32
+        t = sas.random_string(n, seed=21)
+        full = sas.SaNaive.build(t)
+        part = sas.SaNaive.build_part(torch.from_numpy(t).cuda(), 0, 1)
+        qb = queries(t, nq, m, 1)
+        expect = full.search_fixed(qb, m, algo="plain")
+        dq = torch.from_numpy(qb).cuda()
+        for algo in ("plain", "quad", "prefix"):
+            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo)
+            got = eng.search_fixed(dq, m)
+            got2 = eng.search_fixed(dq, m, check=False)
+            eng.assert_no_overflow()
+            exact = eng.search_fixed_exact(dq, m)
+            torch.cuda.synchronize()
+            for g in (got, got2, exact):
+                assert np.array_equal(g.cpu().numpy().astype(np.uint64), expect), algo
+    finally:
+        dist.destroy_process_group()
+
+
+class Loopback:
+    """torch.distributed-shaped exchange between W threads of one process (one per rank);
+    every collective is three barriers: deposit, read, done."""
+
+    class ReduceOp:
+        MAX = "max"
+
+    def __init__(self, W):
+        self.W = W
+        self.bar = threading.Barrier(W)
+        self.slots = [None] * W
+
+    def _swap(self, rank, item):
+        self.slots[rank] = item
+        self.bar.wait()
+        items = list(self.slots)
+        self.bar.wait()
+        return items
+
+    def rank(self, r):
+        lb = self
+
+        class R:
+            ReduceOp = Loopback.ReduceOp
+
+            @staticmethod
+            def all_gather(outs, t, group=None):
+                items = lb._swap(r, t)
+                for i in range(lb.W):
+                    outs[i].copy_(items[i])
+                lb.bar.wait()
+
+            @staticmethod
+            def all_reduce(t, op=None, group=None):
+                import torch
+                items = lb._swap(r, t.clone())
+                t.copy_(torch.stack(items).max(0).values)
+                lb.bar.wait()
+
+            @staticmethod
+            def all_to_all_single(out, inp, out_splits=None, in_splits=None, group=None):
+                items = lb._swap(r, (inp, in_splits))
+                pos = 0
+                for src in range(lb.W):
+                    sin, ssp = items[src]
+                    if ssp is None:
+                        sz = sin.numel() // lb.W
+                        start = r * sz
+                    else:
+                        start, sz = sum(ssp[:r]), ssp[r]
+                    out[pos:pos + sz].copy_(sin[start:start + sz])
+                    pos += sz
+                lb.bar.wait()  # no rank reuses its send buffer before every copy is queued
+        return R
+
+
+@pytest.mark.parametrize("W", [3])
+def test_sharded_parts_loopback(sas, W):
+    """W sas_build_part indexes on one GPU, each driven by its own rank thread: routed,
+    bucketed, exchanged and gathered answers equal the whole index for every rank's
+    queries; a skewed batch into tiny buckets overflows, is redone exactly with
+    check=True and reported with check=False."""
+    import torch
+    from sas_amd.shard import ShardedSearch
+    n, nq, m = 2_000_003, 30_000, 24
+    t = sas.random_string(n, seed=23)
+    full = sas.SaNaive.build(t)
+    dt = torch.from_numpy(t).cuda()
+    parts = [sas.SaNaive.build_part(dt, g, W) for g in range(W)]
+    lb = Loopback(W)
+    qbs = [queries(t, nq, m, 10 + r) for r in range(W)]
+    expect = [full.search_fixed(q, m, algo="plain") for q in qbs]
+    res, errs = {}, []
+
+    def rank_main(r):
+        try:
+            d = lb.rank(r)
+            eng = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="plain")
+            dq = torch.from_numpy(qbs[r]).cuda()
+            a = eng.search_fixed(dq, m)
+            b = eng.search_fixed(dq, m, check=False)
+            eng.assert_no_overflow()
+            c = eng.search_fixed_exact(dq, m)
+            tight = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="quad", slack=0.5, min_cap=0)
+            skew = torch.from_numpy(np.tile(qbs[r][:m], nq // 10).copy()).cuda()
+            sk = tight.search_fixed(skew, m)
+            tight.search_fixed(skew, m, check=False)
+            raised = False
+            try:
+                tight.assert_no_overflow()
+            except RuntimeError:
+                raised = True
+            torch.cuda.synchronize()
+            res[r] = (a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), sk.cpu().numpy(), raised)
+        except Exception as e:  # surfaced below
+            errs.append((r, repr(e)))
+            lb.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errs, errs
+    for r in range(W):
+        a, b, c, sk, raised = res[r]
+        for g in (a, b, c):
+            assert np.array_equal(g.astype(np.uint64), expect[r]), r
+        skew_expect = full.search_fixed(np.tile(qbs[r][:m], nq // 10), m, algo="plain")
+        assert np.array_equal(sk.astype(np.uint64), skew_expect), r
+        assert raised, r
