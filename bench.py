@@ -679,7 +679,11 @@ def main():
     if args.mode == "shard":
         from sas_amd.shard import ShardedSearch
         # each rank builds ONLY its own SA rank range (sas_build_part: no whole-SA step)
-        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True, prefix=args.prefix_chars)  # 40-bit SA
+        # a part holds a 40-bit SA; below 2^32 chars it carries the same inline table as the
+        # replicated index, and PREFIX queries cross the exchange as 8-B packed words
+        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=True, stree=True, prefix=args.prefix_chars,
+                                         prefix_inline=({"ranks": 0, "inline": 1, "inline2": 2, "inline4": 4}
+                                                        [args.prefix_table] if n < (1 << 32) else 0))
         if dist is None:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -47,6 +47,9 @@ typedef struct sas_index sas_index;
 #define SAS_BUILD_VERIFY  (1u << 3)  /* run the adjacency + permutation check on the SA  */
 #define SAS_NO_LDS_TOP    (1u << 4)  /* search: do not serve the top levels from LDS     */
 #define SAS_VALIDATE      (1u << 5)  /* search: reject query bytes > 3 (synchronises)    */
+#define SAS_ROUTE_PACKED  (1u << 26)  /* sas_route_pack(_cap): write each query as one 2-bit
+                                         packed word (m <= 32, 8 B per send slot, the
+                                         sas_search_packed format) instead of its m bytes */
 #define SAS_NO_PREFIX_TABLE (1u << 25) /* sas_search_range: use the tree descents even when
                                         the index has a prefix table                      */
 #define SAS_PREFIX_RANGE  (1u << 24) /* search, PLAIN / LCP: start binary_search from the
@@ -240,6 +243,7 @@ int sas_route_pack(const sas_index* index, const uint64_t* splitter_pos, uint32_
                    const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_counts,
                    uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags);
 
+/* (SAS_ROUTE_PACKED in flags: out_send holds one u64 packed word per slot.) */
 /* sas_route_pack with fixed-capacity buckets: bucket w owns send slots [w*cap, (w+1)*cap)
  * (out_send holds (nsplit + 1) * cap * m bytes), so every rank's all-to-all uses equal splits
  * and needs no host-side counts.  out_counts[w] is the true count; a query past its bucket's
@@ -301,8 +305,11 @@ int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, 
  * declared but unimplemented!() in the reference): global SA ranks
  * [out_lo[k], out_hi[k]) of the suffixes that start with query k; the count
  * is out_hi - out_lo and the positions are SA[out_lo .. out_hi)
- * (sas_copy_sa_range).  Needs SAS_BUILD_QUAD (used if present) or SAS_BUILD_SECTOR.  Ragged queries as in
- * sas_search_batch. */
+ * (sas_copy_sa_range).  Needs SAS_BUILD_TAGGED, SAS_BUILD_QUAD or SAS_BUILD_SECTOR: the
+ * tagged index uses its bucket table; otherwise the prefix table when built beside the quad
+ * tree (unless SAS_NO_PREFIX_TABLE), else the quad tree, else the sector tree.  Both bounds
+ * of a query are bisected in lock step; no probe counts are reported (the reference has no
+ * range search to count against).  Ragged queries as in sas_search_batch. */
 int sas_search_range(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,
                      const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi,
                      void* stream, uint32_t flags);

@@ -915,8 +915,11 @@ __global__ void k_pt_big(const uint64_t* __restrict__ big, const unsigned long l
 static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     const uint64_t sa_n = x->sa_n;
     if (!x->quad_leaves) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX needs SAS_BUILD_QUAD (keys and SA values of the leaves)");
-    if (inl && (x->quad_compact || x->sa_w != 4))
-        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 / _INLINE4 need fused quad leaves and a u32 SA");
+    // inline entries hold a u32 rank and the low 32 bits of the SA value: fused leaves, and
+    // ranks and positions below 2^32 (a 40-bit SA qualifies when n < 2^32, e.g. a part index)
+    if (inl && (x->quad_compact || x->n > 0xFFFFFFFFull || sa_n >= 0xFFFFFFFFull))
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 / _INLINE4 need fused quad leaves, n < 2^32 and "
+                          "fewer than 2^32 - 1 SA entries");
     // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA, 16-B inline ones
     const uint32_t tw = inl ? 16 * inl : (x->sa_w == 5 ? 5 : 4);
     if (tw != 5 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");

@@ -2510,7 +2510,8 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
                                                              const uint64_t* __restrict__ base_slot,
                                                              const uint8_t* __restrict__ qbytes, uint32_t m,
                                                              uint8_t* __restrict__ send,
-                                                             uint64_t* __restrict__ slot_of, uint64_t cap) {
+                                                             uint64_t* __restrict__ slot_of, uint64_t cap,
+                                                             bool packed) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
@@ -2531,6 +2532,11 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
         }
         slot_of[i] = slot;
         const uint8_t* src = qbytes + i * (uint64_t)m;
+        if (packed) {  // SAS_ROUTE_PACKED: the query as one 2-bit word (m <= 32), 8 B per slot
+            uint32_t bad = 0;
+            reinterpret_cast<uint64_t*>(send)[slot] = pack_query_word(src, m, 0, &bad);
+            continue;
+        }
         uint8_t* dst = send + slot * (uint64_t)m;
         if (vec) {
             for (uint32_t k = 0; k < m; k += 16)
@@ -2557,6 +2563,7 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
         SAS_FAIL(EINVAL, "sas_route_pack: null argument");
     if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_route_pack: device pointers only (SAS_DEVICE_PTRS)");
     if (nsplit > SAS_MAX_SPLIT) SAS_FAIL(EINVAL, "sas_route_pack: too many splitters");
+    if ((flags & SAS_ROUTE_PACKED) && m > 32) SAS_FAIL(EINVAL, "sas_route_pack: SAS_ROUTE_PACKED needs m <= 32");
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     const uint32_t W = nsplit + 1;
@@ -2584,7 +2591,8 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
     HIP_TRY(rocprim::exclusive_scan(tmp, tbytes, static_cast<uint64_t*>(cnt), static_cast<uint64_t*>(cnt),
                                     (uint64_t)0, (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
     hipLaunchKernelGGL(k_pack_scatter, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest),
-                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot, cap);
+                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot, cap,
+                       (flags & SAS_ROUTE_PACKED) != 0);
     hipLaunchKernelGGL(k_pack_totals, dim3(1), dim3(256), 0, st, static_cast<uint64_t*>(cnt), W, nblk, nq, out_counts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFreeAsync(dest, st));

@@ -24,6 +24,7 @@ SAS_NO_LDS_TOP = 1 << 4
 SAS_VALIDATE = 1 << 5
 SAS_PREFIX_RANGE = 1 << 24
 SAS_NO_PREFIX_TABLE = 1 << 25
+SAS_ROUTE_PACKED = 1 << 26
 SAS_BUILD_WIDE = 1 << 6
 SAS_BUILD_SECTOR = 1 << 7
 SAS_BUILD_SA40 = 1 << 8

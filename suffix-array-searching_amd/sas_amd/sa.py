@@ -154,10 +154,11 @@ class SaNaive:
     @classmethod
     def build_part(cls, t, part: int, parts: int, lcp: bool = True, stree: bool = True, verify: bool = False,
                    flags: int = 0, sector: bool = True, quad: bool | str = True, llcp: bool | None = None,
-                   prefix: bool | int | None = None, prefix_inline: bool = False) -> "SaNaive":
+                   prefix: bool | int | None = None, prefix_inline: bool | int = False) -> "SaNaive":
         """Sharded-text index that builds ONLY its own SA rank range (sas_build_part):
         part `part` of `parts` contiguous 7-char-prefix bin ranges.  The range is
-        chosen by the library (stats: rank_lo, sa_entries, next_pos)."""
+        chosen by the library (stats: rank_lo, sa_entries, next_pos).  prefix_inline as in
+        build (inline tables need n < 2^32 beside the part's 40-bit SA)."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
@@ -263,28 +264,34 @@ class SaNaive:
                               out.ctypes.data, stream, 0))
         return out[:nq]
 
-    def route_pack(self, splitter_pos, qbytes, m: int, stream=None, cap: int | None = None, send=None):
+    def route_pack(self, splitter_pos, qbytes, m: int, stream=None, cap: int | None = None, send=None,
+                   packed: bool = False):
         """Send side of one sharded step, fused on the GPU (sas_route_pack): CUDA
         tensors in -> (counts int64 [W], send uint8 [nq*m] grouped by shard,
         slot int64 [nq] = send position of each query).  cap: fixed-capacity buckets
-        (sas_route_pack_cap): send holds W*cap*m bytes, bucket w at [w*cap*m, ...), and
-        counts > cap on the device marks an overflow.  `send` may be passed in (reused)."""
+        (sas_route_pack_cap): send holds W*cap slots, bucket w at slots [w*cap, ...), and
+        counts > cap on the device marks an overflow.  packed (m <= 32, SAS_ROUTE_PACKED):
+        each slot is the query's 8-B 2-bit word (send is int64) instead of its m bytes.
+        `send` may be passed in (reused)."""
         import torch
         nq = qbytes.numel() // m
         W = splitter_pos.numel() + 1
         counts = torch.empty(W, dtype=torch.int64, device=qbytes.device)
-        size = (W * cap if cap else nq) * m
-        if send is None or send.numel() < max(size, 1):
-            send = torch.zeros(max(size, 1), dtype=torch.uint8, device=qbytes.device)
+        slots = W * cap if cap else nq
+        size = slots if packed else slots * m
+        dt = torch.int64 if packed else torch.uint8
+        if send is None or send.numel() < max(size, 1) or send.dtype != dt:
+            send = torch.zeros(max(size, 1), dtype=dt, device=qbytes.device)
         slot = torch.empty(max(nq, 1), dtype=torch.int64, device=qbytes.device)
         st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
         sp = splitter_pos.data_ptr() if W > 1 else None
+        fl = _lib.SAS_DEVICE_PTRS | (_lib.SAS_ROUTE_PACKED if packed else 0)
         if cap:
             check(lib().sas_route_pack_cap(self._h, sp, W - 1, qbytes.data_ptr(), m, nq, int(cap), counts.data_ptr(),
-                                           send.data_ptr(), slot.data_ptr(), st, _lib.SAS_DEVICE_PTRS))
+                                           send.data_ptr(), slot.data_ptr(), st, fl))
         else:
             check(lib().sas_route_pack(self._h, sp, W - 1, qbytes.data_ptr(), m, nq, counts.data_ptr(),
-                                       send.data_ptr(), slot.data_ptr(), st, _lib.SAS_DEVICE_PTRS))
+                                       send.data_ptr(), slot.data_ptr(), st, fl))
         return counts, send[:size], slot[:nq]
 
     def verify(self):

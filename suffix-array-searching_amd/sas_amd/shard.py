@@ -6,8 +6,9 @@ positions come back -- the only place this engine uses a collective.
     SaNaive.build_part), splitters = text positions of the first suffix of shards 1..W-1
     (all-gathered once),
     step: route + group by destination into fixed-capacity buckets (sas_route_pack_cap)
-          -> all_to_all query bytes (equal splits) -> local lookup of every received slot
-          -> all_to_all positions back (equal splits) -> gather by send slot.
+          -> all_to_all query bytes (equal splits; PREFIX with m <= 32: 8-B packed words)
+          -> local lookup of every received slot -> all_to_all positions back (equal splits)
+          -> gather by send slot.
 
 Hash-partitioning the SA would break its order (a lower bound would need every
 shard); rank ranges keep each answer on exactly one shard.  The collective is
@@ -70,17 +71,24 @@ class ShardedSearch:
             self._caps[nq] = int(t.item())
         return self._caps[nq]
 
+    def packed(self, m: int) -> bool:
+        """Queries cross the exchange as 8-B 2-bit words (SAS_ROUTE_PACKED) when the local
+        lookup takes them: PREFIX, m <= 32 (4x less all-to-all traffic at m = 32)."""
+        return self.algo == "prefix" and m <= 32 and hasattr(self.index, "search_packed")
+
     def _buffers(self, nq: int, m: int, cap: int):
         import torch
         key = (nq, m)
         if key not in self._bufs:
             W = self.world
-            self._bufs[key] = {
-                "send": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device),
-                "recv": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device),
-                "back": torch.empty(W * cap, dtype=torch.int64, device=self.device),
-                "local": torch.empty(W * cap, dtype=torch.int64, device=self.device),
-            }
+            if self.packed(m):
+                q = {"send": torch.zeros(W * cap, dtype=torch.int64, device=self.device),
+                     "recv": torch.zeros(W * cap, dtype=torch.int64, device=self.device)}
+            else:
+                q = {"send": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device),
+                     "recv": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device)}
+            self._bufs[key] = dict(q, back=torch.empty(W * cap, dtype=torch.int64, device=self.device),
+                                   local=torch.empty(W * cap, dtype=torch.int64, device=self.device))
         return self._bufs[key]
 
     # ---------------------------------------------------------------- steps
@@ -92,9 +100,14 @@ class ShardedSearch:
         nq = qbytes.numel() // m
         cap = self.capacity(nq)
         buf = self._buffers(nq, m, cap)
-        counts, send, slot = self.index.route_pack(self.splitters, qbytes, m, cap=cap, send=buf["send"])
+        pk = self.packed(m)
+        counts, send, slot = self.index.route_pack(self.splitters, qbytes, m, cap=cap, send=buf["send"],
+                                                   **({"packed": True} if pk else {}))
         self.dist.all_to_all_single(buf["recv"], send, group=self.group)
-        self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
+        if pk:
+            self.index.search_packed(buf["recv"], m, algo="prefix", out=buf["local"])
+        else:
+            self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
         self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group)
         over = (counts > cap).any().reshape(1)
         out = buf["back"].index_select(0, slot)

@@ -50,12 +50,14 @@ def test_sharded_nccl_world1(sas):
         n, nq, m = 1_000_003, 50_000, 32
         t = sas.random_string(n, seed=21)
         full = sas.SaNaive.build(t)
-        part = sas.SaNaive.build_part(torch.from_numpy(t).cuda(), 0, 1)
+        # the part index holds a 40-bit SA; n < 2^32 lets it carry the two-suffix inline table
+        part = sas.SaNaive.build_part(torch.from_numpy(t).cuda(), 0, 1, prefix=12, prefix_inline=2)
         qb = queries(t, nq, m, 1)
         expect = full.search_fixed(qb, m, algo="plain")
         dq = torch.from_numpy(qb).cuda()
-        for algo in ("plain", "quad", "prefix"):
+        for algo in ("plain", "quad", "prefix"):  # prefix: 8-B packed words cross the exchange
             eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo)
+            assert eng.packed(m) == (algo == "prefix")
             got = eng.search_fixed(dq, m)
             got2 = eng.search_fixed(dq, m, check=False)
             eng.assert_no_overflow()
@@ -135,7 +137,7 @@ def test_sharded_parts_loopback(sas, W):
     t = sas.random_string(n, seed=23)
     full = sas.SaNaive.build(t)
     dt = torch.from_numpy(t).cuda()
-    parts = [sas.SaNaive.build_part(dt, g, W) for g in range(W)]
+    parts = [sas.SaNaive.build_part(dt, g, W, prefix=12, prefix_inline=2) for g in range(W)]
     lb = Loopback(W)
     qbs = [queries(t, nq, m, 10 + r) for r in range(W)]
     expect = [full.search_fixed(q, m, algo="plain") for q in qbs]
@@ -150,6 +152,8 @@ def test_sharded_parts_loopback(sas, W):
             b = eng.search_fixed(dq, m, check=False)
             eng.assert_no_overflow()
             c = eng.search_fixed_exact(dq, m)
+            pre = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="prefix")  # packed exchange
+            e = pre.search_fixed(dq, m)
             tight = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="quad", slack=0.5, min_cap=0)
             skew = torch.from_numpy(np.tile(qbs[r][:m], nq // 10).copy()).cuda()
             sk = tight.search_fixed(skew, m)
@@ -160,7 +164,7 @@ def test_sharded_parts_loopback(sas, W):
             except RuntimeError:
                 raised = True
             torch.cuda.synchronize()
-            res[r] = (a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), sk.cpu().numpy(), raised)
+            res[r] = (a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), sk.cpu().numpy(), raised, e.cpu().numpy())
         except Exception as e:  # surfaced below
             errs.append((r, repr(e)))
             lb.bar.abort()
@@ -172,9 +176,37 @@ def test_sharded_parts_loopback(sas, W):
         x.join(timeout=120)
     assert not errs, errs
     for r in range(W):
-        a, b, c, sk, raised = res[r]
-        for g in (a, b, c):
+        a, b, c, sk, raised, e = res[r]
+        for g in (a, b, c, e):
             assert np.array_equal(g.astype(np.uint64), expect[r]), r
         skew_expect = full.search_fixed(np.tile(qbs[r][:m], nq // 10), m, algo="plain")
         assert np.array_equal(sk.astype(np.uint64), skew_expect), r
         assert raised, r
+
+
+def test_inline_tables_on_40bit_sa(sas):
+    """The one/two/four-suffix inline prefix tables beside a packed 40-bit SA (allowed while
+    n < 2^32: ranks and positions fit the entries' 32-bit fields) give the u32 index's
+    PREFIX positions, probes and ranges; routing words packed by sas_route_pack equal
+    sas_pack_queries'."""
+    import torch
+    from oracle import pyoracle as O
+    n, m = 500_009, 32
+    t = sas.random_string(n, seed=31)
+    qb = queries(t, 20_000, m, 4)
+    ref = sas.SaNaive.build(t, prefix=10, prefix_inline=2)
+    exp, epr = ref.search_fixed(qb, m, algo="prefix", probes=True)
+    assert np.array_equal(exp, ref.search_fixed(qb, m, algo="plain"))
+    for inl in (1, 2, 4):
+        idx = sas.SaNaive.build(t, sa40=True, prefix=10, prefix_inline=inl)
+        assert idx.stats()["sa_width"] == 5
+        got, pr = idx.search_fixed(qb, m, algo="prefix", probes=True)
+        assert np.array_equal(got, exp), inl
+        if inl == 2:
+            assert np.array_equal(pr, epr)
+    dq = torch.from_numpy(qb).cuda()
+    _, words, slot = ref.route_pack(torch.empty(0, dtype=torch.int64, device="cuda"), dq, m, cap=len(qb) // m,
+                                    packed=True)
+    w2 = sas.SaNaive.pack_queries(dq, m)
+    torch.cuda.synchronize()
+    assert np.array_equal(words.cpu().numpy()[slot.cpu().numpy()], w2.cpu().numpy())
