@@ -308,10 +308,17 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
             if dt * 2 > seconds / 2 or sample >= nq:
                 break
             sample = min(nq, int(sample * max(2.0, (seconds / 2) / max(dt, 1e-3))))
-        rate = sample / dt
+        # the whole query set takes less than seconds/2: repeat it (still the same queries)
+        reps = 1
+        while dt < seconds / 2:
+            t0 = time.perf_counter()
+            O.search_many(t, n, sa, qb, off, ln, algo, threads)
+            dt += time.perf_counter() - t0
+            reps += 1
+        rate = sample * reps / dt
         if best is None or rate > best[0]:
-            best = (rate, algo, sample, dt, pos)
-    rate, algo, sample, dt, pos = best
+            best = (rate, algo, sample, dt, pos, reps)
+    rate, algo, sample, dt, pos, reps = best
     # one thread on a smaller sample of the same queries (1 thread and all cores)
     s1 = min(nq, max(1000, int(rate / threads * seconds / 8)))
     qb = np.concatenate([qbytes_dev[: s1 * m].cpu().numpy(), np.zeros(64, np.uint8)])
@@ -322,7 +329,7 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
             "single_thread_value": one, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
             "sample": f"oracle/{algo} (restates sas/sa_search.rs "
                       f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
-                      f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA, {dt:.1f} s, "
+                      f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA ({reps} passes), {dt:.1f} s, "
                       f"{threads} threads (this process's allotted cores), contiguous chunks "
                       f"(sst/bin/bench.rs:558-573)", "_pos": pos}
 
@@ -735,7 +742,7 @@ def main():
             if args.mode == "shard":
                 # fixed-capacity buckets, no host sync inside the step; the overflow flag is
                 # checked once after the timed loop (engine.assert_no_overflow)
-                dst.copy_(engine.search_fixed(qbytes, m, check=False))
+                engine.search_fixed(qbytes, m, check=False, out=dst)
             elif algo == "prefix_packed":
                 idx.search_packed(packed["w"], m, out=dst)
             else:

@@ -2048,54 +2048,68 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
     uint32_t dev_bad = 0;
     HostPool& pool = HostPool::get();
     int err = 0;
-    auto finish = [&](StageSlot& sl) -> int {
-        HIP_TRY(hipStreamSynchronize(sl.st));
-        const uint64_t k = sl.e - sl.s;
-        par_memcpy(out_pos + sl.s, sl.h_out, k * 8);
-        if (out_probes) memcpy(out_probes + sl.s, sl.h_pr, k * 4);
-        if (validate) dev_bad |= *sl.h_bad;
-        sl.busy = false;
-        return 0;
+    // pieces of one pool job: the copy-out of the slot's previous chunk (positions, probes;
+    // the caller's pages are often touched here for the first time, so page faults spread
+    // over the pool too) and the fill of the new chunk run together
+    constexpr uint64_t OUT_PIECE = 1u << 17;  // positions per copy-out piece (1 MiB)
+    auto copy_out = [&](const StageSlot& sl, uint64_t piece) {
+        const uint64_t b = piece * OUT_PIECE, e = std::min(sl.e - sl.s, b + OUT_PIECE);
+        memcpy(out_pos + sl.s + b, sl.h_out + b, (e - b) * 8);
+        if (out_probes) memcpy(out_probes + sl.s + b, sl.h_pr + b, (e - b) * 4);
     };
-    auto drain = [&]() {
-        for (auto& sl : S.slot)
-            if (sl.busy) {
-                (void)hipStreamSynchronize(sl.st);
-                sl.busy = false;
-            }
+    auto out_pieces = [&](const StageSlot& sl) -> int {
+        return sl.busy ? (int)((sl.e - sl.s + OUT_PIECE - 1) / OUT_PIECE) : 0;
     };
+    // SAS_STAGE_TRACE=1: per-phase host time of the call on stderr (tuning aid)
+    static const bool trace = getenv("SAS_STAGE_TRACE") != nullptr;
+    using clk = std::chrono::steady_clock;
+    double t_wait = 0, t_job = 0, t_enq = 0;
+    auto t_all = clk::now();
     uint64_t s = 0;
-    for (int c = 0; s < nq && !err; c++) {
+    int chunks = 0;
+    for (int c = 0; s < nq && !err; c++, chunks++) {
         StageSlot& sl = S.slot[c % SAS_STAGE_SLOTS];
-        if (sl.busy && (err = finish(sl))) break;
+        auto t0 = clk::now();
+        if (sl.busy) {
+            HIP_TRY(hipStreamSynchronize(sl.st));
+            if (validate) dev_bad |= *sl.h_bad;
+        }
+        auto t1 = clk::now();
+        t_wait += std::chrono::duration<double, std::milli>(t1 - t0).count();
+        const int po = out_pieces(sl);
         SearchArgs a{};
         fill_args(x, a);
         a.m_fixed = m;
         uint64_t k = 0, in_bytes = 0;
         int qw = 1;
-        if (mode == HM_FIXED) {
-            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_bytes / std::max(m, 1u), S.cap_q));
-            in_bytes = k * m;
-            par_memcpy(sl.h_in, qbytes + s * m, in_bytes);
-            qw = qw_for(m);
-        } else if (mode == HM_WORDS) {
-            k = std::min<uint64_t>(nq - s, S.cap_q);
-            in_bytes = k * 8;
-            par_memcpy(sl.h_in, qwords + s, in_bytes);
+        // the new chunk: its extent, and a fill function over `pi` pieces
+        int pi_n = 0;
+        std::function<void(int)> fill;
+        if (mode == HM_FIXED || mode == HM_WORDS) {
+            const uint64_t unit = mode == HM_FIXED ? std::max(m, 1u) : 8;
+            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_bytes / unit, S.cap_q));
+            in_bytes = k * unit;
+            const uint8_t* src = mode == HM_FIXED ? qbytes + s * m : reinterpret_cast<const uint8_t*>(qwords + s);
+            const uint64_t piece = 1u << 20;
+            pi_n = (int)((in_bytes + piece - 1) / piece);
+            fill = [&sl, src, in_bytes, piece](int i) {
+                const uint64_t b = (uint64_t)i * piece;
+                memcpy(sl.h_in + b, src + b, std::min(piece, in_bytes - b));
+            };
+            if (mode == HM_FIXED) qw = qw_for(m);
         } else if (mode == HM_PACK) {
             // smaller chunks than the byte modes: the host packing is the longest stage, and
             // the pipeline fills and drains faster
             k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_q, SAS_STAGE_PACK_Q));
             in_bytes = k * 8;
-            const uint64_t per = 16384;
-            const int parts = (int)((k + per - 1) / per);
+            constexpr uint64_t per = 16384;
+            pi_n = (int)((k + per - 1) / per);
             uint64_t* w = reinterpret_cast<uint64_t*>(sl.h_in);
             const uint8_t* src = qbytes + s * m;
-            pool.run(parts, [&](int pi) {
-                const uint64_t b = pi * per, e = std::min(k, b + per);
-                const uint8_t r = host_pack_words(src + b * m, m, e - b, w + b);
-                if (r & 0xFC) host_bad.fetch_or(1);
-            });
+            fill = [&host_bad, w, src, k, m](int i) {
+                const uint64_t b = (uint64_t)i * per, e = std::min(k, b + per);
+                if (host_pack_words(src + b * m, m, e - b, w + b) & 0xFC) host_bad.fetch_or(1);
+            };
         } else {  // ragged: consecutive queries up to the byte and count caps (at least one)
             uint64_t bytes = 0, e = s;
             uint32_t maxlen = 0;
@@ -2108,14 +2122,24 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
             }
             k = e - s;
             in_bytes = bytes;
-            const uint64_t per = 4096;
-            const int parts = (int)((k + per - 1) / per);
-            pool.run(parts, [&](int pi) {
-                const uint64_t b = pi * per, ee = std::min(k, b + per);
-                for (uint64_t j = b; j < ee; j++) memcpy(sl.h_in + sl.h_off[j], qbytes + qoff[s + j], sl.h_len[j]);
-            });
+            constexpr uint64_t per = 4096;
+            const uint64_t s0 = s;
+            pi_n = (int)((k + per - 1) / per);
+            fill = [&sl, qbytes, qoff, k, s0](int i) {
+                const uint64_t b = (uint64_t)i * per, ee = std::min(k, b + per);
+                for (uint64_t j = b; j < ee; j++) memcpy(sl.h_in + sl.h_off[j], qbytes + qoff[s0 + j], sl.h_len[j]);
+            };
             qw = qw_for(maxlen);
         }
+        // h_out of this slot is read by the copy-out pieces before the new chunk's D2H is
+        // queued below, so both can run in one job
+        pool.run(po + pi_n, [&](int i) {
+            if (i < po) copy_out(sl, (uint64_t)i);
+            else fill(i - po);
+        });
+        auto t2 = clk::now();
+        t_job += std::chrono::duration<double, std::milli>(t2 - t1).count();
+        sl.busy = false;
         HIP_TRY(hipMemcpyAsync(sl.d_in, sl.h_in, in_bytes, hipMemcpyHostToDevice, sl.st));
         if (mode == HM_RAGGED) {
             HIP_TRY(hipMemcpyAsync(sl.d_off, sl.h_off, k * 8, hipMemcpyHostToDevice, sl.st));
@@ -2145,10 +2169,32 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
         sl.s = s;
         sl.e = s + k;
         s += k;
+        t_enq += std::chrono::duration<double, std::milli>(clk::now() - t2).count();
     }
-    for (int c = 0; c < SAS_STAGE_SLOTS && !err; c++)
-        if (S.slot[c].busy) err = finish(S.slot[c]);
-    drain();
+    // drain: the last chunks' copy-outs, all slots in one job
+    if (!err) {
+        int tot = 0, base[SAS_STAGE_SLOTS];
+        for (int c = 0; c < SAS_STAGE_SLOTS; c++) {
+            StageSlot& sl = S.slot[c];
+            if (sl.busy) {
+                HIP_TRY(hipStreamSynchronize(sl.st));
+                if (validate) dev_bad |= *sl.h_bad;
+            }
+            base[c] = tot;
+            tot += out_pieces(sl);
+        }
+        pool.run(tot, [&](int i) {
+            int c = SAS_STAGE_SLOTS - 1;
+            while (c > 0 && i < base[c]) c--;
+            copy_out(S.slot[c], (uint64_t)(i - base[c]));
+        });
+        for (auto& sl : S.slot) sl.busy = false;
+    }
+    if (trace)
+        fprintf(stderr, "[sas stage] mode %d nq %llu chunks %d threads %d: wait %.2f ms, fill+copy-out %.2f ms, "
+                        "enqueue %.2f ms, total %.2f ms\n",
+                mode, (unsigned long long)nq, chunks, pool.size(), t_wait, t_job, t_enq,
+                std::chrono::duration<double, std::milli>(clk::now() - t_all).count());
     if (err) return err;
     if (dev_bad || host_bad.load()) SAS_FAIL(EINVAL, "search: query bytes must be DNA codes 0..3");
     return 0;
@@ -2477,8 +2523,8 @@ extern "C" int sas_route_batch(const sas_index* x, const uint64_t* splitter_pos,
 // ------------------------------------------------------------------ route + pack (sharded step)
 // One sharded-mode step needs the queries grouped by destination shard.  This is
 // a counting sort by destination, fused with the routing and the byte copy:
-//   k_route          dest[i] (as in sas_route)
-//   k_pack_count     per-block histogram of dest (LDS atomics) -> cnt[w * nblk + b]
+//   k_route_count    dest[i] (as in sas_route) + per-block histogram of dest (LDS
+//                    atomics) -> cnt[w * nblk + b] (+ the packed word, SAS_ROUTE_PACKED)
 //   exclusive scan   -> base[w * nblk + b] = first send slot of (bucket w, block b)
 //   k_pack_scatter   slot = base + LDS-atomic rank; copy the query's m bytes to
 //                    send[slot * m]; slot_of[i] = slot (positions come back in
@@ -2488,15 +2534,38 @@ extern "C" int sas_route_batch(const sas_index* x, const uint64_t* splitter_pos,
 #define PACK_ITEMS 8
 #define PACK_CHUNK (PACK_BLOCK * PACK_ITEMS)
 
-__global__ __launch_bounds__(PACK_BLOCK) void k_pack_count(const uint32_t* __restrict__ dest, uint64_t nq, uint32_t W,
-                                                           uint64_t nblk, uint64_t* __restrict__ cnt) {
+// route + per-block histogram in one pass over the queries: dest[i] = the shard of query i
+// (as k_route; no splitters: shard 0 without reading the query), and with PACKED its 2-bit
+// word for the scatter (SAS_ROUTE_PACKED), so the query bytes are read once
+template <bool PACKED>
+__global__ __launch_bounds__(PACK_BLOCK) void k_route_count(const uint64_t* __restrict__ tw, uint64_t n,
+                                                            const uint64_t* __restrict__ sp, uint32_t nsplit,
+                                                            const uint8_t* __restrict__ qbytes, uint32_t m, uint64_t nq,
+                                                            uint64_t nblk, uint64_t* __restrict__ cnt,
+                                                            uint32_t* __restrict__ dest, uint64_t* __restrict__ words) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
+    const uint32_t W = nsplit + 1;
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * PACK_CHUNK;
     for (int it = 0; it < PACK_ITEMS; it++) {
         const uint64_t i = base + (uint64_t)it * PACK_BLOCK + threadIdx.x;
-        if (i < nq) atomicAdd(&h[dest[i]], 1u);
+        if (i >= nq) continue;
+        uint32_t lo = 0;
+        if (PACKED || nsplit) {
+            uint32_t b = 0;
+            QueryRegs<PACKED ? 1 : 4> q;
+            q.load(qbytes + i * (uint64_t)m, m, &b);
+            if (PACKED) words[i] = q.w[0];
+            uint32_t hi = nsplit, lcp;
+            while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
+                const uint32_t mid = (lo + hi) >> 1;
+                if (suffix_less_from<PACKED ? 1 : 4>(tw, n, sp[mid], q, 0, &lcp)) lo = mid + 1;
+                else hi = mid;
+            }
+        }
+        dest[i] = lo;
+        atomicAdd(&h[lo], 1u);
     }
     __syncthreads();
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) cnt[(uint64_t)w * nblk + blockIdx.x] = h[w];
@@ -2511,7 +2580,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
                                                              const uint8_t* __restrict__ qbytes, uint32_t m,
                                                              uint8_t* __restrict__ send,
                                                              uint64_t* __restrict__ slot_of, uint64_t cap,
-                                                             bool packed) {
+                                                             const uint64_t* __restrict__ words) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
@@ -2532,9 +2601,8 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
         }
         slot_of[i] = slot;
         const uint8_t* src = qbytes + i * (uint64_t)m;
-        if (packed) {  // SAS_ROUTE_PACKED: the query as one 2-bit word (m <= 32), 8 B per slot
-            uint32_t bad = 0;
-            reinterpret_cast<uint64_t*>(send)[slot] = pack_query_word(src, m, 0, &bad);
+        if (words) {  // SAS_ROUTE_PACKED: the query's 2-bit word (m <= 32), 8 B per slot
+            reinterpret_cast<uint64_t*>(send)[slot] = words[i];
             continue;
         }
         uint8_t* dst = send + slot * (uint64_t)m;
@@ -2572,32 +2640,37 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
         return 0;
     }
     const uint64_t nblk = (nq + PACK_CHUNK - 1) / PACK_CHUNK;
+    const bool packed = (flags & SAS_ROUTE_PACKED) != 0;
     void* dest = nullptr;
     void* cnt = nullptr;
     void* tmp = nullptr;
+    void* words = nullptr;
     size_t tbytes = 0;
     HIP_TRY(rocprim::exclusive_scan(nullptr, tbytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0,
                                     (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
     HIP_TRY(hipMallocAsync(&dest, nq * 4, st));
     HIP_TRY(hipMallocAsync(&cnt, nblk * W * 8, st));
     HIP_TRY(hipMallocAsync(&tmp, tbytes ? tbytes : 8, st));
-    uint64_t rb = (nq + 255) / 256;
-    if (rb > 65536) rb = 65536;
-    hipLaunchKernelGGL(k_route, dim3((unsigned)rb), dim3(256), 0, st, x->text_w, x->n, splitter_pos, nsplit, qbytes,
-                       m, (const uint64_t*)nullptr, (const uint32_t*)nullptr, nq, static_cast<uint32_t*>(dest),
-                       x->scratch);
-    hipLaunchKernelGGL(k_pack_count, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest), nq,
-                       W, nblk, static_cast<uint64_t*>(cnt));
+    if (packed) HIP_TRY(hipMallocAsync(&words, nq * 8, st));
+    if (packed)
+        hipLaunchKernelGGL(k_route_count<true>, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, x->text_w, x->n,
+                           splitter_pos, nsplit, qbytes, m, nq, nblk, static_cast<uint64_t*>(cnt),
+                           static_cast<uint32_t*>(dest), static_cast<uint64_t*>(words));
+    else
+        hipLaunchKernelGGL(k_route_count<false>, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, x->text_w, x->n,
+                           splitter_pos, nsplit, qbytes, m, nq, nblk, static_cast<uint64_t*>(cnt),
+                           static_cast<uint32_t*>(dest), (uint64_t*)nullptr);
     HIP_TRY(rocprim::exclusive_scan(tmp, tbytes, static_cast<uint64_t*>(cnt), static_cast<uint64_t*>(cnt),
                                     (uint64_t)0, (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
     hipLaunchKernelGGL(k_pack_scatter, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest),
                        nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot, cap,
-                       (flags & SAS_ROUTE_PACKED) != 0);
+                       static_cast<const uint64_t*>(words));
     hipLaunchKernelGGL(k_pack_totals, dim3(1), dim3(256), 0, st, static_cast<uint64_t*>(cnt), W, nblk, nq, out_counts);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipFreeAsync(dest, st));
     HIP_TRY(hipFreeAsync(cnt, st));
     HIP_TRY(hipFreeAsync(tmp, st));
+    if (words) HIP_TRY(hipFreeAsync(words, st));
     return 0;
 }
 

@@ -92,8 +92,9 @@ class ShardedSearch:
         return self._bufs[key]
 
     # ---------------------------------------------------------------- steps
-    def search_fixed(self, qbytes, m: int, check: bool = True):
-        """qbytes: uint8 tensor [nq*m] of this rank's queries -> int64 positions."""
+    def search_fixed(self, qbytes, m: int, check: bool = True, out=None):
+        """qbytes: uint8 tensor [nq*m] of this rank's queries -> int64 positions (written
+        into `out` when given)."""
         if not hasattr(self.index, "route_pack"):
             return self.search_fixed_exact(qbytes, m)
         import torch
@@ -110,14 +111,16 @@ class ShardedSearch:
             self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
         self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group)
         over = (counts > cap).any().reshape(1)
-        out = buf["back"].index_select(0, slot)
+        out = torch.index_select(buf["back"], 0, slot, out=out) if out is not None else \
+            buf["back"].index_select(0, slot)
         if check:
             # one flag per rank, agreed by all (an overflow anywhere changes every rank's
             # exchange): redo the step with exact splits
             flag = over.to(torch.int32)
             self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
             if int(flag.item()):
-                return self.search_fixed_exact(qbytes, m)
+                exact = self.search_fixed_exact(qbytes, m)
+                return out.copy_(exact) if out is not None else exact
         else:
             self.overflow |= over
         return out
