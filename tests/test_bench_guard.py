@@ -1,0 +1,72 @@
+"""bench.py's correctness guard and byte model on the CPU (no GPU): lower_bound_proof accepts
+exact lower bounds and rejects any other occurrence of a repeated query, on an
+oracle-backed stand-in index; bytes_per_lookup never charges LDS- or cache-served tree
+levels to HBM."""
+import numpy as np
+
+import bench
+from oracle import pyoracle as O
+
+
+class OracleIndex:
+    """The three calls lower_bound_proof makes, on the oracle's SA."""
+
+    def __init__(self, t):
+        self.t = t
+        self.n = len(t)
+        self.sa = O.build_sa(t)
+        self.sa_n = self.n
+        self.rank_lo = 0
+        self.tp = O.padded(t)
+
+    def search_range(self, buf, off, lens):
+        lo = np.array([O.prefix_range(self.tp, self.n, self.sa, buf[int(o):int(o) + int(L)])[0]
+                       for o, L in zip(off, lens)], np.uint64)
+        hi = np.array([O.prefix_range(self.tp, self.n, self.sa, buf[int(o):int(o) + int(L)])[1]
+                       for o, L in zip(off, lens)], np.uint64)
+        return lo, hi
+
+    def suffix_array(self, count=None, start=0):
+        return self.sa[start:start + count].astype(np.uint64)
+
+
+def test_lower_bound_proof_accepts_and_rejects():
+    rng = np.random.default_rng(3)
+    blk = rng.integers(0, 4, 50, dtype=np.uint8)
+    t = np.concatenate([rng.integers(0, 4, 3000, dtype=np.uint8), blk, rng.integers(0, 4, 500, dtype=np.uint8), blk,
+                        rng.integers(0, 4, 700, dtype=np.uint8), blk])
+    idx = OracleIndex(t)
+    n, m = len(t), 40
+    offs = list(rng.integers(0, n - m, 200)) + [3000, 3550, 4300]  # the last three: the repeated block
+    qs = [t[o:o + m] for o in offs]
+    right = np.array([O.search_one(idx.tp, n, idx.sa, q)[0] for q in qs], np.uint64)
+    window = lambda p, L: t[p:p + L]  # noqa: E731
+    ids = np.arange(len(qs))
+    assert bench.lower_bound_proof(idx, window, lambda i: qs[i], right, ids) == 0
+    # another occurrence of a repeated query is an occurrence but not the lower bound
+    wrong = right.copy()
+    occ = [o for o in (3000, 3550, 4300) if o != int(right[-1])]
+    wrong[-1] = occ[0]
+    assert np.array_equal(t[int(wrong[-1]):int(wrong[-1]) + m], qs[-1])
+    assert bench.lower_bound_proof(idx, window, lambda i: qs[i], wrong, ids) == 1
+    # a negative query's lower bound (no occurrence) is proven too; n for a query above all
+    neg = [np.full(m, 3, np.uint8), rng.integers(0, 4, m, dtype=np.uint8)]
+    ans = np.array([O.search_one(idx.tp, n, idx.sa, q)[0] for q in neg], np.uint64)
+    assert int(ans[0]) == n
+    assert bench.lower_bound_proof(idx, window, lambda i: neg[i], ans, np.arange(2)) == 0
+    assert bench.lower_bound_proof(idx, window, lambda i: neg[i], ans[::-1].copy(), np.arange(2)) >= 1
+
+
+def test_byte_model_splits_served_levels():
+    st = {"sa_width": 4, "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "quad_entry_bytes": 16,
+          "stree_layers": 8, "stree_lds_layers": 2, "sector_layers": 12, "sector_lds_layers": 3, "quad_layers": 8,
+          "quad_lds_layers": 3, "quad_fan": 17, "tag_chars": 16}
+    n, m = 1 << 30, 32
+    q = bench.bytes_per_lookup("quad", st, n, m, 8.0)
+    # quad at 2^30: 3 LDS layers, the 206 KB / 3.5 MB / 59 MB layers in cache, 1 GB + leaves in HBM
+    assert q["lds"] == 3 * 64 and q["cache"] == 3 * 64 and q["hbm"] == 2 * 64 + m + 8
+    p = bench.bytes_per_lookup("plain", st, n, m, 31.0)
+    assert p["lds"] == 12 * 12 and p["cache"] == 9 * 16 and p["hbm"] == 10 * (4 + m / 4) + m + 8
+    h = bench.bytes_per_lookup("prefix", st, n, m, 1.0)
+    assert h["hbm"] == 32 + m + 8 and h["cache"] == 0 and h["lds"] == 0
+    assert bench._tree_layers(n, 4, 64, 17, 64, 8)[-1] == n // 4 * 64
