@@ -1540,10 +1540,10 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 // suffix < q, "tag > q's tag" proves suffix > q, and only a tie needs the length (m <= p+12)
 // or an exact compare from char p+12 (the sector predicate with L = p + 12).  A lookup is:
 // the bucket word (one aligned 8-B read), the first SAS_TAG_WIN entries of the bucket as
-// independent loads (one or two 128-B lines: a bucket holds ~4 suffixes at n = 4^p), the
-// text past char p+12 of the single candidate whose tag ties q's (a positive query's own
-// suffix), and its position straight from the entry.  Larger buckets continue with a binary
-// search over the rest.
+// 16-B entry pairs (a bucket holds ~4 suffixes at n = 4^p), the text past char p+12 of the
+// single candidate whose tag ties q's (a positive query's own suffix; read as 16-B word
+// pairs, suffix_less_from_x2), and its position straight from the entry.  Larger buckets
+// continue with a binary search over the rest.
 #ifndef SAS_TAG_WIN
 #define SAS_TAG_WIN 8
 #endif
@@ -1573,7 +1573,7 @@ __device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArg
     const uint32_t L = a.tag_p + SAS_TAG_CHARS;
     if (q.m <= L) return (a.n - p) >= (uint64_t)q.m;  // equal padded keys: a shorter suffix is a prefix of q
     uint32_t lcp;
-    return !suffix_less_from<QW>(a.tw, a.n, p, q, L, &lcp);
+    return !suffix_less_from_x2<QW>(a.tw, a.n, p, q, L, &lcp);
 }
 
 // the first min(m, len) chars of suffix(e) are > q, for an entry of the bucket of q's routing
@@ -1586,7 +1586,7 @@ __device__ __forceinline__ bool tag_gt_prefix(uint64_t e, uint32_t Q12, uint32_t
     if (q.m <= L) return T > Q3t;
     if (T != Q12) return T > Q12;
     uint32_t lcp;
-    const bool lt = suffix_less_from<QW>(a.tw, a.n, e & TAG_M40, q, L, &lcp);
+    const bool lt = suffix_less_from_x2<QW>(a.tw, a.n, e & TAG_M40, q, L, &lcp);
     return !lt && lcp < q.m;
 }
 
@@ -1608,20 +1608,35 @@ __device__ __forceinline__ void tagged_lookup(const SearchArgs& a, const Q& q, u
     const uint32_t Q12 = tag_of_key(K64, a.tag_p);
     uint64_t lo, hi;
     tag_bucket(a, K64 >> sh, &lo, &hi);
-    // candidates are ranks lo .. hi (rank hi = the next bucket's first suffix, > q: the
-    // answer when every suffix of the bucket is < q); the window holds the first nw
-    const uint64_t span = hi - lo + 1;
-    const uint32_t nw = span < SAS_TAG_WIN ? (uint32_t)span : (uint32_t)SAS_TAG_WIN;
+    // the bucket's suffixes are ranks [lo, hi); rank hi (the next bucket's first suffix, > q)
+    // is the answer when all of them are < q, and is read only then (by the bisection
+    // below, which ends at hi).  The window holds the first nw entries, loaded as 16-B
+    // aligned entry pairs: half the load instructions of 8-B loads, and fewer L1->L2
+    // requests and TLB lookups, which bound this kernel (the entries carry 16 bytes of
+    // padding, so the pair holding rank sa_n - 1 is readable)
+    const uint64_t cnt = hi - lo;
+    const uint32_t nw = cnt < SAS_TAG_WIN ? (uint32_t)cnt : (uint32_t)SAS_TAG_WIN;
     uint64_t e[SAS_TAG_WIN];
+    {
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const uint32_t o = (uint32_t)(lo & 1);
+        const u64x2* ep = reinterpret_cast<const u64x2*>(ent + (lo & ~1ull));
+        uint64_t w2[SAS_TAG_WIN + 2];
 #pragma unroll
-    for (int j = 0; j < SAS_TAG_WIN; j++)
-        e[j] = ((uint32_t)j < nw && lo + j < sa_n) ? __builtin_nontemporal_load(ent + lo + j) : 0ull;
-    // first slot whose tag is >= q's (or rank hi): every slot before it is < q (tags are
-    // sorted within a bucket)
+        for (int j = 0; j < SAS_TAG_WIN / 2 + 1; j++) {
+            const u64x2 v = (2u * j < o + nw) ? __builtin_nontemporal_load(ep + j) : u64x2{0ull, 0ull};
+            w2[2 * j] = v.x;
+            w2[2 * j + 1] = v.y;
+        }
+#pragma unroll
+        for (int j = 0; j < SAS_TAG_WIN; j++) e[j] = (uint32_t)j < nw ? (o ? w2[j + 1] : w2[j]) : 0ull;
+    }
+    // first slot whose tag is >= q's: every slot before it is < q (tags are sorted within a
+    // bucket)
     uint32_t j0 = nw;
 #pragma unroll
     for (int j = SAS_TAG_WIN - 1; j >= 0; j--)
-        if ((uint32_t)j < nw && (lo + j == hi || (uint32_t)(e[j] >> 40) >= Q12)) j0 = (uint32_t)j;
+        if ((uint32_t)j < nw && (uint32_t)(e[j] >> 40) >= Q12) j0 = (uint32_t)j;
     uint64_t ej = e[0];
 #pragma unroll
     for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
@@ -1629,11 +1644,7 @@ __device__ __forceinline__ void tagged_lookup(const SearchArgs& a, const Q& q, u
     bool done = false;
     if (j0 < nw) {
         const uint64_t r = lo + j0;
-        if (r >= sa_n) {
-            ans = r;
-            pos = a.next_pos;
-            done = true;
-        } else if (r == hi || tag_ge<QW>(ej, Q12, a, q)) {
+        if (tag_ge<QW>(ej, Q12, a, q)) {
             ans = r;
             pos = ej & TAG_M40;
             done = true;
