@@ -8,7 +8,6 @@ fixed-capacity buckets from sas_route_pack_cap, against the whole index.
 Bar: positions bit-identical to the whole index's PLAIN search; an overflowing bucket is
 redone exactly (check=True) or reported (check=False -> assert_no_overflow raises).
 """
-import os
 import socket
 import threading
 
@@ -190,7 +189,6 @@ def test_inline_tables_on_40bit_sa(sas):
     PREFIX positions, probes and ranges; routing words packed by sas_route_pack equal
     sas_pack_queries'."""
     import torch
-    from oracle import pyoracle as O
     n, m = 500_009, 32
     t = sas.random_string(n, seed=31)
     qb = queries(t, 20_000, m, 4)
@@ -210,3 +208,26 @@ def test_inline_tables_on_40bit_sa(sas):
     w2 = sas.SaNaive.pack_queries(dq, m)
     torch.cuda.synchronize()
     assert np.array_equal(words.cpu().numpy()[slot.cpu().numpy()], w2.cpu().numpy())
+
+
+def test_route_pack_argument_errors(sas):
+    """sas_route_pack_cap: cap = 0 and SAS_ROUTE_PACKED with m > 32 are EINVAL."""
+    import torch
+    from sas_amd import _lib
+    from sas_amd._lib import SasError
+    t = sas.random_string(10_007, seed=2)
+    idx = sas.SaNaive.build(t)
+    q = torch.from_numpy(np.concatenate([t[:40], t[100:140]])).cuda()
+    sp = torch.empty(0, dtype=torch.int64, device="cuda")
+    with pytest.raises(SasError):
+        idx.route_pack(sp, q, 40, cap=2, packed=True)  # m > 32
+    counts = torch.empty(1, dtype=torch.int64, device="cuda")
+    send = torch.empty(80, dtype=torch.uint8, device="cuda")
+    slot = torch.empty(2, dtype=torch.int64, device="cuda")
+    rc = _lib.lib().sas_route_pack_cap(idx._h, None, 0, q.data_ptr(), 40, 2, 0, counts.data_ptr(), send.data_ptr(),
+                                       slot.data_ptr(), None, _lib.SAS_DEVICE_PTRS)
+    assert rc != 0
+    c, s2, sl = idx.route_pack(sp, q, 40, cap=2)
+    torch.cuda.synchronize()
+    assert c.tolist() == [2] and sorted(sl.tolist()) == [0, 1]
+    assert torch.equal(s2.view(2, 40)[sl], q.view(2, 40))

@@ -19,8 +19,9 @@ with open(path) as f:
         g[(k, grid, wg)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 with open(out, "w", newline="") as f:
     w = csv.writer(f)
-    w.writerow(["Kernel_Name", "Grid", "Workgroup", "Calls", "AverageNs", "MinNs", "MaxNs", "MedianNs"])
+    w.writerow(["Kernel_Name", "Grid", "Workgroup", "Calls", "AverageNs", "MinNs", "MaxNs", "P10Ns", "MedianNs",
+                "P90Ns"])
     for (k, grid, wg), ds in sorted(g.items(), key=lambda x: -sum(x[1])):
         ds.sort()
         w.writerow([k, "x".join(x for x in grid if x), "x".join(x for x in wg if x), len(ds), sum(ds) / len(ds),
-                    ds[0], ds[-1], ds[len(ds) // 2]])
+                    ds[0], ds[-1], ds[len(ds) // 10], ds[len(ds) // 2], ds[(9 * len(ds)) // 10]])

@@ -1,5 +1,7 @@
 #!/bin/bash
-# Round-2 profiles (run on the GPU box): rocprofv3 kernel stats of the default bench, and the
+# Round-2 profiles (run on the GPU box): rocprofv3 kernel stats of the default bench (without
+# its host-buffer pass, whose 2^19-query chunks launch the headline kernel on the same grid
+# and would mix into its average), and the
 # separate --pmc passes (FETCH_SIZE, WRITE_SIZE, TCC_EA0_RDREQ) of the configs[3] TAGGED run
 # and of the configs[1] PLAIN run, summarised into profiles/pmc_*.json for bench.py.
 set -o pipefail
@@ -8,7 +10,7 @@ mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 what=${1:-all}
 if [ "$what" = all ] || [ "$what" = kt ]; then
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- python3 bench.py > "$out/kt_bench.json" 2> "$out/kt_bench.err" || exit $?
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- python3 bench.py --no-e2e > "$out/kt_bench.json" 2> "$out/kt_bench.err" || exit $?
   python3 tools/kt_by_grid.py "$out/kt/run_kernel_trace.csv" "$out/kt/kernel_stats_by_grid.csv" k_sa_ || exit $?
   find "$out/kt" -name '*kernel_trace.csv' -delete  # per-dispatch rows: too big to bring back
 fi
