@@ -2635,6 +2635,23 @@ __global__ void k_pack_totals(const uint64_t* __restrict__ base_slot, uint32_t W
     }
 }
 
+// The per-step scratch of a sharded step comes from the stream-ordered allocator; a release
+// threshold of "never" keeps the freed blocks in the device's default pool for the next
+// step instead of returning them to the driver at every synchronisation.
+static void keep_async_pool(int device) {
+    static std::mutex mu;
+    static uint64_t done = 0;  // bit per device
+    std::lock_guard<std::mutex> g(mu);
+    if (device < 64 && (done >> device) & 1) return;
+    hipMemPool_t pool;
+    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+        uint64_t thr = UINT64_MAX;
+        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+    }
+    (void)hipGetLastError();
+    if (device < 64) done |= 1ull << device;
+}
+
 static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
                            const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t cap, uint64_t* out_counts,
                            uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
@@ -2650,6 +2667,7 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
         HIP_TRY(hipMemsetAsync(out_counts, 0, W * 8, st));
         return 0;
     }
+    keep_async_pool(x->device);
     const uint64_t nblk = (nq + PACK_CHUNK - 1) / PACK_CHUNK;
     const bool packed = (flags & SAS_ROUTE_PACKED) != 0;
     void* dest = nullptr;
