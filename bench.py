@@ -514,18 +514,6 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     n = args.c4_share * ws
     nq, m = args.nq, args.m
     t0 = time.perf_counter()
-    text = sas_amd.random_string(n, seed=SEED + 1, device=dev)
-    inline = 2 if n < (1 << 32) else 0  # inline entries need ranks and positions below 2^32
-    idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=False, stree=False, sector=False, quad=True, llcp=False,
-                                     prefix=16, prefix_inline=inline)
-    st = idx.stats()
-    off = torch.from_numpy(rank_query_offsets(n, nq, m, rank).astype(np.int64)).to(dev)
-    ar = torch.arange(m, device=dev, dtype=torch.int64)
-    qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
-    for s0 in range(0, nq, 1 << 18):
-        e0 = min(nq, s0 + (1 << 18))
-        qbytes[s0 * m:e0 * m] = text[(off[s0:e0, None] + ar[None, :]).reshape(-1)]
-    del off
     own = None
     if dist is None or not dist.is_initialized():
         import socket
@@ -536,6 +524,31 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
         sk.close()
         tdist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
         dist = own = tdist
+    # the local setup may fail on one rank (e.g. HBM): every rank agrees before the first
+    # collective of the step, so a failure skips the record instead of hanging the others
+    err = None
+    try:
+        text = sas_amd.random_string(n, seed=SEED + 1, device=dev)
+        inline = 2 if n < (1 << 32) else 0  # inline entries need ranks and positions below 2^32
+        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=False, stree=False, sector=False, quad=True,
+                                         llcp=False, prefix=16, prefix_inline=inline)
+        st = idx.stats()
+        off = torch.from_numpy(rank_query_offsets(n, nq, m, rank).astype(np.int64)).to(dev)
+        ar = torch.arange(m, device=dev, dtype=torch.int64)
+        qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
+        for s0 in range(0, nq, 1 << 18):
+            e0 = min(nq, s0 + (1 << 18))
+            qbytes[s0 * m:e0 * m] = text[(off[s0:e0, None] + ar[None, :]).reshape(-1)]
+        del off
+        torch.cuda.synchronize()
+    except Exception as e:  # noqa: BLE001 -- reported in the record
+        err = repr(e)
+    okt = torch.tensor([0 if err else 1], dtype=torch.int32, device=dev)
+    dist.all_reduce(okt, op=dist.ReduceOp.MIN)
+    if not int(okt.item()):
+        if own is not None:
+            own.destroy_process_group()
+        return {"workload": "configs[4]-shaped (sharded text)", "skipped": err or "setup failed on another rank"}
     engine = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix")
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
