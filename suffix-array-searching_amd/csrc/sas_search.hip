@@ -2591,7 +2591,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
                                                              const uint8_t* __restrict__ qbytes, uint32_t m,
                                                              uint8_t* __restrict__ send,
                                                              uint64_t* __restrict__ slot_of, uint64_t cap,
-                                                             const uint64_t* __restrict__ words) {
+                                                             bool packed, const uint64_t* __restrict__ words) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
     __syncthreads();
@@ -2612,8 +2612,9 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
         }
         slot_of[i] = slot;
         const uint8_t* src = qbytes + i * (uint64_t)m;
-        if (words) {  // SAS_ROUTE_PACKED: the query's 2-bit word (m <= 32), 8 B per slot
-            reinterpret_cast<uint64_t*>(send)[slot] = words[i];
+        if (packed) {  // SAS_ROUTE_PACKED: the query's 2-bit word (m <= 32), 8 B per slot
+            uint32_t bad = 0;
+            reinterpret_cast<uint64_t*>(send)[slot] = words ? words[i] : pack_query_word(src, m, 0, &bad);
             continue;
         }
         uint8_t* dst = send + slot * (uint64_t)m;
@@ -2670,6 +2671,9 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
     keep_async_pool(x->device);
     const uint64_t nblk = (nq + PACK_CHUNK - 1) / PACK_CHUNK;
     const bool packed = (flags & SAS_ROUTE_PACKED) != 0;
+    // with splitters the routing reads each query anyway and packs it on the way (words);
+    // without (one part) the routing reads nothing and the scatter packs from the bytes
+    const bool pack_in_route = packed && nsplit > 0;
     void* dest = nullptr;
     void* cnt = nullptr;
     void* tmp = nullptr;
@@ -2680,8 +2684,8 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
     HIP_TRY(hipMallocAsync(&dest, nq * 4, st));
     HIP_TRY(hipMallocAsync(&cnt, nblk * W * 8, st));
     HIP_TRY(hipMallocAsync(&tmp, tbytes ? tbytes : 8, st));
-    if (packed) HIP_TRY(hipMallocAsync(&words, nq * 8, st));
-    if (packed)
+    if (pack_in_route) HIP_TRY(hipMallocAsync(&words, nq * 8, st));
+    if (pack_in_route)
         hipLaunchKernelGGL(k_route_count<true>, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, x->text_w, x->n,
                            splitter_pos, nsplit, qbytes, m, nq, nblk, static_cast<uint64_t*>(cnt),
                            static_cast<uint32_t*>(dest), static_cast<uint64_t*>(words));
@@ -2692,7 +2696,7 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
     HIP_TRY(rocprim::exclusive_scan(tmp, tbytes, static_cast<uint64_t*>(cnt), static_cast<uint64_t*>(cnt),
                                     (uint64_t)0, (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
     hipLaunchKernelGGL(k_pack_scatter, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, static_cast<uint32_t*>(dest),
-                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot, cap,
+                       nq, W, nblk, static_cast<uint64_t*>(cnt), qbytes, m, out_send, out_slot, cap, packed,
                        static_cast<const uint64_t*>(words));
     hipLaunchKernelGGL(k_pack_totals, dim3(1), dim3(256), 0, st, static_cast<uint64_t*>(cnt), W, nblk, nq, out_counts);
     HIP_TRY(hipGetLastError());
