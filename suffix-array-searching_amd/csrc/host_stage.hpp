@@ -14,6 +14,7 @@
 #include "common.hpp"
 
 #include <sched.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -38,8 +39,13 @@
 // calling thread.  One job at a time; the workers are never joined (process lifetime).
 class HostPool {
    public:
+    // one pool per process: a child forked after the pool started has none of its worker
+    // threads, so it builds its own (the parent's stays, unused)
     static HostPool& get() {
-        static HostPool* p = new HostPool();
+        static std::mutex mu;
+        static HostPool* p = nullptr;
+        std::lock_guard<std::mutex> g(mu);
+        if (!p || p->pid_ != getpid()) p = new HostPool();
         return *p;
     }
     int size() const { return (int)workers_ + 1; }
@@ -72,6 +78,7 @@ class HostPool {
         n = std::min(n, 16);
         if (const char* e = getenv("SAS_HOST_THREADS")) n = std::max(1, atoi(e));
         workers_ = (unsigned)(n > 1 ? n - 1 : 0);
+        pid_ = getpid();
         for (unsigned i = 0; i < workers_; i++) std::thread([this] { loop(); }).detach();
     }
     void work() {
@@ -91,6 +98,7 @@ class HostPool {
         }
     }
     unsigned workers_ = 0;
+    pid_t pid_ = 0;
     std::mutex run_mu_, mu_;
     std::condition_variable cv_, done_cv_;
     const std::function<void(int)>* job_ = nullptr;
