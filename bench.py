@@ -325,8 +325,13 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
     t0 = time.perf_counter()
     O.search_many(t, n, sa, qb, np.arange(s1, dtype=np.uint64) * m, np.full(s1, m, np.uint32), algo, 1)
     one = s1 / (time.perf_counter() - t0)
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
     return {"value": rate, "unit": "lookups/s", "cores": threads, "kind": "port",
             "single_thread_value": one, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
+            "affinity_cpus": aff,
+            "cores_note": (f"{threads} = this process's CPU share (OMP_NUM_THREADS); the affinity mask shows {aff} "
+                           f"hardware threads of the whole machine, shared with the other GPUs' processes")
+            if threads < aff else "every CPU of the affinity mask",
             "sample": f"oracle/{algo} (restates sas/sa_search.rs "
                       f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
                       f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA ({reps} passes), {dt:.1f} s, "

@@ -1029,6 +1029,9 @@ __global__ void k_tt_count(uint64_t* __restrict__ table, uint64_t keys) {
     }
 }
 
+#ifndef SAS_TAG_ALLOC_FLAGS
+#define SAS_TAG_ALLOC_FLAGS 0  // hipExtMallocWithFlags flags of the entries and table (A/B)
+#endif
 static int build_tagged(sas_index* x, uint32_t p) {
     const uint64_t sa_n = x->sa_n;
     if (p == 0) {
@@ -1038,7 +1041,7 @@ static int build_tagged(sas_index* x, uint32_t p) {
     }
     if (p > 17) SAS_FAIL(EINVAL, "SAS_BUILD_TAGGED: p must be 1..17");
     DevBuf ent;
-    TRY(ent.alloc(sa_n * 8 + 16, "tagged SA entries"));
+    TRY(ent.alloc_flags(sa_n * 8 + 16, "tagged SA entries", SAS_TAG_ALLOC_FLAGS));
     HIP_TRY(hipMemset(ent.as<uint8_t>() + sa_n * 8, 0, 16));
     const dim3 g(grid_for(sa_n)), b(256);
     if (x->sa_w == 5)
@@ -1055,7 +1058,7 @@ static int build_tagged(sas_index* x, uint32_t p) {
     const uint64_t keys = 1ull << (2 * p);
     const uint64_t cap = (keys + 1) / (PT_SMALL + 1) + 2;
     DevBuf t, big, nbig;
-    TRY(t.alloc((keys + 1) * 8 + 8, "tagged bucket table"));
+    TRY(t.alloc_flags((keys + 1) * 8 + 8, "tagged bucket table", SAS_TAG_ALLOC_FLAGS));
     TRY(big.alloc(cap * 24, "bucket table gap list"));
     TRY(nbig.alloc(8, "bucket table gap count"));
     HIP_TRY(hipMemset(nbig.p, 0, 8));
