@@ -331,6 +331,9 @@ class SaNaive:
             qbytes = _as_u8(qbytes)
             if out is None:
                 out = np.zeros(max(nq, 1), np.uint64)
+            elif not (isinstance(out, np.ndarray) and out.dtype == np.uint64 and out.flags.c_contiguous
+                      and len(out) >= nq):
+                raise ValueError("out: a C-contiguous numpy uint64 array of at least nq entries")
             pr = np.zeros(max(nq, 1), np.uint32) if probes else None
             st = stream
         if qoff is None:
