@@ -1003,6 +1003,8 @@ def main():
                 "frac": achieved / HBM_PEAK_GBPS,
                 "traffic": (head.get("pmc") or {}).get("fabric_bytes_per_lookup"),
                 "traffic_unit": "bytes per lookup (PMC, L2->fabric, Infinity-Cache hits included)",
+                "traffic_bytes_per_launch": (hpmc or {}).get("hbm_bytes_per_launch"),
+                "algorithmic_hbm_bytes_per_launch": hbpl["hbm"] * nq,
                 "traffic_source": (hpmc or {}).get("source"),
                 "kernel": "k_sa_prefix2" if args.algo == "prefix" and pe >= 32 else
                           ("k_sa_prefix" if args.algo == "prefix" else KERNELS.get(args.algo)),
