@@ -238,3 +238,45 @@ def test_tagged_saturated_bucket(sas):
     for k, q in enumerate(qs):
         if not q.any():
             assert (int(lo[k]), int(hi[k])) == (len(q) - 1, n), k
+
+
+def test_tagged_wave_staging_paths(sas):
+    """k_sa_tagged's wave-staged queries: a contiguous batch (staged through LDS), the same
+    queries with shuffled offsets (spans past 16K chars fall back to per-lane loads), a wave
+    of empty queries, a tail wave of 37 queries, and queries that sit at the very end of the
+    device buffer (no slack): every form equals the oracle."""
+    import torch
+    t = O.random_string(400_009, seed=12)
+    n = len(t)
+    sa = O.build_sa(t)
+    idx = sas.SaNaive.build(torch.from_numpy(t).cuda(), tagged=True, lcp=False)
+    rng = np.random.default_rng(3)
+    nq = 64 * 40 + 37
+    lens = rng.integers(0, 260, nq).astype(np.uint32)
+    lens[64:128] = 0  # one wave of empty queries
+    starts = rng.integers(0, n - 260, nq)
+    qs = [t[s:s + l] for s, l in zip(starts, lens)]
+    expect = expected(t, sa, qs)[0]
+    buf = np.concatenate(qs).astype(np.uint8)  # no slack after the last query
+    off = np.zeros(nq, np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    dbuf = torch.from_numpy(buf).cuda()
+    for name, o in (("contiguous", off), ("shuffled", None)):
+        if o is None:  # the same bytes, queries in a different order: offsets jump around
+            perm = rng.permutation(nq)
+            o = off[perm]
+            ln, ex = lens[perm], expect[perm]
+        else:
+            ln, ex = lens, expect
+        got = idx.search_batch(dbuf, torch.from_numpy(o.view(np.int64)).cuda(),
+                               torch.from_numpy(ln.view(np.int32)).cuda(), algo="tagged")
+        torch.cuda.synchronize()
+        bad = np.nonzero(got.cpu().numpy().astype(np.uint64) != ex)[0]
+        assert len(bad) == 0, (name, bad[:5])
+    # fixed-length batch whose count is not a multiple of 64 (a tail wave)
+    m = 40
+    qb = np.concatenate([t[s:s + m] for s in starts[:101]])
+    got = idx.search_fixed(torch.from_numpy(qb).cuda(), m, algo="tagged")
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy().astype(np.uint64),
+                          expected(t, sa, [t[s:s + m] for s in starts[:101]])[0])
