@@ -931,6 +931,41 @@ def main():
                              {"identical_to_headline": same, "lookups_per_s": ws * nq * vsteps / vel})
         log(f"variant {v}: {vk:.3f} ms")
 
+    # occurrence ranges (Search::search_prefix / search_range, sas/util.rs:36-46): the rank
+    # range [lo, hi) of each query's occurrences from the prefix table (k_sa_prefix_range);
+    # checked: every positive query occurs, and SA[lo] is the headline's position
+    ranges = None
+    if args.mode == "replicated":
+        qoff_d = torch.arange(nq, device=dev, dtype=torch.int64) * m
+        qlen_d = torch.full((nq,), m, device=dev, dtype=torch.int32)
+        rsteps = max(3, args.steps // 4)
+        for _ in range(args.warmup):
+            lo_d, hi_d = idx.search_range(qbytes, qoff_d, qlen_d)
+        torch.cuda.synchronize()
+        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        r0.record(stream)
+        for _ in range(rsteps):
+            lo_d, hi_d = idx.search_range(qbytes, qoff_d, qlen_d)
+        r1.record(stream)
+        torch.cuda.synchronize()
+        rms = r0.elapsed_time(r1) / rsteps
+        cnt_d = hi_d - lo_d
+        if bool((cnt_d < 1).any().item()):
+            raise SystemExit("bench: a positive query has an empty occurrence range")
+        rng = np.random.default_rng(5)
+        sids = rng.choice(nq, size=min(nq, 300), replace=False)
+        los = lo_d[torch.from_numpy(sids).to(dev)].cpu().numpy()
+        hp = headline_pos[torch.from_numpy(sids).to(dev)].cpu().numpy()
+        for j in range(len(sids)):
+            if int(idx.suffix_array(count=1, start=int(los[j]))[0]) != int(hp[j]):
+                raise SystemExit("bench: SA[lo] of an occurrence range differs from the headline position")
+        ranges = {"what": "sas_search_range: the SA rank range of each query's occurrences (prefix table + lock-step "
+                          "bisection of both bounds, k_sa_prefix_range)",
+                  "ranges_per_s": nq / (rms * 1e-3), "kernel_ms": rms,
+                  "mean_occurrences": float(cnt_d.double().mean().item()), "verified": True}
+        del qoff_d, qlen_d, lo_d, hi_d, cnt_d
+        log(f"ranges: {rms:.3f} ms")
+
     pe = stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1) if stats["prefix_chars"] else 0
     pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d", 64: "q"}.get(pe, "")
     hpmc = load_pmc(f"{args.algo}{pkey if args.algo == 'prefix' else ''}_n{n}_q{nq}_m{m}")
@@ -1016,6 +1051,7 @@ def main():
                     "ceiling_per_s": RANDOM_REQ_CEILING, "frac": head["pmc"]["requests_frac_of_ceiling"]}},
             "cpu_baseline": cpu,
             "e2e_host": e2e,
+            "occurrence_ranges": ranges,
             "configs": configs,
             "variants": variants,
             "index": idx_stats,
