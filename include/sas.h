@@ -249,10 +249,19 @@ int sas_route_pack(const sas_index* index, const uint64_t* splitter_pos, uint32_
  * and needs no host-side counts.  out_counts[w] is the true count; a query past its bucket's
  * cap is not copied and its out_slot is (nsplit + 1) * cap - 1: the caller checks
  * out_counts[w] <= cap on the device and redoes an overflowing step exactly.  Send slots a
- * bucket does not fill keep their old bytes.  EINVAL if cap == 0. */
+ * bucket does not fill keep their old bytes.  EINVAL if cap == 0.  One pass over the
+ * queries: out_counts is zeroed and accumulated on the stream. */
 int sas_route_pack_cap(const sas_index* index, const uint64_t* splitter_pos, uint32_t nsplit,
                        const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t cap, uint64_t* out_counts,
                        uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags);
+
+/* The sharded step's receive side (device pointers only, SAS_DEVICE_PTRS): out[k] =
+ * back[slot[k]], the positions that came back in send-slot order put in query order; with
+ * overflow non-null, *overflow is set to 1 (never cleared) when some counts[w] > cap,
+ * w < nparts (the out_counts of sas_route_pack_cap), so a caller can defer that check. */
+int sas_shard_gather(const sas_index* index, const uint64_t* back, const uint64_t* slot, uint64_t nq,
+                     const uint64_t* counts, uint32_t nparts, uint64_t cap, uint64_t* out,
+                     uint32_t* overflow, void* stream, uint32_t flags);
 
 int sas_get_stats(const sas_index* index, sas_stats* out);
 

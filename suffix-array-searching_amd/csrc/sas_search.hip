@@ -2544,6 +2544,9 @@ extern "C" int sas_route_batch(const sas_index* x, const uint64_t* splitter_pos,
 #define PACK_BLOCK 1024
 #define PACK_ITEMS 8
 #define PACK_CHUNK (PACK_BLOCK * PACK_ITEMS)
+#ifndef SAS_ROUTE_ITEMS
+#define SAS_ROUTE_ITEMS 8
+#endif
 
 // route + per-block histogram in one pass over the queries: dest[i] = the shard of query i
 // (as k_route; no splitters: shard 0 without reading the query), and with PACKED its 2-bit
@@ -2627,6 +2630,108 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_pack_scatter(const uint32_t* __r
     }
 }
 
+// cap > 0 in one pass over the queries (no dest array, no scan, no second read):
+//   1. each thread routes (and with SAS_ROUTE_PACKED packs) its PACK_ITEMS queries; per
+//      item, each wave takes one LDS atomic per destination present in it (leader lane,
+//      popcount of the ballot), so a lane's rank inside its (block, bucket) share is
+//      that share's running offset + the lanes below it with the same destination;
+//   2. one global atomic per (block, bucket) claims the share's first rank in bucket w
+//      (counts[w], zeroed by the caller of the launch, ends as the bucket's total);
+//   3. query i goes to slot w * cap + claimed + rank, or past the cap is clamped as above.
+template <bool PACKED, int ITEMS>
+__global__ __launch_bounds__(PACK_BLOCK) void k_route_scatter_cap(
+    const uint64_t* __restrict__ tw, uint64_t n, const uint64_t* __restrict__ sp, uint32_t nsplit,
+    const uint8_t* __restrict__ qbytes, uint32_t m, uint64_t nq, uint64_t cap, unsigned long long* __restrict__ counts,
+    uint8_t* __restrict__ send, uint64_t* __restrict__ slot_of) {
+    __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
+    __shared__ uint64_t claimed[SAS_MAX_SPLIT + 1];
+    const uint32_t W = nsplit + 1;
+    for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
+    __syncthreads();
+    const uint64_t base = (uint64_t)blockIdx.x * (PACK_BLOCK * ITEMS);
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t below = (1ull << lane) - 1ull;
+    uint32_t dst[ITEMS], rk[ITEMS];
+    uint64_t wd[ITEMS];
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const uint64_t i = base + (uint64_t)it * PACK_BLOCK + threadIdx.x;
+        const bool valid = i < nq;
+        uint32_t lo = 0;
+        wd[it] = 0;
+        if (valid && (PACKED || nsplit)) {
+            uint32_t b = 0;
+            QueryRegs<PACKED ? 1 : 4> q;
+            q.load(qbytes + i * (uint64_t)m, m, &b);
+            wd[it] = q.w[0];
+            uint32_t hi = nsplit, lcp;
+            while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
+                const uint32_t mid = (lo + hi) >> 1;
+                if (suffix_less_from<PACKED ? 1 : 4>(tw, n, sp[mid], q, 0, &lcp)) lo = mid + 1;
+                else hi = mid;
+            }
+        }
+        dst[it] = lo;
+        rk[it] = 0;
+        uint64_t todo = __ballot(valid);
+        while (todo) {  // wave-uniform: one pass per distinct destination in the wave
+            const int leader = __builtin_ctzll(todo);
+            const uint32_t d = (uint32_t)__shfl((int)lo, leader, 64);
+            const uint64_t same = __ballot(valid && lo == d);
+            uint32_t r0 = 0;
+            if (lane == leader) r0 = atomicAdd(&h[d], (uint32_t)__popcll(same));
+            r0 = (uint32_t)__shfl((int)r0, leader, 64);
+            if (valid && lo == d) rk[it] = r0 + (uint32_t)__popcll(same & below);
+            todo &= ~same;
+        }
+    }
+    __syncthreads();
+    for (uint32_t w = threadIdx.x; w < W; w += blockDim.x)
+        claimed[w] = h[w] ? (uint64_t)atomicAdd(&counts[w], (unsigned long long)h[w]) : 0ull;
+    __syncthreads();
+    const bool vec = (m & 15) == 0 && ((((uintptr_t)qbytes) | ((uintptr_t)send)) & 15) == 0;
+#pragma unroll
+    for (int it = 0; it < ITEMS; it++) {
+        const uint64_t i = base + (uint64_t)it * PACK_BLOCK + threadIdx.x;
+        if (i >= nq) continue;
+        const uint32_t w = dst[it];
+        const uint64_t r = claimed[w] + rk[it];
+        if (r >= cap) {
+            slot_of[i] = (uint64_t)W * cap - 1;
+            continue;
+        }
+        const uint64_t slot = (uint64_t)w * cap + r;
+        slot_of[i] = slot;
+        if (PACKED) {
+            reinterpret_cast<uint64_t*>(send)[slot] = wd[it];
+            continue;
+        }
+        const uint8_t* src = qbytes + i * (uint64_t)m;  // read again: the block read it in pass 1
+        uint8_t* dp = send + slot * (uint64_t)m;
+        if (vec) {
+            for (uint32_t k = 0; k < m; k += 16)
+                *reinterpret_cast<uint4*>(dp + k) = *reinterpret_cast<const uint4*>(src + k);
+        } else {
+            for (uint32_t k = 0; k < m; k++) dp[k] = src[k];
+        }
+    }
+}
+
+// The sharded step's receive side: out[i] = back[slot_of[i]] (the positions returned in
+// send-slot order, put back in query order); block 0 also raises *overflow (plain store
+// of 1, never cleared here) when a bucket's count passed its capacity.
+__global__ void k_shard_gather(const uint64_t* __restrict__ back, const uint64_t* __restrict__ slot_of, uint64_t nq,
+                               const uint64_t* __restrict__ counts, uint32_t W, uint64_t cap,
+                               uint64_t* __restrict__ out, uint32_t* __restrict__ overflow) {
+    if (blockIdx.x == 0 && overflow) {
+        bool over = false;
+        for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) over |= counts[w] > cap;
+        if (over) overflow[0] = 1u;
+    }
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x)
+        out[i] = back[slot_of[i]];
+}
+
 __global__ void k_pack_totals(const uint64_t* __restrict__ base_slot, uint32_t W, uint64_t nblk, uint64_t nq,
                               uint64_t* __restrict__ out_counts) {
     for (uint32_t w = blockIdx.x * blockDim.x + threadIdx.x; w < W; w += gridDim.x * blockDim.x) {
@@ -2668,9 +2773,35 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
         HIP_TRY(hipMemsetAsync(out_counts, 0, W * 8, st));
         return 0;
     }
-    keep_async_pool(x->device);
     const uint64_t nblk = (nq + PACK_CHUNK - 1) / PACK_CHUNK;
     const bool packed = (flags & SAS_ROUTE_PACKED) != 0;
+    if (cap) {  // fixed-capacity buckets: one pass, no scratch
+        HIP_TRY(hipMemsetAsync(out_counts, 0, W * 8, st));
+        auto* c = reinterpret_cast<unsigned long long*>(out_counts);
+        // queries per thread (A/B knob SAS_ROUTE_ITEMS = 2 / 4 / 8)
+        static const int items = [] {
+            const char* e = getenv("SAS_ROUTE_ITEMS");
+            const int v = e ? atoi(e) : SAS_ROUTE_ITEMS;
+            return (v == 2 || v == 4 || v == 8) ? v : SAS_ROUTE_ITEMS;
+        }();
+        const dim3 grid((unsigned)((nq + (uint64_t)PACK_BLOCK * items - 1) / ((uint64_t)PACK_BLOCK * items)));
+#define SAS_RSC(P, I)                                                                                              \
+    hipLaunchKernelGGL((k_route_scatter_cap<P, I>), grid, dim3(PACK_BLOCK), 0, st, x->text_w, x->n, splitter_pos, \
+                       nsplit, qbytes, m, nq, cap, c, out_send, out_slot)
+        if (packed) {
+            if (items == 2) SAS_RSC(true, 2);
+            else if (items == 4) SAS_RSC(true, 4);
+            else SAS_RSC(true, 8);
+        } else {
+            if (items == 2) SAS_RSC(false, 2);
+            else if (items == 4) SAS_RSC(false, 4);
+            else SAS_RSC(false, 8);
+        }
+#undef SAS_RSC
+        HIP_TRY(hipGetLastError());
+        return 0;
+    }
+    keep_async_pool(x->device);
     // with splitters the routing reads each query anyway and packs it on the way (words);
     // without (one part) the routing reads nothing and the scatter packs from the bytes
     const bool pack_in_route = packed && nsplit > 0;
@@ -2718,6 +2849,25 @@ extern "C" int sas_route_pack_cap(const sas_index* x, const uint64_t* splitter_p
                                   uint8_t* out_send, uint64_t* out_slot, void* stream, uint32_t flags) {
     if (cap == 0) SAS_FAIL(EINVAL, "sas_route_pack_cap: cap must be > 0");
     return route_pack_impl(x, splitter_pos, nsplit, qbytes, m, nq, cap, out_counts, out_send, out_slot, stream, flags);
+}
+
+extern "C" int sas_shard_gather(const sas_index* x, const uint64_t* back, const uint64_t* slot, uint64_t nq,
+                                const uint64_t* counts, uint32_t nparts, uint64_t cap, uint64_t* out,
+                                uint32_t* overflow, void* stream, uint32_t flags) {
+    if (!x || (nq && (!back || !slot || !out)) || (overflow && (!counts || nparts == 0)))
+        SAS_FAIL(EINVAL, "sas_shard_gather: null argument");
+    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_shard_gather: device pointers only (SAS_DEVICE_PTRS)");
+    if (nq == 0 && !overflow) return 0;
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    uint64_t blocks = (nq + 255) / 256;
+    const uint64_t capb = (uint64_t)x->num_cus * 8;
+    if (blocks > capb) blocks = capb;
+    if (blocks == 0) blocks = 1;
+    hipLaunchKernelGGL(k_shard_gather, dim3((unsigned)blocks), dim3(256), 0, st, back, slot, nq, counts, nparts, cap,
+                       out, overflow);
+    HIP_TRY(hipGetLastError());
+    return 0;
 }
 
 // ------------------------------------------------------------------ occurrence ranges

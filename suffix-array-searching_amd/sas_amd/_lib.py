@@ -125,6 +125,7 @@ def lib():
     L.sas_route.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, u32]
     L.sas_route_pack.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, vp, vp, u32]
     L.sas_route_pack_cap.argtypes = [vp, vp, u32, vp, u32, u64, u64, vp, vp, vp, vp, u32]
+    L.sas_shard_gather.argtypes = [vp, vp, vp, u64, vp, u32, u64, vp, vp, vp, u32]
     L.sas_route_batch.argtypes = [vp, vp, u32, vp, vp, vp, u64, vp, vp, u32]
     L.sas_build_multi.argtypes = [vp, u64, vp, i32, i32, u32, C.POINTER(vp)]
     L.sas_extract.argtypes = [vp, vp, vp, vp, u64, vp, vp, u32]

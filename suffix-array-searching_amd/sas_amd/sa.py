@@ -294,6 +294,26 @@ class SaNaive:
                                        send.data_ptr(), slot.data_ptr(), st, fl))
         return counts, send[:size], slot[:nq]
 
+    def shard_gather(self, back, slot, out=None, counts=None, cap: int = 0, overflow=None, stream=None):
+        """Receive side of one sharded step (sas_shard_gather): out[k] = back[slot[k]]; with
+        `overflow` (an int32 CUDA tensor of 1, never cleared here) it is set to 1 when some
+        counts[w] > cap."""
+        import torch
+        nq = slot.numel()
+        if out is None:
+            out = torch.empty(nq, dtype=torch.int64, device=slot.device)
+        if out.numel() < nq or out.dtype != torch.int64 or back.dtype != torch.int64 or slot.dtype != torch.int64:
+            raise ValueError("shard_gather: int64 back/slot/out, out of at least len(slot)")
+        if overflow is not None and (counts is None or overflow.dtype != torch.int32):
+            raise ValueError("shard_gather: overflow needs counts and an int32 flag")
+        st = stream if stream is not None else torch.cuda.current_stream(slot.device).cuda_stream
+        check(lib().sas_shard_gather(self._h, back.data_ptr(), slot.data_ptr(), nq,
+                                     counts.data_ptr() if counts is not None else None,
+                                     counts.numel() if counts is not None else 0, int(cap), out.data_ptr(),
+                                     overflow.data_ptr() if overflow is not None else None, st,
+                                     _lib.SAS_DEVICE_PTRS))
+        return out[:nq]
+
     def verify(self):
         check(lib().sas_verify(self._h))
 

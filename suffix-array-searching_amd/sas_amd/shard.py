@@ -53,7 +53,7 @@ class ShardedSearch:
                                                                                               device=device)
         self._caps = {}  # nq -> capacity agreed by every rank
         self._bufs = {}
-        self.overflow = torch.zeros(1, dtype=torch.bool, device=device)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
 
     # ---------------------------------------------------------------- capacity
     def capacity(self, nq: int) -> int:
@@ -110,26 +110,28 @@ class ShardedSearch:
         else:
             self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
         self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group)
-        over = (counts > cap).any().reshape(1)
-        out = torch.index_select(buf["back"], 0, slot, out=out) if out is not None else \
-            buf["back"].index_select(0, slot)
+        # one flag per step (check) or the sticky one (deferred to assert_no_overflow)
+        flag = torch.zeros(1, dtype=torch.int32, device=self.device) if check else self.overflow
+        if hasattr(self.index, "shard_gather"):  # gather + overflow test in one kernel
+            out = self.index.shard_gather(buf["back"], slot, out=out, counts=counts, cap=cap, overflow=flag)
+        else:
+            flag |= (counts > cap).any().reshape(1).to(torch.int32)
+            out = torch.index_select(buf["back"], 0, slot, out=out) if out is not None else \
+                buf["back"].index_select(0, slot)
         if check:
-            # one flag per rank, agreed by all (an overflow anywhere changes every rank's
-            # exchange): redo the step with exact splits
-            flag = over.to(torch.int32)
+            # agreed by all (an overflow anywhere changes every rank's exchange): redo the
+            # step with exact splits
             self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
             if int(flag.item()):
                 exact = self.search_fixed_exact(qbytes, m)
                 return out.copy_(exact) if out is not None else exact
-        else:
-            self.overflow |= over
         return out
 
     def assert_no_overflow(self):
         """After steps run with check=False: every bucket fitted its capacity (so every
         result was exact)."""
         import torch
-        flag = self.overflow.to(torch.int32)
+        flag = self.overflow.clone()
         self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
         if int(flag.item()):
             raise RuntimeError("ShardedSearch: a bucket overflowed its capacity in a check=False step; "

@@ -231,3 +231,54 @@ def test_route_pack_argument_errors(sas):
     torch.cuda.synchronize()
     assert c.tolist() == [2] and sorted(sl.tolist()) == [0, 1]
     assert torch.equal(s2.view(2, 40)[sl], q.view(2, 40))
+
+
+def test_route_pack_cap_one_pass_and_gather(sas):
+    """sas_route_pack_cap (one pass: wave-aggregated bucket ranks, one global claim per
+    block and bucket) with W = 5 parts, byte and packed slots: counts = the histogram of
+    sas_route, every query inside its bucket's slots, slots distinct, bytes / words at
+    their slot; a cap below a bucket's count clamps the overflow to the last slot, and
+    sas_shard_gather puts positions back in query order and raises the overflow flag."""
+    import torch
+    n, W = 300_007, 5
+    t = sas.random_string(n, seed=61)
+    idxs = [sas.SaNaive.build_part(t, g, W, lcp=False, stree=False, sector=False) for g in range(W)]
+    splitters = torch.tensor([int(ix.suffix_array(1)[0]) for ix in idxs[1:]], dtype=torch.int64).cuda()
+    rng = np.random.default_rng(8)
+    for m, packed in ((24, False), (32, False), (32, True), (13, True)):
+        offs = rng.integers(0, n - m, 30_011)
+        qb = np.concatenate([t[o:o + m] for o in offs] + [rng.integers(0, 4, 7001 * m, dtype=np.uint8)])
+        nq = len(qb) // m
+        dq = torch.from_numpy(qb).cuda()
+        dest = idxs[0].route(splitters, dq, m).cpu().numpy().astype(np.int64)
+        hist = np.bincount(dest, minlength=W)
+        cap = int(hist.max()) + 3
+        counts, send, slot = idxs[0].route_pack(splitters, dq, m, cap=cap, packed=packed)
+        c, s, sl = counts.cpu().numpy(), send.cpu().numpy(), slot.cpu().numpy()
+        assert c.tolist() == hist.tolist(), (m, packed)
+        assert len(np.unique(sl)) == nq
+        assert ((sl >= dest * cap) & (sl < dest * cap + hist[dest])).all()
+        if packed:
+            words = sas.SaNaive.pack_queries(dq, m).cpu().numpy()
+            assert np.array_equal(s.view(np.uint64)[sl], words.view(np.uint64))
+        else:
+            assert np.array_equal(s.reshape(W * cap, m)[sl], qb.reshape(nq, m))
+        # gather: "positions" = the slot numbers themselves come back as the query index
+        back = torch.full((W * cap,), -1, dtype=torch.int64, device="cuda")
+        back[slot] = torch.arange(nq, device="cuda")
+        flag = torch.zeros(1, dtype=torch.int32, device="cuda")
+        got = idxs[0].shard_gather(back, slot, counts=counts, cap=cap, overflow=flag)
+        assert np.array_equal(got.cpu().numpy(), np.arange(nq)) and int(flag.item()) == 0
+        # overflow: the largest bucket gets 7 fewer slots than it needs
+        small = int(hist.max()) - 7
+        counts, send, slot = idxs[0].route_pack(splitters, dq, m, cap=small, packed=packed)
+        sl = slot.cpu().numpy()
+        big = hist > small
+        assert counts.cpu().numpy().tolist() == hist.tolist()
+        clamped = sl == W * small - 1
+        assert int(clamped.sum()) >= int((hist[big] - small).sum())
+        ok = ~np.isin(dest, np.nonzero(big)[0])
+        assert ((sl[ok] >= dest[ok] * small) & (sl[ok] < dest[ok] * small + hist[dest[ok]])).all()
+        idxs[0].shard_gather(torch.zeros(W * small, dtype=torch.int64, device="cuda"), slot, counts=counts, cap=small,
+                             overflow=flag)
+        assert int(flag.item()) == 1, (m, packed)
