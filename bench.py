@@ -932,23 +932,28 @@ def main():
         log(f"variant {v}: {vk:.3f} ms")
 
     # occurrence ranges (Search::search_prefix / search_range, sas/util.rs:36-46): the rank
-    # range [lo, hi) of each query's occurrences from the prefix table (k_sa_prefix_range);
-    # checked: every positive query occurs, and SA[lo] is the headline's position
+    # range [lo, hi) of each query's occurrences from the prefix table (inline slots first,
+    # k_sa_prefix2_range; SAS_RANGE_NO_INLINE: both bounds bisected, k_sa_prefix_range);
+    # checked: every positive query occurs, SA[lo] is the headline's position, and the
+    # two kernels agree
     ranges = None
     if args.mode == "replicated":
-        qoff_d = torch.arange(nq, device=dev, dtype=torch.int64) * m
-        qlen_d = torch.full((nq,), m, device=dev, dtype=torch.int32)
-        rsteps = max(3, args.steps // 4)
-        for _ in range(args.warmup):
-            lo_d, hi_d = idx.search_range(qbytes, qoff_d, qlen_d)
-        torch.cuda.synchronize()
-        r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        r0.record(stream)
-        for _ in range(rsteps):
-            lo_d, hi_d = idx.search_range(qbytes, qoff_d, qlen_d)
-        r1.record(stream)
-        torch.cuda.synchronize()
-        rms = r0.elapsed_time(r1) / rsteps
+        def time_ranges(fl):
+            for _ in range(args.warmup):
+                idx.search_range_fixed(qbytes, m, flags=fl)
+            torch.cuda.synchronize()
+            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            rsteps = max(3, args.steps // 4)
+            r0.record(stream)
+            for _ in range(rsteps):
+                res = idx.search_range_fixed(qbytes, m, flags=fl)
+            r1.record(stream)
+            torch.cuda.synchronize()
+            return r0.elapsed_time(r1) / rsteps, res
+        rms, (lo_d, hi_d) = time_ranges(0)
+        bms, (lo_b, hi_b) = time_ranges(sas_amd._lib.SAS_RANGE_NO_INLINE)
+        if not (torch.equal(lo_d, lo_b) and torch.equal(hi_d, hi_b)):
+            raise SystemExit("bench: the inline-slot and bisection range kernels disagree")
         cnt_d = hi_d - lo_d
         if bool((cnt_d < 1).any().item()):
             raise SystemExit("bench: a positive query has an empty occurrence range")
@@ -959,12 +964,13 @@ def main():
         for j in range(len(sids)):
             if int(idx.suffix_array(count=1, start=int(los[j]))[0]) != int(hp[j]):
                 raise SystemExit("bench: SA[lo] of an occurrence range differs from the headline position")
-        ranges = {"what": "sas_search_range: the SA rank range of each query's occurrences (prefix table + lock-step "
-                          "bisection of both bounds, k_sa_prefix_range)",
+        ranges = {"what": "sas_search_range_fixed: the SA rank range of each query's occurrences (prefix table: "
+                          "the inline slots test both bounds, the rest bisected; k_sa_prefix2_range)",
                   "ranges_per_s": nq / (rms * 1e-3), "kernel_ms": rms,
-                  "mean_occurrences": float(cnt_d.double().mean().item()), "verified": True}
-        del qoff_d, qlen_d, lo_d, hi_d, cnt_d
-        log(f"ranges: {rms:.3f} ms")
+                  "bisect_kernel_ms": bms, "mean_occurrences": float(cnt_d.double().mean().item()),
+                  "verified": True}
+        del lo_d, hi_d, lo_b, hi_b, cnt_d
+        log(f"ranges: {rms:.3f} ms (bisection {bms:.3f} ms)")
 
     pe = stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1) if stats["prefix_chars"] else 0
     pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d", 64: "q"}.get(pe, "")

@@ -52,6 +52,9 @@ typedef struct sas_index sas_index;
                                          sas_search_packed format) instead of its m bytes */
 #define SAS_NO_PREFIX_TABLE (1u << 25) /* sas_search_range: use the tree descents even when
                                         the index has a prefix table                      */
+#define SAS_RANGE_NO_INLINE (1u << 27) /* sas_search_range(_fixed): on a two/four-suffix inline
+                                        prefix table, bisect both bounds from the table's rank
+                                        range instead of testing the inline slots first     */
 #define SAS_PREFIX_RANGE  (1u << 24) /* search, PLAIN / LCP: start binary_search from the
                                         prefix table's range of q's first p chars, as the
                                         reference's binary_search does (sas/sa_search.rs:
@@ -316,12 +319,17 @@ int sas_search_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, 
  * is out_hi - out_lo and the positions are SA[out_lo .. out_hi)
  * (sas_copy_sa_range).  Needs SAS_BUILD_TAGGED, SAS_BUILD_QUAD or SAS_BUILD_SECTOR: the
  * tagged index uses its bucket table; otherwise the prefix table when built beside the quad
- * tree (unless SAS_NO_PREFIX_TABLE), else the quad tree, else the sector tree.  Both bounds
- * of a query are bisected in lock step; no probe counts are reported (the reference has no
- * range search to count against).  Ragged queries as in sas_search_batch. */
+ * tree (unless SAS_NO_PREFIX_TABLE), else the quad tree, else the sector tree.  On a
+ * two/four-suffix inline prefix table a query's lane group tests both bounds on the entry's
+ * slots first (one request answers most queries); bounds not found there are bisected in
+ * lock step.  No probe counts are reported (the reference has no range search to count
+ * against).  Ragged queries as in sas_search_batch. */
 int sas_search_range(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,
                      const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi,
                      void* stream, uint32_t flags);
+/* sas_search_range for fixed-length queries qbytes[k*m .. (k+1)*m). */
+int sas_search_range_fixed(const sas_index* index, const uint8_t* qbytes, uint32_t m, uint64_t nq,
+                           uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags);
 /* Copy SA[start .. start+count) (global ranks) out: the text positions of a range. */
 int sas_copy_sa_range(const sas_index* index, uint64_t start, uint64_t count, uint32_t* dst,
                       uint32_t flags);

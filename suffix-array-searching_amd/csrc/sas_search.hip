@@ -1460,6 +1460,96 @@ static void launch_prefix_range(int qw, dim3 grid, dim3 block, hipStream_t st, c
     }
 }
 
+// Occurrence ranges on a G-slot inline prefix table (SAS_BUILD_PREFIX_INLINE2 / _INLINE4):
+// the G lanes of a query read its entry (the first G suffixes of the range of its p-char
+// key) as one request and test both bounds' predicates on every slot: lo = the first slot
+// >= q, hi = the first slot whose first min(m, len) chars are > q (m >= p: the suffixes
+// starting with q all lie in the key's range).  A bound not inside the entry is bisected
+// in [r + G, table[K + 1]) (hi, for m < p: in the range of the 3-padded key), both in
+// lock step as k_sa_prefix_range does; every lane of the group runs the same loop (same
+// addresses: one request per probe).
+template <int QW, int G>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2_range(SearchArgs a, uint64_t* out_hi) {
+    uint32_t bad = 0;
+    const uint32_t sh = 64 - 2 * a.prefix_chars;
+    const uint64_t sa_n = a.sa_n;
+    const uint32_t sub = threadIdx.x & (G - 1);
+    const int lane0 = (int)((threadIdx.x & 63) & ~(uint32_t)(G - 1));
+    const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / G;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G; i < a.nq; i += stride) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);  // every lane of the group: the same addresses, one request
+        const uint64_t K64 = q.w[0];
+        const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
+        const uint64_t K = K64 >> sh;
+        const uint4 e = pt[G * K + sub];
+        const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
+        const uint64_t rank = r0 + sub;
+        const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        // rank sa_n stands for "past every suffix": both bounds are reached there
+        const bool past = rank >= sa_n;
+        const bool ge = past || sector_ge<QW>(key, e.w, K64, a, q);
+        const bool whole = m >= a.prefix_chars;  // hi inside the key's range too
+        const bool gt = past || (whole && sector_gt_prefix<QW>(key, e.w, K64, Q3, a, q));
+        const uint32_t mask = (1u << G) - 1u;
+        const uint32_t gge = (uint32_t)(__ballot(ge) >> lane0) & mask;
+        const uint32_t ggt = (uint32_t)(__ballot(gt) >> lane0) & mask;
+        uint64_t lo, l1, hi, h1;
+        if (gge) {
+            lo = l1 = r0 + (uint32_t)__builtin_ctz(gge);
+        } else {
+            lo = r0 + G;
+            l1 = pt[G * (K + 1)].z;
+        }
+        if (whole) {
+            if (ggt) {
+                hi = h1 = r0 + (uint32_t)__builtin_ctz(ggt);
+            } else {
+                hi = r0 + G;
+                h1 = gge ? pt[G * (K + 1)].z : l1;
+            }
+        } else {
+            prefix_range(a, Q3 >> sh, &hi, &h1);
+        }
+        while (lo < l1 || hi < h1) {
+            const bool g0 = lo < l1, g1 = hi < h1;
+            const uint64_t m0 = (lo + l1) >> 1, m1 = (hi + h1) >> 1;
+            const uint64_t k0 = g0 ? quad_entry_key<false>(a, m0) : 0;
+            const uint64_t k1 = g1 ? quad_entry_key<false>(a, m1) : 0;
+            const uint64_t p0 = (g0 && k0 == K64) ? quad_entry_sa<false, 4>(a, m0) : QUAD_NO_SA;
+            const uint64_t p1 = (g1 && q.m > 32 && k1 == K64) ? quad_entry_sa<false, 4>(a, m1) : QUAD_NO_SA;
+            if (g0) {
+                if (sector_ge<QW>(k0, p0, K64, a, q)) l1 = m0;
+                else lo = m0 + 1;
+            }
+            if (g1) {
+                if (sector_gt_prefix<QW>(k1, p1, K64, Q3, a, q)) h1 = m1;
+                else hi = m1 + 1;
+            }
+        }
+        if (hi < lo) hi = lo;
+        if (sub == 0) {
+            a.out_pos[i] = a.rank_lo + lo;
+            out_hi[i] = a.rank_lo + hi;
+        }
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+template <int G>
+static void launch_prefix2_range(int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a, uint64_t* dhi) {
+    switch (qw) {
+        case 1: hipLaunchKernelGGL((k_sa_prefix2_range<1, G>), grid, block, 0, st, a, dhi); break;
+        case 2: hipLaunchKernelGGL((k_sa_prefix2_range<2, G>), grid, block, 0, st, a, dhi); break;
+        case 4: hipLaunchKernelGGL((k_sa_prefix2_range<4, G>), grid, block, 0, st, a, dhi); break;
+        default: hipLaunchKernelGGL((k_sa_prefix2_range<8, G>), grid, block, 0, st, a, dhi); break;
+    }
+}
+
 // ------------------------------------------------------------------ INTERP
 // interpolation_search<16> (sas/sa_search.rs:376-421), one lane per query.  string_value<16>
 // (sas/util.rs:76-117) of a suffix is the high half of its 32-char packed key; of the query,
@@ -2881,20 +2971,25 @@ static void launch_quad_range(int qw, dim3 grid, dim3 block, hipStream_t st, con
     }
 }
 
-extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
-                                uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
+// ragged (qoff, qlen) or fixed-length (qoff == nullptr: m_fixed chars per query)
+static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixed, const uint64_t* qoff,
+                      const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream,
+                      uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
     if (!x->sec_leaves && !x->quad_leaves && !x->tag_table)
         SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_QUAD, SAS_BUILD_SECTOR or SAS_BUILD_TAGGED");
     const bool quad = x->quad_leaves != nullptr;
+    const bool ragged = qoff != nullptr || qlen != nullptr;
     if (nq == 0) return 0;
-    if (!qbytes || !qoff || !qlen || !out_lo || !out_hi) SAS_FAIL(EINVAL, "sas_search_range: null argument");
+    if (!qbytes || !out_lo || !out_hi || (ragged && (!qoff || !qlen)))
+        SAS_FAIL(EINVAL, "sas_search_range: null argument");
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     bool dev = flags & SAS_DEVICE_PTRS;
     SearchArgs a{};
     fill_args(x, a);
     a.nq = nq;
+    a.m_fixed = ragged ? 0 : m_fixed;
     a.bad = x->scratch;  // per-call flag when read back (see search_impl)
     bool check_bad = !dev || (flags & SAS_VALIDATE);
     DeviceBuf bflag;
@@ -2905,44 +3000,53 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
     }
     DeviceBuf bqb, bqoff, bqlen, blo, bhi;
     uint64_t* dhi = out_hi;
-    int qw = 4;
+    int qw = ragged ? 4 : qw_for(m_fixed);
     if (dev) {
         a.qbytes = qbytes;
         a.qoff = qoff;
         a.qlen = qlen;
         a.out_pos = out_lo;
     } else {
-        uint64_t span = 0, maxlen = 0;
-        for (uint64_t k = 0; k < nq; k++) {
-            uint64_t e = qoff[k] + qlen[k];
-            if (e > span) span = e;
-            if (qlen[k] > maxlen) maxlen = qlen[k];
+        uint64_t span = nq * (uint64_t)m_fixed, maxlen = m_fixed;
+        if (ragged) {
+            span = maxlen = 0;
+            for (uint64_t k = 0; k < nq; k++) {
+                uint64_t e = qoff[k] + qlen[k];
+                if (e > span) span = e;
+                if (qlen[k] > maxlen) maxlen = qlen[k];
+            }
         }
         qw = qw_for(maxlen);
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMalloc(&bqb.p, span + 64));
         if (span) HIP_TRY(hipMemcpy(bqb.p, qbytes, span, hipMemcpyHostToDevice));
-        HIP_TRY(hipMalloc(&bqoff.p, nq * 8));
-        HIP_TRY(hipMalloc(&bqlen.p, nq * 4));
         HIP_TRY(hipMalloc(&blo.p, nq * 8));
         HIP_TRY(hipMalloc(&bhi.p, nq * 8));
-        HIP_TRY(hipMemcpy(bqoff.p, qoff, nq * 8, hipMemcpyHostToDevice));
-        HIP_TRY(hipMemcpy(bqlen.p, qlen, nq * 4, hipMemcpyHostToDevice));
         a.qbytes = static_cast<const uint8_t*>(bqb.p);
-        a.qoff = static_cast<const uint64_t*>(bqoff.p);
-        a.qlen = static_cast<const uint32_t*>(bqlen.p);
+        if (ragged) {
+            HIP_TRY(hipMalloc(&bqoff.p, nq * 8));
+            HIP_TRY(hipMalloc(&bqlen.p, nq * 4));
+            HIP_TRY(hipMemcpy(bqoff.p, qoff, nq * 8, hipMemcpyHostToDevice));
+            HIP_TRY(hipMemcpy(bqlen.p, qlen, nq * 4, hipMemcpyHostToDevice));
+            a.qoff = static_cast<const uint64_t*>(bqoff.p);
+            a.qlen = static_cast<const uint32_t*>(bqlen.p);
+        }
         a.out_pos = static_cast<uint64_t*>(blo.p);
         dhi = static_cast<uint64_t*>(bhi.p);
     }
     if (check_bad) {
         uint64_t vb = (nq + 255) / 256;
         if (vb > 65536) vb = 65536;
-        hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, st, a.qbytes, a.qoff, a.qlen, 0u,
-                           nq, a.bad);
+        hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, st, a.qbytes, a.qoff, a.qlen,
+                           a.m_fixed, nq, a.bad);
     }
-    // the prefix table, when built, replaces the two tree descents (one lane per query)
+    // the prefix table, when built, replaces the two tree descents (one lane per query;
+    // G lanes per query on a G-slot inline table)
     const bool ptab = quad && x->prefix && !(flags & SAS_NO_PREFIX_TABLE);
-    uint64_t blocks = (nq * ((quad && !ptab) ? QUAD_G : 1) + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    const bool pair = ptab && !x->quad_compact && (x->prefix_w == 32 || x->prefix_w == 64) &&
+                      !(flags & SAS_RANGE_NO_INLINE);
+    const uint64_t per = (quad && !ptab) ? QUAD_G : (pair ? x->prefix_w / 16 : 1);
+    uint64_t blocks = (nq * per + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
@@ -2953,6 +3057,9 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
             case 4: hipLaunchKernelGGL(k_sa_tagged_range<4>, grid, block, 0, st, a, dhi); break;
             default: hipLaunchKernelGGL(k_sa_tagged_range<8>, grid, block, 0, st, a, dhi); break;
         }
+    } else if (pair) {
+        if (x->prefix_w == 32) launch_prefix2_range<2>(qw, grid, block, st, a, dhi);
+        else launch_prefix2_range<4>(qw, grid, block, st, a, dhi);
     } else if (ptab) {
         if (!x->quad_compact) launch_prefix_range<false, 4>(qw, grid, block, st, a, dhi);
         else if (x->sa_w == 5) launch_prefix_range<true, 5>(qw, grid, block, st, a, dhi);
@@ -2982,4 +3089,15 @@ extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const
         if (hbad) SAS_FAIL(EINVAL, "sas_search_range: query bytes must be DNA codes 0..3");
     }
     return 0;
+}
+
+extern "C" int sas_search_range(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
+                                uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
+    if (nq && (!qoff || !qlen)) SAS_FAIL(EINVAL, "sas_search_range: null qoff/qlen");
+    return range_impl(x, qbytes, 0, qoff, qlen, nq, out_lo, out_hi, stream, flags);
+}
+
+extern "C" int sas_search_range_fixed(const sas_index* x, const uint8_t* qbytes, uint32_t m, uint64_t nq,
+                                      uint64_t* out_lo, uint64_t* out_hi, void* stream, uint32_t flags) {
+    return range_impl(x, qbytes, m, nullptr, nullptr, nq, out_lo, out_hi, stream, flags);
 }

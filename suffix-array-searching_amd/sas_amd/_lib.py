@@ -24,6 +24,7 @@ SAS_NO_LDS_TOP = 1 << 4
 SAS_VALIDATE = 1 << 5
 SAS_PREFIX_RANGE = 1 << 24
 SAS_NO_PREFIX_TABLE = 1 << 25
+SAS_RANGE_NO_INLINE = 1 << 27
 SAS_ROUTE_PACKED = 1 << 26
 SAS_BUILD_WIDE = 1 << 6
 SAS_BUILD_SECTOR = 1 << 7
@@ -139,6 +140,7 @@ def lib():
     L.sas_copy_sa.argtypes = [vp, vp, u64, u32]
     L.sas_copy_lcp.argtypes = [vp, vp, u64, u32]
     L.sas_search_range.argtypes = [vp, vp, vp, vp, u64, vp, vp, vp, u32]
+    L.sas_search_range_fixed.argtypes = [vp, vp, u32, u64, vp, vp, vp, u32]
     L.sas_copy_sa_range.argtypes = [vp, u64, u64, vp, u32]
     L.sas_copy_sa64.argtypes = [vp, u64, u64, vp, u32]
     L.sas_read_fasta.argtypes = [C.c_char_p, vp, u64, C.POINTER(u64)]

@@ -399,6 +399,24 @@ class SaNaive:
                                      flags))
         return (lo, hi) if dev else (lo[:nq], hi[:nq])
 
+    def search_range_fixed(self, qbytes, m: int, stream=None, flags: int = 0):
+        """search_range for fixed-length queries qbytes[k*m .. (k+1)*m) (sas_search_range_fixed)."""
+        dev = _is_cuda(qbytes)
+        nq = qbytes.numel() // m if dev else len(qbytes) // m
+        if dev:
+            import torch
+            lo = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+            hi = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
+            st = stream if stream is not None else torch.cuda.current_stream(qbytes.device).cuda_stream
+            flags |= _lib.SAS_DEVICE_PTRS
+        else:
+            qbytes = _as_u8(qbytes)
+            lo = np.zeros(max(nq, 1), np.uint64)
+            hi = np.zeros(max(nq, 1), np.uint64)
+            st = stream
+        check(lib().sas_search_range_fixed(self._h, _ptr(qbytes), m, nq, _ptr(lo), _ptr(hi), st, flags))
+        return (lo, hi) if dev else (lo[:nq], hi[:nq])
+
     def search_prefix(self, q) -> np.ndarray:
         """All text positions where q occurs (Search::search_prefix, sas/util.rs:36-40)."""
         q = _as_u8(q)

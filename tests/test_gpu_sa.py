@@ -1011,3 +1011,46 @@ def test_multi_device_handle(sas, devices):
                 got = M.search_batch(buf, off, lens, algo=algo)
                 assert np.array_equal(got, expect), (mode, algo, len(devices), n)
             M.free()
+
+
+def test_occurrence_ranges_inline_slots(sas):
+    """k_sa_prefix2_range: on two- and four-suffix inline prefix tables the lane group tests
+    both bounds on the entry's slots, then bisects what is left.  Ranges equal the oracle's
+    and the plain bisection's (SAS_RANGE_NO_INLINE) for: p from 4 (ranges far larger than an
+    entry: the bisections) to 12 (mostly one entry), fixed lengths below p, at 32 and above
+    (text compares), ragged mixes, misses, above-every-suffix and empty queries, a repetitive
+    text, a 40-bit SA, host and device pointers (sas_search_range_fixed)."""
+    import torch
+    from sas_amd import _lib
+    rng = np.random.default_rng(44)
+    texts = [sas.random_string(200_003, seed=9), np.tile(rng.integers(0, 4, 7, dtype=np.uint8), 20_000)]
+    for t in texts:
+        n = len(t)
+        tp = O.padded(t)
+        for p, inl, sa40 in ((4, 2, False), (8, 4, False), (12, 2, False), (10, 2, True), (12, 4, False)):
+            idx = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=p,
+                                    prefix_inline=inl, sa40=sa40)
+            sa = np.ascontiguousarray(idx.suffix_array(), np.uint32)
+            for m in (3, 8, 32, 40):
+                offs = rng.integers(0, n - m, 1500)
+                qb = np.concatenate([t[o:o + m] for o in offs] + [rng.integers(0, 4, 500 * m, dtype=np.uint8),
+                                                                  np.full(m, 3, np.uint8)])
+                nq = len(qb) // m
+                lo, hi = idx.search_range_fixed(qb, m)
+                lo2, hi2 = idx.search_range_fixed(qb, m, flags=_lib.SAS_RANGE_NO_INLINE)
+                assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2), (n, p, inl, m)
+                dlo, dhi = idx.search_range_fixed(torch.from_numpy(qb).cuda(), m)
+                assert np.array_equal(dlo.cpu().numpy().astype(np.uint64), lo), (n, p, inl, m)
+                assert np.array_equal(dhi.cpu().numpy().astype(np.uint64), hi), (n, p, inl, m)
+                for k in list(range(0, nq, 37)) + [nq - 1]:
+                    q = qb[k * m:(k + 1) * m]
+                    assert (int(lo[k]), int(hi[k])) == O.prefix_range(tp, n, sa, q), (n, p, inl, m, k)
+            qs = [t[o:o + l] for o, l in zip(rng.integers(0, n - 300, 800), rng.integers(0, 300, 800))]
+            qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(0, 40, 300)]
+            qs += [np.zeros(0, np.uint8), np.full(200, 3, np.uint8)]
+            buf, off, lens = pack(qs)
+            lo, hi = idx.search_range(buf, off, lens)
+            lo2, hi2 = idx.search_range(buf, off, lens, flags=_lib.SAS_RANGE_NO_INLINE)
+            assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2), (n, p, inl)
+            for k in range(0, len(qs), 7):
+                assert (int(lo[k]), int(hi[k])) == O.prefix_range(tp, n, sa, qs[k]), (n, p, inl, k)
