@@ -2535,23 +2535,44 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
 }
 
 // ------------------------------------------------------------------ sharded-mode routing
+// Routing compares a query with the splitter suffixes by their first 32 chars (staged in
+// LDS once per block: sk[w] = text_chars32 at splitter w) and reads the text only on a tie
+// of those keys (distinct 32-char keys order as the strings do, zero padding included,
+// as sector_ge relies on): the shard of q = the number of splitter suffixes < q.
+__device__ __forceinline__ void stage_split_keys(const uint64_t* __restrict__ tw, const uint64_t* __restrict__ sp,
+                                                 uint32_t nsplit, uint64_t* sk) {
+    for (uint32_t w = threadIdx.x; w < nsplit; w += blockDim.x) sk[w] = text_chars32(tw, sp[w]);
+}
+
+template <int QW>
+__device__ __forceinline__ uint32_t route_of(const uint64_t* __restrict__ tw, uint64_t n,
+                                             const uint64_t* __restrict__ sp, const uint64_t* sk, uint32_t nsplit,
+                                             const QueryRegs<QW>& q) {
+    uint32_t lo = 0, hi = nsplit, lcp;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        const uint64_t kk = sk[mid];
+        const bool less = kk != q.w[0] ? kk < q.w[0] : suffix_less_from<QW>(tw, n, sp[mid], q, 0, &lcp);
+        if (less) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
 __global__ __launch_bounds__(256) void k_route(const uint64_t* __restrict__ tw, uint64_t n,
                                                const uint64_t* __restrict__ sp, uint32_t nsplit,
                                                const uint8_t* __restrict__ qbytes, uint32_t m,
                                                const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qlen,
                                                uint64_t nq, uint32_t* __restrict__ out, uint32_t* bad) {
+    __shared__ uint64_t sk[SAS_MAX_SPLIT];
+    stage_split_keys(tw, sp, nsplit, sk);
+    __syncthreads();
     uint32_t b = 0;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x) {
         QueryRegs<4> q;
         if (qoff) q.load(qbytes + qoff[i], qlen[i], &b);  // ragged (sas_route_batch)
         else q.load(qbytes + i * (uint64_t)m, m, &b);
-        uint32_t lo = 0, hi = nsplit, lcp;
-        while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
-            uint32_t mid = (lo + hi) >> 1;
-            if (suffix_less_from<4>(tw, n, sp[mid], q, 0, &lcp)) lo = mid + 1;
-            else hi = mid;
-        }
-        out[i] = lo;
+        out[i] = route_of<4>(tw, n, sp, sk, nsplit, q);
     }
     if (b) atomicOr(bad, 1u);
 }
@@ -2648,8 +2669,10 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_route_count(const uint64_t* __re
                                                             uint64_t nblk, uint64_t* __restrict__ cnt,
                                                             uint32_t* __restrict__ dest, uint64_t* __restrict__ words) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
+    __shared__ uint64_t sk[SAS_MAX_SPLIT];
     const uint32_t W = nsplit + 1;
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
+    stage_split_keys(tw, sp, nsplit, sk);
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * PACK_CHUNK;
     for (int it = 0; it < PACK_ITEMS; it++) {
@@ -2661,12 +2684,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_route_count(const uint64_t* __re
             QueryRegs<PACKED ? 1 : 4> q;
             q.load(qbytes + i * (uint64_t)m, m, &b);
             if (PACKED) words[i] = q.w[0];
-            uint32_t hi = nsplit, lcp;
-            while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
-                const uint32_t mid = (lo + hi) >> 1;
-                if (suffix_less_from<PACKED ? 1 : 4>(tw, n, sp[mid], q, 0, &lcp)) lo = mid + 1;
-                else hi = mid;
-            }
+            lo = route_of<PACKED ? 1 : 4>(tw, n, sp, sk, nsplit, q);
         }
         dest[i] = lo;
         atomicAdd(&h[lo], 1u);
@@ -2735,8 +2753,10 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_route_scatter_cap(
     uint8_t* __restrict__ send, uint64_t* __restrict__ slot_of) {
     __shared__ uint32_t h[SAS_MAX_SPLIT + 1];
     __shared__ uint64_t claimed[SAS_MAX_SPLIT + 1];
+    __shared__ uint64_t sk[SAS_MAX_SPLIT];
     const uint32_t W = nsplit + 1;
     for (uint32_t w = threadIdx.x; w < W; w += blockDim.x) h[w] = 0;
+    stage_split_keys(tw, sp, nsplit, sk);
     __syncthreads();
     const uint64_t base = (uint64_t)blockIdx.x * (PACK_BLOCK * ITEMS);
     const int lane = (int)(threadIdx.x & 63);
@@ -2754,12 +2774,7 @@ __global__ __launch_bounds__(PACK_BLOCK) void k_route_scatter_cap(
             QueryRegs<PACKED ? 1 : 4> q;
             q.load(qbytes + i * (uint64_t)m, m, &b);
             wd[it] = q.w[0];
-            uint32_t hi = nsplit, lcp;
-            while (lo < hi) {  // count of splitter suffixes < q (they are sorted)
-                const uint32_t mid = (lo + hi) >> 1;
-                if (suffix_less_from<PACKED ? 1 : 4>(tw, n, sp[mid], q, 0, &lcp)) lo = mid + 1;
-                else hi = mid;
-            }
+            lo = route_of<PACKED ? 1 : 4>(tw, n, sp, sk, nsplit, q);
         }
         dst[it] = lo;
         rk[it] = 0;
