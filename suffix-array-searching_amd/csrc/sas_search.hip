@@ -2120,6 +2120,10 @@ struct DeviceBuf {
     ~DeviceBuf() { if (p) (void)hipFree(p); }
 };
 
+// Occurrence-range kernel for the index's structures (defined with the range kernels below)
+static void launch_range(const sas_index* x, const SearchArgs& a, int qw, uint32_t flags, hipStream_t st,
+                         uint64_t* dhi);
+
 // ------------------------------------------------------------------ host-pointer pipeline
 void sas_stage_pool_free(StagePool* p) {
     if (!p) return;
@@ -2137,12 +2141,16 @@ enum HostMode {
 // Synchronous search of host arrays through the index's pinned staging slots (host_stage.hpp).
 // Returns with out_pos / out_probes filled; EINVAL (after the whole batch) if a query byte
 // is not a DNA code.
+// out_hi non-null: occurrence ranges (launch_range) instead of a search; a chunk then holds
+// at most cap_q / 2 queries and its lo and hi share the slot's position buffers.
 static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, const uint64_t* qoff,
                          const uint32_t* qlen, const uint64_t* qwords, uint32_t m, uint64_t nq, int algo,
-                         uint64_t* out_pos, uint32_t* out_probes, hipStream_t user_st, uint32_t flags) {
+                         uint64_t* out_pos, uint32_t* out_probes, hipStream_t user_st, uint32_t flags,
+                         uint64_t* out_hi = nullptr) {
     StageLease lease;
     TRY_RC(stage_acquire(x, &lease));
     StageSet& S = *lease.set;
+    const uint64_t cap_q = out_hi ? S.cap_q / 2 : S.cap_q;
     HIP_TRY(hipStreamSynchronize(user_st));  // the caller's earlier work on its stream
     const bool validate = mode == HM_FIXED || mode == HM_RAGGED;
     std::atomic<uint32_t> host_bad{0};
@@ -2154,8 +2162,9 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
     // over the pool too) and the fill of the new chunk run together
     constexpr uint64_t OUT_PIECE = 1u << 17;  // positions per copy-out piece (1 MiB)
     auto copy_out = [&](const StageSlot& sl, uint64_t piece) {
-        const uint64_t b = piece * OUT_PIECE, e = std::min(sl.e - sl.s, b + OUT_PIECE);
+        const uint64_t k = sl.e - sl.s, b = piece * OUT_PIECE, e = std::min(k, b + OUT_PIECE);
         memcpy(out_pos + sl.s + b, sl.h_out + b, (e - b) * 8);
+        if (out_hi) memcpy(out_hi + sl.s + b, sl.h_out + k + b, (e - b) * 8);
         if (out_probes) memcpy(out_probes + sl.s + b, sl.h_pr + b, (e - b) * 4);
     };
     auto out_pieces = [&](const StageSlot& sl) -> int {
@@ -2188,7 +2197,7 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
         std::function<void(int)> fill;
         if (mode == HM_FIXED || mode == HM_WORDS) {
             const uint64_t unit = mode == HM_FIXED ? std::max(m, 1u) : 8;
-            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_bytes / unit, S.cap_q));
+            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_bytes / unit, cap_q));
             in_bytes = k * unit;
             const uint8_t* src = mode == HM_FIXED ? qbytes + s * m : reinterpret_cast<const uint8_t*>(qwords + s);
             const uint64_t piece = 1u << 20;
@@ -2201,7 +2210,7 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
         } else if (mode == HM_PACK) {
             // smaller chunks than the byte modes: the host packing is the longest stage, and
             // the pipeline fills and drains faster
-            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(S.cap_q, SAS_STAGE_PACK_Q));
+            k = std::min<uint64_t>(nq - s, std::min<uint64_t>(cap_q, SAS_STAGE_PACK_Q));
             in_bytes = k * 8;
             constexpr uint64_t per = 16384;
             pi_n = (int)((k + per - 1) / per);
@@ -2214,7 +2223,7 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
         } else {  // ragged: consecutive queries up to the byte and count caps (at least one)
             uint64_t bytes = 0, e = s;
             uint32_t maxlen = 0;
-            while (e < nq && e - s < S.cap_q && (e == s || bytes + qlen[e] <= S.cap_bytes)) {
+            while (e < nq && e - s < cap_q && (e == s || bytes + qlen[e] <= S.cap_bytes)) {
                 sl.h_off[e - s] = bytes;
                 sl.h_len[e - s] = qlen[e];
                 bytes += qlen[e];
@@ -2262,8 +2271,13 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
             hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, sl.st, a.qbytes, a.qoff, a.qlen,
                                a.m_fixed, k, a.bad);
         }
-        if ((err = launch_search(x, a, algo, qw, flags | SAS_DEVICE_PTRS, sl.st))) break;
-        HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, k * 8, hipMemcpyDeviceToHost, sl.st));
+        if (out_hi) {
+            launch_range(x, a, qw, flags, sl.st, sl.d_out + k);
+            HIP_TRY(hipGetLastError());
+        } else if ((err = launch_search(x, a, algo, qw, flags | SAS_DEVICE_PTRS, sl.st))) {
+            break;
+        }
+        HIP_TRY(hipMemcpyAsync(sl.h_out, sl.d_out, (out_hi ? 2 : 1) * k * 8, hipMemcpyDeviceToHost, sl.st));
         if (out_probes) HIP_TRY(hipMemcpyAsync(sl.h_pr, sl.d_pr, k * 4, hipMemcpyDeviceToHost, sl.st));
         if (validate) HIP_TRY(hipMemcpyAsync(sl.h_bad, sl.d_bad, 4, hipMemcpyDeviceToHost, sl.st));
         sl.busy = true;
@@ -2986,6 +3000,49 @@ static void launch_quad_range(int qw, dim3 grid, dim3 block, hipStream_t st, con
     }
 }
 
+// Occurrence-range kernel for the index's structures (a.nq queries; lo to a.out_pos, hi to dhi)
+static void launch_range(const sas_index* x, const SearchArgs& a, int qw, uint32_t flags, hipStream_t st,
+                         uint64_t* dhi) {
+    const bool quad = x->quad_leaves != nullptr;
+    // the prefix table, when built, replaces the two tree descents (one lane per query;
+    // G lanes per query on a G-slot inline table)
+    const bool ptab = quad && x->prefix && !(flags & SAS_NO_PREFIX_TABLE);
+    const bool pair = ptab && !x->quad_compact && (x->prefix_w == 32 || x->prefix_w == 64) &&
+                      !(flags & SAS_RANGE_NO_INLINE);
+    const uint64_t per = (quad && !ptab) ? QUAD_G : (pair ? x->prefix_w / 16 : 1);
+    uint64_t blocks = (a.nq * per + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
+    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
+    if (blocks > cap) blocks = cap;
+    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
+    if (x->tag_table) {
+        switch (qw) {
+            case 1: hipLaunchKernelGGL(k_sa_tagged_range<1>, grid, block, 0, st, a, dhi); break;
+            case 2: hipLaunchKernelGGL(k_sa_tagged_range<2>, grid, block, 0, st, a, dhi); break;
+            case 4: hipLaunchKernelGGL(k_sa_tagged_range<4>, grid, block, 0, st, a, dhi); break;
+            default: hipLaunchKernelGGL(k_sa_tagged_range<8>, grid, block, 0, st, a, dhi); break;
+        }
+    } else if (pair) {
+        if (x->prefix_w == 32) launch_prefix2_range<2>(qw, grid, block, st, a, dhi);
+        else launch_prefix2_range<4>(qw, grid, block, st, a, dhi);
+    } else if (ptab) {
+        if (!x->quad_compact) launch_prefix_range<false, 4>(qw, grid, block, st, a, dhi);
+        else if (x->sa_w == 5) launch_prefix_range<true, 5>(qw, grid, block, st, a, dhi);
+        else launch_prefix_range<true, 4>(qw, grid, block, st, a, dhi);
+    } else if (quad && !x->quad_compact) {
+        launch_quad_range<false, 4>(qw, grid, block, st, a, dhi);
+    } else if (quad) {
+        if (x->sa_w == 5) launch_quad_range<true, 5>(qw, grid, block, st, a, dhi);
+        else launch_quad_range<true, 4>(qw, grid, block, st, a, dhi);
+    } else {
+        switch (qw) {
+            case 1: hipLaunchKernelGGL(k_sa_sector_range<1>, grid, block, 0, st, a, dhi); break;
+            case 2: hipLaunchKernelGGL(k_sa_sector_range<2>, grid, block, 0, st, a, dhi); break;
+            case 4: hipLaunchKernelGGL(k_sa_sector_range<4>, grid, block, 0, st, a, dhi); break;
+            default: hipLaunchKernelGGL(k_sa_sector_range<8>, grid, block, 0, st, a, dhi); break;
+        }
+    }
+}
+
 // ragged (qoff, qlen) or fixed-length (qoff == nullptr: m_fixed chars per query)
 static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixed, const uint64_t* qoff,
                       const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream,
@@ -2993,7 +3050,6 @@ static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixe
     if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
     if (!x->sec_leaves && !x->quad_leaves && !x->tag_table)
         SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_QUAD, SAS_BUILD_SECTOR or SAS_BUILD_TAGGED");
-    const bool quad = x->quad_leaves != nullptr;
     const bool ragged = qoff != nullptr || qlen != nullptr;
     if (nq == 0) return 0;
     if (!qbytes || !out_lo || !out_hi || (ragged && (!qoff || !qlen)))
@@ -3001,6 +3057,15 @@ static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixe
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
     bool dev = flags & SAS_DEVICE_PTRS;
+    if (!dev) {
+        // host arrays: the pinned, chunked pipeline unless one query alone exceeds a chunk
+        uint64_t maxlen = m_fixed;
+        if (ragged)
+            for (uint64_t k = 0; k < nq; k++) maxlen = qlen[k] > maxlen ? qlen[k] : maxlen;
+        if (maxlen <= SAS_STAGE_BYTES)
+            return host_pipeline(x, ragged ? HM_RAGGED : HM_FIXED, qbytes, qoff, qlen, nullptr, m_fixed, nq, -1,
+                                 out_lo, nullptr, st, flags, out_hi);
+    }
     SearchArgs a{};
     fill_args(x, a);
     a.nq = nq;
@@ -3055,43 +3120,7 @@ static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixe
         hipLaunchKernelGGL(k_validate_queries, dim3((unsigned)vb), dim3(256), 0, st, a.qbytes, a.qoff, a.qlen,
                            a.m_fixed, nq, a.bad);
     }
-    // the prefix table, when built, replaces the two tree descents (one lane per query;
-    // G lanes per query on a G-slot inline table)
-    const bool ptab = quad && x->prefix && !(flags & SAS_NO_PREFIX_TABLE);
-    const bool pair = ptab && !x->quad_compact && (x->prefix_w == 32 || x->prefix_w == 64) &&
-                      !(flags & SAS_RANGE_NO_INLINE);
-    const uint64_t per = (quad && !ptab) ? QUAD_G : (pair ? x->prefix_w / 16 : 1);
-    uint64_t blocks = (nq * per + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
-    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
-    if (blocks > cap) blocks = cap;
-    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    if (x->tag_table) {
-        switch (qw) {
-            case 1: hipLaunchKernelGGL(k_sa_tagged_range<1>, grid, block, 0, st, a, dhi); break;
-            case 2: hipLaunchKernelGGL(k_sa_tagged_range<2>, grid, block, 0, st, a, dhi); break;
-            case 4: hipLaunchKernelGGL(k_sa_tagged_range<4>, grid, block, 0, st, a, dhi); break;
-            default: hipLaunchKernelGGL(k_sa_tagged_range<8>, grid, block, 0, st, a, dhi); break;
-        }
-    } else if (pair) {
-        if (x->prefix_w == 32) launch_prefix2_range<2>(qw, grid, block, st, a, dhi);
-        else launch_prefix2_range<4>(qw, grid, block, st, a, dhi);
-    } else if (ptab) {
-        if (!x->quad_compact) launch_prefix_range<false, 4>(qw, grid, block, st, a, dhi);
-        else if (x->sa_w == 5) launch_prefix_range<true, 5>(qw, grid, block, st, a, dhi);
-        else launch_prefix_range<true, 4>(qw, grid, block, st, a, dhi);
-    } else if (quad && !x->quad_compact) {
-        launch_quad_range<false, 4>(qw, grid, block, st, a, dhi);
-    } else if (quad) {
-        if (x->sa_w == 5) launch_quad_range<true, 5>(qw, grid, block, st, a, dhi);
-        else launch_quad_range<true, 4>(qw, grid, block, st, a, dhi);
-    } else {
-        switch (qw) {
-            case 1: hipLaunchKernelGGL(k_sa_sector_range<1>, grid, block, 0, st, a, dhi); break;
-            case 2: hipLaunchKernelGGL(k_sa_sector_range<2>, grid, block, 0, st, a, dhi); break;
-            case 4: hipLaunchKernelGGL(k_sa_sector_range<4>, grid, block, 0, st, a, dhi); break;
-            default: hipLaunchKernelGGL(k_sa_sector_range<8>, grid, block, 0, st, a, dhi); break;
-        }
-    }
+    launch_range(x, a, qw, flags, st, dhi);
     HIP_TRY(hipGetLastError());
     if (check_bad || !dev) {
         HIP_TRY(hipStreamSynchronize(st));

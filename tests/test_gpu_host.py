@@ -128,3 +128,30 @@ def test_concurrent_host_calls(env):
     assert not errs, errs
     for k in range(4):
         assert np.array_equal(got[k][1], expect[k]), k
+
+
+def test_ranges_host_pipeline(env):
+    """sas_search_range(_fixed) from host arrays runs through the staging pipeline (chunks
+    of at most half the slot's positions: lo and hi share them): fixed m = 32 over several
+    chunks and ragged lengths equal the device-pointer ranges; a code > 3 is EINVAL."""
+    sas, torch, t, idx = env
+    m, nq = 32, 1_300_000
+    qb = fixed_queries(t, nq, m, 9)
+    lo, hi = idx.search_range_fixed(qb, m)
+    dlo, dhi = idx.search_range_fixed(torch.from_numpy(qb).cuda(), m)
+    assert np.array_equal(lo, dlo.cpu().numpy().astype(np.uint64))
+    assert np.array_equal(hi, dhi.cpu().numpy().astype(np.uint64))
+    assert (hi[nq // 8:] > lo[nq // 8:]).all()  # positives occur
+    rng = np.random.default_rng(3)
+    lens = rng.integers(0, 120, 400_000).astype(np.uint32)
+    offs = rng.integers(0, len(t) - 130, len(lens)).astype(np.uint64)
+    buf = np.concatenate([t, np.zeros(64, np.uint8)])
+    lo, hi = idx.search_range(buf, offs, lens)
+    dlo, dhi = idx.search_range(torch.from_numpy(buf).cuda(), torch.from_numpy(offs.astype(np.int64)).cuda(),
+                                torch.from_numpy(lens.astype(np.int32)).cuda())
+    assert np.array_equal(lo, dlo.cpu().numpy().astype(np.uint64))
+    assert np.array_equal(hi, dhi.cpu().numpy().astype(np.uint64))
+    bad = qb.copy()
+    bad[777 * m + 5] = 9
+    with pytest.raises(sas.SasError):
+        idx.search_range_fixed(bad, m)
