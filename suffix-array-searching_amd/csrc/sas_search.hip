@@ -1637,6 +1637,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 #ifndef SAS_TAG_WIN
 #define SAS_TAG_WIN 8
 #endif
+#ifndef SAS_TAG_WINS
+#define SAS_TAG_WINS 1
+#endif
 #define TAG_M40 (SAS_SA40_MAX - 1)
 // waves per SIMD the long-query (QW >= SAS_TAG_LB_QW) instances are built for
 #ifndef SAS_TAG_LB
@@ -1704,44 +1707,53 @@ __device__ __forceinline__ void tagged_lookup(const SearchArgs& a, const Q& q, u
     // aligned entry pairs: half the load instructions of 8-B loads, and fewer L1->L2
     // requests and TLB lookups, which bound this kernel (the entries carry 16 bytes of
     // padding, so the pair holding rank sa_n - 1 is readable)
-    const uint64_t cnt = hi - lo;
-    const uint32_t nw = cnt < SAS_TAG_WIN ? (uint32_t)cnt : (uint32_t)SAS_TAG_WIN;
-    uint64_t e[SAS_TAG_WIN];
-    {
-        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-        const uint32_t o = (uint32_t)(lo & 1);
-        const u64x2* ep = reinterpret_cast<const u64x2*>(ent + (lo & ~1ull));
-        uint64_t w2[SAS_TAG_WIN + 2];
-#pragma unroll
-        for (int j = 0; j < SAS_TAG_WIN / 2 + 1; j++) {
-            const u64x2 v = (2u * j < o + nw) ? __builtin_nontemporal_load(ep + j) : u64x2{0ull, 0ull};
-            w2[2 * j] = v.x;
-            w2[2 * j + 1] = v.y;
-        }
-#pragma unroll
-        for (int j = 0; j < SAS_TAG_WIN; j++) e[j] = (uint32_t)j < nw ? (o ? w2[j + 1] : w2[j]) : 0ull;
-    }
-    // first slot whose tag is >= q's: every slot before it is < q (tags are sorted within a
-    // bucket)
-    uint32_t j0 = nw;
-#pragma unroll
-    for (int j = SAS_TAG_WIN - 1; j >= 0; j--)
-        if ((uint32_t)j < nw && (uint32_t)(e[j] >> 40) >= Q12) j0 = (uint32_t)j;
-    uint64_t ej = e[0];
-#pragma unroll
-    for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
-    uint64_t ans = 0, pos = 0, start;
+    // SAS_TAG_WINS windows of SAS_TAG_WIN entries are scanned before the bisection: a wave
+    // waits for its slowest lane, and a bucket past one window (~2% of lanes at 4 suffixes
+    // per bucket, so most waves hold one) costs one more dependent read instead of
+    // log2(count - SAS_TAG_WIN) of them
+    uint64_t ans = 0, pos = 0, start = lo;
     bool done = false;
-    if (j0 < nw) {
-        const uint64_t r = lo + j0;
-        if (tag_ge<QW>(ej, Q12, a, q)) {
-            ans = r;
-            pos = ej & TAG_M40;
-            done = true;
+#pragma unroll 1
+    for (int w = 0; w < SAS_TAG_WINS; w++) {
+        const uint64_t wb = lo + (uint64_t)w * SAS_TAG_WIN;
+        const uint64_t rest = hi - wb;
+        const uint32_t nw = rest < SAS_TAG_WIN ? (uint32_t)rest : (uint32_t)SAS_TAG_WIN;
+        uint64_t e[SAS_TAG_WIN];
+        {
+            typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+            const uint32_t o = (uint32_t)(wb & 1);
+            const u64x2* ep = reinterpret_cast<const u64x2*>(ent + (wb & ~1ull));
+            uint64_t w2[SAS_TAG_WIN + 2];
+#pragma unroll
+            for (int j = 0; j < SAS_TAG_WIN / 2 + 1; j++) {
+                const u64x2 v = (2u * j < o + nw) ? __builtin_nontemporal_load(ep + j) : u64x2{0ull, 0ull};
+                w2[2 * j] = v.x;
+                w2[2 * j + 1] = v.y;
+            }
+#pragma unroll
+            for (int j = 0; j < SAS_TAG_WIN; j++) e[j] = (uint32_t)j < nw ? (o ? w2[j + 1] : w2[j]) : 0ull;
         }
-        start = r + 1;  // a tag tie whose suffix is < q
-    } else {
-        start = lo + nw;  // the whole window is < q
+        // first slot whose tag is >= q's: every slot before it is < q (tags are sorted
+        // within a bucket)
+        uint32_t j0 = nw;
+#pragma unroll
+        for (int j = SAS_TAG_WIN - 1; j >= 0; j--)
+            if ((uint32_t)j < nw && (uint32_t)(e[j] >> 40) >= Q12) j0 = (uint32_t)j;
+        uint64_t ej = e[0];
+#pragma unroll
+        for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
+        if (j0 < nw) {
+            const uint64_t r = wb + j0;
+            if (tag_ge<QW>(ej, Q12, a, q)) {
+                ans = r;
+                pos = ej & TAG_M40;
+                done = true;
+            }
+            start = r + 1;  // a tag tie whose suffix is < q
+            break;
+        }
+        start = wb + nw;  // the whole window is < q
+        if (start >= hi) break;
     }
     if (!done) {  // binary search over the rest of the bucket (rank hi if nothing qualifies)
         uint64_t l2 = start, h2 = hi, pr = QUAD_NO_SA;
