@@ -49,7 +49,7 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 RANDOM_REQ_CEILING = 5.084e10
 CACHE_BYTES = 256 << 20  # Infinity Cache (MALL): arrays at most this large count as cache-served
 SEED = 31415  # sas/main.rs:38
-TOP_LDS_LEVELS, TOP2_LEVELS = 12, 21  # binary-search levels served from LDS / the 32 MiB top2 array
+TOP_LDS_LEVELS, TOP2_LEVELS = 12, 23  # binary-search levels served from LDS / the top2 array (index stats win)
 
 KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
@@ -107,9 +107,10 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
     elif algo in ("plain", "lcp", "inline", "llcp", "interp"):
         per = {"plain": sa_w + win, "lcp": sa_w + win, "inline": 16, "llcp": 16, "interp": 16}[algo]
         if algo in ("plain", "lcp", "inline", "llcp"):
-            lds += min(probes, TOP_LDS_LEVELS) * 12
-            cache += max(0.0, min(probes, TOP2_LEVELS) - TOP_LDS_LEVELS) * 16
-            hbm += max(0.0, probes - TOP2_LEVELS) * per
+            t1, t2 = st.get("top_levels", TOP_LDS_LEVELS), st.get("top2_levels", TOP2_LEVELS)
+            lds += min(probes, t1) * 12
+            cache += max(0.0, min(probes, t2) - t1) * 16  # the top2 array (<= 128 MiB) stays in cache
+            hbm += max(0.0, probes - t2) * per
         else:
             hbm += probes * per
     elif algo in ("stree", "quad", "sector"):
@@ -698,7 +699,7 @@ WORKLOADS = {
               "({tb:.0f} GiB), then binary search over the fused {{32-char key, SA}} quad-leaf entries "
               "of the bucket; 2^30 text in HBM, 10^7 len-32 queries",
     "plain": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112), top 12 levels from LDS, "
-             "levels 13-21 from a 32 MiB cache-resident pivot array",
+             "levels 13-23 from a 128 MiB cache-resident pivot array",
     "lcp": "configs[1] + mlr LCP skipping",
     "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (16-B {SA, Llcp, Rlcp, chars} entries)",
     "inline": "configs[1] probe sequence over fused {32-char key, SA} entries",

@@ -156,6 +156,25 @@ class SaNaive {
         return {lo, hi};
     }
 
+    /* occurrence ranges of many queries in one call (the staged host pipeline) */
+    std::vector<std::pair<uint64_t, uint64_t>> search_ranges(const std::vector<Seq>& qs, uint32_t flags = 0) const {
+        std::vector<uint8_t> bytes;
+        std::vector<uint64_t> off(qs.size()), lo(qs.size()), hi(qs.size());
+        std::vector<uint32_t> len(qs.size());
+        for (size_t i = 0; i < qs.size(); i++) {
+            off[i] = bytes.size();
+            len[i] = (uint32_t)qs[i].len;
+            bytes.insert(bytes.end(), qs[i].ptr, qs[i].ptr + qs[i].len);
+        }
+        bytes.resize(bytes.size() + 64, 0);
+        if (!qs.empty())
+            check(sas_search_range(h_, bytes.data(), off.data(), len.data(), qs.size(), lo.data(), hi.data(), nullptr,
+                                   flags));
+        std::vector<std::pair<uint64_t, uint64_t>> r(qs.size());
+        for (size_t i = 0; i < qs.size(); i++) r[i] = {lo[i], hi[i]};
+        return r;
+    }
+
     /* Search::search_prefix (sas/util.rs:36-40, unimplemented!() upstream): every text
      * position where q occurs, in SA order */
     std::vector<size_t> search_prefix(Seq q) const {

@@ -26,12 +26,13 @@
 #define SAS_TEXT_PAD_WORDS 4
 #define SAS_TOP_LEVELS 12             // 4095 pivots: 32 KiB keys + 16 KiB SA in LDS
 #define SAS_TOP_NODES (1u << SAS_TOP_LEVELS)
-// Levels 13..21 of the lockstep binary search (PLAIN, LCP, INLINE) read their pivot
-// (32-char key, SA value) from one 16-B entry of the cache-resident top2 array (32 MiB)
+// Levels 13..23 of the lockstep binary search (PLAIN, LCP, INLINE) read their pivot
+// (32-char key, SA value) from one 16-B entry of the cache-resident top2 array (128 MiB)
 // instead of an SA word and a text window.  Same-box: PLAIN 7.15 ms without it, 5.4-5.7
-// with 17 levels, 5.0-5.2 with 19, 4.70 with 21 (tools/ab_top2.sh).
+// with 17 levels, 5.0-5.2 with 19, 4.70 with 21, 4.50 with 22, 4.27 with 23 (128 MiB,
+// still inside the Infinity Cache; tools/ab_top2.sh, profiles/r2/ab_top2_depth.txt).
 #ifndef SAS_TOP2_LEVELS
-#define SAS_TOP2_LEVELS 21
+#define SAS_TOP2_LEVELS 23
 #endif
 #define SAS_TOP2_NODES (1u << SAS_TOP2_LEVELS)
 #define SAS_STREE_B 16                // keys per node / branching factor - 1
@@ -95,7 +96,7 @@ struct sas_index {
     uint64_t stree_off[SAS_STREE_MAX_LAYERS] = {};
     uint32_t stree_lds_layers = 0;
     uint32_t stree_lds_nodes = 0;
-    uint4* top2 = nullptr;        // [SAS_TOP2_NODES] Eytzinger pivots {key64 lo, hi, SA lo, hi}, index 0
+    uint4* top2 = nullptr;        // [2^top2_levels] Eytzinger pivots {key64 lo, hi, SA lo, hi}, index 0
                                   // unused; the first SAS_TOP_NODES are staged in LDS
     uint32_t top_levels = 0;      // levels served from LDS
     uint32_t top2_levels = 0;     // levels served from LDS or top2

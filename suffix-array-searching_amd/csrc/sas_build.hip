@@ -1363,15 +1363,16 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         x->iters = iters;
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
         x->top2_levels = iters < SAS_TOP2_LEVELS ? iters : SAS_TOP2_LEVELS;
+        // the pivots of the first top2_levels iterations: 2^SAS_TOP2_LEVELS entries (128 MiB at
+        // 23 levels, sized to stay inside the 256 MiB Infinity Cache) or fewer for small texts
+        const uint32_t nodes = 1u << x->top2_levels;
         DevBuf t2;
-        TRY(t2.alloc(SAS_TOP2_NODES * 16, "top2"));
-        const dim3 tg(grid_for(SAS_TOP2_NODES)), tb(256);
+        TRY(t2.alloc((uint64_t)nodes * 16, "top2"));
+        const dim3 tg(grid_for(nodes)), tb(256);
         if (W == 5)
-            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(),
-                               (uint32_t)SAS_TOP2_NODES);
+            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes);
         else
-            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(),
-                               (uint32_t)SAS_TOP2_NODES);
+            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes);
         HIP_TRY(hipGetLastError());
         x->top2 = static_cast<uint4*>(t2.release());
     }
@@ -1409,7 +1410,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.tag_chars = x->tag_p;
     st.tag_table_bytes = x->tag_table ? ((1ull << (2 * x->tag_p)) + 1) * 8 : 0;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
-                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + (uint64_t)SAS_TOP2_NODES * 16;
+                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + ((uint64_t)16 << x->top2_levels);
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -112,6 +112,12 @@ static void test_sa() {
         std::sort(occ.begin(), occ.end());
         EXPECT(occ == scan, "search_prefix %zu: %zu vs %zu occurrences", i, occ.size(), scan.size());
     }
+    {  // many ranges in one call equal the one-query calls
+        const std::vector<sas::Seq> some(qs.begin(), qs.begin() + 300);
+        const auto rs = sa.search_ranges(some);
+        for (size_t i = 0; i < some.size(); i += 7) EXPECT(rs[i] == sa.search_range(some[i]), "search_ranges %zu", i);
+        for (size_t i = 0; i < some.size(); i++) EXPECT(rs[i].second >= rs[i].first, "range order %zu", i);
+    }
     EXPECT(sa.search(qs[0]) == all[0], "Search::search");
     std::fprintf(stderr, "SA: %zu queries, cnt plain %zu (oracle %zu), interp %zu (oracle %zu), prefix %zu\n",
                  qs.size(), cnt_plain, cnt_oracle, cnt_interp, cnt_ointerp, cnt_prefix);

@@ -60,13 +60,15 @@ def test_lower_bound_proof_accepts_and_rejects():
 def test_byte_model_splits_served_levels():
     st = {"sa_width": 4, "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "quad_entry_bytes": 16,
           "stree_layers": 8, "stree_lds_layers": 2, "sector_layers": 12, "sector_lds_layers": 3, "quad_layers": 8,
-          "quad_lds_layers": 3, "quad_fan": 17, "tag_chars": 16}
+          "quad_lds_layers": 3, "quad_fan": 17, "tag_chars": 16, "top_levels": 12, "top2_levels": 21}
     n, m = 1 << 30, 32
     q = bench.bytes_per_lookup("quad", st, n, m, 8.0)
     # quad at 2^30: 3 LDS layers, the 206 KB / 3.5 MB / 59 MB layers in cache, 1 GB + leaves in HBM
     assert q["lds"] == 3 * 64 and q["cache"] == 3 * 64 and q["hbm"] == 2 * 64 + m + 8
     p = bench.bytes_per_lookup("plain", st, n, m, 31.0)
     assert p["lds"] == 12 * 12 and p["cache"] == 9 * 16 and p["hbm"] == 10 * (4 + m / 4) + m + 8
+    p23 = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
+    assert p23["cache"] == 11 * 16 and p23["hbm"] == 8 * (4 + m / 4) + m + 8
     h = bench.bytes_per_lookup("prefix", st, n, m, 1.0)
     assert h["hbm"] == 32 + m + 8 and h["cache"] == 0 and h["lds"] == 0
     assert bench._tree_layers(n, 4, 64, 17, 64, 8)[-1] == n // 4 * 64
