@@ -555,7 +555,7 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
         if own is not None:
             own.destroy_process_group()
         return {"workload": "configs[4]-shaped (sharded text)", "skipped": err or "setup failed on another rank"}
-    engine = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix")
+    engine = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", chunks=args.shard_chunks)
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
@@ -567,19 +567,35 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     el = timed_loop(lambda: engine.search_fixed(qbytes, m, check=False, out=out), args.c4_steps, args.warmup,
                     torch.cuda.synchronize, dist.barrier, reduce_max)
     engine.assert_no_overflow()
+    # the other step shape, for the next round's choice at N > 1 (where the exchanges cross
+    # xGMI): the batch in 2 pieces (or in 1 if the main run used pieces), exchanges async
+    alt_chunks = 2 if args.shard_chunks == 1 else 1
+    alt = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", chunks=alt_chunks)
+    out2 = torch.empty(nq, dtype=torch.int64, device=dev)
+    el2 = timed_loop(lambda: alt.search_fixed(qbytes, m, check=False, out=out2), max(3, args.c4_steps // 2),
+                     args.warmup, torch.cuda.synchronize, dist.barrier, reduce_max)
+    alt.assert_no_overflow()
+    same = torch.tensor([int(bool(torch.equal(out, out2)))], dtype=torch.int32, device=dev)
+    dist.all_reduce(same, op=dist.ReduceOp.MIN)
+    if not int(same.item()):
+        raise SystemExit("bench c4: the pieced step differs from the whole step")
+    del out2
     occ = text[(out[:, None] + ar[None, :]).reshape(-1).clamp_(max=n - 1)]
     ok = torch.tensor([int(bool(torch.equal(occ, qbytes)))], dtype=torch.int32, device=dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if not int(ok.item()):
         raise SystemExit("bench c4: a sharded answer is not an occurrence of its query")
-    cap = engine.capacity(nq)
+    cap = engine.capacity(-(-nq // max(1, args.shard_chunks)))  # per piece
     rec = {"workload": f"configs[4]-shaped: text of {ws} x {args.c4_share} chars sharded by SA rank ranges over "
                        f"{ws} GPU(s) (sas_build_part), {nq} len-{m} queries per GPU routed with RCCL "
                        f"all_to_all_single (fixed-capacity buckets, 8-B packed PREFIX queries), positions back",
            "n": n, "parts": ws, "lookups_per_s": ws * nq * args.c4_steps / el, "ms_per_step": el / args.c4_steps * 1e3,
            "steps": args.c4_steps, "scaling": "weak", "part_sa_entries": st["sa_entries"],
            "prefix_entry_bytes": st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1),
-           "bucket_capacity": cap, "exchange_bytes_per_step_per_rank": 2 * ws * cap * 8,
+           "bucket_capacity": cap, "pieces": args.shard_chunks,
+           "alt_pieces": {"pieces": alt_chunks, "ms_per_step": el2 / max(3, args.c4_steps // 2) * 1e3,
+                          "lookups_per_s": ws * nq * max(3, args.c4_steps // 2) / el2, "identical": True},
+           "exchange_bytes_per_step_per_rank": 2 * ws * cap * 8 * args.shard_chunks,
            "index_bytes": st["index_bytes"], "setup_s": setup, "verified": True}
     idx.free()
     del text, qbytes, out, occ
@@ -740,6 +756,8 @@ def main():
     ap.add_argument("--proof-sample", type=int, default=3000, help="queries per batch proven exact lower bounds")
     ap.add_argument("--no-c4", action="store_true", help="skip the configs[4] (sharded text) sub-record")
     ap.add_argument("--c4-share", type=int, default=1 << 30, help="configs[4]: text chars per GPU")
+    ap.add_argument("--shard-chunks", type=int, default=1,
+                    help="sharded step in this many pieces, exchanges overlapped with the other pieces' work")
     ap.add_argument("--c4-steps", type=int, default=10)
     ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric) + every config's sub-record; "
@@ -786,7 +804,7 @@ def main():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29517")
             dist.init_process_group("nccl", rank=0, world_size=1)
-        engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo)
+        engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo, chunks=args.shard_chunks)
     else:
         idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, prefix=args.prefix_chars,
                                     prefix_inline={"ranks": 0, "inline": 1, "inline2": 2,

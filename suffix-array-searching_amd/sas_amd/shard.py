@@ -39,8 +39,12 @@ class ShardedSearch:
     SLACK = 1.125  # bucket capacity over the balanced share
 
     def __init__(self, index, dist, world: int, rank: int, device, algo: str = "stree", group=None,
-                 slack: float | None = None, min_cap: int = 256):
+                 slack: float | None = None, min_cap: int = 256, chunks: int = 1):
+        """chunks > 1: a step cuts its batch into that many pieces and overlaps one piece's
+        exchanges (all_to_all_single with async_op, on the collective's own stream) with
+        another's routing, lookup and gather.  Every rank must use the same value."""
         import torch
+        self.chunks = max(1, int(chunks))
         self.index, self.dist, self.world, self.rank = index, dist, world, rank
         self.device, self.algo, self.group = device, algo, group
         self.slack = self.SLACK if slack is None else slack
@@ -76,9 +80,9 @@ class ShardedSearch:
         lookup takes them: PREFIX, m <= 32 (4x less all-to-all traffic at m = 32)."""
         return self.algo == "prefix" and m <= 32 and hasattr(self.index, "search_packed")
 
-    def _buffers(self, nq: int, m: int, cap: int):
+    def _buffers(self, nq: int, m: int, cap: int, piece: int = 0):
         import torch
-        key = (nq, m)
+        key = (nq, m, piece)
         if key not in self._bufs:
             W = self.world
             if self.packed(m):
@@ -97,6 +101,8 @@ class ShardedSearch:
         into `out` when given)."""
         if not hasattr(self.index, "route_pack"):
             return self.search_fixed_exact(qbytes, m)
+        if self.chunks > 1 and hasattr(self.index, "shard_gather"):
+            return self._search_pipelined(qbytes, m, check, out)
         import torch
         nq = qbytes.numel() // m
         cap = self.capacity(nq)
@@ -125,6 +131,46 @@ class ShardedSearch:
             if int(flag.item()):
                 exact = self.search_fixed_exact(qbytes, m)
                 return out.copy_(exact) if out is not None else exact
+        return out
+
+    def _search_pipelined(self, qbytes, m: int, check: bool, out):
+        """The step in `self.chunks` pieces of at most cs queries, one capacity for all:
+        send sides and forward exchanges first (each exchange queued on the collective's
+        stream as soon as its piece is packed), then per piece wait -> lookup -> backward
+        exchange, then per piece wait -> gather into its slice of `out`."""
+        import torch
+        nq = qbytes.numel() // m
+        C = self.chunks
+        cs = -(-nq // C)
+        cap = self.capacity(cs)
+        pk = self.packed(m)
+        if out is None:
+            out = torch.empty(nq, dtype=torch.int64, device=self.device)
+        flag = torch.zeros(1, dtype=torch.int32, device=self.device) if check else self.overflow
+        pieces = []
+        for c in range(C):
+            s0, s1 = min(nq, c * cs), min(nq, (c + 1) * cs)
+            buf = self._buffers(cs, m, cap, c)
+            counts, send, slot = self.index.route_pack(self.splitters, qbytes[s0 * m:s1 * m], m, cap=cap,
+                                                       send=buf["send"], **({"packed": True} if pk else {}))
+            w = self.dist.all_to_all_single(buf["recv"], send, group=self.group, async_op=True)
+            pieces.append((s0, s1, buf, counts, slot, w))
+        back = []
+        for s0, s1, buf, counts, slot, w in pieces:
+            w.wait()
+            if pk:
+                self.index.search_packed(buf["recv"], m, algo="prefix", out=buf["local"])
+            else:
+                self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
+            back.append(self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group, async_op=True))
+        for (s0, s1, buf, counts, slot, _), w in zip(pieces, back):
+            w.wait()
+            if s1 > s0:
+                self.index.shard_gather(buf["back"], slot, out=out[s0:s1], counts=counts, cap=cap, overflow=flag)
+        if check:
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
+            if int(flag.item()):
+                return out.copy_(self.search_fixed_exact(qbytes, m))
         return out
 
     def assert_no_overflow(self):

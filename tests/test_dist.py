@@ -118,6 +118,18 @@ class OracleShard:
         send.view(-1, m)[slot[ok]] = qbytes.view(nq, m)[ok]
         return counts, send[: W * cap * m], slot
 
+    def shard_gather(self, back, slot, out=None, counts=None, cap=0, overflow=None):
+        """sas_shard_gather semantics: out[k] = back[slot[k]]; overflow raised (never
+        cleared) when a bucket's count passed cap."""
+        import torch
+        res = back[slot]
+        if overflow is not None and bool((counts > cap).any()):
+            overflow.fill_(1)
+        if out is None:
+            return res
+        out.copy_(res)
+        return out
+
     def search_fixed(self, qbytes, m, algo=None, out=None):
         import torch
         res = self._search(qbytes, m)
@@ -164,6 +176,13 @@ def shard_worker(rank, ws, port, res):
     eng.assert_no_overflow()
     exact = eng.search_fixed_exact(dq, m)  # variable-size exchanges
     assert pos.tolist() == pos2.tolist() == exact.tolist()
+    # the pipelined step: three pieces, async exchanges overlapped with the other pieces' work
+    pipe = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", chunks=3)
+    assert pipe.search_fixed(dq, m).tolist() == exact.tolist()
+    out = torch.full((nq,), -1, dtype=torch.int64)
+    pipe.search_fixed(dq, m, check=False, out=out)
+    pipe.assert_no_overflow()
+    assert out.tolist() == exact.tolist()
     # skewed batch (every query the same) into tiny buckets: the checked step overflows and
     # redoes itself exactly; the deferred one reports the overflow
     tight = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", slack=0.5, min_cap=0)
@@ -173,6 +192,11 @@ def shard_worker(rank, ws, port, res):
     tight.search_fixed(skew, m, check=False)
     with pytest.raises(RuntimeError):
         tight.assert_no_overflow()
+    tight3 = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", slack=0.5, min_cap=0, chunks=3)
+    assert tight3.search_fixed(skew, m).tolist() == got.tolist()  # overflow redone exactly
+    tight3.search_fixed(skew, m, check=False)
+    with pytest.raises(RuntimeError):
+        tight3.assert_no_overflow()
     res[rank] = (qs.tolist(), pos.tolist())
     dist.destroy_process_group()
 

@@ -54,8 +54,9 @@ def test_sharded_nccl_world1(sas):
         qb = queries(t, nq, m, 1)
         expect = full.search_fixed(qb, m, algo="plain")
         dq = torch.from_numpy(qb).cuda()
-        for algo in ("plain", "quad", "prefix"):  # prefix: 8-B packed words cross the exchange
-            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo)
+        for algo, chunks in (("plain", 1), ("quad", 1), ("prefix", 1), ("prefix", 3), ("plain", 2)):
+            # prefix: 8-B packed words cross the exchange; chunks > 1: async RCCL pieces
+            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo, chunks=chunks)
             assert eng.packed(m) == (algo == "prefix")
             got = eng.search_fixed(dq, m)
             got2 = eng.search_fixed(dq, m, check=False)
@@ -108,7 +109,7 @@ class Loopback:
                 lb.bar.wait()
 
             @staticmethod
-            def all_to_all_single(out, inp, out_splits=None, in_splits=None, group=None):
+            def all_to_all_single(out, inp, out_splits=None, in_splits=None, group=None, async_op=False):
                 items = lb._swap(r, (inp, in_splits))
                 pos = 0
                 for src in range(lb.W):
@@ -121,6 +122,13 @@ class Loopback:
                     out[pos:pos + sz].copy_(sin[start:start + sz])
                     pos += sz
                 lb.bar.wait()  # no rank reuses its send buffer before every copy is queued
+                if async_op:  # done already (copies on this rank's stream): a no-op handle
+
+                    class Done:
+                        @staticmethod
+                        def wait():
+                            return True
+                    return Done()
         return R
 
 
@@ -153,6 +161,8 @@ def test_sharded_parts_loopback(sas, W):
             c = eng.search_fixed_exact(dq, m)
             pre = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="prefix")  # packed exchange
             e = pre.search_fixed(dq, m)
+            pipe = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="prefix", chunks=3)  # pieces
+            e3 = pipe.search_fixed(dq, m)
             tight = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="quad", slack=0.5, min_cap=0)
             skew = torch.from_numpy(np.tile(qbs[r][:m], nq // 10).copy()).cuda()
             sk = tight.search_fixed(skew, m)
@@ -163,7 +173,8 @@ def test_sharded_parts_loopback(sas, W):
             except RuntimeError:
                 raised = True
             torch.cuda.synchronize()
-            res[r] = (a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), sk.cpu().numpy(), raised, e.cpu().numpy())
+            res[r] = (a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy(), sk.cpu().numpy(), raised, e.cpu().numpy(),
+                      e3.cpu().numpy())
         except Exception as e:  # surfaced below
             errs.append((r, repr(e)))
             lb.bar.abort()
@@ -175,8 +186,8 @@ def test_sharded_parts_loopback(sas, W):
         x.join(timeout=120)
     assert not errs, errs
     for r in range(W):
-        a, b, c, sk, raised, e = res[r]
-        for g in (a, b, c, e):
+        a, b, c, sk, raised, e, e3 = res[r]
+        for g in (a, b, c, e, e3):
             assert np.array_equal(g.astype(np.uint64), expect[r]), r
         skew_expect = full.search_fixed(np.tile(qbs[r][:m], nq // 10), m, algo="plain")
         assert np.array_equal(sk.astype(np.uint64), skew_expect), r
