@@ -1634,6 +1634,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 // single candidate whose tag ties q's (a positive query's own suffix; read as 16-B word
 // pairs, suffix_less_from_x2), and its position straight from the entry.  Larger buckets
 // continue with a binary search over the rest.
+#ifndef SAS_LLCP_TOP2_LEVELS
+#define SAS_LLCP_TOP2_LEVELS 21
+#endif
 #ifndef SAS_TAG_WIN
 #define SAS_TAG_WIN 8
 #endif
@@ -2010,6 +2013,11 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
+    // LLCP reads one 16-B entry per probe either way, and its own entries carry the interval
+    // lcps that spare text reads: pivot-array levels past SAS_LLCP_TOP2_LEVELS cost it time
+    // (3.08 ms with 21 levels, 3.29 ms with 23; PLAIN and LCP gain from 23, two requests per
+    // probe there)
+    if (algo == SAS_ALGO_LLCP && a.top2_levels > SAS_LLCP_TOP2_LEVELS) a.top2_levels = SAS_LLCP_TOP2_LEVELS;
     const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
