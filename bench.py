@@ -535,7 +535,7 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     err = None
     try:
         text = sas_amd.random_string(n, seed=SEED + 1, device=dev)
-        inline = 2 if n < (1 << 32) else 0  # inline entries need ranks and positions below 2^32
+        inline = 2  # two-suffix inline table (local ranks < 2^32; SA bits 32..39 in slot 1 above 2^32 chars)
         idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=False, stree=False, sector=False, quad=True,
                                          llcp=False, prefix=16, prefix_inline=inline)
         st = idx.stats()

@@ -89,6 +89,8 @@ struct sas_index {
     uint8_t* prefix = nullptr;    // SAS_BUILD_PREFIX: [4^prefix_chars + 1] first rank per p-char key,
     uint32_t prefix_chars = 0;    // prefix_w bytes per entry (4: u32; 5: packed 40-bit, for a 40-bit SA)
     uint32_t prefix_w = 4;
+    bool prefix_hi40 = false;     // inline slots of a text >= 2^32 chars: bits 32..39 of each slot's SA
+                                  // value in slot 1's rank word (only slot 0's rank is read)
     uint4* llcp = nullptr;        // SAS_BUILD_LLCP: {SA[m], Llcp, Rlcp, 2 x 16 chars} per rank m (sas_build.hip)
     uint32_t* stree = nullptr;   // all nodes, 16 u32 each
     uint64_t stree_nodes = 0;

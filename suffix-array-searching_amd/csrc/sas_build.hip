@@ -874,6 +874,13 @@ __device__ __forceinline__ void pt_fill_range(uint8_t* t, uint64_t lo, uint64_t 
         uint4 ev[G];
 #pragma unroll
         for (int j = 0; j < G; j++) ev[j] = pt_inline_entry(leaves, sa_n, r + j);
+        if (G >= 2) {  // bits 32..39 of every slot's SA value, in slot 1's (unread) rank word
+            uint32_t hb = 0;
+#pragma unroll
+            for (int j = 0; j < G; j++)
+                if (r + j < sa_n) hb |= (leaves[r + j].w & 0xFFu) << (8 * j);
+            ev[G >= 2 ? 1 : 0].z = hb;
+        }
         for (uint64_t x = lo; x <= hi; x += step) {
 #pragma unroll
             for (int j = 0; j < G; j++) reinterpret_cast<uint4*>(t)[G * x + j] = ev[j];
@@ -915,11 +922,12 @@ __global__ void k_pt_big(const uint64_t* __restrict__ big, const unsigned long l
 static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     const uint64_t sa_n = x->sa_n;
     if (!x->quad_leaves) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX needs SAS_BUILD_QUAD (keys and SA values of the leaves)");
-    // inline entries hold a u32 rank and the low 32 bits of the SA value: fused leaves, and
-    // ranks and positions below 2^32 (a 40-bit SA qualifies when n < 2^32, e.g. a part index)
-    if (inl && (x->quad_compact || x->n > 0xFFFFFFFFull || sa_n >= 0xFFFFFFFFull))
-        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 / _INLINE4 need fused quad leaves, n < 2^32 and "
-                          "fewer than 2^32 - 1 SA entries");
+    // inline entries hold a u32 rank and the low 32 bits of each slot's SA value: fused
+    // leaves and ranks below 2^32; the one-suffix table also needs positions below 2^32, the
+    // two/four-suffix ones carry bits 32..39 in slot 1 (a part index of a 2^33-char text)
+    if (inl && (x->quad_compact || sa_n >= 0xFFFFFFFFull || (inl == 1 && x->n > 0xFFFFFFFFull)))
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 / _INLINE4 need fused quad leaves and fewer than "
+                          "2^32 - 1 SA entries (SAS_BUILD_PREFIX_INLINE also n < 2^32)");
     // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA, 16-B inline ones
     const uint32_t tw = inl ? 16 * inl : (x->sa_w == 5 ? 5 : 4);
     if (tw != 5 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
@@ -967,6 +975,7 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     t.release();
     x->prefix_chars = p;
     x->prefix_w = tw;
+    x->prefix_hi40 = inl >= 2 && x->n > 0xFFFFFFFFull;
     return 0;
 }
 

@@ -51,6 +51,7 @@ struct SearchArgs {
     const uint8_t* prefix;   // SAS_BUILD_PREFIX table (k_sa_prefix): u32 or packed 40-bit entries
     uint32_t prefix_chars;
     uint32_t prefix_w;       // bytes per table entry (4 or 5)
+    uint32_t prefix_hi40;    // inline slots: SA bits 32..39 in slot 1's rank word
     const uint4* top2;
     uint32_t top_levels;
     uint32_t top2_levels;
@@ -1308,7 +1309,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
 // r .. r + G - 1) of the range of q's p-char key.  A G-lane group reads the entry as one
 // request (16 B per lane), each lane tests one suffix, and the group ballot takes the
 // first that is >= q; only if all are < q does the search go on in [r + G, table[K+1]).
-template <int QW, int G>
+// HI40 (a part index of a text >= 2^32 chars): slot 1's rank word holds bits 32..39 of
+// every slot's SA value, one byte per slot.
+template <int QW, int G, bool HI40 = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     uint32_t bad = 0;
     const uint32_t sh = 64 - 2 * a.prefix_chars;
@@ -1361,15 +1364,17 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
         const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + G * K + sub) : pt[G * K + sub];
         const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
         const uint64_t rank = r0 + sub;
+        const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
+        const uint64_t pe = HI40 ? ((uint64_t)e.w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32)) : (uint64_t)e.w;
         // rank sa_n stands for "past every suffix": it is the answer if reached
-        const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), e.w, K64, a, q);
+        const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), pe, K64, a, q);
         const uint32_t grp = (uint32_t)(__ballot(ok) >> lane0) & ((1u << G) - 1u);
         const uint32_t j = grp ? (uint32_t)__builtin_ctz(grp) : 0u;
         const uint32_t pw = (uint32_t)__shfl((int)e.w, lane0 + (int)j, 64);
         uint64_t ans, pos;
         if (grp) {
             ans = r0 + j;
-            pos = ans >= sa_n ? a.next_pos : pw;
+            pos = ans >= sa_n ? a.next_pos : (HI40 ? ((uint64_t)pw | ((uint64_t)((hb >> (8 * j)) & 0xFFu) << 32)) : pw);
         } else {
             uint64_t lo = r0 + G, hi = pt[G * (K + 1)].z, pr = QUAD_NO_SA;
             while (lo < hi) {
@@ -1468,7 +1473,7 @@ static void launch_prefix_range(int qw, dim3 grid, dim3 block, hipStream_t st, c
 // in [r + G, table[K + 1]) (hi, for m < p: in the range of the 3-padded key), both in
 // lock step as k_sa_prefix_range does; every lane of the group runs the same loop (same
 // addresses: one request per probe).
-template <int QW, int G>
+template <int QW, int G, bool HI40 = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2_range(SearchArgs a, uint64_t* out_hi) {
     uint32_t bad = 0;
     const uint32_t sh = 64 - 2 * a.prefix_chars;
@@ -1490,11 +1495,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2_range(SearchArgs
         const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
         const uint64_t rank = r0 + sub;
         const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
+        const uint64_t pe = HI40 ? ((uint64_t)e.w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32)) : (uint64_t)e.w;
         // rank sa_n stands for "past every suffix": both bounds are reached there
         const bool past = rank >= sa_n;
-        const bool ge = past || sector_ge<QW>(key, e.w, K64, a, q);
+        const bool ge = past || sector_ge<QW>(key, pe, K64, a, q);
         const bool whole = m >= a.prefix_chars;  // hi inside the key's range too
-        const bool gt = past || (whole && sector_gt_prefix<QW>(key, e.w, K64, Q3, a, q));
+        const bool gt = past || (whole && sector_gt_prefix<QW>(key, pe, K64, Q3, a, q));
         const uint32_t mask = (1u << G) - 1u;
         const uint32_t gge = (uint32_t)(__ballot(ge) >> lane0) & mask;
         const uint32_t ggt = (uint32_t)(__ballot(gt) >> lane0) & mask;
@@ -1540,14 +1547,21 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2_range(SearchArgs
     if (bad) atomicOr(a.bad, 1u);
 }
 
+template <int G, bool HI40>
+static void launch_prefix2_range_h(int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a,
+                                   uint64_t* dhi) {
+    switch (qw) {
+        case 1: hipLaunchKernelGGL((k_sa_prefix2_range<1, G, HI40>), grid, block, 0, st, a, dhi); break;
+        case 2: hipLaunchKernelGGL((k_sa_prefix2_range<2, G, HI40>), grid, block, 0, st, a, dhi); break;
+        case 4: hipLaunchKernelGGL((k_sa_prefix2_range<4, G, HI40>), grid, block, 0, st, a, dhi); break;
+        default: hipLaunchKernelGGL((k_sa_prefix2_range<8, G, HI40>), grid, block, 0, st, a, dhi); break;
+    }
+}
+
 template <int G>
 static void launch_prefix2_range(int qw, dim3 grid, dim3 block, hipStream_t st, const SearchArgs& a, uint64_t* dhi) {
-    switch (qw) {
-        case 1: hipLaunchKernelGGL((k_sa_prefix2_range<1, G>), grid, block, 0, st, a, dhi); break;
-        case 2: hipLaunchKernelGGL((k_sa_prefix2_range<2, G>), grid, block, 0, st, a, dhi); break;
-        case 4: hipLaunchKernelGGL((k_sa_prefix2_range<4, G>), grid, block, 0, st, a, dhi); break;
-        default: hipLaunchKernelGGL((k_sa_prefix2_range<8, G>), grid, block, 0, st, a, dhi); break;
-    }
+    if (a.prefix_hi40) launch_prefix2_range_h<G, true>(qw, grid, block, st, a, dhi);
+    else launch_prefix2_range_h<G, false>(qw, grid, block, st, a, dhi);
 }
 
 // ------------------------------------------------------------------ INTERP
@@ -1960,6 +1974,8 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_PREFIX5(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 5>)
 #define K_PREFIX2(Q) (k_sa_prefix2<Q, 2>)
 #define K_PREFIX4(Q) (k_sa_prefix2<Q, 4>)
+#define K_PREFIX2H(Q) (k_sa_prefix2<Q, 2, true>)
+#define K_PREFIX4H(Q) (k_sa_prefix2<Q, 4, true>)
 #define K_PREFIX16(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 16>)
     if (algo == SAS_ALGO_QUAD) {
         // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
@@ -1968,6 +1984,8 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
     } else if (algo == SAS_ALGO_PREFIX) {
         if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) }
         else if (a.prefix_w == 16 && !KO) { QW_CASE(K_PREFIX16) }
+        else if (a.prefix_w == 32 && !KO && a.prefix_hi40) { QW_CASE(K_PREFIX2H) }
+        else if (a.prefix_w == 64 && !KO && a.prefix_hi40) { QW_CASE(K_PREFIX4H) }
         else if (a.prefix_w == 32 && !KO) { QW_CASE(K_PREFIX2) }
         else if (a.prefix_w == 64 && !KO) { QW_CASE(K_PREFIX4) }
         else { QW_CASE(K_PREFIX) }
@@ -2072,6 +2090,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.prefix = x->prefix;
     a.prefix_chars = x->prefix_chars;
     a.prefix_w = x->prefix_w;
+    a.prefix_hi40 = x->prefix_hi40;
     a.top2 = x->top2;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;

@@ -293,3 +293,35 @@ def test_route_pack_cap_one_pass_and_gather(sas):
         idxs[0].shard_gather(torch.zeros(W * small, dtype=torch.int64, device="cuda"), slot, counts=counts, cap=small,
                              overflow=flag)
         assert int(flag.item()) == 1, (m, packed)
+
+
+def test_inline_slots_above_2e32(sas):
+    """A part index of a 1.5 x 2^32-char text (local ranks < 2^32, positions up to 33 bits)
+    carries the two- and four-suffix inline tables with bits 32..39 of each slot's SA value
+    in slot 1: PREFIX (bytes and packed words) equals PLAIN on the same part, and the
+    inline-slot ranges equal the bisection's; part of the answers lie past 2^32."""
+    import torch
+    from sas_amd import _lib
+    n, m, W, g = 3 << 31, 32, 4, 3
+    t = sas.random_string(n, seed=41, device="cuda")
+    rng = np.random.default_rng(6)
+    nq = 400_000
+    off = torch.from_numpy(rng.integers(0, n - m, nq)).cuda()
+    ar = torch.arange(m, device="cuda")
+    q = t[(off[:, None] + ar[None, :]).reshape(-1)].contiguous()
+    q[: 20_000 * m] = torch.from_numpy(rng.integers(0, 4, 20_000 * m, dtype=np.uint8)).cuda()  # misses
+    for inl in (2, 4):
+        part = sas.SaNaive.build_part(t, g, W, lcp=False, stree=False, sector=False, llcp=False, prefix=15,
+                                      prefix_inline=inl)
+        plain = part.search_fixed(q, m, algo="plain")
+        pre = part.search_fixed(q, m, algo="prefix")
+        pk = part.search_packed(sas.SaNaive.pack_queries(q, m), m)
+        torch.cuda.synchronize()
+        assert torch.equal(plain, pre) and torch.equal(plain, pk), inl
+        # a quarter of the lower bounds lie in this part, a third of those past 2^32
+        assert int((plain >= (1 << 32)).sum().item()) > nq // 20
+        lo, hi = part.search_range_fixed(q, m)
+        lo2, hi2 = part.search_range_fixed(q, m, flags=_lib.SAS_RANGE_NO_INLINE)
+        torch.cuda.synchronize()
+        assert torch.equal(lo, lo2) and torch.equal(hi, hi2), inl
+        part.free()

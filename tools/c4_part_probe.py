@@ -1,7 +1,7 @@
 """Rehearse one rank of the driver's 8-GPU configs[4] record on one GPU: the 2^33-char
 text (8 x the per-GPU share), this rank's part (sas_build_part, the bench's flags), setup
 time, index bytes, and the local PREFIX lookup of 10^7 packed len-32 queries (the part's
-share of a step).  usage: c4_part_probe.py [parts] [part]   (GPU box)"""
+share of a step).  usage: c4_part_probe.py [parts] [part] [inline]   (GPU box)"""
 import json
 import sys
 import time
@@ -19,7 +19,7 @@ t0 = time.perf_counter()
 text = sas_amd.random_string(n, seed=31416, device="cuda")
 torch.cuda.synchronize()
 t1 = time.perf_counter()
-inline = 2 if n < (1 << 32) else 0
+inline = int(sys.argv[3]) if len(sys.argv) > 3 else 2  # 0: the 40-bit rank table
 idx = sas_amd.SaNaive.build_part(text, g, W, lcp=False, stree=False, sector=False, quad=True, llcp=False, prefix=16,
                                  prefix_inline=inline)
 torch.cuda.synchronize()
