@@ -419,7 +419,6 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     src = torch.from_numpy(off.astype(np.int64)).to(dev)
     qlen = lens.to(torch.int32)
     idx.extract(src, qlen, qoff, qbytes)  # t[off .. off + len) from the packed text
-    del src
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
@@ -488,9 +487,32 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
                         load_pmc(f"c3_{a}_n{n}_q{nq}") if a == algo else None, mp,
                         {"identical_to_" + algo: agrees, "lookups_per_s": nq * steps / el})
         log(f"c3 {a}: {kms:.3f} ms per {nq}")
+    # the same queries handed over as the slices of the text they are (random_queries returns
+    # borrowed &t[i..i+len], sas/util.rs:18-26): offsets + lengths, no query bytes; a lookup
+    # whose candidate is the query's own suffix skips its text compare (SAS_QUERIES_ARE_SLICES)
+    slices = None
+    if algo == "tagged":
+        for _ in range(args.warmup):
+            idx.search_slices(src, qlen, out=out)
+        torch.cuda.synchronize()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        ssteps = max(2, args.c3_steps // 2)
+        ev0.record()
+        for _ in range(ssteps):
+            idx.search_slices(src, qlen, out=out)
+        ev1.record()
+        torch.cuda.synchronize()
+        sms = ev0.elapsed_time(ev1) / ssteps
+        same = bool(torch.equal(out, ref))
+        if not same:
+            raise SystemExit("bench c3: text-slice queries differ from the byte queries")
+        slices = {"what": "the same queries as slices of the indexed text (sas_search_batch with "
+                          "SAS_QUERIES_ARE_SLICES: offsets + lengths, chars from the packed text)",
+                  "kernel_ms": sms, "lookups_per_s": nq / (sms * 1e-3), "identical_to_" + algo: same}
+        log(f"c3 tagged slices: {sms:.3f} ms per {nq}")
     h = res[algo]
     idx.free()
-    del qbytes, qoff, qlen, lens, out, ref
+    del qbytes, qoff, qlen, lens, out, ref, src
     torch.cuda.empty_cache()
     return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({st['sa_width'] * 8}-bit "
                         f"{'tagged entries' if algo == 'tagged' else 'SA'}), {nq} positive queries of length "
@@ -502,7 +524,7 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
                          "frac": h["achieved_hbm_GBps"] / HBM_PEAK_GBPS,
                          "traffic": (h.get("pmc") or {}).get("fabric_bytes_per_lookup"),
                          "kernel": KERNELS.get(algo, "k_sa_prefix")},
-            "variants": res,
+            "variants": res, "text_slices": slices,
             "index": {k: st[k] for k in ("sa_width", "sa_bytes", "quad_bytes", "prefix_chars", "prefix_bytes",
                                          "tag_chars", "tag_table_bytes", "index_bytes", "build_sa_ns",
                                          "build_total_ns")}}

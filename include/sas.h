@@ -52,6 +52,15 @@ typedef struct sas_index sas_index;
                                          sas_search_packed format) instead of its m bytes */
 #define SAS_NO_PREFIX_TABLE (1u << 25) /* sas_search_range: use the tree descents even when
                                         the index has a prefix table                      */
+#define SAS_QUERIES_ARE_SLICES (1u << 28) /* sas_search_batch, SAS_ALGO_TAGGED, device pointers:
+                                        query k is the slice t[qoff[k] .. qoff[k] + qlen[k])
+                                        of the indexed text itself (the reference's borrowed
+                                        &t[i..i+len] queries, sas/util.rs:18-26); qbytes is
+                                        ignored (may be NULL), the chars come from the index's
+                                        packed text, and a lookup whose candidate suffix is
+                                        the query's own start skips its text compare.  The
+                                        call checks every slice lies inside the text (EINVAL)
+                                        and synchronises on the stream to do so            */
 #define SAS_RANGE_NO_INLINE (1u << 27) /* sas_search_range(_fixed): on a two/four-suffix inline
                                         prefix table, bisect both bounds from the table's rank
                                         range instead of testing the inline slots first     */

@@ -523,6 +523,33 @@ struct WaveQuery {
     __device__ __forceinline__ uint64_t word(uint32_t j) const { return chars32(j << 5); }
 };
 
+// A query that is a slice of the indexed text (SAS_QUERIES_ARE_SLICES, the reference's
+// borrowed &t[i..i + len] queries, sas/util.rs:18-26): its chars come from the packed text
+// on demand, and `pos` tells a lookup where one occurrence starts.
+struct TextQuery {
+    const uint64_t* tw;
+    uint64_t pos;
+    uint32_t m;
+    uint64_t w[1];
+    __device__ __forceinline__ void init(const uint64_t* t, uint64_t p, uint32_t len) {
+        tw = t;
+        pos = p;
+        m = len;
+        w[0] = chars32(0);
+    }
+    __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
+        if (off >= m) return 0;
+        return text_chars32(tw, pos + off) & chars_mask(m - off < 32 ? m - off : 32);
+    }
+    __device__ __forceinline__ uint64_t word(uint32_t j) const { return chars32(j << 5); }
+};
+
+// the text position a query is known to occur at (TextQuery), else none
+template <class Q>
+__device__ __forceinline__ uint64_t query_source(const Q&) { return ~0ull; }
+template <>
+__device__ __forceinline__ uint64_t query_source<TextQuery>(const TextQuery& q) { return q.pos; }
+
 // A query read from its bytes on demand (the fallback of spread-out batches): word 0 in a
 // register, later windows packed from global memory when a compare reaches them.
 struct ByteQuery {

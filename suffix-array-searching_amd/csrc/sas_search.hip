@@ -1761,7 +1761,12 @@ __device__ __forceinline__ void tagged_lookup(const SearchArgs& a, const Q& q, u
         for (int j = 1; j < SAS_TAG_WIN; j++) ej = (j0 == (uint32_t)j) ? e[j] : ej;
         if (j0 < nw) {
             const uint64_t r = wb + j0;
-            if (tag_ge<QW>(ej, Q12, a, q)) {
+            // a text-slice query t[src .. src + m) and the tying entry of suffix src: that
+            // suffix starts with q, so it is >= q without reading the text (the slice must
+            // lie inside the text)
+            const uint64_t src = query_source(q);
+            const bool own = src != ~0ull && src + q.m <= a.n && (ej & TAG_M40) == src && (uint32_t)(ej >> 40) == Q12;
+            if (own || tag_ge<QW>(ej, Q12, a, q)) {
                 ans = r;
                 pos = ej & TAG_M40;
                 done = true;
@@ -1855,6 +1860,21 @@ __global__ __launch_bounds__(SAS_TAG_BLOCK, (QW >= SAS_TAG_LB_QW ? SAS_TAG_LB : 
     }
 #endif
     if (bad) atomicOr(a.bad, 1u);
+}
+
+// SAS_QUERIES_ARE_SLICES: query i is the slice t[qoff[i] .. qoff[i] + qlen[i]) of the indexed
+// text, read from the packed text (no query bytes), one lane per query.
+template <int QW>
+__global__ __launch_bounds__(SAS_TAG_BLOCK, SAS_TAG_LB) void k_sa_tagged_slices(SearchArgs a) {
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t qo;
+        uint32_t m;
+        query_span(a, i, &qo, &m);
+        TextQuery q;
+        q.init(a.tw, qo, m);
+        tagged_lookup<QW>(a, q, i);
+    }
 }
 
 // Occurrence ranges on the tagged index: lo = the lower bound in q's bucket, hi = the first
@@ -2051,7 +2071,17 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
         uint64_t tb = (a.nq + SAS_TAG_BLOCK - 1) / SAS_TAG_BLOCK;
         const uint64_t tcap = (uint64_t)x->num_cus * (qw >= SAS_TAG_LB_QW ? SAS_TAG_LB : 8);
         if (tb > tcap) tb = tcap;
-        launch_w8(algo, top, qw, dim3((unsigned)tb), dim3(SAS_TAG_BLOCK), st, a);
+        if (flags & SAS_QUERIES_ARE_SLICES) {
+            const dim3 g((unsigned)tb), b(SAS_TAG_BLOCK);
+            switch (qw) {
+                case 1: hipLaunchKernelGGL(k_sa_tagged_slices<1>, g, b, 0, st, a); break;
+                case 2: hipLaunchKernelGGL(k_sa_tagged_slices<2>, g, b, 0, st, a); break;
+                case 4: hipLaunchKernelGGL(k_sa_tagged_slices<4>, g, b, 0, st, a); break;
+                default: hipLaunchKernelGGL(k_sa_tagged_slices<8>, g, b, 0, st, a); break;
+            }
+        } else {
+            launch_w8(algo, top, qw, dim3((unsigned)tb), dim3(SAS_TAG_BLOCK), st, a);
+        }
     } else if (algo == SAS_ALGO_INTERP) {
         if (x->quad_leaves && !x->quad_compact) launch_interp<4, true>(qw, grid, block, st, a, range);
         else if (x->sa_w == 8) launch_interp<8, false>(qw, grid, block, st, a, range);
@@ -2356,6 +2386,46 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
 
 // Host-pointer calls stage through plain hipMalloc + synchronous copies: the
 // stream-ordered allocator + pageable async copies raced on the null stream.
+// queries t[qoff[k] .. qoff[k] + qlen[k]) of the indexed text (SAS_QUERIES_ARE_SLICES)
+__global__ void k_validate_slices(const uint64_t* __restrict__ qoff, const uint32_t* __restrict__ qlen, uint64_t nq,
+                                  uint64_t n, uint32_t* __restrict__ bad) {
+    uint32_t b = 0;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * blockDim.x)
+        b |= (qoff[i] > n || qlen[i] > n - qoff[i]) ? 1u : 0u;
+    if (b) atomicOr(bad, 1u);
+}
+
+static int slices_impl(const sas_index* x, const uint64_t* qoff, const uint32_t* qlen, uint64_t nq, int algo,
+                       uint64_t* out_pos, uint32_t* out_probes, void* stream, uint32_t flags) {
+    if (algo != SAS_ALGO_TAGGED) SAS_FAIL(EINVAL, "SAS_QUERIES_ARE_SLICES: SAS_ALGO_TAGGED only");
+    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "SAS_QUERIES_ARE_SLICES: device pointers only (SAS_DEVICE_PTRS)");
+    if (!qoff || !qlen) SAS_FAIL(EINVAL, "SAS_QUERIES_ARE_SLICES: null qoff/qlen");
+    HIP_TRY(hipSetDevice(x->device));
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    SearchArgs a{};
+    fill_args(x, a);
+    a.nq = nq;
+    a.qoff = qoff;
+    a.qlen = qlen;
+    a.out_pos = out_pos;
+    a.out_probes = out_probes;
+    a.bad = x->scratch;
+    // every slice inside the text: checked first, always (an out-of-range slice would read
+    // past the packed text); the call synchronises to read the flag back
+    DeviceBuf bflag;
+    HIP_TRY(hipMalloc(&bflag.p, 4));
+    HIP_TRY(hipMemsetAsync(bflag.p, 0, 4, st));
+    uint64_t vb = (nq + 255) / 256;
+    if (vb > 65536) vb = 65536;
+    hipLaunchKernelGGL(k_validate_slices, dim3((unsigned)vb), dim3(256), 0, st, qoff, qlen, nq, x->n,
+                       static_cast<uint32_t*>(bflag.p));
+    uint32_t hbad = 0;
+    HIP_TRY(hipMemcpyAsync(&hbad, bflag.p, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (hbad) SAS_FAIL(EINVAL, "SAS_QUERIES_ARE_SLICES: a slice reaches past the text");
+    return launch_search(x, a, algo, 4, flags, st);
+}
+
 static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t* qoff, const uint32_t* qlen,
                        uint32_t m_fixed, uint64_t nq, int algo, uint64_t* out_pos, uint32_t* out_probes,
                        void* stream, uint32_t flags) {
@@ -2363,6 +2433,7 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
     TRY_RC(check_algo(x, algo, flags, "search"));
     if (nq == 0) return 0;
     if (!out_pos) SAS_FAIL(EINVAL, "search: null out_pos");
+    if (flags & SAS_QUERIES_ARE_SLICES) return slices_impl(x, qoff, qlen, nq, algo, out_pos, out_probes, stream, flags);
     if (!qbytes) SAS_FAIL(EINVAL, "search: null qbytes");
     bool ragged = qoff != nullptr;
     if (ragged && !qlen) SAS_FAIL(EINVAL, "search: qoff without qlen");

@@ -25,6 +25,7 @@ SAS_VALIDATE = 1 << 5
 SAS_PREFIX_RANGE = 1 << 24
 SAS_NO_PREFIX_TABLE = 1 << 25
 SAS_RANGE_NO_INLINE = 1 << 27
+SAS_QUERIES_ARE_SLICES = 1 << 28
 SAS_ROUTE_PACKED = 1 << 26
 SAS_BUILD_WIDE = 1 << 6
 SAS_BUILD_SECTOR = 1 << 7

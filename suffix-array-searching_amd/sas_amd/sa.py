@@ -338,6 +338,23 @@ class SaNaive:
         nq = int(qoff.numel() if dev else len(qoff))
         return self._run(qbytes, qoff, qlen, 0, nq, algo, probes, stream, out, flags, dev)
 
+    def search_slices(self, qoff, qlen, algo: str = "tagged", probes: bool = False, stream=None, out=None,
+                      flags: int = 0):
+        """Queries that are slices of the indexed text, t[qoff[k] : qoff[k] + qlen[k]] (the
+        reference's borrowed &t[i..i+len] queries; SAS_QUERIES_ARE_SLICES): torch CUDA int64
+        offsets / int32 lengths in, no query bytes -> torch CUDA positions out."""
+        import torch
+        if not (_is_cuda(qoff) and _is_cuda(qlen)):
+            raise ValueError("search_slices: torch CUDA qoff / qlen")
+        nq = int(qoff.numel())
+        if out is None:
+            out = torch.empty(nq, dtype=torch.int64, device=qoff.device)
+        pr = torch.empty(nq, dtype=torch.int32, device=qoff.device) if probes else None
+        st = stream if stream is not None else torch.cuda.current_stream(qoff.device).cuda_stream
+        check(lib().sas_search_batch(self._h, None, _ptr(qoff), _ptr(qlen), nq, _lib.ALGOS[algo], _ptr(out),
+                                     _ptr(pr), st, flags | _lib.SAS_DEVICE_PTRS | _lib.SAS_QUERIES_ARE_SLICES))
+        return (out, pr) if probes else out
+
     def _run(self, qbytes, qoff, qlen, m, nq, algo, probes, stream, out, flags, dev):
         a = _lib.ALGOS[algo]
         if dev:

@@ -280,3 +280,35 @@ def test_tagged_wave_staging_paths(sas):
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().astype(np.uint64),
                           expected(t, sa, [t[s:s + m] for s in starts[:101]])[0])
+
+
+def test_tagged_text_slices(sas):
+    """SAS_QUERIES_ARE_SLICES: queries given as slices t[off : off + len] of the indexed text
+    (no query bytes; the tie with the query's own suffix skips the text compare) give the
+    oracle's positions and the byte queries' probes, on random and repeat-rich texts,
+    lengths 0..300 including slices that end at the text's end; a slice past the end is
+    EINVAL."""
+    import torch
+    rng = np.random.default_rng(17)
+    for name, t in texts(rng).items():
+        n = len(t)
+        idx = sas.SaNaive.build(t, lcp=False, tagged=True)
+        lens = rng.integers(0, 300, 4000)
+        offs = np.array([rng.integers(0, max(1, n - l + 1)) for l in lens], np.int64)
+        lens = np.minimum(lens, n - offs)
+        offs = np.concatenate([offs, [n - 1, n - 5, n, 0]])
+        lens = np.concatenate([lens, [1, 5, 0, min(n, 257)]])
+        qs = [t[o:o + l] for o, l in zip(offs, lens)]
+        exp, _ = expected(t, np.ascontiguousarray(O.build_sa(t), np.uint32), qs)
+        dq_off = torch.from_numpy(offs).cuda()
+        dq_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+        got, pr = idx.search_slices(dq_off, dq_len, probes=True)
+        buf, off, ln = pack(qs)
+        byt, bpr = idx.search_batch(buf, off, ln, algo="tagged", probes=True)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().astype(np.uint64), exp), name
+        assert np.array_equal(byt, exp), name
+        assert np.array_equal(pr.cpu().numpy().astype(np.uint32), bpr), name
+        with pytest.raises(sas.SasError):
+            idx.search_slices(torch.tensor([n - 3], dtype=torch.int64, device="cuda"),
+                              torch.tensor([4], dtype=torch.int32, device="cuda"))
