@@ -102,8 +102,9 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
     elif algo == "tagged":
         hbm += 8 + min(n / 4 ** st["tag_chars"] + 1, 8) * 8 + max(0.0, m - st["tag_chars"] - 12) / 4
     elif range_flag:  # PLAIN / LCP from the prefix table's range: table entry + SA word + window per probe
-        entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)
-        hbm += entry + max(0.0, probes - 1) * (sa_w + win)
+        entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)  # (INTERP: a fused 16-B entry per probe)
+        per = 16 if (algo == "interp" and st["quad_entry_bytes"] == 16) else sa_w + win
+        hbm += entry + max(0.0, probes - 1) * per
     elif algo in ("plain", "lcp", "inline", "llcp", "interp"):
         per = {"plain": sa_w + win, "lcp": sa_w + win, "inline": 16, "llcp": 16, "interp": 16}[algo]
         if algo in ("plain", "lcp", "inline", "llcp"):
@@ -760,7 +761,8 @@ def main():
     ap.add_argument("--m", type=int, default=32, help="query length")
     ap.add_argument("--algo", default=None, choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
                                                      "prefix", "tagged", "interp"])
-    ap.add_argument("--variants", default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,interp,prefix_packed",
+    ap.add_argument("--variants",
+                    default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,interp,interp_range,prefix_packed",
                     help="other algos timed beside the headline one")
     ap.add_argument("--prefix-chars", type=int, default=16,
                     help="p of the prefix table in chars (the reference's main.rs intends -p 20 key BITS)")

@@ -12,7 +12,7 @@ what=${1:-all}
 if [ "$what" = all ] || [ "$what" = kt ]; then
   # without the prefix_packed variant and configs[4] (both launch k_sa_prefix2 on the
   # headline's grid with packed words), so that grid's average is the headline's alone
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- python3 bench.py --no-e2e --no-c4 --variants plain,plain_range,lcp,llcp,stree,sector,quad,inline,interp > "$out/kt_bench.json" 2> "$out/kt_bench.err" || exit $?
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- python3 bench.py --no-e2e --no-c4 --variants plain,plain_range,lcp,llcp,stree,sector,quad,inline,interp,interp_range > "$out/kt_bench.json" 2> "$out/kt_bench.err" || exit $?
   python3 tools/kt_by_grid.py "$out/kt/run_kernel_trace.csv" "$out/kt/kernel_stats_by_grid.csv" k_sa_ || exit $?
   find "$out/kt" -name '*kernel_trace.csv' -delete  # per-dispatch rows: too big to bring back
 fi
