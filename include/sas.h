@@ -288,7 +288,8 @@ int sas_copy_lcp(const sas_index* index, uint32_t* dst, uint64_t count, uint32_t
 /* 2-bit packed fixed-length queries, m <= 32: word i holds query i's chars, the first in
  * bits 63..62, zero padded (how the reference packs DNA for its interpolation search,
  * string_value<K>, sas/util.rs:76-117).  A lookup then reads 8 B of query instead of m.
- * sas_pack_queries: device pointers only (SAS_DEVICE_PTRS); EINVAL on codes > 3.
+ * sas_pack_queries: device pointers (SAS_DEVICE_PTRS: a kernel on `stream`) or host arrays
+ * (packed on the host's worker pool, AVX2 or BMI2 where the CPU has them); EINVAL on codes > 3.
  * sas_search_packed: SAS_ALGO_PREFIX only; host or device pointers per flags. */
 int sas_pack_queries(const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_words, void* stream,
                      uint32_t flags);

@@ -169,9 +169,51 @@ static inline bool host_has_bmi2() {
     return has;
 }
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+// AVX2 variant for m = 32 (one query = one 32-B vector): vpmaddubsw joins char pairs
+// (4·c0 + c1), vpmaddwd joins pairs of those (64·c0 + 16·c1 + 4·c2 + c3, the byte of 4
+// chars, first char high), vpshufb + a dword gather bring the 8 bytes together in char
+// order, and a byte swap puts the first char in bits 63..62.
+typedef char sas_v32qi __attribute__((vector_size(32)));
+typedef short sas_v16hi __attribute__((vector_size(32)));
+typedef int sas_v8si __attribute__((vector_size(32)));
+typedef long long sas_v4di __attribute__((vector_size(32)));
+
+__attribute__((target("avx2"))) static uint8_t host_pack32_words_avx2(const uint8_t* q, uint64_t nq, uint64_t* out) {
+    const sas_v32qi pair = {4, 1, 4, 1, 4, 1, 4, 1, 4, 1, 4, 1, 4, 1, 4, 1,
+                            4, 1, 4, 1, 4, 1, 4, 1, 4, 1, 4, 1, 4, 1, 4, 1};
+    const sas_v16hi quad = {16, 1, 16, 1, 16, 1, 16, 1, 16, 1, 16, 1, 16, 1, 16, 1};
+    const sas_v32qi pick = {0, 4, 8, 12, -128, -128, -128, -128, -128, -128, -128, -128, -128, -128, -128, -128,
+                            0, 4, 8, 12, -128, -128, -128, -128, -128, -128, -128, -128, -128, -128, -128, -128};
+    sas_v4di acc = {0, 0, 0, 0};
+    for (uint64_t i = 0; i < nq; i++, q += 32) {
+        sas_v32qi v;
+        memcpy(&v, q, 32);
+        acc |= (sas_v4di)v;
+        const sas_v16hi p2 = __builtin_ia32_pmaddubsw256(v, pair);
+        const sas_v8si p4 = __builtin_ia32_pmaddwd256(p2, quad);
+        const sas_v8si b = (sas_v8si)__builtin_ia32_pshufb256((sas_v32qi)p4, pick);
+        const uint64_t w = (uint64_t)(uint32_t)b[0] | ((uint64_t)(uint32_t)b[4] << 32);
+        out[i] = __builtin_bswap64(w);
+    }
+    const uint64_t bad = (uint64_t)(acc[0] | acc[1] | acc[2] | acc[3]);
+    uint8_t r = 0;
+    for (int k = 0; k < 8; k++) r |= (uint8_t)(bad >> (8 * k));
+    return r;
+}
+
+static inline bool host_has_avx2() {
+    static const bool has = __builtin_cpu_supports("avx2") && getenv("SAS_NO_AVX2") == nullptr;
+    return has;
+}
+#endif
+
 // fixed-length queries of m <= 32 chars -> 2-bit packed words (first char in bits 63..62,
 // zero padded); returns the OR of every byte (a code > 3 shows in the bits 0xFC)
 static inline uint8_t host_pack_words(const uint8_t* q, uint32_t m, uint64_t nq, uint64_t* out) {
+#if !defined(__HIP_DEVICE_COMPILE__)
+    if (m == 32 && host_has_avx2()) return host_pack32_words_avx2(q, nq, out);
+#endif
     if (host_has_bmi2()) return host_pack_words_bmi2(q, m, nq, out);
     uint64_t bad = 0;
     if (m == 32) {

@@ -2557,9 +2557,18 @@ __global__ void k_pack_queries(const uint8_t* __restrict__ qb, uint32_t m, uint6
 extern "C" int sas_pack_queries(const uint8_t* qbytes, uint32_t m, uint64_t nq, uint64_t* out_words, void* stream,
                                 uint32_t flags) {
     if (m > 32) SAS_FAIL(EINVAL, "sas_pack_queries: m must be <= 32");
-    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_pack_queries: device pointers only (SAS_DEVICE_PTRS)");
     if (nq == 0) return 0;
     if (!qbytes || !out_words) SAS_FAIL(EINVAL, "sas_pack_queries: null argument");
+    if (!(flags & SAS_DEVICE_PTRS)) {  // host arrays: the staging pipeline's packer on the host pool
+        std::atomic<uint32_t> bad{0};
+        constexpr uint64_t per = 16384;
+        HostPool::get().run((int)((nq + per - 1) / per), [&](int i) {
+            const uint64_t b = (uint64_t)i * per, e = std::min(nq, b + per);
+            if (host_pack_words(qbytes + b * m, m, e - b, out_words + b) & 0xFC) bad.fetch_or(1);
+        });
+        if (bad.load()) SAS_FAIL(EINVAL, "sas_pack_queries: query bytes must be DNA codes 0..3");
+        return 0;
+    }
     hipStream_t st = static_cast<hipStream_t>(stream);
     DeviceBuf bflag;
     HIP_TRY(hipMalloc(&bflag.p, 4));

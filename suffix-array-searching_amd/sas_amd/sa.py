@@ -217,7 +217,14 @@ class SaNaive:
     @staticmethod
     def pack_queries(qbytes, m: int, stream=None):
         """2-bit packed fixed-length queries (sas_pack_queries; m <= 32): torch CUDA
-        uint8 in -> torch CUDA int64 words out (first char in bits 63..62)."""
+        uint8 in -> torch CUDA int64 words out (first char in bits 63..62); numpy uint8 in
+        -> numpy uint64 out, packed on the host."""
+        if not _is_cuda(qbytes):
+            qbytes = _as_u8(qbytes)
+            nq = len(qbytes) // m if m else 0
+            out = np.zeros(max(nq, 1), np.uint64)
+            check(lib().sas_pack_queries(_ptr(qbytes), m, nq, _ptr(out), None, 0))
+            return out[:nq]
         import torch
         nq = qbytes.numel() // m if m else 0
         out = torch.empty(nq, dtype=torch.int64, device=qbytes.device)
