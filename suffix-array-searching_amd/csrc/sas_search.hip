@@ -2595,8 +2595,7 @@ extern "C" int sas_search_packed(const sas_index* x, const uint64_t* qwords, uin
     if (!qwords || !out_pos) SAS_FAIL(EINVAL, "sas_search_packed: null argument");
     HIP_TRY(hipSetDevice(x->device));
     hipStream_t st = static_cast<hipStream_t>(stream);
-    const bool dev = flags & SAS_DEVICE_PTRS;
-    if (!dev)
+    if (!(flags & SAS_DEVICE_PTRS))  // host words: the pinned staging pipeline
         return host_pipeline(x, HM_WORDS, nullptr, nullptr, nullptr, qwords, m, nq, algo, out_pos, out_probes, st,
                              flags);
     SearchArgs a{};
@@ -2604,31 +2603,10 @@ extern "C" int sas_search_packed(const sas_index* x, const uint64_t* qwords, uin
     a.nq = nq;
     a.m_fixed = m;
     a.bad = x->scratch;  // packed words hold no invalid codes
-    DeviceBuf bw, bout, bprobes;
-    if (dev) {
-        a.qwords = qwords;
-        a.out_pos = out_pos;
-        a.out_probes = out_probes;
-    } else {
-        HIP_TRY(hipStreamSynchronize(st));
-        HIP_TRY(hipMalloc(&bw.p, nq * 8));
-        HIP_TRY(hipMemcpy(bw.p, qwords, nq * 8, hipMemcpyHostToDevice));
-        HIP_TRY(hipMalloc(&bout.p, nq * 8));
-        a.qwords = static_cast<const uint64_t*>(bw.p);
-        a.out_pos = static_cast<uint64_t*>(bout.p);
-        if (out_probes) {
-            HIP_TRY(hipMalloc(&bprobes.p, nq * 4));
-            a.out_probes = static_cast<uint32_t*>(bprobes.p);
-        }
-    }
-    int rc = launch_search(x, a, algo, 1, flags | SAS_DEVICE_PTRS, st);
-    if (rc) return rc;
-    if (!dev) {
-        HIP_TRY(hipStreamSynchronize(st));
-        HIP_TRY(hipMemcpy(out_pos, a.out_pos, nq * 8, hipMemcpyDeviceToHost));
-        if (out_probes) HIP_TRY(hipMemcpy(out_probes, a.out_probes, nq * 4, hipMemcpyDeviceToHost));
-    }
-    return 0;
+    a.qwords = qwords;
+    a.out_pos = out_pos;
+    a.out_probes = out_probes;
+    return launch_search(x, a, algo, 1, flags, st);
 }
 
 extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint32_t m, uint64_t nq, int algo,
