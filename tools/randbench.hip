@@ -8,6 +8,10 @@
 //   rand128  : random 128-B line, 8 x 16-B loads by one lane
 //   rand16   : one random 16-B slot per lane
 //   rand32pair: one random 32-B slot per lane pair, 16 B per lane (the PREFIX entry read)
+//   rand32pair_nt: the same with non-temporal loads (as k_sa_prefix2 issues them)
+//
+// argv: buffer MiB, accesses, reps, allocation (0 hipMalloc, 1 hipDeviceMallocUncached,
+// 2 hipDeviceMallocFinegrained), shapes to run (bit mask, default all)
 //
 // Prints one JSON line per kernel: accesses/s and bytes moved per the access shape.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/randbench tools/randbench.hip
@@ -38,7 +42,7 @@ __global__ __launch_bounds__(1024) void k_rand(const uint8_t* __restrict__ p, ui
                                                uint32_t seed, uint32_t* out) {
     uint32_t acc = 0;
     uint64_t lines = bytes / 128;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; SHAPE != 5 && i < accesses;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; SHAPE < 5 && i < accesses;
          i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
         uint64_t line = h % lines;
@@ -72,6 +76,17 @@ __global__ __launch_bounds__(1024) void k_rand(const uint8_t* __restrict__ p, ui
             acc ^= t.x ^ t.y ^ t.z ^ t.w;
         }
     }
+    if (SHAPE == 6) {  // SHAPE 5 with non-temporal loads
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        const uint32_t sub = threadIdx.x & 1;
+        for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / 2; i < accesses;
+             i += (uint64_t)gridDim.x * blockDim.x / 2) {
+            uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
+            const uint8_t* b = p + (h % lines) * 128 + ((h >> 40) & 3) * 32;
+            const u32x4 t = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(b) + sub);
+            acc ^= t.x ^ t.y ^ t.z ^ t.w;
+        }
+    }
     if (acc == 0x12345678u) out[0] = acc;
 }
 
@@ -79,9 +94,12 @@ int main(int argc, char** argv) {
     uint64_t bytes = (argc > 1 ? strtoull(argv[1], 0, 10) : 4096ull) << 20;  // MiB
     uint64_t accesses = argc > 2 ? strtoull(argv[2], 0, 10) : 100000000ull;
     int reps = argc > 3 ? atoi(argv[3]) : 5;
+    const int alloc = argc > 4 ? atoi(argv[4]) : 0;
+    const unsigned mask = argc > 5 ? (unsigned)strtoul(argv[5], 0, 0) : 0x7fu;
     uint8_t* p;
     uint32_t* out;
-    CHECK(hipMalloc(&p, bytes));
+    if (alloc == 0) CHECK(hipMalloc(&p, bytes));
+    else CHECK(hipExtMallocWithFlags((void**)&p, bytes, alloc == 1 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained));
     CHECK(hipMalloc(&out, 64));
     CHECK(hipMemset(p, 1, bytes));
     int cus = 256;
@@ -92,9 +110,9 @@ int main(int argc, char** argv) {
     CHECK(hipEventCreate(&e1));
     float ms;
     auto report = [&](const char* name, double acc, double bytes_per) {
-        printf("{\"kernel\": \"%s\", \"buffer_MiB\": %llu, \"accesses\": %.0f, \"ms\": %.4f, \"accesses_per_s\": %.4g, "
+        printf("{\"kernel\": \"%s\", \"alloc\": %d, \"buffer_MiB\": %llu, \"accesses\": %.0f, \"ms\": %.4f, \"accesses_per_s\": %.4g, "
                "\"GBps_at_shape_bytes\": %.1f, \"GBps_at_128B_lines\": %.1f}\n",
-               name, (unsigned long long)(bytes >> 20), acc, ms, acc / (ms * 1e-3), acc * bytes_per / (ms * 1e-3) / 1e9,
+               name, alloc, (unsigned long long)(bytes >> 20), acc, ms, acc / (ms * 1e-3), acc * bytes_per / (ms * 1e-3) / 1e9,
                acc * (bytes_per < 128 ? 128 : bytes_per) / (ms * 1e-3) / 1e9);
         fflush(stdout);
     };
@@ -110,6 +128,7 @@ int main(int argc, char** argv) {
     ms /= reps;
     report("stream16", (double)(bytes / 16), 16);
 #define RUN(S, NAME, BPER)                                                                                    \
+    if (mask & (1u << S)) {                                                                                 \
     hipLaunchKernelGGL(k_rand<S>, grd, blk, 0, 0, p, bytes, accesses, 1u, out);                             \
     CHECK(hipDeviceSynchronize());                                                                          \
     CHECK(hipEventRecord(e0));                                                                              \
@@ -118,12 +137,14 @@ int main(int argc, char** argv) {
     CHECK(hipEventSynchronize(e1));                                                                         \
     CHECK(hipEventElapsedTime(&ms, e0, e1));                                                                \
     ms /= reps;                                                                                             \
-    report(NAME, (double)accesses, BPER);
+    report(NAME, (double)accesses, BPER);                                                                   \
+    }
     RUN(0, "rand4", 4)
     RUN(1, "rand8x2", 16)
     RUN(2, "rand64", 64)
     RUN(3, "rand128", 128)
     RUN(4, "rand16", 16)
     RUN(5, "rand32pair", 32)
+    RUN(6, "rand32pair_nt", 32)
     return 0;
 }
