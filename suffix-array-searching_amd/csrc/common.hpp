@@ -410,6 +410,54 @@ __device__ __forceinline__ bool suffix_less_from_x2(const uint64_t* __restrict__
     return lenS < (uint64_t)q.m;
 }
 
+// suffix_less_from_x2 with the first PRE word pairs the compare can need loaded together:
+// a positive query matches its own suffix to the end, so the compare always runs over every
+// window and the plain loop's pair loads form a dependent chain ((m - h) / 64 round trips).
+// Windows past the preloaded 2 PRE - 2 continue as suffix_less_from_x2 does.
+template <int PRE, class Q>
+__device__ __forceinline__ bool suffix_less_from_pre(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
+                                                     const Q& q, uint32_t h, uint32_t* lcp) {
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const uint64_t lenS = n - p;
+    const uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
+    if (h < L) {
+        const uint64_t w0 = (p + h) >> 5;
+        const uint32_t sh = (uint32_t)((p + h) & 31) << 1;
+        const uint32_t o = (uint32_t)(w0 & 1);
+        const u64x2* tp = reinterpret_cast<const u64x2*>(tw) + (w0 >> 1);
+        const uint32_t nwin = (L - h + 31) >> 5;  // windows; window r reads words w0 + r, w0 + r + 1
+        const uint32_t npair = (o + nwin) / 2 + 1;  // pairs holding words w0 .. w0 + nwin
+        uint64_t W[2 * PRE];
+#pragma unroll
+        for (int j = 0; j < PRE; j++) {
+            const u64x2 v = (uint32_t)j < npair ? tp[j] : u64x2{0ull, 0ull};
+            W[2 * j] = v.x;
+            W[2 * j + 1] = v.y;
+        }
+#pragma unroll
+        for (int r = 0; r < 2 * PRE - 2; r++) {
+            const uint32_t off = h + 32u * r;
+            if (off >= L) {
+                *lcp = L;
+                return lenS < (uint64_t)q.m;
+            }
+            const uint64_t lo = o ? W[r + 1] : W[r], hi = o ? W[r + 2] : W[r + 1];
+            const uint32_t c = L - off < 32 ? L - off : 32;
+            const uint64_t mk = chars_mask(c);
+            const uint64_t a = (sh ? ((lo << sh) | (hi >> (64 - sh))) : lo) & mk;
+            const uint64_t b = q.chars32(off) & mk;
+            if (a != b) {
+                *lcp = off + (uint32_t)(__clzll(a ^ b) >> 1);
+                return a < b;
+            }
+        }
+        const uint32_t h2 = h + 32u * (2 * PRE - 2);
+        if (h2 < L) return suffix_less_from_x2<1>(tw, n, p, q, h2, lcp);
+    }
+    *lcp = L;
+    return lenS < (uint64_t)q.m;
+}
+
 // Same decision when the first 32 chars of the suffix are already known (key).
 template <int QW, class Q>
 __device__ __forceinline__ bool suffix_less_key(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
@@ -440,8 +488,15 @@ __device__ __forceinline__ bool suffix_less_key(const uint64_t* __restrict__ tw,
 // of every query (the configs[3] shape: ~12 of its ~19 requests per lookup); instead the
 // wave reads the span once, coalesced (lane l reads 16-B block l, l+64, ...), packs it 2 bits
 // per char into LDS, and each lane reads its query words from there.  A span longer than
-// SAS_WQ_WORDS words (16K chars) falls back to per-lane loads.
-#define SAS_WQ_WORDS 512
+// SAS_WQ_WORDS - 1 words (16,608 chars: 64 queries of 256 chars and the 16-B alignment fit,
+// configs[3]'s longest) falls back to per-lane loads.
+#ifndef SAS_WQ_WORDS
+#define SAS_WQ_WORDS 520
+#endif
+// 16-B blocks a lane loads before it packs any (0: the plain loop)
+#ifndef SAS_WQ_UNROLL
+#define SAS_WQ_UNROLL 8
+#endif
 
 __device__ __forceinline__ uint64_t wave_min_u64(uint64_t v) {
 #pragma unroll
@@ -491,7 +546,26 @@ __device__ __forceinline__ bool wave_stage_queries(const uint8_t* __restrict__ q
     if (span > (uint64_t)(SAS_WQ_WORDS - 1) * 32) return false;
     const uint32_t nblk = (uint32_t)((span + 15) >> 4);
     const uint4* src = reinterpret_cast<const uint4*>(qbytes + base);
+#if SAS_WQ_UNROLL > 1
+    // all of a lane's blocks in flight before the first wait: the span (~8 blocks per lane at
+    // configs[3]'s mean length) costs one memory round trip, not one per pair of blocks.  The
+    // lookup state is not live yet, so the buffer costs no occupancy
+    for (uint32_t b0 = lane; b0 < nblk; b0 += 64 * SAS_WQ_UNROLL) {
+        uint4 v[SAS_WQ_UNROLL];
+#pragma unroll
+        for (int k = 0; k < SAS_WQ_UNROLL; k++) {
+            const uint32_t b = b0 + 64u * k;
+            v[k] = b < nblk ? src[b] : make_uint4(0u, 0u, 0u, 0u);
+        }
+#pragma unroll
+        for (int k = 0; k < SAS_WQ_UNROLL; k++) {
+            const uint32_t b = b0 + 64u * k;
+            if (b < nblk) L32[b ^ 1] = pack16(v[k]);
+        }
+    }
+#else
     for (uint32_t b = lane; b < nblk; b += 64) L32[b ^ 1] = pack16(src[b]);
+#endif
     // zero the rest of the last word and one guard word after it
     const uint32_t nw = (nblk + 1) >> 1, z = nblk + lane;
     if (z < 2 * nw + 2) L32[z ^ 1] = 0;

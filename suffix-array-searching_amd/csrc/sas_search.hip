@@ -1658,6 +1658,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 #define SAS_TAG_WINS 1
 #endif
 #define TAG_M40 (SAS_SA40_MAX - 1)
+// text word pairs the tie compare loads together before its first compare (0: one pair at a
+// time, suffix_less_from_x2)
+#ifndef SAS_TAG_PRE
+#define SAS_TAG_PRE 0
+#endif
 // waves per SIMD the long-query (QW >= SAS_TAG_LB_QW) instances are built for
 #ifndef SAS_TAG_LB
 #define SAS_TAG_LB 5
@@ -1683,7 +1688,11 @@ __device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArg
     const uint32_t L = a.tag_p + SAS_TAG_CHARS;
     if (q.m <= L) return (a.n - p) >= (uint64_t)q.m;  // equal padded keys: a shorter suffix is a prefix of q
     uint32_t lcp;
+#if SAS_TAG_PRE
+    return !suffix_less_from_pre<SAS_TAG_PRE>(a.tw, a.n, p, q, L, &lcp);
+#else
     return !suffix_less_from_x2<QW>(a.tw, a.n, p, q, L, &lcp);
+#endif
 }
 
 // the first min(m, len) chars of suffix(e) are > q, for an entry of the bucket of q's routing

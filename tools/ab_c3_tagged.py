@@ -22,40 +22,43 @@ t = sas_amd.random_string(n, seed=31415, device="cuda")
 idx = sas_amd.SaNaive.build(t, lcp=False, tagged=True)
 del t
 torch.cuda.empty_cache()
-off, ln, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=256, len_lo=8, len_hi=257)
-lens = torch.from_numpy(ln.astype(np.int32)).cuda()
-qoff = torch.zeros(nq, dtype=torch.int64, device="cuda")
-qoff[1:] = torch.cumsum(lens.long(), 0)[:-1]
-qb = torch.zeros(int(lens.sum().item()) + 64, dtype=torch.uint8, device="cuda")
-idx.extract(torch.from_numpy(off.astype(np.int64)).cuda(), lens, qoff, qb)
-out = torch.empty(nq, dtype=torch.int64, device="cuda")
-ref = None
-# each variant library drives the SAME index object: the handle layout is shared
-handle = idx._h
-for rep in range(2):
-    for pk in pkgs:
-        lib = ctypes.CDLL(os.path.join(pk, "libsas_amd.so")) if pk != pkgs[0] else sas_amd._lib.lib()
-        for algo in algos:
-            a = sas_amd._lib.ALGOS[algo]
-            st = torch.cuda.current_stream().cuda_stream
+for spec in os.environ.get("AB_LENS", "8-257").split(","):
+    lo_, hi_ = (int(x) for x in spec.split("-"))
+    ref = None
+    off, ln, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=256, len_lo=lo_, len_hi=hi_)
+    lens = torch.from_numpy(ln.astype(np.int32)).cuda()
+    qoff = torch.zeros(nq, dtype=torch.int64, device="cuda")
+    qoff[1:] = torch.cumsum(lens.long(), 0)[:-1]
+    qb = torch.zeros(int(lens.sum().item()) + 64, dtype=torch.uint8, device="cuda")
+    idx.extract(torch.from_numpy(off.astype(np.int64)).cuda(), lens, qoff, qb)
+    out = torch.empty(nq, dtype=torch.int64, device="cuda")
+    ref = None
+    # each variant library drives the SAME index object: the handle layout is shared
+    handle = idx._h
+    for rep in range(2):
+        for pk in pkgs:
+            lib = ctypes.CDLL(os.path.join(pk, "libsas_amd.so")) if pk != pkgs[0] else sas_amd._lib.lib()
+            for algo in algos:
+                a = sas_amd._lib.ALGOS[algo]
+                st = torch.cuda.current_stream().cuda_stream
 
-            def call():
-                rc = lib.sas_search_batch(handle, ctypes.c_void_p(qb.data_ptr()), ctypes.c_void_p(qoff.data_ptr()),
-                                          ctypes.c_void_p(lens.data_ptr()), ctypes.c_uint64(nq), a,
-                                          ctypes.c_void_p(out.data_ptr()), None, ctypes.c_void_p(st),
-                                          ctypes.c_uint32(sas_amd._lib.SAS_DEVICE_PTRS))
-                assert rc == 0, rc
-            call()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
-            for _ in range(3):
+                def call():
+                    rc = lib.sas_search_batch(handle, ctypes.c_void_p(qb.data_ptr()), ctypes.c_void_p(qoff.data_ptr()),
+                                              ctypes.c_void_p(lens.data_ptr()), ctypes.c_uint64(nq), a,
+                                              ctypes.c_void_p(out.data_ptr()), None, ctypes.c_void_p(st),
+                                              ctypes.c_uint32(sas_amd._lib.SAS_DEVICE_PTRS))
+                    assert rc == 0, rc
                 call()
-            e1.record()
-            torch.cuda.synchronize()
-            ok = True
-            if ref is None:
-                ref = out.clone()
-            else:
-                ok = bool(torch.equal(out, ref))
-            print(f"rep{rep} {os.path.basename(os.path.dirname(os.path.abspath(pk)))} {algo}: "
-                  f"{e0.elapsed_time(e1) / 3:.3f} ms per {nq} identical={ok}", flush=True)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(3):
+                    call()
+                e1.record()
+                torch.cuda.synchronize()
+                ok = True
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    ok = bool(torch.equal(out, ref))
+                print(f"rep{rep} {os.path.basename(os.path.dirname(os.path.abspath(pk)))} {algo}: "
+                      f"{e0.elapsed_time(e1) / 3:.3f} ms per {nq} len [{lo_}, {hi_}) identical={ok}", flush=True)
