@@ -242,7 +242,7 @@ def test_tagged_saturated_bucket(sas):
 
 def test_tagged_wave_staging_paths(sas):
     """k_sa_tagged's wave-staged queries: a contiguous batch (staged through LDS), the same
-    queries with shuffled offsets (spans past 16K chars fall back to per-lane loads), a wave
+    queries with shuffled offsets (spans past 16,608 chars fall back to per-lane loads), a wave
     of empty queries, a tail wave of 37 queries, and queries that sit at the very end of the
     device buffer (no slack): every form equals the oracle."""
     import torch
@@ -280,6 +280,23 @@ def test_tagged_wave_staging_paths(sas):
     torch.cuda.synchronize()
     assert np.array_equal(got.cpu().numpy().astype(np.uint64),
                           expected(t, sa, [t[s:s + m] for s in starts[:101]])[0])
+    # the largest staged span: 64 queries of 256 chars starting 15 bytes past a 16-B block
+    # (16,399 chars, inside the 16,608-char stage), and 64 of 260 chars (past it: per-lane
+    # loads); each batch offset into a larger device buffer, with a few misses
+    for m, skew in ((256, 15), (256, 1), (260, 15)):
+        nq2 = 64 * 3 + 5
+        qs2 = [t[s:s + m] for s in starts[:nq2]]
+        qs2[7] = rng.integers(0, 4, m, dtype=np.uint8)
+        qs2[100] = np.full(m, 3, np.uint8)
+        raw = torch.zeros(16 + nq2 * m, dtype=torch.uint8, device="cuda")
+        raw[skew:skew + nq2 * m] = torch.from_numpy(np.concatenate(qs2)).cuda()
+        o2 = torch.arange(nq2, dtype=torch.int64, device="cuda") * m + skew
+        l2 = torch.full((nq2,), m, dtype=torch.int32, device="cuda")
+        got = idx.search_batch(raw, o2, l2, algo="tagged")
+        torch.cuda.synchronize()
+        ex2 = expected(t, sa, qs2)[0]
+        bad = np.nonzero(got.cpu().numpy().astype(np.uint64) != ex2)[0]
+        assert len(bad) == 0, (m, skew, bad[:5])
 
 
 def test_tagged_text_slices(sas):
