@@ -50,6 +50,7 @@ RANDOM_REQ_CEILING = 5.084e10
 CACHE_BYTES = 256 << 20  # Infinity Cache (MALL): arrays at most this large count as cache-served
 SEED = 31415  # sas/main.rs:38
 TOP_LDS_LEVELS, TOP2_LEVELS = 12, 23  # binary-search levels served from LDS / the top2 array (index stats win)
+TOP2_CACHE_LEVELS = 23  # top2 levels inside the Infinity Cache (SAS_TOP2_CACHE_LEVELS); deeper ones are HBM
 
 KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
@@ -109,8 +110,14 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         per = {"plain": sa_w + win, "lcp": sa_w + win, "inline": 16, "llcp": 16, "interp": 16}[algo]
         if algo in ("plain", "lcp", "inline", "llcp"):
             t1, t2 = st.get("top_levels", TOP_LDS_LEVELS), st.get("top2_levels", TOP2_LEVELS)
+            if algo == "inline":
+                t2 = min(t2, TOP2_CACHE_LEVELS)  # launch_search caps INLINE's pivot levels
+            elif algo == "llcp":
+                t2 = min(t2, 21)  # and LLCP's (SAS_LLCP_TOP2_LEVELS)
+            tc = min(t2, TOP2_CACHE_LEVELS)  # the array's first 2^23 entries (128 MiB) stay in cache
             lds += min(probes, t1) * 12
-            cache += max(0.0, min(probes, t2) - t1) * 16  # the top2 array (<= 128 MiB) stays in cache
+            cache += max(0.0, min(probes, tc) - t1) * 16
+            hbm += max(0.0, min(probes, t2) - tc) * 16  # deeper pivot levels: one 16-B HBM entry each
             hbm += max(0.0, probes - t2) * per
         else:
             hbm += probes * per

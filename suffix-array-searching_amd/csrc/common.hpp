@@ -26,13 +26,20 @@
 #define SAS_TEXT_PAD_WORDS 4
 #define SAS_TOP_LEVELS 12             // 4095 pivots: 32 KiB keys + 16 KiB SA in LDS
 #define SAS_TOP_NODES (1u << SAS_TOP_LEVELS)
-// Levels 13..23 of the lockstep binary search (PLAIN, LCP, INLINE) read their pivot
-// (32-char key, SA value) from one 16-B entry of the cache-resident top2 array (128 MiB)
-// instead of an SA word and a text window.  Same-box: PLAIN 7.15 ms without it, 5.4-5.7
-// with 17 levels, 5.0-5.2 with 19, 4.70 with 21, 4.50 with 22, 4.27 with 23 (128 MiB,
-// still inside the Infinity Cache; tools/ab_top2.sh, profiles/r2/ab_top2_depth.txt).
+// Levels 13.. of the lockstep binary search (PLAIN, LCP, INLINE) read their pivot
+// (32-char key, SA value) from one 16-B entry of the top2 array instead of an SA word and a
+// text window.  Same-box: PLAIN 7.15 ms without it, 5.4-5.7 with 17 levels, 5.0-5.2 with
+// 19, 4.70 with 21, 4.50 with 22, 4.27 with 23 (128 MiB, the levels that stay inside the
+// Infinity Cache; profiles/r2/ab_top2_depth.txt).  Past those, a level from HBM is still
+// one request instead of two: 3.81 ms with 25 levels, 3.58 with 26, 3.11 with 28, 2.71
+// with 30 (16 GiB at n = 2^30) and 31 (profiles/r2/ab_top2_deeper*.txt).  Levels past
+// SAS_TOP2_CACHE_LEVELS are built only into free HBM (SAS_TOP2_RESERVE left over).
 #ifndef SAS_TOP2_LEVELS
-#define SAS_TOP2_LEVELS 23
+#define SAS_TOP2_LEVELS 30
+#endif
+#define SAS_TOP2_CACHE_LEVELS 23
+#ifndef SAS_TOP2_RESERVE
+#define SAS_TOP2_RESERVE (24ull << 30)
 #endif
 #define SAS_TOP2_NODES (1u << SAS_TOP2_LEVELS)
 #define SAS_STREE_B 16                // keys per node / branching factor - 1

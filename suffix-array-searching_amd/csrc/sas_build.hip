@@ -1371,9 +1371,24 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         uint32_t iters = 64 - __builtin_clzll(sa_n);  // ilog2(len) + 1 (sas/sa_search.rs:171)
         x->iters = iters;
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
-        x->top2_levels = iters < SAS_TOP2_LEVELS ? iters : SAS_TOP2_LEVELS;
-        // the pivots of the first top2_levels iterations: 2^SAS_TOP2_LEVELS entries (128 MiB at
-        // 23 levels, sized to stay inside the 256 MiB Infinity Cache) or fewer for small texts
+        // the pivots of the first top2_levels iterations, 2^top2_levels 16-B entries: the
+        // SAS_TOP2_CACHE_LEVELS that stay inside the 256 MiB Infinity Cache (128 MiB), then
+        // deeper levels up to SAS_TOP2_LEVELS while free HBM leaves SAS_TOP2_RESERVE for the
+        // rest of the build (a tagged index's entries and bucket table) and the caller's
+        // batches.  The probe sequence, and so every result, is the same at any depth.
+        uint32_t lv = iters < SAS_TOP2_LEVELS ? iters : SAS_TOP2_LEVELS;
+        const uint32_t lv0 = iters < SAS_TOP2_CACHE_LEVELS ? iters : SAS_TOP2_CACHE_LEVELS;
+        if (lv > lv0) {
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
+                (void)hipGetLastError();
+                fr = 0;
+            }
+            const uint64_t reserve =
+                SAS_TOP2_RESERVE + ((flags & SAS_BUILD_TAGGED) ? sa_n * 8 + ((32ull << 30) + 16) : 0);
+            while (lv > lv0 && ((uint64_t)16 << lv) + reserve > (uint64_t)fr) lv--;
+        }
+        x->top2_levels = lv;
         const uint32_t nodes = 1u << x->top2_levels;
         DevBuf t2;
         TRY(t2.alloc((uint64_t)nodes * 16, "top2"));

@@ -1651,6 +1651,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 #ifndef SAS_LLCP_TOP2_LEVELS
 #define SAS_LLCP_TOP2_LEVELS 21
 #endif
+#ifndef SAS_INLINE_TOP2_LEVELS
+#define SAS_INLINE_TOP2_LEVELS 23
+#endif
 #ifndef SAS_TAG_WIN
 #define SAS_TAG_WIN 8
 #endif
@@ -2065,6 +2068,9 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     // (3.08 ms with 21 levels, 3.29 ms with 23; PLAIN and LCP gain from 23, two requests per
     // probe there)
     if (algo == SAS_ALGO_LLCP && a.top2_levels > SAS_LLCP_TOP2_LEVELS) a.top2_levels = SAS_LLCP_TOP2_LEVELS;
+    // INLINE's own probes read one 16-B fused entry in rank order, whose last levels share
+    // lines; the pivot array past its cache-resident levels only moves them apart
+    if (algo == SAS_ALGO_INLINE && a.top2_levels > SAS_INLINE_TOP2_LEVELS) a.top2_levels = SAS_INLINE_TOP2_LEVELS;
     const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
