@@ -47,10 +47,17 @@ HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level par
 # independent random 4-B loads over a 4 GiB buffer, one 128-B line each: the chip's
 # random-request ceiling (tools/randbench.hip, profiles/r1/randbench_calibration.jsonl)
 RANDOM_REQ_CEILING = 5.084e10
+# the same random 4-B loads over a 64 MiB buffer (Infinity-Cache resident): the ceiling of
+# requests the cache-resident arrays serve (profiles/r1/randbench_calibration.jsonl)
+CACHE_REQ_CEILING = 5.731e10
 CACHE_BYTES = 256 << 20  # Infinity Cache (MALL): arrays at most this large count as cache-served
 SEED = 31415  # sas/main.rs:38
-TOP_LDS_LEVELS, TOP2_LEVELS = 12, 23  # binary-search levels served from LDS / the top2 array (index stats win)
-TOP2_CACHE_LEVELS = 23  # top2 levels inside the Infinity Cache (SAS_TOP2_CACHE_LEVELS); deeper ones are HBM
+# binary-search levels served from LDS / the pivot array (the index's stats win): the library
+# default builds the 23 cache-resident levels (SAS_TOP2_CACHE_LEVELS, 128 MiB); deeper levels
+# (SAS_BUILD_TOP2_LEVELS, e.g. 30 = 16 GiB) are HBM reads
+TOP_LDS_LEVELS, TOP2_LEVELS = 12, 23
+TOP2_CACHE_LEVELS = 23
+C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: pivots of levels 24-30 from HBM
 
 KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
@@ -119,6 +126,12 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             cache += max(0.0, min(probes, tc) - t1) * 16
             hbm += max(0.0, min(probes, t2) - tc) * 16  # deeper pivot levels: one 16-B HBM entry each
             hbm += max(0.0, probes - t2) * per
+            # random 128-B-line requests per lookup by where they are served: one per
+            # cache-resident pivot level; one per HBM pivot level; two per SA probe (the SA
+            # word, then the text window: PLAIN / LCP) or one (a 16-B entry); the query stream
+            reqs = {"cache": max(0.0, min(probes, tc) - t1),
+                    "hbm": max(0.0, min(probes, t2) - tc) + max(0.0, probes - t2) * (2 if per != 16 else 1)
+                    + (8.0 if packed else m) / 128}
         else:
             hbm += probes * per
     elif algo in ("stree", "quad", "sector"):
@@ -138,7 +151,29 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         h, c, l = _classify(sizes, node, lds_l)
         hbm, cache, lds = h + max(0.0, probes - H) * tail + (max(0.0, m - 32) / 4 if algo != "stree" else 0), c, l
     hbm += io
-    return {"hbm": hbm, "cache": cache, "lds": lds, "section_8d_plain": P * (4 + m) + m + 8}
+    out = {"hbm": hbm, "cache": cache, "lds": lds, "section_8d_plain": P * (4 + m) + m + 8}
+    if algo in ("plain", "lcp", "inline", "llcp") and not range_flag:
+        out["requests_model"] = reqs
+    return out
+
+
+def request_split(bpl: dict, pmc, lookups: int, kernel_ms: float):
+    """A PLAIN-family kernel's measured L2->fabric requests split by where they are served:
+    `hbm` = the model's HBM-level requests (bytes_per_lookup's requests_model), `cache` = the
+    rest of the PMC count (the cache-resident pivot levels' L2 misses, served by the Infinity
+    Cache).  Each share is priced at its own measured random-request ceiling; `frac` = that
+    floor over the kernel's time (<= 1 when the model holds)."""
+    if not pmc or not pmc.get("rdreq_per_launch") or "requests_model" not in bpl:
+        return None
+    total = pmc["rdreq_per_launch"] / lookups
+    hbm = min(total, bpl["requests_model"]["hbm"])
+    cache = total - hbm
+    floor_s = lookups * (hbm / RANDOM_REQ_CEILING + cache / CACHE_REQ_CEILING)
+    return {"per_lookup": total, "hbm_per_lookup": hbm, "cache_per_lookup": cache,
+            "hbm_ceiling_per_s": RANDOM_REQ_CEILING, "cache_ceiling_per_s": CACHE_REQ_CEILING,
+            "floor_ms": floor_s * 1e3, "frac": floor_s / (kernel_ms * 1e-3),
+            "basis": "hbm = model (pivot levels past the cache-resident ones: 1 each; SA probes: SA word + text "
+                     "window; query stream m/128), cache = PMC TCC_EA0_RDREQ minus hbm"}
 
 
 # ---------------------------------------------------------------- harness
@@ -202,13 +237,21 @@ def dist_env():
 def load_pmc(key: str):
     """The committed rocprofv3 --pmc summary of this exact workload
     (profiles/pmc_<key>.json, written by tools/pmc_to_json.py): HBM bytes and L2->fabric
-    read requests per launch, or None."""
+    read requests per launch, or None.  Counters are attached only when the summary was
+    collected on a library of the same source hash as the one loaded now (sas_source_hash);
+    a summary of another build comes back as {"stale": ...} and is never reported as
+    traffic."""
+    import sas_amd
     path = os.path.join(REPO, "profiles", f"pmc_{key}.json")
     if not os.path.exists(path):
         return None
     d = json.load(open(path))
+    src, lib_hash = d.get("source_hash"), sas_amd.source_hash()
+    rel = os.path.relpath(path, REPO)
+    if src != lib_hash:
+        return {"stale": True, "source": rel, "pmc_source_hash": src, "library_source_hash": lib_hash}
     return {"hbm_bytes_per_launch": d.get("hbm_bytes_per_launch"), "rdreq_per_launch": d.get("TCC_EA0_RDREQ"),
-            "source": os.path.relpath(path, REPO)}
+            "source": rel, "source_hash": src}
 
 
 def host_cpu() -> str:
@@ -241,13 +284,20 @@ def record(name, lookups, kernel_ms, wall_s, bpl, idx_bytes, pmc, probes, extra=
          "achieved_hbm_GBps": bpl["hbm"] * lookups / (kernel_ms * 1e-3) / 1e9,
          "achieved_cache_GBps": bpl["cache"] * lookups / (kernel_ms * 1e-3) / 1e9,
          "index_bytes": idx_bytes}
-    if pmc and pmc.get("hbm_bytes_per_launch"):
+    if pmc and pmc.get("stale"):
+        r["pmc"] = {"stale": True, "note": "the committed counters were collected on another build "
+                                           "(source hash differs): not reported", **pmc}
+    elif pmc and pmc.get("hbm_bytes_per_launch"):
         r["pmc"] = {"fabric_bytes_per_lookup": pmc["hbm_bytes_per_launch"] / lookups,
                     "fabric_GBps": pmc["hbm_bytes_per_launch"] / (kernel_ms * 1e-3) / 1e9,
                     "requests_per_lookup": (pmc["rdreq_per_launch"] or 0) / lookups,
-                    "requests_frac_of_ceiling": (pmc["rdreq_per_launch"] or 0) / (kernel_ms * 1e-3) /
-                    RANDOM_REQ_CEILING,
-                    "source": pmc["source"]}
+                    "source": pmc["source"], "source_hash": pmc["source_hash"]}
+        split = request_split(bpl, pmc, lookups, kernel_ms)
+        if split:  # mixed cache / HBM requests: each share against its own ceiling
+            r["pmc"]["requests_split"] = split
+        else:
+            r["pmc"]["requests_frac_of_ceiling"] = (pmc["rdreq_per_launch"] or 0) / (kernel_ms * 1e-3) / \
+                RANDOM_REQ_CEILING
     if extra:
         r.update(extra)
     return r
@@ -590,7 +640,9 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
         if own is not None:
             own.destroy_process_group()
         return {"workload": "configs[4]-shaped (sharded text)", "skipped": err or "setup failed on another rank"}
-    engine = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", chunks=args.shard_chunks)
+    # the capacity is agreed once for this batch size (max_nq): the steps run no collective
+    # beyond the exchanges, and at N = 1 the exchanges are the identity (no collective at all)
+    engine = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", chunks=args.shard_chunks, max_nq=nq)
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
@@ -605,7 +657,7 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     # the other step shape, for the next round's choice at N > 1 (where the exchanges cross
     # xGMI): the batch in 2 pieces (or in 1 if the main run used pieces), exchanges async
     alt_chunks = 2 if args.shard_chunks == 1 else 1
-    alt = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", chunks=alt_chunks)
+    alt = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", chunks=alt_chunks, max_nq=nq)
     out2 = torch.empty(nq, dtype=torch.int64, device=dev)
     el2 = timed_loop(lambda: alt.search_fixed(qbytes, m, check=False, out=out2), max(3, args.c4_steps // 2),
                      args.warmup, torch.cuda.synchronize, dist.barrier, reduce_max)
@@ -615,6 +667,19 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     if not int(same.item()):
         raise SystemExit("bench c4: the pieced step differs from the whole step")
     del out2
+    rccl1 = None
+    if ws == 1:  # the same step with the world-1 exchanges sent through RCCL (self copies)
+        eng1 = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", max_nq=nq, exchange_self=True)
+        out3 = torch.empty(nq, dtype=torch.int64, device=dev)
+        el3 = timed_loop(lambda: eng1.search_fixed(qbytes, m, check=False, out=out3), max(3, args.c4_steps // 2),
+                         args.warmup, torch.cuda.synchronize, dist.barrier, reduce_max)
+        eng1.assert_no_overflow()
+        if not bool(torch.equal(out, out3)):
+            raise SystemExit("bench c4: the RCCL world-1 exchange differs from the identity exchange")
+        rccl1 = {"ms_per_step": el3 / max(3, args.c4_steps // 2) * 1e3,
+                 "lookups_per_s": nq * max(3, args.c4_steps // 2) / el3, "identical": True,
+                 "what": "exchange_self: the count, query and position exchanges through the world-1 RCCL group"}
+        del out3
     occ = text[(out[:, None] + ar[None, :]).reshape(-1).clamp_(max=n - 1)]
     ok = torch.tensor([int(bool(torch.equal(occ, qbytes)))], dtype=torch.int32, device=dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
@@ -623,14 +688,18 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     cap = engine.capacity(-(-nq // max(1, args.shard_chunks)))  # per piece
     rec = {"workload": f"configs[4]-shaped: text of {ws} x {args.c4_share} chars sharded by SA rank ranges over "
                        f"{ws} GPU(s) (sas_build_part), {nq} len-{m} queries per GPU routed with RCCL "
-                       f"all_to_all_single (fixed-capacity buckets, 8-B packed PREFIX queries), positions back",
+                       f"all_to_all_single (fixed-capacity buckets, 8-B packed PREFIX queries, per-bucket counts "
+                       f"exchanged so only filled slots are searched), positions back"
+                       + (" -- at N = 1 every query is local: the exchanges are the identity, no collective "
+                          "(rccl_world1 times them through RCCL)" if ws == 1 else ""),
            "n": n, "parts": ws, "lookups_per_s": ws * nq * args.c4_steps / el, "ms_per_step": el / args.c4_steps * 1e3,
            "steps": args.c4_steps, "scaling": "weak", "part_sa_entries": st["sa_entries"],
            "prefix_entry_bytes": st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1),
            "bucket_capacity": cap, "pieces": args.shard_chunks,
            "alt_pieces": {"pieces": alt_chunks, "ms_per_step": el2 / max(3, args.c4_steps // 2) * 1e3,
                           "lookups_per_s": ws * nq * max(3, args.c4_steps // 2) / el2, "identical": True},
-           "exchange_bytes_per_step_per_rank": 2 * ws * cap * 8 * args.shard_chunks,
+           "exchange_bytes_per_step_per_rank": 2 * ws * cap * 8 * args.shard_chunks if ws > 1 else 0,
+           "rccl_world1": rccl1,
            "index_bytes": st["index_bytes"], "setup_s": setup, "verified": True}
     idx.free()
     del text, qbytes, out, occ
@@ -749,8 +818,8 @@ WORKLOADS = {
               "with p live) of {e}-B inline entries holding each bucket's first {k} suffixes "
               "({tb:.0f} GiB), then binary search over the fused {{32-char key, SA}} quad-leaf entries "
               "of the bucket; 2^30 text in HBM, 10^7 len-32 queries",
-    "plain": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112), top 12 levels from LDS, "
-             "levels 13-23 from a 128 MiB cache-resident pivot array",
+    "plain": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112): levels 1-{t1} from LDS, "
+             "levels {t1p}-{t2} from the {pb} pivot array ({where}), the rest read SA[mid] and a text window",
     "lcp": "configs[1] + mlr LCP skipping",
     "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (16-B {SA, Llcp, Rlcp, chars} entries)",
     "inline": "configs[1] probe sequence over fused {32-char key, SA} entries",
@@ -761,6 +830,16 @@ WORKLOADS = {
     "interp": "interpolation_search<16> (sas/sa_search.rs:376-421) over fused {32-char key, SA} entries",
     "tagged": "tagged SA entries + bucket table",
 }
+
+
+def plain_label(st: dict) -> str:
+    """configs[1]'s workload text from the index's own pivot depth (sas_stats.top2_levels)."""
+    t1, t2 = st["top_levels"], st["top2_levels"]
+    hbm = t2 > TOP2_CACHE_LEVELS
+    return WORKLOADS["plain"].format(
+        t1=t1, t1p=t1 + 1, t2=t2, pb=(f"{(16 << t2) >> 30} GiB" if (16 << t2) >= 1 << 30 else f"{(16 << t2) >> 20} MiB"),
+        where=(f"levels {t1 + 1}-{TOP2_CACHE_LEVELS} cache-resident, {TOP2_CACHE_LEVELS + 1}-{t2} one 16-B HBM entry "
+               f"each" if hbm else "cache-resident"))
 
 
 def main():
@@ -782,6 +861,10 @@ def main():
                     help="inline2: 32-B entries holding each range's first two suffixes, read by lane pairs "
                          "(4^16 x 32 B = 128 GiB); inline: 16-B entries with the first suffix (64 GiB); "
                          "ranks: u32 ranks only (sas/sa_search.rs:59-75's table)")
+    ap.add_argument("--c1-deep-levels", type=int, default=C1_DEEP_TOP2_LEVELS,
+                    help="configs[1]'s second figure: PLAIN with this many pivot-array levels (0: skip)")
+    ap.add_argument("--top2-levels", type=int, default=0,
+                    help="pivot-array depth of the headline index (SAS_BUILD_TOP2_LEVELS; 0 = library default 23)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the configs[3] sub-record")
@@ -840,11 +923,11 @@ def main():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             os.environ.setdefault("MASTER_PORT", "29517")
             dist.init_process_group("nccl", rank=0, world_size=1)
-        engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo, chunks=args.shard_chunks)
+        engine = ShardedSearch(idx, dist, ws, rank, dev, algo=args.algo, chunks=args.shard_chunks, max_nq=nq)
     else:
         idx = sas_amd.SaNaive.build(text, lcp=True, stree=True, prefix=args.prefix_chars,
                                     prefix_inline={"ranks": 0, "inline": 1, "inline2": 2,
-                                                   "inline4": 4}[args.prefix_table])
+                                                   "inline4": 4}[args.prefix_table], top2_levels=args.top2_levels)
     stats = idx.stats()
     off = rank_query_offsets(n, nq, m, rank)
     off_t = torch.from_numpy(off.astype(np.int64)).to(dev)
@@ -981,10 +1064,51 @@ def main():
         bpl = bytes_per_lookup("prefix" if v == "prefix_packed" else vbase, stats, n, m, vmean,
                                range_flag=bool(vfl), packed=v == "prefix_packed")
         key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector"}.get(v)
-        pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}") if key else None
+        pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}" + (f"_t{stats['top2_levels']}" if key == "plain" else "")) \
+            if key else None
         variants[v] = record(v, nq, vk, vel, bpl, stats["index_bytes"], pmc, vmean,
                              {"identical_to_headline": same, "lookups_per_s": ws * nq * vsteps / vel})
         log(f"variant {v}: {vk:.3f} ms")
+
+    # configs[1]'s second figure: the same PLAIN probe sequence on an index whose pivot array
+    # holds C1_DEEP_TOP2_LEVELS levels (SAS_BUILD_TOP2_LEVELS; 16 GiB at 30): levels past the
+    # cache-resident 23 read one 16-B HBM entry instead of an SA word and a text window
+    deep = None
+    if args.mode == "replicated" and "plain" in variants and args.c1_deep_levels:
+        didx = sas_amd.SaNaive.build(text, lcp=False, stree=False, sector=False, quad=False, llcp=False,
+                                     prefix=False, top2_levels=args.c1_deep_levels)
+        dst = didx.stats()
+        dout = torch.empty_like(out)
+
+        def dstep():
+            didx.search_fixed(qbytes, m, algo="plain", out=dout)
+        dsteps = max(3, args.steps // 4)
+        for _ in range(2):
+            dstep()
+        torch.cuda.synchronize()
+        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        tt = time.perf_counter()
+        d0.record(stream)
+        for _ in range(dsteps):
+            dstep()
+        d1.record(stream)
+        torch.cuda.synchronize()
+        del_s = time.perf_counter() - tt
+        dk = d0.elapsed_time(d1) / dsteps
+        if not bool(torch.equal(dout, headline_pos)):
+            raise SystemExit("bench: PLAIN on the deep pivot array differs from the headline")
+        _, dpr = didx.search_fixed(qbytes, m, algo="plain", probes=True)
+        dmean = float(dpr.double().mean().item())
+        dbpl = bytes_per_lookup("plain", dst, n, m, dmean)
+        deep = record("plain", nq, dk, del_s, dbpl, dst["index_bytes"],
+                      load_pmc(f"plain_n{n}_q{nq}_m{m}_t{dst['top2_levels']}"), dmean,
+                      {"identical_to_headline": True, "lookups_per_s": ws * nq * dsteps / del_s,
+                       "workload": plain_label(dst), "pivot_levels": dst["top2_levels"],
+                       "pivot_bytes": 16 << dst["top2_levels"]})
+        didx.free()
+        del dout, dpr
+        torch.cuda.empty_cache()
+        log(f"c1 plain, {dst['top2_levels']} pivot levels: {dk:.3f} ms")
 
     # occurrence ranges (Search::search_prefix / search_range, sas/util.rs:36-46): the rank
     # range [lo, hi) of each query's occurrences from the prefix table (inline slots first,
@@ -1047,7 +1171,10 @@ def main():
         log("c0 done")
     if args.mode == "replicated":
         if "plain" in variants:
-            configs["c1"] = dict(variants["plain"], workload=WORKLOADS["plain"])
+            configs["c1"] = dict(variants["plain"], workload=plain_label(stats),
+                                 pivot_levels=stats["top2_levels"], pivot_bytes=16 << stats["top2_levels"])
+            if deep is not None:
+                configs["c1"]["deep_pivots"] = deep
         best2 = max((v for v in ("quad", "sector", "stree") if v in variants),
                     key=lambda v: variants[v]["kernel_lookups_per_s"], default=None)
         if best2:
@@ -1107,9 +1234,10 @@ def main():
                 "kernel_ms": kernel_ms, "bytes_per_lookup": hbpl, "mean_probes": mean_probes,
                 # what bounds this path: random 128-B-line requests (PMC L2->fabric reads of this
                 # workload, query stream included), against the measured random-request ceiling
-                "requests": None if not head.get("pmc") else {
+                "requests": None if not (head.get("pmc") or {}).get("requests_per_lookup") else {
                     "per_lookup": head["pmc"]["requests_per_lookup"],
-                    "ceiling_per_s": RANDOM_REQ_CEILING, "frac": head["pmc"]["requests_frac_of_ceiling"]}},
+                    "ceiling_per_s": RANDOM_REQ_CEILING, "frac": head["pmc"]["requests_frac_of_ceiling"]},
+                "pmc_stale": bool((head.get("pmc") or {}).get("stale"))},
             "cpu_baseline": cpu,
             "e2e_host": e2e,
             "occurrence_ranges": ranges,

@@ -118,6 +118,15 @@ typedef struct sas_index sas_index;
                                         table beside 128 GiB of entries).  The entries
                                         replace the SA (sa_width 8).  Combines with LCP;
                                         not with the trees, LLCP or SAS_BUILD_PREFIX*  */
+#define SAS_BUILD_TOP2_LEVELS(L) ((uint32_t)(L) << 27) /* bits 27..31: depth L (1..31) of
+                                        the binary-search pivot array (PLAIN / LCP / INLINE /
+                                        LLCP): the pivots of the first L lockstep iterations,
+                                        one 16-B {32-char key, SA} entry each, 2^L x 16 B.
+                                        0 = the default, 23 levels (128 MiB, resident in the
+                                        256 MiB Infinity Cache); deeper levels are HBM reads
+                                        (one request instead of an SA word and a text window)
+                                        and cost 16 GiB at L = 30.  Clamped to the iteration
+                                        count; results never depend on L                   */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry
                                         {SA[m] 40 bits, Llcp 12 bits, Rlcp 12 bits, 16 chars
@@ -274,6 +283,23 @@ int sas_route_pack_cap(const sas_index* index, const uint64_t* splitter_pos, uin
 int sas_shard_gather(const sas_index* index, const uint64_t* back, const uint64_t* slot, uint64_t nq,
                      const uint64_t* counts, uint32_t nparts, uint64_t cap, uint64_t* out,
                      uint32_t* overflow, void* stream, uint32_t flags);
+
+/* The sharded step's local lookup over the received slots (device pointers only,
+ * SAS_DEVICE_PTRS): slot b*cap + j (b < nbuckets, j < cap) holds a query iff
+ * j < counts[b] (the counts each source rank sent, e.g. sas_route_pack_cap's out_counts
+ * after a count exchange); only those slots are searched and written, the others are
+ * skipped without a read.  queries: m bytes per slot, or with SAS_ROUTE_PACKED one u64
+ * 2-bit word per slot (SAS_ALGO_PREFIX, m <= 32).  Algorithms: PLAIN, LCP, LLCP, PREFIX,
+ * and QUAD for m <= 32 (ENOTSUP otherwise: search every slot with sas_search_fixed).
+ * EINVAL if nbuckets * cap >= 2^32.  Asynchronous on `stream`. */
+int sas_search_buckets(const sas_index* index, const void* queries, uint32_t m, uint32_t nbuckets,
+                       uint64_t cap, const uint64_t* counts, int algo, uint64_t* out_pos, void* stream,
+                       uint32_t flags);
+
+/* The source hash the library was built from (the Makefile's sha256 over csrc/ and
+ * include/, 16 hex digits): profiles record it, so counters collected on one build are
+ * never attached to another. */
+const char* sas_source_hash(void);
 
 int sas_get_stats(const sas_index* index, sas_stats* out);
 

@@ -32,16 +32,12 @@
 // 19, 4.70 with 21, 4.50 with 22, 4.27 with 23 (128 MiB, the levels that stay inside the
 // Infinity Cache; profiles/r2/ab_top2_depth.txt).  Past those, a level from HBM is still
 // one request instead of two: 3.81 ms with 25 levels, 3.58 with 26, 3.11 with 28, 2.71
-// with 30 (16 GiB at n = 2^30) and 31 (profiles/r2/ab_top2_deeper*.txt).  Levels past
-// SAS_TOP2_CACHE_LEVELS are built only into free HBM (SAS_TOP2_RESERVE left over).
-#ifndef SAS_TOP2_LEVELS
-#define SAS_TOP2_LEVELS 30
-#endif
+// with 30 (16 GiB at n = 2^30) and 31 (profiles/r2/ab_top2_deeper*.txt).  The depth is a
+// build parameter (SAS_BUILD_TOP2_LEVELS(L) in sas.h), never derived from free memory:
+// the default is the SAS_TOP2_CACHE_LEVELS cache-resident levels, deeper levels are the
+// caller's explicit choice (and an ENOMEM if they do not fit).
 #define SAS_TOP2_CACHE_LEVELS 23
-#ifndef SAS_TOP2_RESERVE
-#define SAS_TOP2_RESERVE (24ull << 30)
-#endif
-#define SAS_TOP2_NODES (1u << SAS_TOP2_LEVELS)
+#define SAS_TOP2_MAX_LEVELS 31
 #define SAS_STREE_B 16                // keys per node / branching factor - 1
 #define SAS_STREE_MAX_LAYERS 16
 #define SAS_STREE_LDS_NODES 1024      // <= 64 KiB of top S-tree layers in LDS
@@ -141,6 +137,7 @@ struct sas_index {
     uint32_t tag_p = 0;
     sas_stats stats = {};
     mutable StagePool* stage = nullptr;  // created by the first host-pointer search
+    mutable hipMemPool_t route_pool = nullptr;  // stream-ordered scratch of sas_route_pack (first use)
 };
 
 struct sst_index {

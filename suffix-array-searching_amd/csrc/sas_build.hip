@@ -1094,6 +1094,11 @@ static void free_index(sas_index* x) {
                      x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     sas_stage_pool_free(x->stage);
+    if (x->route_pool) {  // its blocks were freed stream-ordered: drain before destroying
+        (void)hipSetDevice(x->device);
+        (void)hipDeviceSynchronize();
+        (void)hipMemPoolDestroy(x->route_pool);
+    }
     delete x;
 }
 
@@ -1372,22 +1377,13 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         x->iters = iters;
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
         // the pivots of the first top2_levels iterations, 2^top2_levels 16-B entries: the
-        // SAS_TOP2_CACHE_LEVELS that stay inside the 256 MiB Infinity Cache (128 MiB), then
-        // deeper levels up to SAS_TOP2_LEVELS while free HBM leaves SAS_TOP2_RESERVE for the
-        // rest of the build (a tagged index's entries and bucket table) and the caller's
-        // batches.  The probe sequence, and so every result, is the same at any depth.
-        uint32_t lv = iters < SAS_TOP2_LEVELS ? iters : SAS_TOP2_LEVELS;
-        const uint32_t lv0 = iters < SAS_TOP2_CACHE_LEVELS ? iters : SAS_TOP2_CACHE_LEVELS;
-        if (lv > lv0) {
-            size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) != hipSuccess) {
-                (void)hipGetLastError();
-                fr = 0;
-            }
-            const uint64_t reserve =
-                SAS_TOP2_RESERVE + ((flags & SAS_BUILD_TAGGED) ? sa_n * 8 + ((32ull << 30) + 16) : 0);
-            while (lv > lv0 && ((uint64_t)16 << lv) + reserve > (uint64_t)fr) lv--;
-        }
+        // SAS_TOP2_CACHE_LEVELS that stay inside the 256 MiB Infinity Cache (128 MiB) unless
+        // the caller asks for another depth (SAS_BUILD_TOP2_LEVELS).  The depth is never
+        // taken from free memory, so a text always gets the same index.  The probe sequence,
+        // and so every result, is the same at any depth.
+        const uint32_t req = (flags >> 27) & 31u;
+        const uint32_t want = req ? req : SAS_TOP2_CACHE_LEVELS;
+        const uint32_t lv = iters < want ? iters : want;
         x->top2_levels = lv;
         const uint32_t nodes = 1u << x->top2_levels;
         DevBuf t2;

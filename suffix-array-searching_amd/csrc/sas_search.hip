@@ -89,7 +89,18 @@ struct SearchArgs {
     uint64_t* out_pos;
     uint32_t* out_probes;
     uint32_t* bad;
+    const uint64_t* bcounts; // sas_search_buckets: queries per bucket (null: every slot is a query)
+    uint32_t bcap;           // slots per bucket
 };
+
+// sas_search_buckets (the sharded step's received slots): slot i is place i % bcap of
+// bucket i / bcap, and only places below that bucket's count hold a query; the others are
+// skipped (no reads, no output).  The host checks nq = buckets x bcap < 2^32.
+__device__ __forceinline__ bool slot_live(const SearchArgs& a, uint64_t i) {
+    if (!a.bcounts) return true;
+    const uint32_t b = (uint32_t)i / a.bcap;
+    return (uint64_t)((uint32_t)i - b * a.bcap) < a.bcounts[b];
+}
 
 __device__ __forceinline__ void query_ptr(const SearchArgs& a, uint64_t i, const uint8_t** qb, uint32_t* m) {
     if (a.qoff) {
@@ -173,6 +184,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
     const uint64_t n = a.n;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!slot_live(a, i)) continue;
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
@@ -928,6 +940,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
     uint32_t bad = 0;
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
     for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
+        if (!slot_live(a, i)) continue;  // group-uniform: the 4 lanes share i
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
@@ -1209,6 +1222,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
     const uint64_t sa_n = a.sa_n;
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (uint64_t)gridDim.x * blockDim.x) {
+        if (!slot_live(a, i)) continue;
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
@@ -1322,7 +1336,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / G;
     // fixed 32-char queries at 16-B aligned addresses: the pair splits each query load
     const bool split = SAS_PREFIX_SPLITQ && G == 2 && QW == 1 && a.qoff == nullptr && a.qwords == nullptr &&
-                       a.m_fixed == 32 &&
+                       a.m_fixed == 32 && a.bcounts == nullptr &&
                        (((uintptr_t)a.qbytes) & 15) == 0;
     auto qload = [&](uint64_t k) -> uint4 {
         const uint4* p = reinterpret_cast<const uint4*>(a.qbytes + k * 32) + sub;
@@ -1332,6 +1346,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     uint4 vnext = make_uint4(0, 0, 0, 0);
     if (SAS_PREFIX_QPREFETCH && split && i0 < a.nq) vnext = qload(i0);
     for (uint64_t i = i0; i < a.nq; i += stride) {
+        if (!slot_live(a, i)) continue;  // group-uniform: the G lanes share i
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
@@ -2624,6 +2639,38 @@ extern "C" int sas_search_packed(const sas_index* x, const uint64_t* qwords, uin
     return launch_search(x, a, algo, 1, flags, st);
 }
 
+extern "C" int sas_search_buckets(const sas_index* x, const void* queries, uint32_t m, uint32_t nbuckets,
+                                  uint64_t cap, const uint64_t* counts, int algo, uint64_t* out_pos, void* stream,
+                                  uint32_t flags) {
+    if (!x) SAS_FAIL(EINVAL, "sas_search_buckets: null index");
+    TRY_RC(check_algo(x, algo, flags & ~SAS_PREFIX_RANGE, "sas_search_buckets"));
+    if (!(flags & SAS_DEVICE_PTRS)) SAS_FAIL(EINVAL, "sas_search_buckets: device pointers only (SAS_DEVICE_PTRS)");
+    if (flags & SAS_PREFIX_RANGE) SAS_FAIL(EINVAL, "sas_search_buckets: SAS_PREFIX_RANGE is not supported");
+    const bool packed = (flags & SAS_ROUTE_PACKED) != 0;
+    if (m == 0 || (packed && (m > 32 || algo != SAS_ALGO_PREFIX)))
+        SAS_FAIL(EINVAL, "sas_search_buckets: m >= 1; packed words need SAS_ALGO_PREFIX and m <= 32");
+    // the kernels that skip unfilled slots: one lane (or one lane group) per query
+    const bool ok = algo == SAS_ALGO_PLAIN || algo == SAS_ALGO_LCP || algo == SAS_ALGO_LLCP ||
+                    algo == SAS_ALGO_PREFIX || (algo == SAS_ALGO_QUAD && m <= 32);
+    if (!ok || x->sa_w == 8) SAS_FAIL(ENOTSUP, "sas_search_buckets: PLAIN, LCP, LLCP, PREFIX, or QUAD with m <= 32");
+    const uint64_t nq = (uint64_t)nbuckets * cap;
+    if (nq == 0) return 0;
+    if (cap >= (1ull << 32) || nq >= (1ull << 32)) SAS_FAIL(EINVAL, "sas_search_buckets: buckets x cap >= 2^32");
+    if (!queries || !counts || !out_pos) SAS_FAIL(EINVAL, "sas_search_buckets: null argument");
+    HIP_TRY(hipSetDevice(x->device));
+    SearchArgs a{};
+    fill_args(x, a);
+    a.nq = nq;
+    a.m_fixed = m;
+    a.bad = x->scratch;  // device pointers: codes unchecked, as sas_search_fixed without SAS_VALIDATE
+    if (packed) a.qwords = static_cast<const uint64_t*>(queries);
+    else a.qbytes = static_cast<const uint8_t*>(queries);
+    a.out_pos = out_pos;
+    a.bcounts = counts;
+    a.bcap = (uint32_t)cap;
+    return launch_search(x, a, algo, packed ? 1 : qw_for(m), flags, static_cast<hipStream_t>(stream));
+}
+
 extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint32_t m, uint64_t nq, int algo,
                               uint64_t* d_out_pos, int reps, void* stream, uint32_t flags, double* kernel_ns,
                               double* call_ns) {
@@ -2972,21 +3019,26 @@ __global__ void k_pack_totals(const uint64_t* __restrict__ base_slot, uint32_t W
     }
 }
 
-// The per-step scratch of a sharded step comes from the stream-ordered allocator; a release
-// threshold of "never" keeps the freed blocks in the device's default pool for the next
-// step instead of returning them to the driver at every synchronisation.
-static void keep_async_pool(int device) {
+// The scratch of an exact (variable-size) sharded step comes from a stream-ordered pool
+// owned by the index (created on first use, destroyed by sas_free).  Its release threshold
+// of "never" keeps freed blocks for the next step; the device's default pool, which other
+// libraries in the process share, is left alone.
+static int route_pool(const sas_index* x, hipMemPool_t* out) {
     static std::mutex mu;
-    static uint64_t done = 0;  // bit per device
     std::lock_guard<std::mutex> g(mu);
-    if (device < 64 && (done >> device) & 1) return;
-    hipMemPool_t pool;
-    if (hipDeviceGetDefaultMemPool(&pool, device) == hipSuccess) {
+    if (!x->route_pool) {
+        hipMemPoolProps pp{};
+        pp.allocType = hipMemAllocationTypePinned;
+        pp.location.type = hipMemLocationTypeDevice;
+        pp.location.id = x->device;
+        hipMemPool_t pool = nullptr;
+        HIP_TRY(hipMemPoolCreate(&pool, &pp));
         uint64_t thr = UINT64_MAX;
-        (void)hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr);
+        HIP_TRY(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &thr));
+        x->route_pool = pool;
     }
-    (void)hipGetLastError();
-    if (device < 64) done |= 1ull << device;
+    *out = x->route_pool;
+    return 0;
 }
 
 static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uint32_t nsplit,
@@ -3032,7 +3084,8 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
         HIP_TRY(hipGetLastError());
         return 0;
     }
-    keep_async_pool(x->device);
+    hipMemPool_t pool;
+    TRY_RC(route_pool(x, &pool));
     // with splitters the routing reads each query anyway and packs it on the way (words);
     // without (one part) the routing reads nothing and the scatter packs from the bytes
     const bool pack_in_route = packed && nsplit > 0;
@@ -3043,10 +3096,10 @@ static int route_pack_impl(const sas_index* x, const uint64_t* splitter_pos, uin
     size_t tbytes = 0;
     HIP_TRY(rocprim::exclusive_scan(nullptr, tbytes, (uint64_t*)nullptr, (uint64_t*)nullptr, (uint64_t)0,
                                     (size_t)(nblk * W), rocprim::plus<uint64_t>(), st));
-    HIP_TRY(hipMallocAsync(&dest, nq * 4, st));
-    HIP_TRY(hipMallocAsync(&cnt, nblk * W * 8, st));
-    HIP_TRY(hipMallocAsync(&tmp, tbytes ? tbytes : 8, st));
-    if (pack_in_route) HIP_TRY(hipMallocAsync(&words, nq * 8, st));
+    HIP_TRY(hipMallocFromPoolAsync(&dest, nq * 4, pool, st));
+    HIP_TRY(hipMallocFromPoolAsync(&cnt, nblk * W * 8, pool, st));
+    HIP_TRY(hipMallocFromPoolAsync(&tmp, tbytes ? tbytes : 8, pool, st));
+    if (pack_in_route) HIP_TRY(hipMallocFromPoolAsync(&words, nq * 8, pool, st));
     if (pack_in_route)
         hipLaunchKernelGGL(k_route_count<true>, dim3((unsigned)nblk), dim3(PACK_BLOCK), 0, st, x->text_w, x->n,
                            splitter_pos, nsplit, qbytes, m, nq, nblk, static_cast<uint64_t*>(cnt),

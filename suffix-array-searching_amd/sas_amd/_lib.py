@@ -42,6 +42,13 @@ SAS_BUILD_PREFIX_INLINE4 = 1 << 22
 SAS_BUILD_TAGGED = 1 << 23
 
 
+def SAS_BUILD_TOP2_LEVELS(levels: int) -> int:
+    """Depth of the binary-search pivot array (sas.h SAS_BUILD_TOP2_LEVELS; 0 = default 23)."""
+    if not 0 <= int(levels) <= 31:
+        raise ValueError(f"top2_levels must be in 0..31, not {levels}")
+    return int(levels) << 27
+
+
 def SAS_BUILD_PREFIX_P(p: int) -> int:
     return (int(p) & 31) << 16
 
@@ -128,6 +135,8 @@ def lib():
     L.sas_route_pack.argtypes = [vp, vp, u32, vp, u32, u64, vp, vp, vp, vp, u32]
     L.sas_route_pack_cap.argtypes = [vp, vp, u32, vp, u32, u64, u64, vp, vp, vp, vp, u32]
     L.sas_shard_gather.argtypes = [vp, vp, vp, u64, vp, u32, u64, vp, vp, vp, u32]
+    L.sas_search_buckets.argtypes = [vp, vp, u32, u32, u64, vp, i32, vp, vp, u32]
+    L.sas_source_hash.restype = C.c_char_p
     L.sas_route_batch.argtypes = [vp, vp, u32, vp, vp, vp, u64, vp, vp, u32]
     L.sas_build_multi.argtypes = [vp, u64, vp, i32, i32, u32, C.POINTER(vp)]
     L.sas_extract.argtypes = [vp, vp, vp, vp, u64, vp, vp, u32]
@@ -169,3 +178,8 @@ def lib():
 def check(rc: int):
     if rc != 0:
         raise SasError(rc, lib().sas_last_error().decode())
+
+
+def source_hash() -> str:
+    """The source hash compiled into the loaded libsas_amd.so (sas_source_hash)."""
+    return lib().sas_source_hash().decode()

@@ -98,7 +98,7 @@ class SaNaive:
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool | None = None,
               sa40: bool = False, quad: bool | str | None = None, llcp: bool | None = None,
               prefix: bool | int | None = None, prefix_inline: bool | int = False,
-              tagged: bool | int = False) -> "SaNaive":
+              tagged: bool | int = False, top2_levels: int = 0) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
@@ -112,7 +112,9 @@ class SaNaive:
         SAS_BUILD_PREFIX_INLINE2); fused quad leaves, u32 SA.  tagged: the SA as 8-B tagged
         entries + a bucket table over the first p chars (SAS_BUILD_TAGGED; True = p chosen by
         the library, an int = that p) for algo="tagged"; it replaces the SA and leaves out the
-        trees, LLCP and the prefix tables (their defaults turn off)."""
+        trees, LLCP and the prefix tables (their defaults turn off).  top2_levels: depth of
+        the binary-search pivot array (SAS_BUILD_TOP2_LEVELS; 0 = the library default, the
+        23 cache-resident levels; 30 = 16 GiB of HBM-resident pivots at n = 2^30)."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         if tagged is not False:
@@ -128,6 +130,7 @@ class SaNaive:
         flags |= _lib.SAS_BUILD_LLCP if llcp else 0
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         flags |= _lib.SAS_BUILD_SA40 if sa40 else 0
+        flags |= _lib.SAS_BUILD_TOP2_LEVELS(top2_levels)
         flags |= _quad_flags(quad) | _prefix_flags(prefix, quad, n if rank_range is None else rank_range[1] - rank_range[0],
                                                    prefix_inline)
         sa_ptr, sa_w = None, 4
@@ -154,7 +157,8 @@ class SaNaive:
     @classmethod
     def build_part(cls, t, part: int, parts: int, lcp: bool = True, stree: bool = True, verify: bool = False,
                    flags: int = 0, sector: bool = True, quad: bool | str = True, llcp: bool | None = None,
-                   prefix: bool | int | None = None, prefix_inline: bool | int = False) -> "SaNaive":
+                   prefix: bool | int | None = None, prefix_inline: bool | int = False,
+                   top2_levels: int = 0) -> "SaNaive":
         """Sharded-text index that builds ONLY its own SA rank range (sas_build_part):
         part `part` of `parts` contiguous 7-char-prefix bin ranges.  The range is
         chosen by the library (stats: rank_lo, sa_entries, next_pos).  prefix_inline as in
@@ -165,6 +169,7 @@ class SaNaive:
         flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
         llcp = (n < (1 << 31)) if llcp is None else llcp
         flags |= _quad_flags(quad) | (_lib.SAS_BUILD_LLCP if llcp else 0) | _prefix_flags(prefix, quad, n, prefix_inline)
+        flags |= _lib.SAS_BUILD_TOP2_LEVELS(top2_levels)
         if _is_cuda(t):
             flags |= _lib.SAS_DEVICE_PTRS
         h = C.c_void_p()
@@ -251,6 +256,28 @@ class SaNaive:
         check(lib().sas_search_packed(self._h, qwords.ctypes.data, m, nq, _lib.ALGOS[algo], out.ctypes.data,
                                       pr.ctypes.data if probes else None, None, 0))
         return (out[:nq], pr[:nq]) if probes else out[:nq]
+
+    def search_buckets(self, queries, m: int, cap: int, counts, algo: str = "prefix", out=None, stream=None):
+        """The sharded step's local lookup (sas_search_buckets): `queries` holds
+        counts.numel() buckets of `cap` slots (uint8, m bytes a slot, or int64 2-bit words
+        for PREFIX with m <= 32), bucket b's first counts[b] slots are queries; only those
+        are searched and written into `out` (int64, one per slot).  torch CUDA tensors."""
+        import torch
+        nb = int(counts.numel())
+        packed = queries.dtype == torch.int64
+        need = nb * cap * (1 if packed else m)
+        if counts.dtype != torch.int64 or not counts.is_contiguous() or queries.numel() < need or \
+                not queries.is_contiguous() or (not packed and queries.dtype != torch.uint8):
+            raise ValueError("search_buckets: int64 counts, and uint8 bytes or int64 words for every slot")
+        if out is None:
+            out = torch.empty(nb * cap, dtype=torch.int64, device=queries.device)
+        if out.dtype != torch.int64 or out.numel() < nb * cap:
+            raise ValueError("search_buckets: int64 out of one entry per slot")
+        st = stream if stream is not None else torch.cuda.current_stream(queries.device).cuda_stream
+        fl = _lib.SAS_DEVICE_PTRS | (_lib.SAS_ROUTE_PACKED if packed else 0)
+        check(lib().sas_search_buckets(self._h, _ptr(queries), m, nb, int(cap), _ptr(counts), _lib.ALGOS[algo],
+                                       _ptr(out), st, fl))
+        return out
 
     def route(self, splitter_pos, qbytes, m: int, stream=None):
         """Sharded mode: shard id of each fixed-length query = number of splitter
@@ -353,6 +380,9 @@ class SaNaive:
         import torch
         if not (_is_cuda(qoff) and _is_cuda(qlen)):
             raise ValueError("search_slices: torch CUDA qoff / qlen")
+        if qoff.dtype != torch.int64 or qlen.dtype != torch.int32 or not qoff.is_contiguous() or \
+                not qlen.is_contiguous() or qoff.numel() != qlen.numel():
+            raise ValueError("search_slices: contiguous int64 qoff and int32 qlen of the same length")
         nq = int(qoff.numel())
         if out is None:
             out = torch.empty(nq, dtype=torch.int64, device=qoff.device)

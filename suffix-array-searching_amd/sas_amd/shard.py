@@ -16,11 +16,22 @@ shard); rank ranges keep each answer on exactly one shard.  The collective is
 gloo in the CPU tests).  Payload per query: m bytes out, 8 bytes back.
 
 Fixed-capacity buckets (cap = nq * slack / W per destination, agreed by all ranks) make
-both exchanges equal-split, so a step issues no host synchronisation: no count exchange,
-no .tolist().  A bucket that overflows its cap is detected on the device; with
-`check=True` (the default) the step reads that one flag and redoes itself with exact
-variable-size exchanges, so results are always exact; `check=False` defers the flag to
-`assert_no_overflow()` (the bench calls it once after its timed loop).
+both exchanges equal-split, so a step issues no host synchronisation: no .tolist(), no
+.item().  The per-bucket counts cross in a W-element all-to-all beside the queries, and the
+local lookup searches only the filled slots of each received bucket (sas_search_buckets),
+so the ranks together search exactly the queries they were given, not W * cap slots each.
+A bucket that overflows its cap is detected on the device; with `check=True` (the default)
+the step reads that one flag and redoes itself with exact variable-size exchanges, so
+results are always exact; `check=False` defers the flag to `assert_no_overflow()` (the
+bench calls it once after its timed loop).
+
+The capacity is agreed by a collective that every rank runs: once, in the constructor, for
+a declared `max_nq` (steps of at most that many queries then run no extra collective), or
+at the start of every step otherwise.  Ranks may pass different batch sizes either way.
+
+At world size 1 every query is the rank's own: the exchanges are the identity, so the step
+routes, searches and gathers with no collective (`exchange_self=True` sends them through the
+process group anyway, which is how the world-1 RCCL test exercises the exchange path).
 """
 from __future__ import annotations
 
@@ -34,55 +45,73 @@ class ShardedSearch:
     """`index` needs: .route(splitters, qbytes, m) -> dest shard per query,
     .search_fixed(qbytes, m, algo=...) -> positions (int64), .suffix_array(1) ->
     its first SA value; the GPU implementation (sas_amd.SaNaive) also has
-    .route_pack(splitters, qbytes, m, cap=None) (the fused send side)."""
+    .route_pack(splitters, qbytes, m, cap=None) (the fused send side),
+    .search_buckets(recv, m, cap, counts, algo=...) (the bounded local lookup) and
+    .shard_gather(back, slot, ...) (the receive side)."""
 
     SLACK = 1.125  # bucket capacity over the balanced share
 
     def __init__(self, index, dist, world: int, rank: int, device, algo: str = "stree", group=None,
-                 slack: float | None = None, min_cap: int = 256, chunks: int = 1):
+                 slack: float | None = None, min_cap: int = 256, chunks: int = 1, max_nq: int | None = None,
+                 exchange_self: bool = False):
         """chunks > 1: a step cuts its batch into that many pieces and overlaps one piece's
         exchanges (all_to_all_single with async_op, on the collective's own stream) with
-        another's routing, lookup and gather.  Every rank must use the same value."""
+        another's routing, lookup and gather.  Every rank must use the same value.
+        max_nq: the largest batch any step of this rank will pass; the bucket capacity is then
+        agreed here, once (a collective every rank runs), and steps add none.  Without it every
+        step agrees on its capacity first (one all_reduce and a host read per step)."""
         import torch
         self.chunks = max(1, int(chunks))
         self.index, self.dist, self.world, self.rank = index, dist, world, rank
         self.device, self.algo, self.group = device, algo, group
         self.slack = self.SLACK if slack is None else slack
         self.min_cap = min_cap
+        self.exchange = world > 1 or exchange_self
         first = torch.tensor([int(index.suffix_array(1)[0])], dtype=torch.int64, device=device)
         firsts = [torch.empty_like(first) for _ in range(world)]
         dist.all_gather(firsts, first, group=group)
         # first suffix of shards 1..W-1, in increasing suffix order
         self.splitters = torch.cat(firsts[1:]).to(torch.int64) if world > 1 else torch.empty(0, dtype=torch.int64,
                                                                                               device=device)
-        self._caps = {}  # nq -> capacity agreed by every rank
         self._bufs = {}
         self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
+        self.max_nq = None if max_nq is None else int(max_nq)
+        self._cap_fixed = None
+        if self.max_nq is not None:
+            self._cap_fixed = self._agree(self._local_cap(-(-self.max_nq // self.chunks)))
 
     # ---------------------------------------------------------------- capacity
-    def capacity(self, nq: int) -> int:
-        """Per-destination bucket capacity for a batch of nq queries: every rank must use
-        the same one (equal all-to-all splits), so it is the MAX over ranks, agreed once
-        per batch size."""
+    def _local_cap(self, nq: int) -> int:
+        if self.world == 1:
+            return max(nq, 1)
+        return max(1, min(nq, int(nq * self.slack / self.world) + self.min_cap))
+
+    def _agree(self, cap: int) -> int:
+        """MAX over ranks (a collective: every rank calls it at the same point)."""
         import torch
-        if nq not in self._caps:
-            if self.world == 1:
-                cap = nq
-            else:
-                cap = min(nq, int(nq * self.slack / self.world) + self.min_cap)
-            t = torch.tensor([max(cap, 1)], dtype=torch.int64, device=self.device)
-            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
-            self._caps[nq] = int(t.item())
-        return self._caps[nq]
+        t = torch.tensor([cap], dtype=torch.int64, device=self.device)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+        return int(t.item())
+
+    def capacity(self, nq: int) -> int:
+        """Per-destination bucket capacity for a piece of nq queries: every rank must use the
+        same one (equal all-to-all splits).  With max_nq it is the constructor's agreed value
+        (no collective); otherwise the MAX over ranks of each rank's own need, agreed now --
+        every rank runs this collective at the start of every step, whatever its nq."""
+        if self._cap_fixed is not None:
+            if nq > -(-self.max_nq // self.chunks):
+                raise ValueError(f"ShardedSearch: a piece of {nq} queries exceeds max_nq={self.max_nq}")
+            return self._cap_fixed
+        return self._agree(self._local_cap(nq))
 
     def packed(self, m: int) -> bool:
         """Queries cross the exchange as 8-B 2-bit words (SAS_ROUTE_PACKED) when the local
         lookup takes them: PREFIX, m <= 32 (4x less all-to-all traffic at m = 32)."""
         return self.algo == "prefix" and m <= 32 and hasattr(self.index, "search_packed")
 
-    def _buffers(self, nq: int, m: int, cap: int, piece: int = 0):
+    def _buffers(self, m: int, cap: int, piece: int = 0):
         import torch
-        key = (nq, m, piece)
+        key = (m, cap, piece)
         if key not in self._bufs:
             W = self.world
             if self.packed(m):
@@ -92,10 +121,36 @@ class ShardedSearch:
                 q = {"send": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device),
                      "recv": torch.zeros(W * cap * m, dtype=torch.uint8, device=self.device)}
             self._bufs[key] = dict(q, back=torch.empty(W * cap, dtype=torch.int64, device=self.device),
-                                   local=torch.empty(W * cap, dtype=torch.int64, device=self.device))
+                                   local=torch.empty(W * cap, dtype=torch.int64, device=self.device),
+                                   rcounts=torch.empty(W, dtype=torch.int64, device=self.device))
         return self._bufs[key]
 
     # ---------------------------------------------------------------- steps
+    def _forward(self, buf, send, counts, async_op=False):
+        """Queries (and their per-bucket counts) to their owners.  Returns the received
+        slots, the received counts and the pending works."""
+        if not self.exchange:  # world 1: the exchange is the identity
+            return send, counts, []
+        w1 = self.dist.all_to_all_single(buf["rcounts"], counts, group=self.group, async_op=async_op)
+        w2 = self.dist.all_to_all_single(buf["recv"], send, group=self.group, async_op=async_op)
+        return buf["recv"], buf["rcounts"], [w for w in (w1, w2) if w is not None]
+
+    def _lookup(self, buf, recv, rcounts, m: int, cap: int):
+        """The local lookup of the filled received slots (positions into buf["local"])."""
+        pk = self.packed(m)
+        if hasattr(self.index, "search_buckets"):
+            return self.index.search_buckets(recv, m, cap, rcounts, algo="prefix" if pk else self.algo,
+                                             out=buf["local"])
+        if pk:  # without the bounded lookup every slot is searched
+            return self.index.search_packed(recv, m, algo="prefix", out=buf["local"])
+        return self.index.search_fixed(recv, m, algo=self.algo, out=buf["local"])
+
+    def _backward(self, buf, local, async_op=False):
+        if not self.exchange:
+            return local, None
+        w = self.dist.all_to_all_single(buf["back"], local, group=self.group, async_op=async_op)
+        return buf["back"], w
+
     def search_fixed(self, qbytes, m: int, check: bool = True, out=None):
         """qbytes: uint8 tensor [nq*m] of this rank's queries -> int64 positions (written
         into `out` when given)."""
@@ -106,28 +161,25 @@ class ShardedSearch:
         import torch
         nq = qbytes.numel() // m
         cap = self.capacity(nq)
-        buf = self._buffers(nq, m, cap)
+        buf = self._buffers(m, cap)
         pk = self.packed(m)
         counts, send, slot = self.index.route_pack(self.splitters, qbytes, m, cap=cap, send=buf["send"],
                                                    **({"packed": True} if pk else {}))
-        self.dist.all_to_all_single(buf["recv"], send, group=self.group)
-        if pk:
-            self.index.search_packed(buf["recv"], m, algo="prefix", out=buf["local"])
-        else:
-            self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
-        self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group)
+        recv, rcounts, _ = self._forward(buf, send, counts)
+        local = self._lookup(buf, recv, rcounts, m, cap)
+        back, _ = self._backward(buf, local)
         # one flag per step (check) or the sticky one (deferred to assert_no_overflow)
         flag = torch.zeros(1, dtype=torch.int32, device=self.device) if check else self.overflow
         if hasattr(self.index, "shard_gather"):  # gather + overflow test in one kernel
-            out = self.index.shard_gather(buf["back"], slot, out=out, counts=counts, cap=cap, overflow=flag)
+            out = self.index.shard_gather(back, slot, out=out, counts=counts, cap=cap, overflow=flag)
         else:
             flag |= (counts > cap).any().reshape(1).to(torch.int32)
-            out = torch.index_select(buf["back"], 0, slot, out=out) if out is not None else \
-                buf["back"].index_select(0, slot)
+            out = torch.index_select(back, 0, slot, out=out) if out is not None else back.index_select(0, slot)
         if check:
             # agreed by all (an overflow anywhere changes every rank's exchange): redo the
             # step with exact splits
-            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
+            if self.world > 1:
+                self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
             if int(flag.item()):
                 exact = self.search_fixed_exact(qbytes, m)
                 return out.copy_(exact) if out is not None else exact
@@ -150,25 +202,25 @@ class ShardedSearch:
         pieces = []
         for c in range(C):
             s0, s1 = min(nq, c * cs), min(nq, (c + 1) * cs)
-            buf = self._buffers(cs, m, cap, c)
+            buf = self._buffers(m, cap, c)
             counts, send, slot = self.index.route_pack(self.splitters, qbytes[s0 * m:s1 * m], m, cap=cap,
                                                        send=buf["send"], **({"packed": True} if pk else {}))
-            w = self.dist.all_to_all_single(buf["recv"], send, group=self.group, async_op=True)
-            pieces.append((s0, s1, buf, counts, slot, w))
+            recv, rcounts, works = self._forward(buf, send, counts, async_op=True)
+            pieces.append((s0, s1, buf, counts, slot, recv, rcounts, works))
         back = []
-        for s0, s1, buf, counts, slot, w in pieces:
-            w.wait()
-            if pk:
-                self.index.search_packed(buf["recv"], m, algo="prefix", out=buf["local"])
-            else:
-                self.index.search_fixed(buf["recv"], m, algo=self.algo, out=buf["local"])
-            back.append(self.dist.all_to_all_single(buf["back"], buf["local"], group=self.group, async_op=True))
-        for (s0, s1, buf, counts, slot, _), w in zip(pieces, back):
-            w.wait()
+        for s0, s1, buf, counts, slot, recv, rcounts, works in pieces:
+            for w in works:
+                w.wait()
+            local = self._lookup(buf, recv, rcounts, m, cap)
+            back.append(self._backward(buf, local, async_op=True))
+        for (s0, s1, buf, counts, slot, *_), (bk, w) in zip(pieces, back):
+            if w is not None:
+                w.wait()
             if s1 > s0:
-                self.index.shard_gather(buf["back"], slot, out=out[s0:s1], counts=counts, cap=cap, overflow=flag)
+                self.index.shard_gather(bk, slot, out=out[s0:s1], counts=counts, cap=cap, overflow=flag)
         if check:
-            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
+            if self.world > 1:
+                self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
             if int(flag.item()):
                 return out.copy_(self.search_fixed_exact(qbytes, m))
         return out
@@ -176,13 +228,12 @@ class ShardedSearch:
     def assert_no_overflow(self):
         """After steps run with check=False: every bucket fitted its capacity (so every
         result was exact)."""
-        import torch
         flag = self.overflow.clone()
-        self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
+        if self.world > 1:
+            self.dist.all_reduce(flag, op=self.dist.ReduceOp.MAX, group=self.group)
         if int(flag.item()):
             raise RuntimeError("ShardedSearch: a bucket overflowed its capacity in a check=False step; "
                                "raise slack or run with check=True")
-
     def search_fixed_exact(self, qbytes, m: int):
         """Variable-size exchanges (counts first): exact for any routing, two host syncs."""
         import torch

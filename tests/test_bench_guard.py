@@ -72,3 +72,52 @@ def test_byte_model_splits_served_levels():
     h = bench.bytes_per_lookup("prefix", st, n, m, 1.0)
     assert h["hbm"] == 32 + m + 8 and h["cache"] == 0 and h["lds"] == 0
     assert bench._tree_layers(n, 4, 64, 17, 64, 8)[-1] == n // 4 * 64
+
+
+def test_byte_model_hbm_pivot_levels():
+    """The deep pivot array (SAS_BUILD_TOP2_LEVELS = 30): levels 13-23 cache-resident, 24-30
+    one 16-B HBM entry each, level 31 an SA word + a text window; requests by tier."""
+    st = {"sa_width": 4, "top_levels": 12, "top2_levels": 30}
+    n, m = 1 << 30, 32
+    p30 = bench.bytes_per_lookup("plain", st, n, m, 31.0)
+    assert p30["lds"] == 12 * 12 and p30["cache"] == 11 * 16
+    assert p30["hbm"] == 7 * 16 + 1 * (4 + m / 4) + m + 8
+    assert p30["requests_model"] == {"cache": 11.0, "hbm": 7 + 2 * 1 + m / 128}
+    # fewer probes than the pivot levels (a short range): no SA-level term
+    p20 = bench.bytes_per_lookup("plain", st, n, m, 20.0)
+    assert p20["hbm"] == m + 8 and p20["cache"] == 8 * 16
+    # INLINE stays on the cache-resident 23 levels whatever the array holds (launch_search)
+    pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
+    assert pin["hbm"] == 8 * 16 + m + 8 and pin["requests_model"]["hbm"] == 8 + m / 128
+    # the split: model HBM requests first, the rest of the PMC count is cache-served
+    bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
+    assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
+    nq, kms = 10_000_000, 5.0
+    sp = bench.request_split(bpl, {"rdreq_per_launch": 20.0 * nq}, nq, kms)
+    assert abs(sp["hbm_per_lookup"] - 16.25) < 1e-9 and abs(sp["cache_per_lookup"] - 3.75) < 1e-9
+    floor = nq * (16.25 / bench.RANDOM_REQ_CEILING + 3.75 / bench.CACHE_REQ_CEILING)
+    assert abs(sp["frac"] - floor / (kms * 1e-3)) < 1e-12 and sp["frac"] < 1
+    assert bench.request_split(bench.bytes_per_lookup("prefix", {"sa_width": 4, "prefix_bytes": (4 ** 16 + 1) * 32,
+                                                                  "prefix_chars": 16, "quad_entry_bytes": 16},
+                                                      n, m, 1.0), {"rdreq_per_launch": 1.0}, nq, kms) is None
+
+
+def test_pmc_attached_only_for_the_same_source_hash(tmp_path, monkeypatch):
+    import json
+    import sas_amd
+    prof = tmp_path / "profiles"
+    prof.mkdir()
+    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    json.dump({"hbm_bytes_per_launch": 1e9, "TCC_EA0_RDREQ": 1e7, "source_hash": sas_amd.source_hash()},
+              open(prof / "pmc_same.json", "w"))
+    json.dump({"hbm_bytes_per_launch": 1e9, "TCC_EA0_RDREQ": 1e7, "source_hash": "0000000000000000"},
+              open(prof / "pmc_other.json", "w"))
+    json.dump({"hbm_bytes_per_launch": 1e9, "TCC_EA0_RDREQ": 1e7}, open(prof / "pmc_unstamped.json", "w"))
+    assert bench.load_pmc("same")["hbm_bytes_per_launch"] == 1e9
+    assert bench.load_pmc("other")["stale"] and bench.load_pmc("unstamped")["stale"]
+    assert bench.load_pmc("missing") is None
+    bpl = {"hbm": 100.0, "cache": 0.0, "lds": 0.0}
+    r = bench.record("x", 10, 1.0, 1.0, bpl, 0, bench.load_pmc("other"), 1.0)
+    assert r["pmc"]["stale"] and "fabric_bytes_per_lookup" not in r["pmc"]
+    r = bench.record("x", 10, 1.0, 1.0, bpl, 0, bench.load_pmc("same"), 1.0)
+    assert r["pmc"]["fabric_bytes_per_lookup"] == 1e8

@@ -83,6 +83,7 @@ class OracleShard:
         self.n = len(t)
         self.sa = sa_full[lo:hi]
         self.next = int(sa_full[hi]) if hi < self.n else self.n
+        self.searched = 0  # slots searched by search_buckets
 
     def suffix_array(self, count):
         return self.sa[:count]
@@ -128,6 +129,19 @@ class OracleShard:
         if out is None:
             return res
         out.copy_(res)
+        return out
+
+    def search_buckets(self, recv, m, cap, counts, algo=None, out=None):
+        """sas_search_buckets semantics: only the first counts[b] slots of bucket b are
+        searched and written; the rest of `out` is left alone.  Counts the lookups."""
+        import torch
+        if out is None:
+            out = torch.full((counts.numel() * cap,), -1, dtype=torch.int64)
+        for b, c in enumerate(counts.tolist()):
+            c = min(int(c), cap)
+            if c:
+                out[b * cap:b * cap + c] = self._search(recv[b * cap * m:(b * cap + c) * m], m)
+            self.searched += c
         return out
 
     def search_fixed(self, qbytes, m, algo=None, out=None):
@@ -197,6 +211,23 @@ def shard_worker(rank, ws, port, res):
     tight3.search_fixed(skew, m, check=False)
     with pytest.raises(RuntimeError):
         tight3.assert_no_overflow()
+    # the bounded lookup: the ranks together search exactly the queries they were given (not
+    # W * cap slots each); ranks pass different batch sizes, and change them between steps,
+    # with the per-step capacity agreement and with a declared max_nq
+    for mx in (None, nq):
+        shard = OracleShard(t, sa, lo, hi)
+        eng2 = ShardedSearch(shard, dist, ws, rank, "cpu", max_nq=mx)
+        total = 0
+        for step in range(3):
+            k = nq - 17 * ((rank + step) % 3)  # differs across ranks and steps
+            got = eng2.search_fixed(dq[:k * m], m)
+            assert got.tolist() == exact.tolist()[:k]
+            total += k
+        both = torch.tensor([shard.searched, total], dtype=torch.int64)
+        dist.all_reduce(both)
+        assert both[0] == both[1], (int(both[0]), int(both[1]))
+    with pytest.raises(ValueError):
+        ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", max_nq=10).search_fixed(dq, m)
     res[rank] = (qs.tolist(), pos.tolist())
     dist.destroy_process_group()
 

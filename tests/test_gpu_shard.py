@@ -54,9 +54,12 @@ def test_sharded_nccl_world1(sas):
         qb = queries(t, nq, m, 1)
         expect = full.search_fixed(qb, m, algo="plain")
         dq = torch.from_numpy(qb).cuda()
-        for algo, chunks in (("plain", 1), ("quad", 1), ("prefix", 1), ("prefix", 3), ("plain", 2)):
-            # prefix: 8-B packed words cross the exchange; chunks > 1: async RCCL pieces
-            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo, chunks=chunks)
+        for algo, chunks, xself in (("plain", 1, True), ("quad", 1, True), ("prefix", 1, True), ("prefix", 3, True),
+                                    ("plain", 2, True), ("prefix", 1, False), ("prefix", 2, False)):
+            # prefix: 8-B packed words cross the exchange; chunks > 1: async RCCL pieces;
+            # exchange_self: the world-1 exchanges still go through RCCL (default: identity)
+            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo, chunks=chunks,
+                                exchange_self=xself, max_nq=nq if chunks == 1 else None)
             assert eng.packed(m) == (algo == "prefix")
             got = eng.search_fixed(dq, m)
             got2 = eng.search_fixed(dq, m, check=False)
@@ -67,6 +70,78 @@ def test_sharded_nccl_world1(sas):
                 assert np.array_equal(g.cpu().numpy().astype(np.uint64), expect), algo
     finally:
         dist.destroy_process_group()
+
+
+def test_search_buckets_skips_unfilled_slots(sas):
+    """sas_search_buckets: bucket b's first counts[b] slots are searched (positions equal
+    sas_search_fixed's), the rest are neither read nor written; counts > cap means the
+    whole bucket.  Bytes and packed words, PLAIN / QUAD / PREFIX."""
+    import torch
+    n, m, cap = 300_007, 32, 1000
+    t = sas.random_string(n, seed=31)
+    idx = sas.SaNaive.build(torch.from_numpy(t).cuda(), prefix=10, prefix_inline=2)
+    counts = torch.tensor([0, 1, 999, 1000, 5000, 17], dtype=torch.int64, device="cuda")
+    nb = counts.numel()
+    qb = torch.from_numpy(queries(t, nb * cap, m, 4)).cuda()
+    words = sas.SaNaive.pack_queries(qb, m)
+    live = (torch.arange(nb * cap, device="cuda") % cap) < torch.repeat_interleave(counts.clamp(max=cap), cap)
+    for algo in ("plain", "quad", "prefix"):
+        expect = idx.search_fixed(qb, m, algo=algo)
+        for q in ((qb, words) if algo == "prefix" else (qb,)):
+            out = torch.full((nb * cap,), -7, dtype=torch.int64, device="cuda")
+            idx.search_buckets(q, m, cap, counts, algo=algo, out=out)
+            torch.cuda.synchronize()
+            assert torch.equal(out[live], expect[live]), algo
+            assert bool((out[~live] == -7).all()), algo
+            assert int(live.sum()) == 0 + 1 + 999 + 1000 + 1000 + 17
+    with pytest.raises(sas.SasError):  # SECTOR has no bounded kernel: ENOTSUP
+        idx.search_buckets(qb, m, cap, counts, algo="sector")
+
+
+def test_c4_record_shape_world1(sas):
+    """The configs[4] record's exact shape at N = 1: a 2^30-char text, its one part built
+    with sas_build_part and the two-suffix inline table (p = 16), 10^7 len-32 queries
+    through ShardedSearch with the packed exchange (RCCL world-1 group, both the forced
+    exchange and the default identity), positions bit-identical to the replicated index's
+    PREFIX output (built first, searched, freed: the two indexes do not fit together)."""
+    import torch
+    import torch.distributed as dist
+    from sas_amd.shard import ShardedSearch
+    n, nq, m = 1 << 30, 10_000_000, 32
+    text = sas.random_string(n, seed=31416, device="cuda")
+    full = sas.SaNaive.build(text, lcp=False, stree=False, sector=False, llcp=False, prefix=16, prefix_inline=2)
+    off = torch.from_numpy(sas.random_queries(n, nq, seed=31416, word_pos=n, margin=200, len_lo=m,
+                                              len_hi=m + 1)[0].astype(np.int64)).cuda()
+    ar = torch.arange(m, device="cuda", dtype=torch.int64)
+    qb = torch.empty(nq * m, dtype=torch.uint8, device="cuda")
+    for s0 in range(0, nq, 1 << 18):
+        e0 = min(nq, s0 + (1 << 18))
+        qb[s0 * m:e0 * m] = text[(off[s0:e0, None] + ar[None, :]).reshape(-1)]
+    expect = full.search_fixed(qb, m, algo="prefix")
+    torch.cuda.synchronize()
+    full.free()
+    torch.cuda.empty_cache()
+    part = sas.SaNaive.build_part(text, 0, 1, lcp=False, stree=False, sector=False, quad=True, llcp=False,
+                                  prefix=16, prefix_inline=2)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        for xself in (True, False):
+            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo="prefix", max_nq=nq,
+                                exchange_self=xself)
+            assert eng.packed(m)
+            out = torch.empty(nq, dtype=torch.int64, device="cuda")
+            for _ in range(2):
+                eng.search_fixed(qb, m, check=False, out=out)
+            eng.assert_no_overflow()
+            torch.cuda.synchronize()
+            assert torch.equal(out, expect), xself
+    finally:
+        dist.destroy_process_group()
+        part.free()
 
 
 class Loopback:

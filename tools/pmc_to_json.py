@@ -24,14 +24,18 @@ from __future__ import annotations
 import argparse
 import csv
 import json
+import re
 from collections import defaultdict
 
 
 def per_dispatch(path, kernel):
+    """Counter sums per dispatch of `kernel` (the name itself, then its template arguments or
+    parameter list: k_sa_prefix2 does not match k_sa_prefix2_range)."""
+    pat = re.compile(r"(^|[^\w])" + re.escape(kernel) + r"\s*[<(]")
     vals = defaultdict(lambda: defaultdict(float))
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel not in row.get("Kernel_Name", ""):
+            if not pat.search(row.get("Kernel_Name", "")):
                 continue
             vals[row["Dispatch_Id"]][row["Counter_Name"]] += float(row["Counter_Value"])
     return vals
@@ -52,10 +56,20 @@ def main():
     ap.add_argument("--req")
     ap.add_argument("--out", required=True)
     ap.add_argument("--algo-bytes", type=float, default=None, help="algorithmic bytes per lookup")
+    ap.add_argument("--source-hash", default=None,
+                    help="source hash of the library the counters were collected on (default: the in-tree "
+                         "libsas_amd.so's sas_source_hash); bench.py reports the counters only for that build")
     a = ap.parse_args()
     fetch_kib, nf = mean_counter(a.fetch, a.kernel, "FETCH_SIZE")
     write_kib, nw = mean_counter(a.write, a.kernel, "WRITE_SIZE")
-    out = {"kernel": a.kernel, "dispatches_fetch": nf, "dispatches_write": nw,
+    if a.source_hash is None:
+        import os
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                        "suffix-array-searching_amd"))
+        import sas_amd
+        a.source_hash = sas_amd.source_hash()
+    out = {"kernel": a.kernel, "source_hash": a.source_hash, "dispatches_fetch": nf, "dispatches_write": nw,
            "FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib}
     read_bytes = 2 * fetch_kib * 1024 if fetch_kib is not None else None
     out["read_bytes_2xFETCH"] = read_bytes
