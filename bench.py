@@ -391,11 +391,13 @@ def cpu_baseline(text_dev, idx, qbytes_dev, m, nq, seconds: float):
             "cores_note": (f"{threads} = this process's CPU share (OMP_NUM_THREADS); the affinity mask shows {aff} "
                            f"hardware threads of the whole machine, shared with the other GPUs' processes")
             if threads < aff else "every CPU of the affinity mask",
-            # not measured (the box's share is `threads`): the whole machine at this run's
-            # per-thread rate, linear in threads -- an upper bound, since the search is bound
-            # by memory latency and the sockets' memory channels are shared
-            "whole_machine_model": {"threads": aff, "value": rate / threads * aff,
-                                    "basis": f"{rate / threads:.4g} lookups/s per thread at {threads} threads x {aff}"},
+            # every affinity CPU is deliberately not used: the GPU box allots each GPU's
+            # process a 16-core share (it exports OMP_NUM_THREADS=16) and its operating rules
+            # size worker pools to that share, the other CPUs serving the other GPUs' jobs
+            "all_affinity_value": None,
+            "all_affinity_note": (f"not measured: the box's rules cap this process's worker pools at its "
+                                  f"{threads}-core share of the {aff} affinity CPUs" if threads < aff else
+                                  "the measured value uses every affinity CPU"),
             "sample": f"oracle/{algo} (restates sas/sa_search.rs "
                       f"{'98-112' if algo == 'binary_search' else '198-239 batch_c<16>'}) on {sample} of the "
                       f"same len-{m} queries over the same 2^{int(np.log2(n))} text/SA ({reps} passes), {dt:.1f} s, "

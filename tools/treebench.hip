@@ -152,6 +152,67 @@ __global__ __launch_bounds__(1024, 8) void k_chain_ilp2(const uint8_t* __restric
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// TB_MIXED=G: one lookup per LANE; cooperative levels (W > 1000) are read by the lane's
+// group of G for each of its G lookups in turn (G independent 16-B loads per lane, issued
+// together, one request per node), per-lane levels by the lane alone (the k_sa_quad4x
+// pattern).  TB_QBYTES=B: each lookup first reads B query bytes, a wave's 64 queries as one
+// contiguous span with coalesced 16-B loads (the wave-staged queries of k_sa_tagged).
+template <int G>
+__global__ __launch_bounds__(256, 5) void k_chain_mixed(const uint8_t* __restrict__ p, Layout lay, uint64_t lookups,
+                                                        uint32_t seed, uint32_t* out, const uint8_t* __restrict__ qb,
+                                                        uint32_t qbytes) {
+    uint32_t acc = 0;
+    const uint32_t sub = threadIdx.x % G, lane = threadIdx.x & 63;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < lookups;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t h = mix(i * 0x9E3779B97F4A7C15ull + seed);
+        uint32_t dep = 0;
+        if (qb) {
+            const uint64_t wbase = (i - lane) * qbytes;
+            uint32_t x = 0;
+            for (uint32_t o = lane * 16; o < 64 * qbytes; o += 64 * 16) {
+                const u32x4 v = *reinterpret_cast<const u32x4*>(qb + wbase + o);
+                x ^= v.x ^ v.w;
+            }
+            h ^= (uint64_t)(x & 0x80000000u);
+        }
+        for (int l = 0; l < lay.L; l++) {
+            h = h * 0x9E3779B97F4A7C15ull + l + (dep & 0x80000000u);
+            if (lay.width[l] > 1000) {
+                const int wb = lay.width[l] - 1000;
+                u32x4 t[G];
+#pragma unroll
+                for (int k = 0; k < G; k++) {
+                    const uint64_t hk = __shfl(h, (int)((lane & ~(uint32_t)(G - 1)) + k), 64);
+                    const u32x4* node = reinterpret_cast<const u32x4*>(p + lay.base[l] + node_idx_coop(hk, lay.units[l]) * wb);
+                    t[k] = node[sub % (wb / 16)];
+                }
+                uint32_t mine = 0;
+#pragma unroll
+                for (int k = 0; k < G; k++) {
+                    uint32_t d = t[k].x ^ t[k].y ^ t[k].z ^ t[k].w;
+                    for (int o = 1; o < G; o <<= 1) d ^= __shfl_xor(d, o, G);
+                    mine = (sub == (uint32_t)k) ? d : mine;
+                }
+                dep = mine;
+                continue;
+            }
+            const uint64_t node = ((h >> 32) * lay.units[l]) >> 32;
+            const u32x4* v = reinterpret_cast<const u32x4*>(p + lay.base[l] + node * lay.width[l]);
+            if (lay.width[l] < 16) {
+                dep = lay.width[l] == 8 ? (uint32_t)*reinterpret_cast<const uint64_t*>(v)
+                                        : *reinterpret_cast<const uint32_t*>(v);
+                continue;
+            }
+            u32x4 t = __builtin_nontemporal_load(v);
+            if (lay.width[l] >= 32) t ^= __builtin_nontemporal_load(v + 1);
+            dep = t.x ^ t.y ^ t.z ^ t.w;
+        }
+        acc ^= dep;
+    }
+    if (acc == 0x12345678u) out[0] = acc;
+}
+
 int main(int argc, char** argv) {
     if (argc < 4) { fprintf(stderr, "usage: treebench <lookups> <reps> <layout>...\n"); return 2; }
     uint64_t lookups = strtoull(argv[1], 0, 10);
@@ -230,6 +291,12 @@ int main(int argc, char** argv) {
         CHECK(hipMalloc(&rbuf, lookups * 8));
         io = Io{qbuf, rbuf};
     }
+    const uint32_t mqb = getenv("TB_QBYTES") ? (uint32_t)atoi(getenv("TB_QBYTES")) : 0;
+    uint8_t* mq = nullptr;
+    if (mqb) {
+        CHECK(hipMalloc(&mq, lookups * mqb + 1024));
+        CHECK(hipMemset(mq, 1, lookups * mqb + 1024));
+    }
     for (size_t k = 0; k < lays.size(); k++) {
         for (int nt = 0; nt < 1; nt++) {
             Layout L = lays[k];
@@ -238,8 +305,14 @@ int main(int argc, char** argv) {
             for (int l = 0; l < L.L; l++) if (L.width[l] > 1000) G = (L.width[l] - 1000) / 16 > G ? (L.width[l] - 1000) / 16 : G;
             bool ilp2 = getenv("TB_ILP2") != nullptr;
             bool xcdp = getenv("TB_XCD") != nullptr;
+            const int mixed = getenv("TB_MIXED") ? atoi(getenv("TB_MIXED")) : 0;
             auto launch = [&](uint32_t sd) {
-                if (xcdp) hipLaunchKernelGGL(k_chain_xcd, grd, blk, 0, 0, p, L, lookups, sd, out);
+                if (mixed) {
+                    const dim3 b2(256), g2(cus * 5);
+                    if (mixed == 8) hipLaunchKernelGGL(k_chain_mixed<8>, g2, b2, 0, 0, p, L, lookups, sd, out, mq, mqb);
+                    else if (mixed == 4) hipLaunchKernelGGL(k_chain_mixed<4>, g2, b2, 0, 0, p, L, lookups, sd, out, mq, mqb);
+                    else hipLaunchKernelGGL(k_chain_mixed<1>, g2, b2, 0, 0, p, L, lookups, sd, out, mq, mqb);
+                } else if (xcdp) hipLaunchKernelGGL(k_chain_xcd, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else if (ilp2) hipLaunchKernelGGL(k_chain_ilp2, grd, blk, 0, 0, p, L, lookups, sd, out);
                 else if (G == 8) hipLaunchKernelGGL(k_chain<8>, grd, blk, 0, 0, p, L, lookups, sd, out, io);
                 else if (G == 4) hipLaunchKernelGGL(k_chain<4>, grd, blk, 0, 0, p, L, lookups, sd, out, io);
