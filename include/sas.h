@@ -127,6 +127,18 @@ typedef struct sas_index sas_index;
                                         (one request instead of an SA word and a text window)
                                         and cost 16 GiB at L = 30.  Clamped to the iteration
                                         count; results never depend on L                   */
+#define SAS_BUILD_TAG_LINES (1u << 24) /* with SAS_BUILD_TAGGED: the tagged entries as one
+                                        128-B line per p-char bucket {first rank 40 bits |
+                                        count 24 bits, overflow offset, the 14 entries of ranks
+                                        first .. first + 13} (slots past the bucket's count hold
+                                        the next buckets' first suffixes, so the line ends with
+                                        the answer to "every suffix of the bucket is < q") plus
+                                        an overflow array with ranks first + 14 .. first + count
+                                        of the larger buckets.  A lookup reads its line as one
+                                        request of an 8-lane group: bucket and first entries
+                                        together.  p = SAS_BUILD_PREFIX_P or ceil(log4 n) - 2
+                                        (15 at n = 2^34: 128 GiB of lines, ~16 suffixes each).
+                                        No SA array: TAGGED lookups, ranges and sas_copy_sa64 */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry
                                         {SA[m] 40 bits, Llcp 12 bits, Rlcp 12 bits, 16 chars
@@ -206,6 +218,10 @@ typedef struct sas_stats {
     uint64_t tag_table_bytes; /* SAS_BUILD_TAGGED bucket table, (4^p + 1) x 8 B       */
     uint64_t index_bytes;    /* every HBM array of the index together (text, SA or tagged
                                 entries, LCP, LLCP, trees, tables, top2)              */
+    uint32_t tag_line_slots; /* SAS_BUILD_TAG_LINES: entries per 128-B bucket line (14), else 0;
+                                tag_table_bytes is then the lines, sa_bytes the overflow */
+    uint32_t reserved0;
+    uint64_t tag_overflow_entries; /* SAS_BUILD_TAG_LINES: entries in the overflow array */
 } sas_stats;
 
 const char* sas_last_error(void);

@@ -135,6 +135,13 @@ struct sas_index {
     // min(rank count of key x, 2^24 - 1) << 40} for x in [0, 4^tag_p]
     uint64_t* tag_table = nullptr;
     uint32_t tag_p = 0;
+    // SAS_BUILD_TAG_LINES (no SA, no tag_table): line b = 16 u64 {first rank | min(count,
+    // 2^24 - 1) << 40, overflow offset, entries of ranks first .. first + SAS_TL_SLOTS - 1}
+    // (an entry past sa_n is SAS_TL_END); tag_ovf holds ranks first + SAS_TL_SLOTS .. first +
+    // count of every bucket with count >= SAS_TL_SLOTS, bucket after bucket
+    uint64_t* tag_lines = nullptr;
+    uint64_t* tag_ovf = nullptr;
+    uint64_t tag_ovf_n = 0;
     sas_stats stats = {};
     mutable StagePool* stage = nullptr;  // created by the first host-pointer search
     mutable hipMemPool_t route_pool = nullptr;  // stream-ordered scratch of sas_route_pack (first use)
@@ -169,6 +176,8 @@ struct sst_index {
 // W = 8: the tagged SA of SAS_BUILD_TAGGED, u64 entries {SA 40 bits | 12 chars << 40}
 // (sas_build.hip, build_tagged): the SA value is the low 40 bits.
 #define SAS_TAG_CHARS 12
+#define SAS_TL_SLOTS 14                  // entries per 128-B bucket line (SAS_BUILD_TAG_LINES)
+#define SAS_TL_END ((1ull << 40) - 1)    // entry standing for rank sa_n (the answer is next_pos)
 template <int W>
 struct SaView {
     const uint8_t* p;

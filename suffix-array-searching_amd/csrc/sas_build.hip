@@ -995,13 +995,16 @@ __global__ void k_tag_entries(const uint64_t* __restrict__ tw, SaView<W> sa, uin
     }
 }
 
-__device__ __forceinline__ uint64_t tag_key(const uint64_t* tw, const uint64_t* ent, uint64_t r, uint32_t p) {
-    return text_chars32(tw, ent[r] & (SAS_SA40_MAX - 1)) >> (64 - 2 * p);
+// p-char key of the suffix at rank r (S: SaView<4|5> over an SA, SaView<8> over tagged entries)
+template <class S>
+__device__ __forceinline__ uint64_t tag_key(const uint64_t* tw, S ent, uint64_t r, uint32_t p) {
+    return text_chars32(tw, ent[r]) >> (64 - 2 * p);
 }
 
 // Rank r with a new p-char key fills table(key(r-1), key(r)] = r (rank sa_n fills the rest
 // up to 4^p); gaps longer than PT_SMALL go to a list that whole workgroups fill.
-__global__ void k_tt_fill(const uint64_t* __restrict__ tw, const uint64_t* __restrict__ ent, uint64_t sa_n,
+template <class S>
+__global__ void k_tt_fill(const uint64_t* __restrict__ tw, S ent, uint64_t sa_n,
                           uint32_t p, uint64_t* __restrict__ table, uint64_t* __restrict__ big,
                           unsigned long long* __restrict__ nbig, uint64_t big_cap) {
     const uint64_t top = 1ull << (2 * p);
@@ -1071,9 +1074,8 @@ static int build_tagged(sas_index* x, uint32_t p) {
     TRY(big.alloc(cap * 24, "bucket table gap list"));
     TRY(nbig.alloc(8, "bucket table gap count"));
     HIP_TRY(hipMemset(nbig.p, 0, 8));
-    const uint64_t* ep = reinterpret_cast<const uint64_t*>(x->sa);
-    hipLaunchKernelGGL(k_tt_fill, dim3(grid_for(sa_n + 1)), b, 0, 0, x->text_w, ep, sa_n, p, t.as<uint64_t>(),
-                       big.as<uint64_t>(), nbig.as<unsigned long long>(), cap);
+    hipLaunchKernelGGL(k_tt_fill<SaView<8>>, dim3(grid_for(sa_n + 1)), b, 0, 0, x->text_w, SaView<8>{x->sa}, sa_n, p,
+                       t.as<uint64_t>(), big.as<uint64_t>(), nbig.as<unsigned long long>(), cap);
     hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(),
                        t.as<uint64_t>());
     hipLaunchKernelGGL(k_tt_count, dim3(grid_for(keys)), b, 0, 0, t.as<uint64_t>(), keys);
@@ -1091,7 +1093,7 @@ static int build_tagged(sas_index* x, uint32_t p) {
 static void free_index(sas_index* x) {
     if (!x) return;
     void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->scratch, x->sec_inner,
-                     x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table};
+                     x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table, x->tag_lines, x->tag_ovf};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     sas_stage_pool_free(x->stage);
     if (x->route_pool) {  // its blocks were freed stream-ordered: drain before destroying
@@ -1146,8 +1148,202 @@ static int verify_sa(const uint64_t* tw, uint64_t n, const uint8_t* sa, uint32_t
 
 extern "C" int sas_verify(const sas_index* index) {
     if (!index) SAS_FAIL(EINVAL, "sas_verify: null index");
+    if (index->tag_lines)
+        SAS_FAIL(ENOTSUP, "sas_verify: a bucket-line index holds no SA array (verify at build: SAS_BUILD_VERIFY)");
     HIP_TRY(hipSetDevice(index->device));
     return verify_sa(index->text_w, index->n, index->sa, index->sa_w, index->sa_n, index->sa_n == index->n);
+}
+
+// ------------------------------------------------------------------ bucket lines
+// SAS_BUILD_TAG_LINES: the tagged entries as one 128-B line per p-char bucket (common.hpp,
+// sas_index::tag_lines): {first rank | min(count, 2^24 - 1) << 40, overflow offset, entries of
+// ranks first .. first + 13}, and the overflow array with ranks first + 14 .. first + count of
+// every bucket of >= 14 suffixes.  Built from the SA: first ranks (k_tt_fill), overflow
+// offsets (a block scan of max(count - 13, 0)), then every slot and overflow entry computed
+// from SA[r] and its text.  Peak: the SA, the lines, the first-rank table, then the overflow
+// array after the table is gone.
+#define TL_BLOCK 1024
+#define TL_PER 4  // buckets per thread in the offset scan
+
+template <int W>
+__device__ __forceinline__ uint64_t tl_make(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint64_t r,
+                                            uint32_t p) {
+    if (r >= sa_n) return SAS_TL_END;
+    const uint64_t s = sa[r];
+    return s | (((text_chars32(tw, s) << (2 * p)) >> 40) << 40);
+}
+
+// overflow entries of bucket b: ranks first + 14 .. first + count (the last, rank first + count,
+// is the next bucket's first suffix)
+__device__ __forceinline__ uint64_t tl_ovf_need(const uint64_t* __restrict__ t, uint64_t b) {
+    const uint64_t c = t[b + 1] - t[b];
+    return c >= SAS_TL_SLOTS ? c - SAS_TL_SLOTS + 1 : 0;
+}
+
+__device__ __forceinline__ uint64_t tl_block_excl_scan(uint64_t v, uint64_t* lds, uint64_t* total) {
+    const uint32_t lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+    uint64_t inc = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t t = (uint64_t)__shfl_up((long long)inc, o, 64);
+        if (lane >= (uint32_t)o) inc += t;
+    }
+    if (lane == 63) lds[wid] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (uint32_t w = 0; w < nw; w++) {
+            const uint64_t t = lds[w];
+            lds[w] = acc;
+            acc += t;
+        }
+        lds[nw] = acc;
+    }
+    __syncthreads();
+    *total = lds[nw];
+    return lds[wid] + inc - v;
+}
+
+__global__ __launch_bounds__(TL_BLOCK) void k_tl_sums(const uint64_t* __restrict__ t, uint64_t keys,
+                                                      uint64_t* __restrict__ bsum) {
+    __shared__ uint64_t lds[TL_BLOCK / 64 + 1];
+    const uint64_t b0 = ((uint64_t)blockIdx.x * TL_BLOCK + threadIdx.x) * TL_PER;
+    uint64_t v = 0;
+    for (int k = 0; k < TL_PER; k++)
+        if (b0 + k < keys) v += tl_ovf_need(t, b0 + k);
+    uint64_t tot;
+    tl_block_excl_scan(v, lds, &tot);
+    if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
+}
+
+// headers: line b's first rank | count and overflow offset (bsum: exclusive block offsets);
+// line `keys` is a terminal header {sa_n} so a saturated count reads the next line's rank
+__global__ __launch_bounds__(TL_BLOCK) void k_tl_hdr(const uint64_t* __restrict__ t, uint64_t keys,
+                                                     const uint64_t* __restrict__ bsum, uint64_t* __restrict__ lines) {
+    __shared__ uint64_t lds[TL_BLOCK / 64 + 1];
+    const uint64_t b0 = ((uint64_t)blockIdx.x * TL_BLOCK + threadIdx.x) * TL_PER;
+    uint64_t need[TL_PER], v = 0;
+    for (int k = 0; k < TL_PER; k++) {
+        need[k] = b0 + k < keys ? tl_ovf_need(t, b0 + k) : 0;
+        v += need[k];
+    }
+    uint64_t tot;
+    uint64_t off = bsum[blockIdx.x] + tl_block_excl_scan(v, lds, &tot);
+    for (int k = 0; k < TL_PER; k++) {
+        const uint64_t b = b0 + k;
+        if (b < keys) {
+            const uint64_t first = t[b], c = t[b + 1] - first;
+            lines[b * 16] = first | ((c < 0xFFFFFFull ? c : 0xFFFFFFull) << 40);
+            lines[b * 16 + 1] = off;
+            off += need[k];
+        } else if (b == keys) {
+            lines[b * 16] = t[b];
+            lines[b * 16 + 1] = 0;
+        }
+    }
+}
+
+template <int W>
+__global__ void k_tl_slots(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint64_t keys,
+                           uint64_t* __restrict__ lines) {
+    GRID_STRIDE(k, keys * SAS_TL_SLOTS) {
+        const uint64_t b = k / SAS_TL_SLOTS, j = k - b * SAS_TL_SLOTS;
+        const uint64_t first = lines[b * 16] & (SAS_SA40_MAX - 1);
+        lines[b * 16 + 2 + j] = tl_make<W>(tw, sa, sa_n, first + j, p);
+    }
+}
+
+template <int W>
+__global__ void k_tl_ovf(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint64_t keys,
+                         const uint64_t* __restrict__ lines, uint64_t* __restrict__ ovf) {
+    GRID_STRIDE(b, keys) {
+        const uint64_t first = lines[b * 16] & (SAS_SA40_MAX - 1);
+        const uint64_t c = (lines[(b + 1) * 16] & (SAS_SA40_MAX - 1)) - first;
+        if (c < SAS_TL_SLOTS) continue;
+        const uint64_t o = lines[b * 16 + 1];
+        for (uint64_t j = SAS_TL_SLOTS; j <= c; j++) ovf[o + j - SAS_TL_SLOTS] = tl_make<W>(tw, sa, sa_n, first + j, p);
+    }
+}
+
+template <int W>
+static int build_tag_lines_w(sas_index* x, uint32_t p) {
+    const uint64_t sa_n = x->sa_n, keys = 1ull << (2 * p);
+    const dim3 b(256);
+    // 1. first rank of every bucket (the tagged table's fill, from the SA)
+    const uint64_t cap = (keys + 1) / (PT_SMALL + 1) + 2;
+    DevBuf t, big, nbig;
+    TRY(t.alloc((keys + 1) * 8 + 8, "bucket first ranks"));
+    TRY(big.alloc(cap * 24, "bucket table gap list"));
+    TRY(nbig.alloc(8, "bucket table gap count"));
+    HIP_TRY(hipMemset(nbig.p, 0, 8));
+    hipLaunchKernelGGL(k_tt_fill<SaView<W>>, dim3(grid_for(sa_n + 1)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p,
+                       t.as<uint64_t>(), big.as<uint64_t>(), nbig.as<unsigned long long>(), cap);
+    hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(),
+                       t.as<uint64_t>());
+    HIP_TRY(hipGetLastError());
+    uint64_t nb = 0;
+    HIP_TRY(hipMemcpy(&nb, nbig.p, 8, hipMemcpyDeviceToHost));
+    if (nb > cap) SAS_FAIL(EFAULT, "bucket lines: gap list overflow");
+    big.alloc(0, "free");
+    // 2. overflow offsets: block sums, their exclusive scan, the headers
+    const uint64_t per_blk = (uint64_t)TL_BLOCK * TL_PER;
+    const uint64_t nblk = (keys + 1 + per_blk - 1) / per_blk;
+    DevBuf bsum, tmp, lines;
+    TRY(bsum.alloc(nblk * 8, "bucket lines block sums"));
+    hipLaunchKernelGGL(k_tl_sums, dim3((unsigned)nblk), dim3(TL_BLOCK), 0, 0, t.as<uint64_t>(), keys,
+                       bsum.as<uint64_t>());
+    HIP_TRY(hipGetLastError());
+    uint64_t last = 0;
+    HIP_TRY(hipMemcpy(&last, bsum.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost));
+    size_t tb = 0;
+    HIP_TRY(rocprim::exclusive_scan(nullptr, tb, bsum.as<uint64_t>(), bsum.as<uint64_t>(), (uint64_t)0, (size_t)nblk,
+                                    rocprim::plus<uint64_t>(), (hipStream_t)0));
+    TRY(tmp.alloc(tb ? tb : 8, "scan scratch"));
+    HIP_TRY(rocprim::exclusive_scan(tmp.p, tb, bsum.as<uint64_t>(), bsum.as<uint64_t>(), (uint64_t)0, (size_t)nblk,
+                                    rocprim::plus<uint64_t>(), (hipStream_t)0));
+    uint64_t lastx = 0;
+    HIP_TRY(hipMemcpy(&lastx, bsum.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost));
+    const uint64_t novf = lastx + last;
+    TRY(lines.alloc((keys + 1) * 128, "bucket lines"));
+    hipLaunchKernelGGL(k_tl_hdr, dim3((unsigned)nblk), dim3(TL_BLOCK), 0, 0, t.as<uint64_t>(), keys,
+                       bsum.as<uint64_t>(), lines.as<uint64_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    t.alloc(0, "free");
+    bsum.alloc(0, "free");
+    tmp.alloc(0, "free");
+    // 3. the slots and the overflow entries, from the SA and the text
+    DevBuf ovf;
+    TRY(ovf.alloc(novf * 8 + 32, "bucket lines overflow"));
+    HIP_TRY(hipMemset(ovf.as<uint8_t>() + novf * 8, 0, 32));  // pair loads may read 2 entries past the end
+    hipLaunchKernelGGL(k_tl_slots<W>, dim3(grid_for(keys * SAS_TL_SLOTS)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n,
+                       p, keys, lines.as<uint64_t>());
+    hipLaunchKernelGGL(k_tl_ovf<W>, dim3(grid_for(keys)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, keys,
+                       lines.as<uint64_t>(), ovf.as<uint64_t>());
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipDeviceSynchronize());
+    // the lines and the overflow hold every SA value: the plain SA goes
+    (void)hipFree(x->sa);
+    x->sa = nullptr;
+    x->sa_w = 8;
+    x->tag_lines = lines.as<uint64_t>();
+    lines.release();
+    x->tag_ovf = ovf.as<uint64_t>();
+    ovf.release();
+    x->tag_ovf_n = novf;
+    x->tag_p = p;
+    return 0;
+}
+
+static int build_tag_lines(sas_index* x, uint32_t p) {
+    if (p == 0) {
+        uint32_t l4 = 0;  // ceil(log4(sa_n)) - 2: ~4-16 suffixes per line
+        while (l4 < 32 && (1ull << (2 * l4)) < x->sa_n) l4++;
+        p = l4 < 3 ? 1 : l4 - 2;
+        if (p > 15) p = 15;
+    }
+    if (p < 1 || p > 15) SAS_FAIL(EINVAL, "SAS_BUILD_TAG_LINES: p must be 1..15 (4^15 lines are 128 GiB)");
+    return x->sa_w == 5 ? build_tag_lines_w<5>(x, p) : build_tag_lines_w<4>(x, p);
 }
 
 static int build_stree(sas_index* x) {
@@ -1396,7 +1592,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         HIP_TRY(hipGetLastError());
         x->top2 = static_cast<uint4*>(t2.release());
     }
-    if (flags & SAS_BUILD_TAGGED) TRY(build_tagged(x, (flags >> 16) & 31));
+    if ((flags & SAS_BUILD_TAGGED) && (flags & SAS_BUILD_TAG_LINES)) TRY(build_tag_lines(x, (flags >> 16) & 31));
+    else if (flags & SAS_BUILD_TAGGED) TRY(build_tagged(x, (flags >> 16) & 31));
     HIP_TRY(hipMalloc(&x->scratch, 64));
     HIP_TRY(hipMemset(x->scratch, 0, 64));
     HIP_TRY(hipDeviceSynchronize());
@@ -1404,7 +1601,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     sas_stats& st = x->stats;
     st.n = n;
     st.text_bytes = x->text_words * 8;
-    st.sa_bytes = sa_n * x->sa_w;
+    st.sa_bytes = x->tag_lines ? x->tag_ovf_n * 8 : sa_n * x->sa_w;  // bucket lines: the overflow array
     st.sa_width = x->sa_w;
     st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
     st.llcp_bytes = x->llcp ? sa_n * 16 : 0;
@@ -1428,7 +1625,10 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.quad_fan = x->quad_leaves ? x->quad_fan : 0;
     st.top2_levels = x->top2_levels;
     st.tag_chars = x->tag_p;
-    st.tag_table_bytes = x->tag_table ? ((1ull << (2 * x->tag_p)) + 1) * 8 : 0;
+    st.tag_table_bytes = x->tag_table   ? ((1ull << (2 * x->tag_p)) + 1) * 8
+                         : x->tag_lines ? ((1ull << (2 * x->tag_p)) + 1) * 128 : 0;
+    st.tag_line_slots = x->tag_lines ? SAS_TL_SLOTS : 0;
+    st.tag_overflow_entries = x->tag_ovf_n;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
                      st.sector_bytes + st.quad_bytes + st.tag_table_bytes + ((uint64_t)16 << x->top2_levels);
     st.build_total_ns = now_ns() - t0;
@@ -1515,6 +1715,24 @@ __global__ void k_widen_sa(SaView<W> sa, uint64_t start, uint64_t count, uint64_
     GRID_STRIDE(i, count) out[i] = sa[start + i];
 }
 
+// SAS_BUILD_TAG_LINES: SA[r] from the line of r's bucket (the last line whose first rank is
+// <= r: a binary search over the line headers), its slot or its overflow entry
+__global__ void k_tl_sa(const uint64_t* __restrict__ lines, const uint64_t* __restrict__ ovf, uint64_t keys,
+                        uint64_t start, uint64_t count, uint64_t* __restrict__ out) {
+    GRID_STRIDE(i, count) {
+        const uint64_t r = start + i;
+        uint64_t lo = 0, hi = keys;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if ((lines[mid * 16] & (SAS_SA40_MAX - 1)) > r) hi = mid;
+            else lo = mid + 1;
+        }
+        const uint64_t b = lo - 1, j = r - (lines[b * 16] & (SAS_SA40_MAX - 1));
+        const uint64_t e = j < SAS_TL_SLOTS ? lines[b * 16 + 2 + j] : ovf[lines[b * 16 + 1] + j - SAS_TL_SLOTS];
+        out[i] = e & (SAS_SA40_MAX - 1);
+    }
+}
+
 extern "C" int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t count, uint64_t* dst, uint32_t flags) {
     if (!index || (count && !dst)) SAS_FAIL(EINVAL, "sas_copy_sa64: null argument");
     if (start < index->rank_lo || start - index->rank_lo + count > index->sa_n)
@@ -1528,7 +1746,10 @@ extern "C" int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t co
         out = tmp.as<uint64_t>();
     }
     uint64_t s0 = start - index->rank_lo;
-    if (index->sa_w == 8)
+    if (index->tag_lines)
+        hipLaunchKernelGGL(k_tl_sa, dim3(grid_for(count)), dim3(256), 0, 0, index->tag_lines, index->tag_ovf,
+                           1ull << (2 * index->tag_p), s0, count, out);
+    else if (index->sa_w == 8)
         hipLaunchKernelGGL(k_widen_sa<8>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<8>{index->sa}, s0, count, out);
     else if (index->sa_w == 5)
         hipLaunchKernelGGL(k_widen_sa<5>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<5>{index->sa}, s0, count, out);

@@ -80,6 +80,8 @@ struct SearchArgs {
     uint32_t quad_lds_nodes;
     const uint64_t* tag_table;  // SAS_BUILD_TAGGED bucket table (sa = tagged entries, W = 8)
     uint32_t tag_p;
+    const uint64_t* tag_lines;  // SAS_BUILD_TAG_LINES: 128-B bucket lines (common.hpp)
+    const uint64_t* tag_ovf;    // and their overflow entries
     const uint8_t* qbytes;
     const uint64_t* qwords;  // sas_search_packed: 2-bit packed fixed-length queries (PREFIX)
     const uint64_t* qoff;
@@ -1947,6 +1949,271 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_range(SearchArgs 
     if (bad) atomicOr(a.bad, 1u);
 }
 
+// ------------------------------------------------------------------ TAGGED on bucket lines
+// SAS_BUILD_TAG_LINES (sas_build.hip, build_tag_lines): line b holds bucket b's header
+// {first rank | count, overflow offset} and the entries of ranks first .. first + 13, so the
+// bucket word and the first window of the tagged lookup above are one 128-B request.  An
+// 8-lane group reads the lines of its 8 queries (one per lane) together, 16 B per lane
+// (lane 0 the header, lane s the slots 2s - 2 and 2s - 1), finds in each the first slot of
+// the bucket whose tag is >= the query's (group ballot), and hands it to the query's lane;
+// the rest -- the tie's text compare, a larger bucket's overflow window -- is per lane.
+// Slots past the bucket's count hold the next buckets' first suffixes, so "every suffix of
+// the bucket is < q" finds its answer (the first suffix after the bucket, rank first + count)
+// in the same line whenever count < 14 (and at overflow index count - 14 otherwise).
+#define TL_G 8
+// waves per SIMD the line kernels are built for: the 8 line loads a lane keeps in flight take
+// 32 VGPRs (at 5 waves the kernel spills)
+#ifndef SAS_TL_LB
+#define SAS_TL_LB 4
+#endif
+#ifndef SAS_TL_WIN
+#define SAS_TL_WIN 8  // overflow entries a lane reads before bisecting the rest
+#endif
+
+__device__ __forceinline__ uint64_t tl_entry(const SearchArgs& a, uint64_t b, uint64_t ovf, uint64_t j) {
+    return j < SAS_TL_SLOTS ? __builtin_nontemporal_load(a.tag_lines + b * 16 + 2 + j)
+                            : __builtin_nontemporal_load(a.tag_ovf + ovf + (j - SAS_TL_SLOTS));
+}
+
+// bucket b's suffix count from its header word (a saturated count reads the next line's rank)
+__device__ __forceinline__ uint64_t tl_count(const SearchArgs& a, uint64_t b, uint64_t h0) {
+    const uint64_t c = h0 >> 40;
+    return c == 0xFFFFFFull ? (a.tag_lines[(b + 1) * 16] & TAG_M40) - (h0 & TAG_M40) : c;
+}
+
+// The lookup after the line: f = the first slot j < min(count, 14) whose tag is >= q's (or
+// that bound), ef = slot f's entry when f < 14.  The answer is entry j of the bucket for the
+// first j in [0, count] whose suffix is >= q (j = count: the next bucket's first suffix).
+template <int QW, class Q>
+__device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint64_t i, uint64_t b, uint64_t h0,
+                                          uint64_t ovf, uint32_t f, uint64_t ef, uint32_t Q12) {
+    const uint64_t first = h0 & TAG_M40;
+    const uint64_t cnt = tl_count(a, b, h0);
+    const uint32_t lim = cnt < SAS_TL_SLOTS ? (uint32_t)cnt : (uint32_t)SAS_TL_SLOTS;
+    uint64_t j = 0, e = 0, start;
+    bool done = false;
+    if (f < lim) {
+        // a text-slice query and the tying entry of its own suffix: >= q without the text
+        const uint64_t src = query_source(q);
+        const bool own = src != ~0ull && src + q.m <= a.n && (ef & TAG_M40) == src && (uint32_t)(ef >> 40) == Q12;
+        if (own || tag_ge<QW>(ef, Q12, a, q)) {
+            j = f;
+            e = ef;
+            done = true;
+        }
+        start = (uint64_t)f + 1;
+    } else {
+        start = lim;  // every slot of the bucket in the line is < q
+    }
+    if (!done && start == cnt) {  // the first suffix after the bucket
+        j = cnt;
+        e = (f == cnt && cnt < SAS_TL_SLOTS) ? ef : tl_entry(a, b, ovf, cnt);
+        done = true;
+    }
+    if (!done && start >= SAS_TL_SLOTS) {
+        // one window of the overflow entries [start, cnt] (entry cnt is >= q whatever its tag),
+        // loaded as 16-B aligned pairs
+        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+        const uint64_t rest = cnt + 1 - start;
+        const uint32_t nw = rest < SAS_TL_WIN ? (uint32_t)rest : (uint32_t)SAS_TL_WIN;
+        const uint64_t ab = ovf + (start - SAS_TL_SLOTS);
+        const uint32_t o = (uint32_t)(ab & 1);
+        const u64x2* ep = reinterpret_cast<const u64x2*>(a.tag_ovf + (ab & ~1ull));
+        uint64_t w2[SAS_TL_WIN + 2];
+#pragma unroll
+        for (int k = 0; k < SAS_TL_WIN / 2 + 1; k++) {
+            const u64x2 v = (2u * k < o + nw) ? __builtin_nontemporal_load(ep + k) : u64x2{0ull, 0ull};
+            w2[2 * k] = v.x;
+            w2[2 * k + 1] = v.y;
+        }
+        uint64_t ew[SAS_TL_WIN];
+#pragma unroll
+        for (int k = 0; k < SAS_TL_WIN; k++) ew[k] = (uint32_t)k < nw ? (o ? w2[k + 1] : w2[k]) : 0ull;
+        uint32_t k0 = nw;
+#pragma unroll
+        for (int k = SAS_TL_WIN - 1; k >= 0; k--)
+            if ((uint32_t)k < nw && (start + k == cnt || (uint32_t)(ew[k] >> 40) >= Q12)) k0 = (uint32_t)k;
+        uint64_t ek0 = ew[0];
+#pragma unroll
+        for (int k = 1; k < SAS_TL_WIN; k++) ek0 = (k0 == (uint32_t)k) ? ew[k] : ek0;
+        if (k0 < nw) {
+            const uint64_t r = start + k0;
+            const uint64_t src = query_source(q);
+            const bool own = src != ~0ull && src + q.m <= a.n && (ek0 & TAG_M40) == src && (uint32_t)(ek0 >> 40) == Q12;
+            if (r == cnt || own || tag_ge<QW>(ek0, Q12, a, q)) {
+                j = r;
+                e = ek0;
+                done = true;
+            }
+            start = r + 1;
+        } else {
+            start += nw;
+        }
+    }
+    if (!done) {  // binary search over [start, cnt): entry cnt is >= q
+        uint64_t l2 = start, h2 = cnt, pe = 0;
+        bool have = false;
+        while (l2 < h2) {
+            const uint64_t mid = (l2 + h2) >> 1;
+            const uint64_t fm = tl_entry(a, b, ovf, mid);
+            if (tag_ge<QW>(fm, Q12, a, q)) {
+                h2 = mid;
+                pe = fm;
+                have = true;
+            } else {
+                l2 = mid + 1;
+            }
+        }
+        j = l2;
+        e = (have && l2 < cnt) ? pe : tl_entry(a, b, ovf, l2);
+    }
+    const uint64_t s = e & TAG_M40;
+    a.out_pos[i] = s == SAS_TL_END ? a.next_pos : s;
+    if (a.out_probes) {  // the reference's cnt: the table, then binary_search over [first, first + cnt)
+        uint32_t probes = 1;
+        for (uint64_t l2 = 0, h2 = cnt; l2 < h2; probes++) {
+            const uint64_t mid = (l2 + h2) >> 1;
+            if (mid < j) l2 = mid + 1;
+            else h2 = mid;
+        }
+        a.out_probes[i] = probes;
+    }
+    (void)first;
+}
+
+// The cooperative part: every lane of the wave calls it together (act: the lane holds query i).
+template <int QW, class Q>
+__device__ __forceinline__ void tl_lookup(const SearchArgs& a, const Q& q, bool act, uint64_t i) {
+    const uint32_t lane = threadIdx.x & 63, sub = lane & (TL_G - 1), g0 = lane & ~(uint32_t)(TL_G - 1);
+    const uint32_t sh = 64 - 2 * a.tag_p;
+    const uint64_t K64 = act ? q.w[0] : 0ull;
+    const uint64_t b = K64 >> sh;
+    const uint32_t Q12 = tag_of_key(K64, a.tag_p);
+    const uint4* L4 = reinterpret_cast<const uint4*>(a.tag_lines);
+    uint4 v[TL_G];
+#pragma unroll
+    for (int k = 0; k < TL_G; k++) {
+        const uint64_t bk = (uint64_t)__shfl((long long)b, (int)g0 + k, 64);
+        v[k] = nt_load4(L4 + bk * 8 + sub);
+    }
+    uint64_t my_h0 = 0, my_h1 = 0, my_ef = 0;
+    uint32_t my_f = 0;
+#pragma unroll
+    for (int k = 0; k < TL_G; k++) {
+        const uint64_t lo64 = ((uint64_t)v[k].y << 32) | v[k].x, hi64 = ((uint64_t)v[k].w << 32) | v[k].z;
+        const uint64_t h0 = (uint64_t)__shfl((long long)lo64, (int)g0, 64);
+        const uint64_t h1 = (uint64_t)__shfl((long long)hi64, (int)g0, 64);
+        const uint64_t c = h0 >> 40;  // a saturated count is >= 14 as well
+        const uint32_t lim = c < SAS_TL_SLOTS ? (uint32_t)c : (uint32_t)SAS_TL_SLOTS;
+        const uint32_t Qk = (uint32_t)__shfl((int)Q12, (int)g0 + k, 64);
+        const uint32_t j0 = 2 * sub - 2;  // slots of this lane (lane 0: the header)
+        const bool ge0 = sub != 0 && j0 < lim && (uint32_t)(lo64 >> 40) >= Qk;
+        const bool ge1 = sub != 0 && j0 + 1 < lim && (uint32_t)(hi64 >> 40) >= Qk;
+        uint32_t cand = ge0 ? j0 : (ge1 ? j0 + 1 : 64u);
+#pragma unroll
+        for (int o = 1; o < TL_G; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_xor((int)cand, o, TL_G);
+            cand = t < cand ? t : cand;
+        }
+        const uint32_t f = cand == 64u ? lim : cand;
+        const uint64_t mine = (f & 1) ? hi64 : lo64;
+        const int src = (int)g0 + (f < SAS_TL_SLOTS ? (int)(f >> 1) + 1 : 0);
+        const uint64_t ef = (uint64_t)__shfl((long long)mine, src, 64);
+        if (sub == (uint32_t)k) {
+            my_h0 = h0;
+            my_h1 = h1;
+            my_f = f;
+            my_ef = ef;
+        }
+    }
+    if (act) tl_finish<QW>(a, q, i, b, my_h0, my_h1, my_f, my_ef, Q12);
+}
+
+template <int QW>
+__global__ __launch_bounds__(SAS_TAG_BLOCK, SAS_TL_LB) void k_sa_tagged_lines(SearchArgs a) {
+    // wave-uniform loop over batches of 64 consecutive queries, staged as in k_sa_tagged
+    __shared__ uint32_t wq[SAS_TAG_BLOCK / 64][2 * SAS_WQ_WORDS];
+    uint32_t* L32 = wq[threadIdx.x >> 6];
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); b0 < a.nq;
+         b0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = b0 + lane;
+        const bool act = i < a.nq;
+        uint64_t qo = 0;
+        uint32_t m = 0;
+        if (act) query_span(a, i, &qo, &m);
+        uint64_t base;
+        if (wave_stage_queries(a.qbytes, qo, m, act, L32, &base)) {
+            WaveQuery q;
+            q.init(L32, act ? (uint32_t)(qo - base) : 0u, act ? m : 0u);
+            tl_lookup<QW>(a, q, act, i);
+        } else {
+            ByteQuery q;
+            q.init(a.qbytes + qo, act ? m : 0u);
+            tl_lookup<QW>(a, q, act, i);
+        }
+    }
+}
+
+// SAS_QUERIES_ARE_SLICES on bucket lines
+template <int QW>
+__global__ __launch_bounds__(SAS_TAG_BLOCK, SAS_TL_LB) void k_sa_tagged_lines_slices(SearchArgs a) {
+    for (uint64_t b0 = blockIdx.x * (uint64_t)blockDim.x + (threadIdx.x & ~63u); b0 < a.nq;
+         b0 += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = b0 + (threadIdx.x & 63);
+        const bool act = i < a.nq;
+        uint64_t qo = 0;
+        uint32_t m = 0;
+        if (act) query_span(a, i, &qo, &m);
+        TextQuery q;
+        q.init(a.tw, qo, m);
+        tl_lookup<QW>(a, q, act, i);
+    }
+}
+
+// Occurrence ranges on bucket lines: both bounds bisected in their buckets (entries by
+// bucket index: slot or overflow), as k_sa_tagged_range does over rank-ordered entries.
+template <int QW>
+__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_lines_range(SearchArgs a, uint64_t* out_hi) {
+    uint32_t bad = 0;
+    const uint32_t sh = 64 - 2 * a.tag_p;
+    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
+         i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint8_t* qb;
+        uint32_t m;
+        query_ptr(a, i, &qb, &m);
+        QueryRegs<QW> q;
+        q.load(qb, m, &bad);
+        const uint64_t K64 = q.w[0];
+        const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
+        const uint32_t Q12 = tag_of_key(K64, a.tag_p), Q3t = tag_of_key(Q3, a.tag_p);
+        const uint64_t b0 = K64 >> sh, b1 = (m <= L ? Q3 : K64) >> sh;
+        const uint64_t h00 = a.tag_lines[b0 * 16], h10 = a.tag_lines[b1 * 16];
+        const uint64_t o0 = a.tag_lines[b0 * 16 + 1], o1 = a.tag_lines[b1 * 16 + 1];
+        uint64_t lo = 0, l1 = tl_count(a, b0, h00), hi = 0, h1 = tl_count(a, b1, h10);
+        while (lo < l1 || hi < h1) {
+            const bool g0 = lo < l1, g1 = hi < h1;
+            const uint64_t m0 = (lo + l1) >> 1, m1 = (hi + h1) >> 1;
+            const uint64_t e0 = g0 ? tl_entry(a, b0, o0, m0) : 0;
+            const uint64_t e1 = g1 ? tl_entry(a, b1, o1, m1) : 0;
+            if (g0) {
+                if (tag_ge<QW>(e0, Q12, a, q)) l1 = m0;
+                else lo = m0 + 1;
+            }
+            if (g1) {
+                if (tag_gt_prefix<QW>(e1, Q12, Q3t, a, q)) h1 = m1;
+                else hi = m1 + 1;
+            }
+        }
+        uint64_t rlo = (h00 & TAG_M40) + lo, rhi = (h10 & TAG_M40) + hi;
+        if (rhi < rlo) rhi = rlo;
+        a.out_pos[i] = a.rank_lo + rlo;
+        out_hi[i] = a.rank_lo + rhi;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
 // Validation pass (SAS_VALIDATE, host-pointer calls): every byte of every query must be a
 // DNA code 0..3, including those past the words a search kernel holds in registers.
 __global__ void k_validate_queries(const uint8_t* __restrict__ qb, const uint64_t* __restrict__ qoff,
@@ -2099,9 +2366,22 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     const bool range = (flags & SAS_PREFIX_RANGE) != 0;
     if (algo == SAS_ALGO_TAGGED) {
         uint64_t tb = (a.nq + SAS_TAG_BLOCK - 1) / SAS_TAG_BLOCK;
-        const uint64_t tcap = (uint64_t)x->num_cus * (qw >= SAS_TAG_LB_QW ? SAS_TAG_LB : 8);
+        const uint64_t tcap = (uint64_t)x->num_cus * (x->tag_lines ? SAS_TL_LB : (qw >= SAS_TAG_LB_QW ? SAS_TAG_LB : 8));
         if (tb > tcap) tb = tcap;
-        if (flags & SAS_QUERIES_ARE_SLICES) {
+        if (x->tag_lines) {
+            const dim3 g((unsigned)tb), b(SAS_TAG_BLOCK);
+            const bool sl = (flags & SAS_QUERIES_ARE_SLICES) != 0;
+#define SAS_TL_LAUNCH(Q)                                                                           \
+    if (sl) hipLaunchKernelGGL(k_sa_tagged_lines_slices<Q>, g, b, 0, st, a);                       \
+    else hipLaunchKernelGGL(k_sa_tagged_lines<Q>, g, b, 0, st, a)
+            switch (qw) {
+                case 1: SAS_TL_LAUNCH(1); break;
+                case 2: SAS_TL_LAUNCH(2); break;
+                case 4: SAS_TL_LAUNCH(4); break;
+                default: SAS_TL_LAUNCH(8); break;
+            }
+#undef SAS_TL_LAUNCH
+        } else if (flags & SAS_QUERIES_ARE_SLICES) {
             const dim3 g((unsigned)tb), b(SAS_TAG_BLOCK);
             switch (qw) {
                 case 1: hipLaunchKernelGGL(k_sa_tagged_slices<1>, g, b, 0, st, a); break;
@@ -2189,6 +2469,8 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.quad_lds_nodes = x->quad_lds_nodes;
     a.tag_table = x->tag_table;
     a.tag_p = x->tag_p;
+    a.tag_lines = x->tag_lines;
+    a.tag_ovf = x->tag_ovf;
 }
 
 // Algorithm / index / flag compatibility, shared by the search entry points.
@@ -2204,7 +2486,10 @@ static int check_algo(const sas_index* x, int algo, uint32_t flags, const char* 
         SAS_FAIL(EINVAL, w + ": SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, w + ": SAS_ALGO_STREE needs SAS_BUILD_STREE");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, w + ": SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
-    if (algo == SAS_ALGO_TAGGED && !x->tag_table) SAS_FAIL(EINVAL, w + ": SAS_ALGO_TAGGED needs SAS_BUILD_TAGGED");
+    if (algo == SAS_ALGO_TAGGED && !x->tag_table && !x->tag_lines)
+        SAS_FAIL(EINVAL, w + ": SAS_ALGO_TAGGED needs SAS_BUILD_TAGGED");
+    if (x->tag_lines && (algo != SAS_ALGO_TAGGED || (flags & SAS_PREFIX_RANGE)))
+        SAS_FAIL(ENOTSUP, w + ": a bucket-line index (SAS_BUILD_TAG_LINES) has no SA array: SAS_ALGO_TAGGED only");
     if (x->sa_w == 8 && algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP && algo != SAS_ALGO_INTERP &&
         algo != SAS_ALGO_TAGGED)
         SAS_FAIL(EINVAL, w + ": a tagged index (SAS_BUILD_TAGGED) serves TAGGED, PLAIN, LCP and INTERP");
@@ -3179,7 +3464,14 @@ static void launch_range(const sas_index* x, const SearchArgs& a, int qw, uint32
     uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
     if (blocks > cap) blocks = cap;
     dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
-    if (x->tag_table) {
+    if (x->tag_lines) {
+        switch (qw) {
+            case 1: hipLaunchKernelGGL(k_sa_tagged_lines_range<1>, grid, block, 0, st, a, dhi); break;
+            case 2: hipLaunchKernelGGL(k_sa_tagged_lines_range<2>, grid, block, 0, st, a, dhi); break;
+            case 4: hipLaunchKernelGGL(k_sa_tagged_lines_range<4>, grid, block, 0, st, a, dhi); break;
+            default: hipLaunchKernelGGL(k_sa_tagged_lines_range<8>, grid, block, 0, st, a, dhi); break;
+        }
+    } else if (x->tag_table) {
         switch (qw) {
             case 1: hipLaunchKernelGGL(k_sa_tagged_range<1>, grid, block, 0, st, a, dhi); break;
             case 2: hipLaunchKernelGGL(k_sa_tagged_range<2>, grid, block, 0, st, a, dhi); break;
@@ -3213,7 +3505,7 @@ static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixe
                       const uint32_t* qlen, uint64_t nq, uint64_t* out_lo, uint64_t* out_hi, void* stream,
                       uint32_t flags) {
     if (!x) SAS_FAIL(EINVAL, "sas_search_range: null index");
-    if (!x->sec_leaves && !x->quad_leaves && !x->tag_table)
+    if (!x->sec_leaves && !x->quad_leaves && !x->tag_table && !x->tag_lines)
         SAS_FAIL(EINVAL, "sas_search_range: needs SAS_BUILD_QUAD, SAS_BUILD_SECTOR or SAS_BUILD_TAGGED");
     const bool ragged = qoff != nullptr || qlen != nullptr;
     if (nq == 0) return 0;

@@ -40,6 +40,7 @@ SAS_BUILD_PREFIX_INLINE = 1 << 15
 SAS_BUILD_PREFIX_INLINE2 = 1 << 21
 SAS_BUILD_PREFIX_INLINE4 = 1 << 22
 SAS_BUILD_TAGGED = 1 << 23
+SAS_BUILD_TAG_LINES = 1 << 24
 
 
 def SAS_BUILD_TOP2_LEVELS(levels: int) -> int:
@@ -78,6 +79,7 @@ class SasStats(C.Structure):
         ("quad_fan", C.c_uint32), ("top2_levels", C.c_uint32), ("llcp_bytes", C.c_uint64),
         ("prefix_bytes", C.c_uint64), ("prefix_chars", C.c_uint32), ("tag_chars", C.c_uint32),
         ("tag_table_bytes", C.c_uint64), ("index_bytes", C.c_uint64),
+        ("tag_line_slots", C.c_uint32), ("reserved0", C.c_uint32), ("tag_overflow_entries", C.c_uint64),
     ]
 
     def as_dict(self):

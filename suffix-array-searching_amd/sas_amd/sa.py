@@ -98,7 +98,7 @@ class SaNaive:
               rank_range: tuple[int, int] | None = None, flags: int = 0, sector: bool | None = None,
               sa40: bool = False, quad: bool | str | None = None, llcp: bool | None = None,
               prefix: bool | int | None = None, prefix_inline: bool | int = False,
-              tagged: bool | int = False, top2_levels: int = 0) -> "SaNaive":
+              tagged: bool | int = False, top2_levels: int = 0, tag_lines: bool = False) -> "SaNaive":
         """Index over t.  rank_range=(lo, hi): sharded-text mode, hold only global SA
         ranks [lo, hi) (sas_build_shard); `sa` is then the FULL suffix array or None
         (u32 or u64 array).  sa40: store a packed 40-bit SA and use the bucketed
@@ -114,13 +114,17 @@ class SaNaive:
         the library, an int = that p) for algo="tagged"; it replaces the SA and leaves out the
         trees, LLCP and the prefix tables (their defaults turn off).  top2_levels: depth of
         the binary-search pivot array (SAS_BUILD_TOP2_LEVELS; 0 = the library default, the
-        23 cache-resident levels; 30 = 16 GiB of HBM-resident pivots at n = 2^30)."""
+        23 cache-resident levels; 30 = 16 GiB of HBM-resident pivots at n = 2^30).
+        tag_lines (with tagged): the tagged entries as 128-B bucket lines + an overflow array
+        (SAS_BUILD_TAG_LINES; p = ceil(log4 n) - 2 unless tagged gives it): one request gives a
+        lookup its bucket and first 14 entries; algo="tagged" only, no SA array."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         if tagged is not False:
             stree, sector, quad, prefix = bool(stree), bool(sector), quad or False, prefix or False
             llcp = bool(llcp)
             flags |= _lib.SAS_BUILD_TAGGED | (0 if tagged is True else _lib.SAS_BUILD_PREFIX_P(int(tagged)))
+            flags |= _lib.SAS_BUILD_TAG_LINES if tag_lines else 0
         stree = True if stree is None else stree
         sector = True if sector is None else sector
         quad = True if quad is None else quad

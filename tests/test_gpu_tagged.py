@@ -175,6 +175,51 @@ def test_tagged_matches_oracle(sas, p):
                 assert (int(lo[k]), int(hi[k])) == O.prefix_range(tp, n, sa, qs[k]), (name, k)
 
 
+@pytest.mark.parametrize("p", [None, 1, 3, 7])
+def test_tag_lines_match_oracle(sas, p):
+    """Bucket lines (SAS_BUILD_TAG_LINES) for several p (1: a few huge buckets, every lookup
+    in the overflow array; 7: ~1-12 suffixes a line, slots past the count), u32- and
+    40-bit-built SAs, on random and repeat-rich texts: positions, cnt, ranges and the SA
+    equal the oracle's and the rank-ordered tagged index's; no SA array behind it."""
+    rng = np.random.default_rng(60 + (p or 0))
+    for name, t in texts(rng).items():
+        n = len(t)
+        sa = O.build_sa(t)
+        qs = mixed_queries(t, rng)
+        buf, off, lens = pack(qs)
+        epos, erank = expected(t, sa, qs)
+        for sa40 in (False, True):
+            idx = sas.SaNaive.build(t, tagged=True if p is None else p, sa40=sa40, verify=True, lcp=False,
+                                    tag_lines=True)
+            st = idx.stats()
+            pp = st["tag_chars"]
+            assert st["tag_line_slots"] == 14 and st["tag_table_bytes"] == (4 ** pp + 1) * 128
+            assert st["sa_bytes"] == st["tag_overflow_entries"] * 8
+            assert np.array_equal(idx.suffix_array(), sa.astype(np.uint64)), name
+            got, cnt = idx.search_batch(buf, off, lens, algo="tagged", probes=True)
+            bad = np.nonzero(got != epos)[0]
+            assert len(bad) == 0, (name, p, sa40, bad[:5], [qs[i] for i in bad[:2]])
+            ecnt = table_cnt(t, sa, qs, erank, pp)
+            assert np.array_equal(cnt, ecnt), (name, p, np.nonzero(cnt != ecnt)[0][:5])
+            lo, hi = idx.search_range(buf, off, lens)
+            tp = O.padded(t)
+            for k in range(0, len(qs), 7):
+                assert (int(lo[k]), int(hi[k])) == O.prefix_range(tp, n, sa, qs[k]), (name, k)
+            for algo in ("plain", "lcp", "interp"):
+                with pytest.raises(sas.SasError):
+                    idx.search_batch(buf, off, lens, algo=algo)
+            with pytest.raises(sas.SasError):
+                idx.verify()
+            # overflow entries: ranks first + 14 .. first + count of each bucket of >= 14
+            keys = np.zeros(n, np.int64)
+            tpi = tp.astype(np.int64)
+            for j in range(pp):
+                keys = keys * 4 + tpi[sa.astype(np.int64) + j]
+            c = np.bincount(keys, minlength=4 ** pp)
+            assert st["tag_overflow_entries"] == int(np.sum(np.where(c >= 14, c - 13, 0))), name
+            idx.free()
+
+
 def test_tagged_device_ragged_and_validation(sas):
     """Device-pointer ragged batches (odd offsets, no slack after the last query) and
     SAS_VALIDATE: a bad code anywhere in a query -- including past the words the kernel
@@ -213,16 +258,19 @@ def test_tagged_device_ragged_and_validation(sas):
                           torch.full((1,), 250, dtype=torch.int32, device="cuda"), flags=_lib.SAS_VALIDATE)
 
 
-def test_tagged_saturated_bucket(sas):
+@pytest.mark.parametrize("lines", [False, True])
+def test_tagged_saturated_bucket(sas, lines):
     """A bucket with >= 2^24 suffixes saturates the 24-bit count: the lookup reads the next
-    bucket word for its end.  All-A text: SA[r] = n - 1 - r, every suffix in bucket 0."""
+    bucket word (the next line's first rank) for its end.  All-A text: SA[r] = n - 1 - r,
+    every suffix in bucket 0."""
     import torch
     n = (1 << 24) + 1000
     t = torch.zeros(n, dtype=torch.uint8, device="cuda")
-    idx = sas.SaNaive.build(t, tagged=True, lcp=False)
+    idx = sas.SaNaive.build(t, tagged=True, lcp=False, tag_lines=lines)
     st = idx.stats()
     p = st["tag_chars"]
-    assert p == 13  # ceil(log4 n): 4^12 = 2^24 < n; one bucket holds all n > 2^24 - 1 suffixes
+    # ceil(log4 n) (minus 2 for lines): 4^12 = 2^24 < n; one bucket holds all n > 2^24 - 1 suffixes
+    assert p == (11 if lines else 13)
     sa = idx.suffix_array(count=5)
     assert sa.tolist() == [n - 1 - r for r in range(5)]
     ms = [1, 5, 11, 12, 13, 27, 28, 29, 100, 257, 4000, n, n + 1]
@@ -240,7 +288,8 @@ def test_tagged_saturated_bucket(sas):
             assert (int(lo[k]), int(hi[k])) == (len(q) - 1, n), k
 
 
-def test_tagged_wave_staging_paths(sas):
+@pytest.mark.parametrize("lines", [False, True])
+def test_tagged_wave_staging_paths(sas, lines):
     """k_sa_tagged's wave-staged queries: a contiguous batch (staged through LDS), the same
     queries with shuffled offsets (spans past 16,608 chars fall back to per-lane loads), a wave
     of empty queries, a tail wave of 37 queries, and queries that sit at the very end of the
@@ -249,7 +298,7 @@ def test_tagged_wave_staging_paths(sas):
     t = O.random_string(400_009, seed=12)
     n = len(t)
     sa = O.build_sa(t)
-    idx = sas.SaNaive.build(torch.from_numpy(t).cuda(), tagged=True, lcp=False)
+    idx = sas.SaNaive.build(torch.from_numpy(t).cuda(), tagged=True, lcp=False, tag_lines=lines)
     rng = np.random.default_rng(3)
     nq = 64 * 40 + 37
     lens = rng.integers(0, 260, nq).astype(np.uint32)
@@ -299,7 +348,8 @@ def test_tagged_wave_staging_paths(sas):
         assert len(bad) == 0, (m, skew, bad[:5])
 
 
-def test_tagged_text_slices(sas):
+@pytest.mark.parametrize("lines", [False, True])
+def test_tagged_text_slices(sas, lines):
     """SAS_QUERIES_ARE_SLICES: queries given as slices t[off : off + len] of the indexed text
     (no query bytes; the tie with the query's own suffix skips the text compare) give the
     oracle's positions and the byte queries' probes, on random and repeat-rich texts,
@@ -309,7 +359,7 @@ def test_tagged_text_slices(sas):
     rng = np.random.default_rng(17)
     for name, t in texts(rng).items():
         n = len(t)
-        idx = sas.SaNaive.build(t, lcp=False, tagged=True)
+        idx = sas.SaNaive.build(t, lcp=False, tagged=True, tag_lines=lines)
         lens = rng.integers(0, 300, 4000)
         offs = np.array([rng.integers(0, max(1, n - l + 1)) for l in lens], np.int64)
         lens = np.minimum(lens, n - offs)
