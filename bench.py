@@ -107,6 +107,11 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         hbm += entry  # the table entry (inline entries hold the range's first suffixes)
         leaf = 16 if st["quad_entry_bytes"] == 16 else 8 + sa_w
         hbm += max(0.0, probes - 1) * leaf
+    elif algo == "tagged" and st.get("tag_line_slots"):
+        # bucket lines: the 128-B line (header + 14 entries), the entries of a mean bucket past
+        # the line (overflow), the text past the (p + 12)-char key
+        hbm += 128 + max(0.0, n / 4 ** st["tag_chars"] + 1 - st["tag_line_slots"]) * 8 + \
+            max(0.0, m - st["tag_chars"] - 12) / 4
     elif algo == "tagged":
         hbm += 8 + min(n / 4 ** st["tag_chars"] + 1, 8) * 8 + max(0.0, m - st["tag_chars"] - 12) / 4
     elif range_flag:  # PLAIN / LCP from the prefix table's range: table entry + SA word + window per probe
@@ -457,23 +462,35 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     """configs[3]-shaped run: n = 2^34 chars (16 GiB of byte-coded text; BASELINE's
     "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and 10^8 positive
     queries of mixed length 8..256 (random_queries with len in [8, 257), sas/util.rs:18-26),
-    ragged, through sas_search_batch on device buffers.  TAGGED: 8-B tagged SA entries + a
-    p = 16 bucket table (SAS_BUILD_TAGGED); PREFIX / QUAD: compact key-only quad leaves
-    beside the 40-bit SA (+ a p = 16 40-bit rank table for PREFIX)."""
+    ragged, through sas_search_batch on device buffers.  TAGGED on bucket lines
+    (SAS_BUILD_TAGGED | SAS_BUILD_TAG_LINES, p = 15: a bucket's header and first 14 entries in
+    one 128-B line) by default (--c3-layout lines); then, as the cross-check, the rank-ordered
+    tagged index (8-B tagged SA entries + a p = 16 bucket table) with TAGGED and the
+    extra algorithms, whose positions must be identical.  PREFIX / QUAD: compact key-only quad
+    leaves beside the 40-bit SA (+ a p = 16 40-bit rank table for PREFIX).  The indexes are
+    built one after the other from a host copy of the text (two do not fit in HBM together,
+    nor does a device byte copy beside the bucket-line build)."""
     n = args.c3_n
     nq = args.c3_nq
     t0 = time.perf_counter()
     text = sas_amd.random_string(n, seed=SEED, device=dev)
-    # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
-    if algo == "tagged":
-        idx = sas_amd.SaNaive.build(text, lcp=False, verify=True, tagged=True)
-    else:
-        idx = sas_amd.SaNaive.build(text, lcp=False, stree=algo == "stree", sector=False,
-                                    quad="compact" if algo in ("quad", "prefix") else False, verify=True,
-                                    llcp=False, prefix=16 if algo == "prefix" else False)
-    st = idx.stats()
-    del text  # queries are cut from, and answers checked against, the index's packed text
+    htext = text.cpu().numpy()
+    del text
     torch.cuda.empty_cache()
+
+    def build(kind):
+        # verify: the reference's adjacency assertion (sas/sa_search.rs:36-38) + permutation, on the GPU
+        if kind in ("lines", "tagged"):
+            return sas_amd.SaNaive.build(htext, lcp=False, verify=True, tagged=True, tag_lines=kind == "lines")
+        return sas_amd.SaNaive.build(htext, lcp=False, stree=kind == "stree", sector=False,
+                                     quad="compact" if kind in ("quad", "prefix") else False, verify=True,
+                                     llcp=False, prefix=16 if kind == "prefix" else False)
+    lines = algo == "tagged" and args.c3_layout == "lines"
+    phases = [("lines", (algo,)), ("tagged", (algo,) + tuple(x for x in extra_algos if x != algo))] if lines else \
+        [(algo, (algo,) + tuple(x for x in extra_algos if x != algo))]
+    idx = build(phases[0][0])
+    st = idx.stats()
+    # queries are cut from, and answers checked against, the index's packed text
     off, ln, _ = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n + rank * 8 * nq, margin=256, len_lo=8,
                                         len_hi=257)
     lens = torch.from_numpy(ln.astype(np.int64)).to(dev)
@@ -487,112 +504,128 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     out = torch.empty(nq, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()
     setup = time.perf_counter() - t0
-    log(f"c3 setup {setup:.1f} s ({algo}, n={n}, nq={nq})")
+    log(f"c3 setup {setup:.1f} s ({phases[0][0]}, n={n}, nq={nq})")
     mean_m = total / nq
-    res, ref = {}, None
-    for a in (algo,) + tuple(x for x in extra_algos if x != algo):
-        def step():
-            idx.search_batch(qbytes, qoff, qlen, algo=a, out=out)
-        steps = args.c3_steps if a == algo else max(2, args.c3_steps // 2)
-        for _ in range(args.warmup):
-            step()
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        tt = time.perf_counter()
-        ev0.record()
-        for _ in range(steps):
-            step()
-        ev1.record()
-        torch.cuda.synchronize()
-        el = time.perf_counter() - tt
-        kms = ev0.elapsed_time(ev1) / steps
-        if ref is None:
-            ref = out.clone()
-            # guard 1: each answer is an occurrence of its query (positive queries)
-            okc = True
-            chunk = 1 << 20
-            for s in range(0, nq, chunk):
-                e = min(nq, s + chunk)
-                span = int((qoff[e - 1] + lens[e - 1] - qoff[s]).item())
-                got = torch.empty(span, dtype=torch.uint8, device=dev)
-                idx.extract(out[s:e].contiguous(), qlen[s:e].contiguous(), (qoff[s:e] - qoff[s]).contiguous(), got)
-                okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + span]))
-            if not okc:
-                raise SystemExit(f"bench c3: {a} returned a non-occurrence position")
-            # guard 2: exact lower bounds on a sample
-            rng = np.random.default_rng(7)
-            ids = np.sort(rng.choice(nq, size=min(nq, args.proof_sample), replace=False))
-            dids = torch.from_numpy(ids).to(dev)
-            qo_h = qoff[dids].cpu().numpy()
-            hq = {}
-            for j, i in enumerate(ids):
-                hq[int(i)] = qbytes[int(qo_h[j]):int(qo_h[j]) + int(ln[i])].cpu().numpy()
+    res, ref, stats_of, slices = {}, None, {}, None
+    for pi, (kind, algos) in enumerate(phases):
+        if pi > 0:
+            idx.free()
+            torch.cuda.empty_cache()
+            tb = time.perf_counter()
+            idx = build(kind)
+            log(f"c3 {kind} index built in {time.perf_counter() - tb:.1f} s")
+        kst = idx.stats()
+        stats_of[kind] = kst
+        for a in algos:
+            name = "tagged_lines" if kind == "lines" else a
 
-            def window(p, L):
-                L = min(L, n - p)
-                if L <= 0:
-                    return np.zeros(0, np.uint8)
-                o = torch.empty(L, dtype=torch.uint8, device=dev)
-                idx.extract(torch.tensor([p], dtype=torch.int64, device=dev),
-                            torch.tensor([L], dtype=torch.int32, device=dev),
-                            torch.zeros(1, dtype=torch.int64, device=dev), o)
-                return o.cpu().numpy()
-            nbad = lower_bound_proof(idx, window, lambda i: hq[i], out[dids].cpu().numpy(), ids)
-            if nbad:
-                raise SystemExit(f"bench c3: {nbad} of {len(ids)} sampled answers are not exact lower bounds")
-            agrees = True
-        else:
-            agrees = bool(torch.equal(out, ref))
-            if not agrees:
-                raise SystemExit(f"bench c3: {a} differs from {algo}")
-        _, pr = idx.search_batch(qbytes, qoff, qlen, algo=a, probes=True)
-        mp = float(pr.double().mean().item())
-        bpl = bytes_per_lookup(a, st, n, mean_m, mp)
-        res[a] = record(a, nq, kms, el, bpl, st["index_bytes"],
-                        load_pmc(f"c3_{a}_n{n}_q{nq}") if a == algo else None, mp,
-                        {"identical_to_" + algo: agrees, "lookups_per_s": nq * steps / el})
-        log(f"c3 {a}: {kms:.3f} ms per {nq}")
-    # the same queries handed over as the slices of the text they are (random_queries returns
-    # borrowed &t[i..i+len], sas/util.rs:18-26): offsets + lengths, no query bytes; a lookup
-    # whose candidate is the query's own suffix skips its text compare (SAS_QUERIES_ARE_SLICES)
-    slices = None
-    if algo == "tagged":
-        for _ in range(args.warmup):
-            idx.search_slices(src, qlen, out=out)
-        torch.cuda.synchronize()
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        ssteps = max(2, args.c3_steps // 2)
-        ev0.record()
-        for _ in range(ssteps):
-            idx.search_slices(src, qlen, out=out)
-        ev1.record()
-        torch.cuda.synchronize()
-        sms = ev0.elapsed_time(ev1) / ssteps
-        same = bool(torch.equal(out, ref))
-        if not same:
-            raise SystemExit("bench c3: text-slice queries differ from the byte queries")
-        slices = {"what": "the same queries as slices of the indexed text (sas_search_batch with "
-                          "SAS_QUERIES_ARE_SLICES: offsets + lengths, chars from the packed text)",
-                  "kernel_ms": sms, "lookups_per_s": nq / (sms * 1e-3), "identical_to_" + algo: same}
-        log(f"c3 tagged slices: {sms:.3f} ms per {nq}")
-    h = res[algo]
+            def step():
+                idx.search_batch(qbytes, qoff, qlen, algo=a, out=out)
+            steps = args.c3_steps if ref is None else max(2, args.c3_steps // 2)
+            for _ in range(args.warmup):
+                step()
+            torch.cuda.synchronize()
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            tt = time.perf_counter()
+            ev0.record()
+            for _ in range(steps):
+                step()
+            ev1.record()
+            torch.cuda.synchronize()
+            el = time.perf_counter() - tt
+            kms = ev0.elapsed_time(ev1) / steps
+            if ref is None:
+                ref = out.clone()
+                # guard 1: each answer is an occurrence of its query (positive queries)
+                okc = True
+                chunk = 1 << 20
+                for s in range(0, nq, chunk):
+                    e = min(nq, s + chunk)
+                    span = int((qoff[e - 1] + lens[e - 1] - qoff[s]).item())
+                    got = torch.empty(span, dtype=torch.uint8, device=dev)
+                    idx.extract(out[s:e].contiguous(), qlen[s:e].contiguous(), (qoff[s:e] - qoff[s]).contiguous(),
+                                got)
+                    okc &= bool(torch.equal(got, qbytes[qoff[s]:qoff[s] + span]))
+                if not okc:
+                    raise SystemExit(f"bench c3: {name} returned a non-occurrence position")
+                # guard 2: exact lower bounds on a sample
+                rng = np.random.default_rng(7)
+                ids = np.sort(rng.choice(nq, size=min(nq, args.proof_sample), replace=False))
+                dids = torch.from_numpy(ids).to(dev)
+                qo_h = qoff[dids].cpu().numpy()
+                hq = {}
+                for j, i in enumerate(ids):
+                    hq[int(i)] = qbytes[int(qo_h[j]):int(qo_h[j]) + int(ln[i])].cpu().numpy()
+
+                def window(p, L):
+                    L = min(L, n - p)
+                    if L <= 0:
+                        return np.zeros(0, np.uint8)
+                    o = torch.empty(L, dtype=torch.uint8, device=dev)
+                    idx.extract(torch.tensor([p], dtype=torch.int64, device=dev),
+                                torch.tensor([L], dtype=torch.int32, device=dev),
+                                torch.zeros(1, dtype=torch.int64, device=dev), o)
+                    return o.cpu().numpy()
+                nbad = lower_bound_proof(idx, window, lambda i: hq[i], out[dids].cpu().numpy(), ids)
+                if nbad:
+                    raise SystemExit(f"bench c3: {nbad} of {len(ids)} sampled answers are not exact lower bounds")
+                agrees = True
+            else:
+                agrees = bool(torch.equal(out, ref))
+                if not agrees:
+                    raise SystemExit(f"bench c3: {name} differs from the first record")
+            _, pr = idx.search_batch(qbytes, qoff, qlen, algo=a, probes=True)
+            mp = float(pr.double().mean().item())
+            bpl = bytes_per_lookup(a, kst, n, mean_m, mp)
+            pmc_key = f"c3_{name}_n{n}_q{nq}"
+            res[name] = record(name, nq, kms, el, bpl, kst["index_bytes"], load_pmc(pmc_key) if a == algo else None,
+                               mp, {"identical_to_first": agrees, "lookups_per_s": nq * steps / el,
+                                    "index": "bucket lines (SAS_BUILD_TAG_LINES)" if kind == "lines" else
+                                    ("rank-ordered tagged entries + bucket table" if kind == "tagged" else kind)})
+            log(f"c3 {name}: {kms:.3f} ms per {nq}")
+            if pi == 0 and algo == "tagged":
+                # the same queries handed over as the slices of the text they are (random_queries
+                # returns borrowed &t[i..i+len], sas/util.rs:18-26): offsets + lengths, no query
+                # bytes; a lookup whose candidate is the query's own suffix skips its text compare
+                for _ in range(args.warmup):
+                    idx.search_slices(src, qlen, out=out)
+                torch.cuda.synchronize()
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ssteps = max(2, args.c3_steps // 2)
+                ev0.record()
+                for _ in range(ssteps):
+                    idx.search_slices(src, qlen, out=out)
+                ev1.record()
+                torch.cuda.synchronize()
+                sms = ev0.elapsed_time(ev1) / ssteps
+                same = bool(torch.equal(out, ref))
+                if not same:
+                    raise SystemExit("bench c3: text-slice queries differ from the byte queries")
+                slices = {"what": "the same queries as slices of the indexed text (sas_search_batch with "
+                                  "SAS_QUERIES_ARE_SLICES: offsets + lengths, chars from the packed text)",
+                          "kernel_ms": sms, "lookups_per_s": nq / (sms * 1e-3), "identical_to_first": same}
+                log(f"c3 {name} slices: {sms:.3f} ms per {nq}")
+    first = "tagged_lines" if lines else algo
+    h = res[first]
     idx.free()
-    del qbytes, qoff, qlen, lens, out, ref, src
+    del qbytes, qoff, qlen, lens, out, ref, src, htext
     torch.cuda.empty_cache()
-    return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({st['sa_width'] * 8}-bit "
-                        f"{'tagged entries' if algo == 'tagged' else 'SA'}), {nq} positive queries of length "
+    kst = stats_of[phases[0][0]]
+    return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({kst['sa_width'] * 8}-bit "
+                        f"{'tagged entries' if algo == 'tagged' else 'SA'}"
+                        f"{' in 128-B bucket lines' if lines else ''}), {nq} positive queries of length "
                         f"8..256 (mean {mean_m:.1f}), ragged",
-            "algo": algo, "lookups_per_s": h["lookups_per_s"], "kernel_ms": h["kernel_ms"],
-            "ns_per_lookup": h["ns_per_lookup"], "index_bytes": st["index_bytes"], "setup_s": setup,
+            "algo": first, "lookups_per_s": h["lookups_per_s"], "kernel_ms": h["kernel_ms"],
+            "ns_per_lookup": h["ns_per_lookup"], "index_bytes": kst["index_bytes"], "setup_s": setup,
             "proof_sample": args.proof_sample, "verified": True,
             "roofline": {"bound": "hbm", "achieved": h["achieved_hbm_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": h["achieved_hbm_GBps"] / HBM_PEAK_GBPS,
                          "traffic": (h.get("pmc") or {}).get("fabric_bytes_per_lookup"),
-                         "kernel": KERNELS.get(algo, "k_sa_prefix")},
+                         "kernel": "k_sa_tagged_lines" if lines else KERNELS.get(algo, "k_sa_prefix")},
             "variants": res, "text_slices": slices,
-            "index": {k: st[k] for k in ("sa_width", "sa_bytes", "quad_bytes", "prefix_chars", "prefix_bytes",
-                                         "tag_chars", "tag_table_bytes", "index_bytes", "build_sa_ns",
-                                         "build_total_ns")}}
+            "index": {k: kst[k] for k in ("sa_width", "sa_bytes", "quad_bytes", "prefix_chars", "prefix_bytes",
+                                          "tag_chars", "tag_table_bytes", "tag_line_slots", "tag_overflow_entries",
+                                          "index_bytes", "build_sa_ns", "build_total_ns")}}
 
 
 def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
@@ -874,6 +907,9 @@ def main():
     ap.add_argument("--c3-n", type=int, default=1 << 34)
     ap.add_argument("--c3-nq", type=int, default=100_000_000)
     ap.add_argument("--c3-steps", type=int, default=5)
+    ap.add_argument("--c3-layout", default="lines", choices=["lines", "tagged"],
+                    help="configs[3] index: tagged entries in 128-B bucket lines (SAS_BUILD_TAG_LINES) or "
+                         "rank-ordered with a bucket table; with lines the rank-ordered index runs as the cross-check")
     ap.add_argument("--proof-sample", type=int, default=3000, help="queries per batch proven exact lower bounds")
     ap.add_argument("--no-c4", action="store_true", help="skip the configs[4] (sharded text) sub-record")
     ap.add_argument("--c4-share", type=int, default=1 << 30, help="configs[4]: text chars per GPU")

@@ -177,7 +177,8 @@ struct sst_index {
 // (sas_build.hip, build_tagged): the SA value is the low 40 bits.
 #define SAS_TAG_CHARS 12
 #define SAS_TL_SLOTS 14                  // entries per 128-B bucket line (SAS_BUILD_TAG_LINES)
-#define SAS_TL_END ((1ull << 40) - 1)    // entry standing for rank sa_n (the answer is next_pos)
+#define SAS_TL_END ((1ull << 40) - 1)    // SA field standing for rank sa_n (the answer is next_pos)
+#define SAS_TL_TAG_MAX (0xFFFFFFull << 40)  // the tag of a slot past its bucket's suffixes
 template <int W>
 struct SaView {
     const uint8_t* p;

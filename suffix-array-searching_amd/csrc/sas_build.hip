@@ -1243,13 +1243,17 @@ __global__ __launch_bounds__(TL_BLOCK) void k_tl_hdr(const uint64_t* __restrict_
     }
 }
 
+// slot j of line b: rank first + j; a slot past the bucket's count (a later bucket's suffix,
+// > every query routed to b) carries the tag 0xFFFFFF, so a lookup's "first slot whose tag is
+// >= q's" never passes it and needs no count
 template <int W>
 __global__ void k_tl_slots(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint64_t keys,
                            uint64_t* __restrict__ lines) {
     GRID_STRIDE(k, keys * SAS_TL_SLOTS) {
         const uint64_t b = k / SAS_TL_SLOTS, j = k - b * SAS_TL_SLOTS;
-        const uint64_t first = lines[b * 16] & (SAS_SA40_MAX - 1);
-        lines[b * 16 + 2 + j] = tl_make<W>(tw, sa, sa_n, first + j, p);
+        const uint64_t h = lines[b * 16], first = h & (SAS_SA40_MAX - 1);
+        const uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p);
+        lines[b * 16 + 2 + j] = j < (h >> 40) ? e : (e | SAS_TL_TAG_MAX);
     }
 }
 
@@ -1261,7 +1265,8 @@ __global__ void k_tl_ovf(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t
         const uint64_t c = (lines[(b + 1) * 16] & (SAS_SA40_MAX - 1)) - first;
         if (c < SAS_TL_SLOTS) continue;
         const uint64_t o = lines[b * 16 + 1];
-        for (uint64_t j = SAS_TL_SLOTS; j <= c; j++) ovf[o + j - SAS_TL_SLOTS] = tl_make<W>(tw, sa, sa_n, first + j, p);
+        for (uint64_t j = SAS_TL_SLOTS; j <= c; j++)
+            ovf[o + j - SAS_TL_SLOTS] = tl_make<W>(tw, sa, sa_n, first + j, p) | (j == c ? SAS_TL_TAG_MAX : 0ull);
     }
 }
 

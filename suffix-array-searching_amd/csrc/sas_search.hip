@@ -1981,74 +1981,98 @@ __device__ __forceinline__ uint64_t tl_count(const SearchArgs& a, uint64_t b, ui
     return c == 0xFFFFFFull ? (a.tag_lines[(b + 1) * 16] & TAG_M40) - (h0 & TAG_M40) : c;
 }
 
-// The lookup after the line: f = the first slot j < min(count, 14) whose tag is >= q's (or
-// that bound), ef = slot f's entry when f < 14.  The answer is entry j of the bucket for the
-// first j in [0, count] whose suffix is >= q (j = count: the next bucket's first suffix).
+// text word pairs a bucket-line lookup loads together for its tie's compare (the compare from
+// char p + 12 of a 132-char query spans ~4 windows: loaded lazily they are ~3 dependent round
+// trips of the whole wave); 0: the lazy pair loop (suffix_less_from_x2)
+#ifndef SAS_TL_PRE
+#define SAS_TL_PRE 3
+#endif
+
+// suffix(e) >= q for an entry of q's bucket (tag_ge), the tie's text compare preloading
+template <int QW, class Q>
+__device__ __forceinline__ bool tl_ge(uint64_t e, uint32_t Q12, const SearchArgs& a, const Q& q) {
+    const uint32_t T = (uint32_t)(e >> 40);
+    if (T != Q12) return T > Q12;
+    const uint64_t p = e & TAG_M40;
+    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+    if (q.m <= L) return (a.n - p) >= (uint64_t)q.m;
+    const uint64_t src = query_source(q);  // a text-slice query's own suffix starts with q
+    if (src != ~0ull && src + q.m <= a.n && p == src) return true;
+    uint32_t lcp;
+#if SAS_TL_PRE
+    return !suffix_less_from_pre<SAS_TL_PRE>(a.tw, a.n, p, q, L, &lcp);
+#else
+    return !suffix_less_from_x2<QW>(a.tw, a.n, p, q, L, &lcp);
+#endif
+}
+
+// The lookup after the line: f = the first slot j < 14 whose tag is >= q's (14 if none), ef =
+// slot f's entry when f < 14, h0 / ovf = the line's header.  Slots past the bucket's count
+// carry the tag 0xFFFFFF, so f <= count when count < 14, and f == count finds the first suffix
+// after the bucket.  The answer is entry j of the bucket for the first j in [0, count] whose
+// suffix is >= q (j = count: the next bucket's first suffix).  A wave waits for its slowest
+// lane at every step, so the loads of the lanes that need the overflow window are issued
+// before the other lanes' text compares wait for theirs: one round trip serves both.
 template <int QW, class Q>
 __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint64_t i, uint64_t b, uint64_t h0,
                                           uint64_t ovf, uint32_t f, uint64_t ef, uint32_t Q12) {
-    const uint64_t first = h0 & TAG_M40;
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     const uint64_t cnt = tl_count(a, b, h0);
-    const uint32_t lim = cnt < SAS_TL_SLOTS ? (uint32_t)cnt : (uint32_t)SAS_TL_SLOTS;
-    uint64_t j = 0, e = 0, start;
-    bool done = false;
-    if (f < lim) {
-        // a text-slice query and the tying entry of its own suffix: >= q without the text
-        const uint64_t src = query_source(q);
-        const bool own = src != ~0ull && src + q.m <= a.n && (ef & TAG_M40) == src && (uint32_t)(ef >> 40) == Q12;
-        if (own || tag_ge<QW>(ef, Q12, a, q)) {
-            j = f;
-            e = ef;
-            done = true;
-        }
-        start = (uint64_t)f + 1;
-    } else {
-        start = lim;  // every slot of the bucket in the line is < q
-    }
-    if (!done && start == cnt) {  // the first suffix after the bucket
-        j = cnt;
-        e = (f == cnt && cnt < SAS_TL_SLOTS) ? ef : tl_entry(a, b, ovf, cnt);
-        done = true;
-    }
-    if (!done && start >= SAS_TL_SLOTS) {
-        // one window of the overflow entries [start, cnt] (entry cnt is >= q whatever its tag),
-        // loaded as 16-B aligned pairs
-        typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-        const uint64_t rest = cnt + 1 - start;
-        const uint32_t nw = rest < SAS_TL_WIN ? (uint32_t)rest : (uint32_t)SAS_TL_WIN;
-        const uint64_t ab = ovf + (start - SAS_TL_SLOTS);
-        const uint32_t o = (uint32_t)(ab & 1);
-        const u64x2* ep = reinterpret_cast<const u64x2*>(a.tag_ovf + (ab & ~1ull));
-        uint64_t w2[SAS_TL_WIN + 2];
+    // the overflow window [14, cnt] (entry cnt is >= q whatever its tag), as 16-B aligned pairs
+    const bool ovfl = f >= SAS_TL_SLOTS && cnt > SAS_TL_SLOTS;
+    const uint64_t rest = ovfl ? cnt + 1 - SAS_TL_SLOTS : 0;
+    const uint32_t nw = rest < SAS_TL_WIN ? (uint32_t)rest : (uint32_t)SAS_TL_WIN;
+    const uint32_t o = (uint32_t)(ovf & 1);
+    uint64_t w2[SAS_TL_WIN + 2];
+    if (ovfl) {
+        const u64x2* ep = reinterpret_cast<const u64x2*>(a.tag_ovf + (ovf & ~1ull));
 #pragma unroll
         for (int k = 0; k < SAS_TL_WIN / 2 + 1; k++) {
             const u64x2 v = (2u * k < o + nw) ? __builtin_nontemporal_load(ep + k) : u64x2{0ull, 0ull};
             w2[2 * k] = v.x;
             w2[2 * k + 1] = v.y;
         }
+    }
+    uint64_t j = 0, e = 0, start = SAS_TL_SLOTS;
+    bool done = false;
+    if (f < SAS_TL_SLOTS) {
+        if (f >= cnt || tl_ge<QW>(ef, Q12, a, q)) {  // f == cnt: the first suffix after the bucket
+            j = f;
+            e = ef;
+            done = true;
+        }
+        start = (uint64_t)f + 1;  // a tie whose suffix is < q: the search goes on
+    } else if (cnt == SAS_TL_SLOTS) {  // every suffix of the bucket is < q: the next one's first
+        j = cnt;
+        e = tl_entry(a, b, ovf, cnt);
+        done = true;
+    } else if (ovfl) {
         uint64_t ew[SAS_TL_WIN];
 #pragma unroll
         for (int k = 0; k < SAS_TL_WIN; k++) ew[k] = (uint32_t)k < nw ? (o ? w2[k + 1] : w2[k]) : 0ull;
         uint32_t k0 = nw;
 #pragma unroll
         for (int k = SAS_TL_WIN - 1; k >= 0; k--)
-            if ((uint32_t)k < nw && (start + k == cnt || (uint32_t)(ew[k] >> 40) >= Q12)) k0 = (uint32_t)k;
+            if ((uint32_t)k < nw && (SAS_TL_SLOTS + k == cnt || (uint32_t)(ew[k] >> 40) >= Q12)) k0 = (uint32_t)k;
         uint64_t ek0 = ew[0];
 #pragma unroll
         for (int k = 1; k < SAS_TL_WIN; k++) ek0 = (k0 == (uint32_t)k) ? ew[k] : ek0;
         if (k0 < nw) {
-            const uint64_t r = start + k0;
-            const uint64_t src = query_source(q);
-            const bool own = src != ~0ull && src + q.m <= a.n && (ek0 & TAG_M40) == src && (uint32_t)(ek0 >> 40) == Q12;
-            if (r == cnt || own || tag_ge<QW>(ek0, Q12, a, q)) {
+            const uint64_t r = SAS_TL_SLOTS + k0;
+            if (r == cnt || tl_ge<QW>(ek0, Q12, a, q)) {
                 j = r;
                 e = ek0;
                 done = true;
             }
             start = r + 1;
         } else {
-            start += nw;
+            start = SAS_TL_SLOTS + nw;
         }
+    }
+    if (!done && start == cnt) {  // the first suffix after the bucket
+        j = cnt;
+        e = tl_entry(a, b, ovf, cnt);
+        done = true;
     }
     if (!done) {  // binary search over [start, cnt): entry cnt is >= q
         uint64_t l2 = start, h2 = cnt, pe = 0;
@@ -2078,10 +2102,14 @@ __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint6
         }
         a.out_probes[i] = probes;
     }
-    (void)first;
 }
 
-// The cooperative part: every lane of the wave calls it together (act: the lane holds query i).
+// The cooperative part: every lane of the wave calls it together (act: the lane holds query
+// i).  Lane s of a group holds 16 B of each of the group's 8 lines (s = 0: the header; s >= 1:
+// slots 2s - 2, 2s - 1); per line the group finds the first slot of the bucket whose tag is >=
+// the line's query's tag (a min over the group), and hands that slot's entry and the header
+// to the query's lane.  (Measured slower, same box: each lane loading its own line's header
+// as a ninth 16-B load, and ballots in place of the min: 2.04-2.07 vs 1.90-1.92 ms per 2*10^7.)
 template <int QW, class Q>
 __device__ __forceinline__ void tl_lookup(const SearchArgs& a, const Q& q, bool act, uint64_t i) {
     const uint32_t lane = threadIdx.x & 63, sub = lane & (TL_G - 1), g0 = lane & ~(uint32_t)(TL_G - 1);
