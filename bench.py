@@ -488,6 +488,8 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     lines = algo == "tagged" and args.c3_layout == "lines"
     phases = [("lines", (algo,)), ("tagged", (algo,) + tuple(x for x in extra_algos if x != algo))] if lines else \
         [(algo, (algo,) + tuple(x for x in extra_algos if x != algo))]
+    if args.c3_no_cross:
+        phases = phases[:1]
     idx = build(phases[0][0])
     st = idx.stats()
     # queries are cut from, and answers checked against, the index's packed text
@@ -907,6 +909,8 @@ def main():
     ap.add_argument("--c3-n", type=int, default=1 << 34)
     ap.add_argument("--c3-nq", type=int, default=100_000_000)
     ap.add_argument("--c3-steps", type=int, default=5)
+    ap.add_argument("--c3-no-cross", action="store_true",
+                    help="configs[3]: time the first index only (no rank-ordered cross-check index)")
     ap.add_argument("--c3-layout", default="lines", choices=["lines", "tagged"],
                     help="configs[3] index: tagged entries in 128-B bucket lines (SAS_BUILD_TAG_LINES) or "
                          "rank-ordered with a bucket table; with lines the rank-ordered index runs as the cross-check")

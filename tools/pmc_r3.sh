@@ -3,7 +3,7 @@
 # TCC_EA0_RDREQ + 32B + hit/miss) over bench.py for each record whose traffic bench.py
 # reports, summarised into gpurun_out/pmc_r3/pmc_<key>.json stamped with the library's
 # source hash (copy them into profiles/ to have bench.py attach them).
-# usage: tools/pmc_r3.sh [keys...]   keys: prefix plain23 plain30 quad c3
+# usage: tools/pmc_r3.sh [keys...]   keys: prefix plain23 plain30 quad c3 (bucket lines)
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/pmc_r3
@@ -16,7 +16,7 @@ for k in $keys; do
     plain23) args="$base --algo plain"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t23 ;;
     plain30) args="$base --algo plain --top2-levels 30"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t30 ;;
     quad)    args="$base --algo quad"; kern=k_sa_quad; nq=10000000; name=quad_n1073741824_q10000000_m32 ;;
-    c3)      args="--workload c3 --c3-steps 2 --warmup 1"; kern=k_sa_tagged; nq=100000000; name=c3_tagged_n17179869184_q100000000 ;;
+    c3)      args="--workload c3 --c3-steps 2 --warmup 1 --c3-no-cross"; kern=k_sa_tagged_lines; nq=100000000; name=c3_tagged_lines_n17179869184_q100000000 ;;
     *) echo "unknown key $k"; exit 2 ;;
   esac
   d=$out/$k
