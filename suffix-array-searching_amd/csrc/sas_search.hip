@@ -1981,11 +1981,13 @@ __device__ __forceinline__ uint64_t tl_count(const SearchArgs& a, uint64_t b, ui
     return c == 0xFFFFFFull ? (a.tag_lines[(b + 1) * 16] & TAG_M40) - (h0 & TAG_M40) : c;
 }
 
-// text word pairs a bucket-line lookup loads together for its tie's compare (the compare from
-// char p + 12 of a 132-char query spans ~4 windows: loaded lazily they are ~3 dependent round
-// trips of the whole wave); 0: the lazy pair loop (suffix_less_from_x2)
+// text word pairs a bucket-line lookup loads together for its tie's compare: 5 pairs (80 B)
+// cover chars [p + 12, 256) of any suffix, so no compare of a query of <= 256 chars waits for a
+// second round trip (loaded lazily they are ~3 dependent round trips of the whole wave).  Same
+// box, 2*10^7 ragged 8..256 at n = 2^34: 5 pairs 1.91 ms, 4 pairs 1.99, 3 pairs 2.05-2.07
+// (gpurun_out A/B, profiles/r3/); 0: the lazy pair loop (suffix_less_from_x2)
 #ifndef SAS_TL_PRE
-#define SAS_TL_PRE 3
+#define SAS_TL_PRE 5
 #endif
 
 // suffix(e) >= q for an entry of q's bucket (tag_ge), the tie's text compare preloading

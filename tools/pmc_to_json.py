@@ -41,10 +41,21 @@ def per_dispatch(path, kernel):
     return vals
 
 
+STAT = "median"
+
+
 def mean_counter(path, kernel, name):
+    """The counter over the kernel's dispatches: their median by default (the bench's one
+    out_probes dispatch reads more than the timed ones and would skew a mean), or the mean
+    (--stat mean)."""
     d = per_dispatch(path, kernel)
-    xs = [v[name] for v in d.values() if name in v]
-    return (sum(xs) / len(xs), len(xs)) if xs else (None, 0)
+    xs = sorted(v[name] for v in d.values() if name in v)
+    if not xs:
+        return None, 0
+    if STAT == "mean":
+        return sum(xs) / len(xs), len(xs)
+    k = len(xs) // 2
+    return (xs[k] if len(xs) % 2 else (xs[k - 1] + xs[k]) / 2), len(xs)
 
 
 def main():
@@ -59,7 +70,10 @@ def main():
     ap.add_argument("--source-hash", default=None,
                     help="source hash of the library the counters were collected on (default: the in-tree "
                          "libsas_amd.so's sas_source_hash); bench.py reports the counters only for that build")
+    ap.add_argument("--stat", default="median", choices=["median", "mean"], help="over the kernel's dispatches")
     a = ap.parse_args()
+    global STAT
+    STAT = a.stat
     fetch_kib, nf = mean_counter(a.fetch, a.kernel, "FETCH_SIZE")
     write_kib, nw = mean_counter(a.write, a.kernel, "WRITE_SIZE")
     if a.source_hash is None:
@@ -69,7 +83,8 @@ def main():
                                         "suffix-array-searching_amd"))
         import sas_amd
         a.source_hash = sas_amd.source_hash()
-    out = {"kernel": a.kernel, "source_hash": a.source_hash, "dispatches_fetch": nf, "dispatches_write": nw,
+    out = {"kernel": a.kernel, "source_hash": a.source_hash, "dispatch_stat": a.stat, "dispatches_fetch": nf,
+           "dispatches_write": nw,
            "FETCH_SIZE_KiB": fetch_kib, "WRITE_SIZE_KiB": write_kib}
     read_bytes = 2 * fetch_kib * 1024 if fetch_kib is not None else None
     out["read_bytes_2xFETCH"] = read_bytes
