@@ -849,6 +849,94 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
                                    f"on all {sample} queries, {threads} threads, {dt:.2f} s", "agrees": cpu_ok}})
 
 
+def ref_sizes(frm: int = 5, to: int = 30, dense: bool = False):
+    """sizes() of the reference's u32 bench (sst/bin/bench.rs:453-471): bytes 2^from .. 2^to
+    (and 5/4, 3/2, 7/4 of each power with --dense)."""
+    v = []
+    for b in range(frm, to):
+        v.append(1 << b)
+        if dense:
+            v += [(1 << b) * 5 // 4, (1 << b) * 3 // 2, (1 << b) * 7 // 4]
+    v.append(1 << to)
+    return v
+
+
+def run_sst_sweep(args, torch, sas_amd, dev):
+    """The reference's u32 size sweep (sst/bin/bench.rs:50-110, 453-471): gen_vals of the
+    largest size (vals[0] = MAX), each size takes its prefix and sorts it; 10^6 uniform queries
+    (gen_queries, next_multiple_of(768)); per size every GPU layout (kernel time, HIP events)
+    and the CPU restatements of the reference's two ends of the '40x' claim (readme.org:8):
+    SortedVec::binary_search on 1 thread and STree16 left_max batch_final::<128> on 1 and all
+    allotted threads (the reference times 1 and 6, :497-498).  Every GPU layout's answers
+    must equal SortedVec's on every query."""
+    from oracle import pyoracle as O
+    sizes = ref_sizes(5, args.sweep_to, args.sweep_dense)
+    nmax = sizes[-1] // 4
+    rng = np.random.default_rng(SEED)
+    allv = rng.integers(0, O.MAX, nmax, dtype=np.uint64).astype(np.uint32)
+    allv[0] = O.MAX
+    nq = -(-1_000_000 // 768) * 768
+    qs = rng.integers(0, O.MAX, nq, dtype=np.uint64).astype(np.uint32)
+    dq = torch.from_numpy(qs.view(np.int32)).to(dev)
+    dout = torch.empty(nq, dtype=torch.int32, device=dev)
+    threads = host_threads()
+    layouts = {
+        "SortedVec": lambda v: sas_amd.SortedVec.new(v),
+        "Eytzinger": lambda v: sas_amd.Eytzinger.new(v),
+        "STree16_left_max": lambda v: sas_amd.STree16.new_params(v, True, False, False),
+        "PartitionedSTree16M_b16": lambda v: sas_amd.PartitionedSTree16M.new(v, 16),
+        "DirectMap": lambda v: sas_amd.DirectMap.new(v),
+    }
+    rows = []
+    for size in sizes:
+        vals = np.sort(allv[: max(1, size // 4)])
+        ref = O.SortedVec(vals).query(qs)
+        row = {"size_bytes": size, "keys": len(vals), "gpu": {}, "cpu": {}}
+        for name, mk in layouts.items():
+            try:
+                idx = mk(vals)
+            except Exception as e:  # noqa: BLE001 -- a layout that cannot take this size is skipped
+                row["gpu"][name] = {"skipped": repr(e)[:120]}
+                continue
+            idx.query(dq)
+            kns = idx.time_query(dq, dout, reps=args.steps, stream=torch.cuda.current_stream(dev).cuda_stream)
+            got = dout.cpu().numpy().view(np.uint32)
+            if not np.array_equal(got, ref):
+                raise SystemExit(f"bench sst sweep: {name} differs from SortedVec at {size} B")
+            row["gpu"][name] = {"lookups_per_s": nq / (kns * 1e-9), "ns_per_lookup": kns / nq,
+                                "layers": idx.layers(), "index_bytes": idx.size()}
+            idx.free()
+        sv = O.SortedVec(vals)
+        t0 = time.perf_counter()
+        sv.query(qs)
+        row["cpu"]["SortedVec_binary_search_1t"] = nq / (time.perf_counter() - t0)
+        tree = O.STree(vals, left_max=True)
+        for th in sorted({1, threads}):
+            t0 = time.perf_counter()
+            got = tree.query_batch(qs, th)
+            row["cpu"][f"STree16_left_max_batch_final128_{th}t"] = nq / (time.perf_counter() - t0)
+            if not np.array_equal(got, ref):
+                raise SystemExit(f"bench sst sweep: CPU STree16 differs from SortedVec at {size} B")
+        row["cpu_stree_over_binary_search_1t"] = (row["cpu"]["STree16_left_max_batch_final128_1t"] /
+                                                  row["cpu"]["SortedVec_binary_search_1t"])
+        best = max((k for k in row["gpu"] if "lookups_per_s" in row["gpu"][k]),
+                   key=lambda k: row["gpu"][k]["lookups_per_s"])
+        row["gpu_best"] = best
+        row["gpu_best_over_cpu_binary_search_1t"] = (row["gpu"][best]["lookups_per_s"] /
+                                                     row["cpu"]["SortedVec_binary_search_1t"])
+        rows.append(row)
+        log(f"sweep {size} B: best {best} {row['gpu'][best]['lookups_per_s']:.3g}/s, CPU STree/binary "
+            f"{row['cpu_stree_over_binary_search_1t']:.1f}x")
+    emit({"metric": "u32 static-search-tree lookups/s across the reference's size sweep (32 B .. 2^%d B)" %
+                    args.sweep_to,
+          "value": rows[-1]["gpu"][rows[-1]["gpu_best"]]["lookups_per_s"], "unit": "lookups/s", "n_gpus": 1,
+          "steps": args.steps, "warmup": 1, "higher_is_better": True, "dtype": "u32", "vs_baseline": None,
+          "data": "synthetic: gen_vals / gen_queries shapes (sst/util.rs:16-42), prefixes of one draw",
+          "config": {"workload": "sst u32 size sweep (sst/bin/bench.rs:453-471)", "queries": nq,
+                     "cpu_threads": threads, "dense": args.sweep_dense},
+          "sweep": rows})
+
+
 # ---------------------------------------------------------------- configs[1] / [2] (headline)
 WORKLOADS = {
     "prefix": "PREFIX: p = {p}-char bucket table (the reference's prefix table, sas/sa_search.rs:59-95, "
@@ -924,6 +1012,10 @@ def main():
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric) + every config's sub-record; "
                          "c3: the configs[3] record alone; sst: the u32 static-search-tree path")
     ap.add_argument("--positive", action="store_true", help="sst workload: queries drawn from the keys")
+    ap.add_argument("--sweep", action="store_true",
+                    help="sst workload: the reference's size sweep (32 B .. 2^--sweep-to B) instead of one size")
+    ap.add_argument("--sweep-to", type=int, default=30, help="sst sweep: largest size 2^k bytes")
+    ap.add_argument("--sweep-dense", action="store_true", help="sst sweep: also 5/4, 3/2, 7/4 of each power")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
@@ -945,6 +1037,8 @@ def main():
     if args.workload == "c3":
         return run_c3(args, torch, sas_amd, dev, ws, rank)
     if args.workload == "sst":
+        if args.sweep:
+            return run_sst_sweep(args, torch, sas_amd, dev)
         return run_sst(args, torch, sas_amd, dev, ws, rank)
     if args.algo is None:
         args.algo = "prefix"

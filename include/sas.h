@@ -128,8 +128,8 @@ typedef struct sas_index sas_index;
                                         and cost 16 GiB at L = 30.  Clamped to the iteration
                                         count; results never depend on L                   */
 #define SAS_BUILD_TAG_LINES (1u << 24) /* with SAS_BUILD_TAGGED: the tagged entries as one
-                                        128-B line per p-char bucket {first rank 40 bits |
-                                        count 24 bits, overflow offset, the 14 entries of ranks
+                                        128-B line per p-char bucket {overflow offset 40 bits
+                                        | count 24 bits, first rank, the 14 entries of ranks
                                         first .. first + 13} (slots past the bucket's count hold
                                         the next buckets' first suffixes, so the line ends with
                                         the answer to "every suffix of the bucket is < q") plus

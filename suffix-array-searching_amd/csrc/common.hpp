@@ -135,8 +135,8 @@ struct sas_index {
     // min(rank count of key x, 2^24 - 1) << 40} for x in [0, 4^tag_p]
     uint64_t* tag_table = nullptr;
     uint32_t tag_p = 0;
-    // SAS_BUILD_TAG_LINES (no SA, no tag_table): line b = 16 u64 {first rank | min(count,
-    // 2^24 - 1) << 40, overflow offset, entries of ranks first .. first + SAS_TL_SLOTS - 1}
+    // SAS_BUILD_TAG_LINES (no SA, no tag_table): line b = 16 u64 {overflow offset | min(count,
+    // 2^24 - 1) << 40, first rank, entries of ranks first .. first + SAS_TL_SLOTS - 1}
     // (an entry past sa_n is SAS_TL_END); tag_ovf holds ranks first + SAS_TL_SLOTS .. first +
     // count of every bucket with count >= SAS_TL_SLOTS, bucket after bucket
     uint64_t* tag_lines = nullptr;

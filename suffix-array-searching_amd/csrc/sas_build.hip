@@ -1216,8 +1216,9 @@ __global__ __launch_bounds__(TL_BLOCK) void k_tl_sums(const uint64_t* __restrict
     if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-// headers: line b's first rank | count and overflow offset (bsum: exclusive block offsets);
-// line `keys` is a terminal header {sa_n} so a saturated count reads the next line's rank
+// headers: line b's {overflow offset | count << 40, first rank} (bsum: exclusive block
+// offsets; the word a lookup needs first holds all it needs of the header); line `keys` is a
+// terminal header {0, sa_n} so a saturated count reads the next line's first rank
 __global__ __launch_bounds__(TL_BLOCK) void k_tl_hdr(const uint64_t* __restrict__ t, uint64_t keys,
                                                      const uint64_t* __restrict__ bsum, uint64_t* __restrict__ lines) {
     __shared__ uint64_t lds[TL_BLOCK / 64 + 1];
@@ -1233,12 +1234,12 @@ __global__ __launch_bounds__(TL_BLOCK) void k_tl_hdr(const uint64_t* __restrict_
         const uint64_t b = b0 + k;
         if (b < keys) {
             const uint64_t first = t[b], c = t[b + 1] - first;
-            lines[b * 16] = first | ((c < 0xFFFFFFull ? c : 0xFFFFFFull) << 40);
-            lines[b * 16 + 1] = off;
+            lines[b * 16] = off | ((c < 0xFFFFFFull ? c : 0xFFFFFFull) << 40);
+            lines[b * 16 + 1] = first;
             off += need[k];
         } else if (b == keys) {
-            lines[b * 16] = t[b];
-            lines[b * 16 + 1] = 0;
+            lines[b * 16] = 0;
+            lines[b * 16 + 1] = t[b];
         }
     }
 }
@@ -1251,7 +1252,7 @@ __global__ void k_tl_slots(const uint64_t* __restrict__ tw, SaView<W> sa, uint64
                            uint64_t* __restrict__ lines) {
     GRID_STRIDE(k, keys * SAS_TL_SLOTS) {
         const uint64_t b = k / SAS_TL_SLOTS, j = k - b * SAS_TL_SLOTS;
-        const uint64_t h = lines[b * 16], first = h & (SAS_SA40_MAX - 1);
+        const uint64_t h = lines[b * 16], first = lines[b * 16 + 1];
         const uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p);
         lines[b * 16 + 2 + j] = j < (h >> 40) ? e : (e | SAS_TL_TAG_MAX);
     }
@@ -1261,10 +1262,10 @@ template <int W>
 __global__ void k_tl_ovf(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint64_t keys,
                          const uint64_t* __restrict__ lines, uint64_t* __restrict__ ovf) {
     GRID_STRIDE(b, keys) {
-        const uint64_t first = lines[b * 16] & (SAS_SA40_MAX - 1);
-        const uint64_t c = (lines[(b + 1) * 16] & (SAS_SA40_MAX - 1)) - first;
+        const uint64_t first = lines[b * 16 + 1];
+        const uint64_t c = lines[(b + 1) * 16 + 1] - first;
         if (c < SAS_TL_SLOTS) continue;
-        const uint64_t o = lines[b * 16 + 1];
+        const uint64_t o = lines[b * 16] & (SAS_SA40_MAX - 1);
         for (uint64_t j = SAS_TL_SLOTS; j <= c; j++)
             ovf[o + j - SAS_TL_SLOTS] = tl_make<W>(tw, sa, sa_n, first + j, p) | (j == c ? SAS_TL_TAG_MAX : 0ull);
     }
@@ -1729,11 +1730,12 @@ __global__ void k_tl_sa(const uint64_t* __restrict__ lines, const uint64_t* __re
         uint64_t lo = 0, hi = keys;
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
-            if ((lines[mid * 16] & (SAS_SA40_MAX - 1)) > r) hi = mid;
+            if (lines[mid * 16 + 1] > r) hi = mid;
             else lo = mid + 1;
         }
-        const uint64_t b = lo - 1, j = r - (lines[b * 16] & (SAS_SA40_MAX - 1));
-        const uint64_t e = j < SAS_TL_SLOTS ? lines[b * 16 + 2 + j] : ovf[lines[b * 16 + 1] + j - SAS_TL_SLOTS];
+        const uint64_t b = lo - 1, j = r - lines[b * 16 + 1];
+        const uint64_t e = j < SAS_TL_SLOTS ? lines[b * 16 + 2 + j]
+                                            : ovf[(lines[b * 16] & (SAS_SA40_MAX - 1)) + j - SAS_TL_SLOTS];
         out[i] = e & (SAS_SA40_MAX - 1);
     }
 }

@@ -1978,7 +1978,7 @@ __device__ __forceinline__ uint64_t tl_entry(const SearchArgs& a, uint64_t b, ui
 // bucket b's suffix count from its header word (a saturated count reads the next line's rank)
 __device__ __forceinline__ uint64_t tl_count(const SearchArgs& a, uint64_t b, uint64_t h0) {
     const uint64_t c = h0 >> 40;
-    return c == 0xFFFFFFull ? (a.tag_lines[(b + 1) * 16] & TAG_M40) - (h0 & TAG_M40) : c;
+    return c == 0xFFFFFFull ? a.tag_lines[(b + 1) * 16 + 1] - a.tag_lines[b * 16 + 1] : c;
 }
 
 // text word pairs a bucket-line lookup loads together for its tie's compare: 5 pairs (80 B)
@@ -2009,7 +2009,7 @@ __device__ __forceinline__ bool tl_ge(uint64_t e, uint32_t Q12, const SearchArgs
 }
 
 // The lookup after the line: f = the first slot j < 14 whose tag is >= q's (14 if none), ef =
-// slot f's entry when f < 14, h0 / ovf = the line's header.  Slots past the bucket's count
+// slot f's entry when f < 14, h0 = the line's header word {overflow offset | count}.  Slots past the bucket's count
 // carry the tag 0xFFFFFF, so f <= count when count < 14, and f == count finds the first suffix
 // after the bucket.  The answer is entry j of the bucket for the first j in [0, count] whose
 // suffix is >= q (j = count: the next bucket's first suffix).  A wave waits for its slowest
@@ -2017,9 +2017,9 @@ __device__ __forceinline__ bool tl_ge(uint64_t e, uint32_t Q12, const SearchArgs
 // before the other lanes' text compares wait for theirs: one round trip serves both.
 template <int QW, class Q>
 __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint64_t i, uint64_t b, uint64_t h0,
-                                          uint64_t ovf, uint32_t f, uint64_t ef, uint32_t Q12) {
+                                          uint32_t f, uint64_t ef, uint32_t Q12) {
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
-    const uint64_t cnt = tl_count(a, b, h0);
+    const uint64_t cnt = tl_count(a, b, h0), ovf = h0 & TAG_M40;
     // the overflow window [14, cnt] (entry cnt is >= q whatever its tag), as 16-B aligned pairs
     const bool ovfl = f >= SAS_TL_SLOTS && cnt > SAS_TL_SLOTS;
     const uint64_t rest = ovfl ? cnt + 1 - SAS_TL_SLOTS : 0;
@@ -2106,12 +2106,36 @@ __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint6
     }
 }
 
+// Exchanges inside an aligned group of 8 lanes without address registers: ds_swizzle in bit
+// mode (lane' = ((lane & and) | or) ^ xor within each 32-lane half) and DPP quad_perm.
+__device__ __forceinline__ uint32_t g8_swz(uint32_t v, int pattern_k) {
+    switch (pattern_k) {  // broadcast from lane k of the group: and 0x18, or k
+        case 0: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (0 << 5));
+        case 1: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (1 << 5));
+        case 2: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (2 << 5));
+        case 3: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (3 << 5));
+        case 4: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (4 << 5));
+        case 5: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (5 << 5));
+        case 6: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (6 << 5));
+        default: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (7 << 5));
+    }
+}
+__device__ __forceinline__ uint32_t g8_min(uint32_t c) {
+    uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+    c = t < c ? t : c;
+    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+    c = t < c ? t : c;
+    t = (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x1F | (4 << 10));  // lane ^ 4
+    return t < c ? t : c;
+}
+
 // The cooperative part: every lane of the wave calls it together (act: the lane holds query
 // i).  Lane s of a group holds 16 B of each of the group's 8 lines (s = 0: the header; s >= 1:
 // slots 2s - 2, 2s - 1); per line the group finds the first slot of the bucket whose tag is >=
 // the line's query's tag (a min over the group), and hands that slot's entry and the header
-// to the query's lane.  (Measured slower, same box: each lane loading its own line's header
-// as a ninth 16-B load, and ballots in place of the min: 2.04-2.07 vs 1.90-1.92 ms per 2*10^7.)
+// word {overflow offset | count} to the query's lane.  (Measured slower, same box: each lane
+// loading its own line's header as a ninth 16-B load, and ballots in place of the min:
+// 2.04-2.07 vs 1.90-1.92 ms per 2*10^7, profiles/r3/ab_lines_v2_vs_v1.txt.)
 template <int QW, class Q>
 __device__ __forceinline__ void tl_lookup(const SearchArgs& a, const Q& q, bool act, uint64_t i) {
     const uint32_t lane = threadIdx.x & 63, sub = lane & (TL_G - 1), g0 = lane & ~(uint32_t)(TL_G - 1);
@@ -2123,40 +2147,34 @@ __device__ __forceinline__ void tl_lookup(const SearchArgs& a, const Q& q, bool 
     uint4 v[TL_G];
 #pragma unroll
     for (int k = 0; k < TL_G; k++) {
-        const uint64_t bk = (uint64_t)__shfl((long long)b, (int)g0 + k, 64);
+        const uint64_t bk = ((uint64_t)g8_swz((uint32_t)(b >> 32), k) << 32) | g8_swz((uint32_t)b, k);
         v[k] = nt_load4(L4 + bk * 8 + sub);
     }
-    uint64_t my_h0 = 0, my_h1 = 0, my_ef = 0;
+    uint64_t my_h0 = 0, my_ef = 0;
     uint32_t my_f = 0;
 #pragma unroll
     for (int k = 0; k < TL_G; k++) {
         const uint64_t lo64 = ((uint64_t)v[k].y << 32) | v[k].x, hi64 = ((uint64_t)v[k].w << 32) | v[k].z;
-        const uint64_t h0 = (uint64_t)__shfl((long long)lo64, (int)g0, 64);
-        const uint64_t h1 = (uint64_t)__shfl((long long)hi64, (int)g0, 64);
-        const uint64_t c = h0 >> 40;  // a saturated count is >= 14 as well
-        const uint32_t lim = c < SAS_TL_SLOTS ? (uint32_t)c : (uint32_t)SAS_TL_SLOTS;
-        const uint32_t Qk = (uint32_t)__shfl((int)Q12, (int)g0 + k, 64);
+        const uint32_t c32 = g8_swz(v[k].y, 0);  // the header word's high half: count << 8 | offset bits
+        const uint64_t h0 = ((uint64_t)c32 << 32) | g8_swz(v[k].x, 0);
+        const uint32_t c = c32 >> 8;  // a saturated count is >= 14 as well
+        const uint32_t lim = c < SAS_TL_SLOTS ? c : (uint32_t)SAS_TL_SLOTS;
+        const uint32_t Qk = g8_swz(Q12, k);
         const uint32_t j0 = 2 * sub - 2;  // slots of this lane (lane 0: the header)
         const bool ge0 = sub != 0 && j0 < lim && (uint32_t)(lo64 >> 40) >= Qk;
         const bool ge1 = sub != 0 && j0 + 1 < lim && (uint32_t)(hi64 >> 40) >= Qk;
-        uint32_t cand = ge0 ? j0 : (ge1 ? j0 + 1 : 64u);
-#pragma unroll
-        for (int o = 1; o < TL_G; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_xor((int)cand, o, TL_G);
-            cand = t < cand ? t : cand;
-        }
+        const uint32_t cand = g8_min(ge0 ? j0 : (ge1 ? j0 + 1 : 64u));
         const uint32_t f = cand == 64u ? lim : cand;
         const uint64_t mine = (f & 1) ? hi64 : lo64;
         const int src = (int)g0 + (f < SAS_TL_SLOTS ? (int)(f >> 1) + 1 : 0);
         const uint64_t ef = (uint64_t)__shfl((long long)mine, src, 64);
         if (sub == (uint32_t)k) {
             my_h0 = h0;
-            my_h1 = h1;
             my_f = f;
             my_ef = ef;
         }
     }
-    if (act) tl_finish<QW>(a, q, i, b, my_h0, my_h1, my_f, my_ef, Q12);
+    if (act) tl_finish<QW>(a, q, i, b, my_h0, my_f, my_ef, Q12);
 }
 
 template <int QW>
@@ -2220,7 +2238,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_lines_range(Searc
         const uint32_t Q12 = tag_of_key(K64, a.tag_p), Q3t = tag_of_key(Q3, a.tag_p);
         const uint64_t b0 = K64 >> sh, b1 = (m <= L ? Q3 : K64) >> sh;
         const uint64_t h00 = a.tag_lines[b0 * 16], h10 = a.tag_lines[b1 * 16];
-        const uint64_t o0 = a.tag_lines[b0 * 16 + 1], o1 = a.tag_lines[b1 * 16 + 1];
+        const uint64_t o0 = h00 & TAG_M40, o1 = h10 & TAG_M40;
         uint64_t lo = 0, l1 = tl_count(a, b0, h00), hi = 0, h1 = tl_count(a, b1, h10);
         while (lo < l1 || hi < h1) {
             const bool g0 = lo < l1, g1 = hi < h1;
@@ -2236,7 +2254,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_lines_range(Searc
                 else hi = m1 + 1;
             }
         }
-        uint64_t rlo = (h00 & TAG_M40) + lo, rhi = (h10 & TAG_M40) + hi;
+        uint64_t rlo = a.tag_lines[b0 * 16 + 1] + lo, rhi = a.tag_lines[b1 * 16 + 1] + hi;
         if (rhi < rlo) rhi = rlo;
         a.out_pos[i] = a.rank_lo + rlo;
         out_hi[i] = a.rank_lo + rhi;

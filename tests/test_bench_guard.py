@@ -121,3 +121,10 @@ def test_pmc_attached_only_for_the_same_source_hash(tmp_path, monkeypatch):
     assert r["pmc"]["stale"] and "fabric_bytes_per_lookup" not in r["pmc"]
     r = bench.record("x", 10, 1.0, 1.0, bpl, 0, bench.load_pmc("same"), 1.0)
     assert r["pmc"]["fabric_bytes_per_lookup"] == 1e8
+
+
+def test_reference_sweep_sizes():
+    """sizes() of sst/bin/bench.rs:453-471: 2^5 .. 2^to bytes, dense adds 5/4, 3/2, 7/4."""
+    assert bench.ref_sizes(5, 8) == [32, 64, 128, 256]
+    assert bench.ref_sizes(5, 7, dense=True) == [32, 40, 48, 56, 64, 80, 96, 112, 128]
+    assert bench.ref_sizes()[-1] == 1 << 30 and len(bench.ref_sizes()) == 26
