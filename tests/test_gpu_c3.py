@@ -6,9 +6,12 @@ sas/util.rs:18-26), on the two indexes the bench uses at that size.
   PLAIN and LCP give identical positions;
 * the 40-bit SA index with compact key-only quad leaves and a p = 16 40-bit rank table:
   PREFIX, QUAD and PLAIN give the same positions as the tagged index;
+* the bucket-line index (SAS_BUILD_TAG_LINES, p = 15, the bench's configs[3] record; built
+  from a host copy of the text): TAGGED, byte queries and text slices, the same positions;
+  its ranges and SA values equal the tagged index's;
 * every answer is an occurrence of its query (positive queries), and 3000 sampled answers
   are proven exact lower bounds on the index's own SA: SA[lo] = answer and
-  suffix(SA[lo-1]) < q, with lo from sas_search_range; the two indexes' ranges agree.
+  suffix(SA[lo-1]) < q, with lo from sas_search_range; the indexes' ranges agree.
 """
 import numpy as np
 import pytest
@@ -111,4 +114,24 @@ def test_c3_full_size():
         assert torch.equal(r.cpu(), ref), algo
     lo_q, hi_q = idx.search_range(buf, off_s, lens_s)
     assert np.array_equal(lo_q, lo_t) and np.array_equal(hi_q, hi_t)
+    sa_probe = [int(idx.suffix_array(count=1, start=int(lo_t[j]))[0]) for j in range(0, len(ids), 100)]
     idx.free()
+    torch.cuda.empty_cache()
+
+    # the bucket-line index (from a host copy: a device byte text does not fit beside its build)
+    ht = sas_amd.random_string(N, seed=31415, device="cuda").cpu().numpy()
+    torch.cuda.empty_cache()
+    lines = sas_amd.SaNaive.build(ht, lcp=False, verify=True, tagged=True, tag_lines=True)
+    del ht
+    st = lines.stats()
+    assert st["tag_chars"] == 15 and st["tag_line_slots"] == 14 and st["sa_entries"] == N
+    r = lines.search_batch(qb, qoff, qlen, algo="tagged")
+    torch.cuda.synchronize()
+    assert torch.equal(r.cpu(), ref)
+    r = lines.search_slices(src, qlen)
+    torch.cuda.synchronize()
+    assert torch.equal(r.cpu(), ref)
+    lo_l, hi_l = lines.search_range(buf, off_s, lens_s)
+    assert np.array_equal(lo_l, lo_t) and np.array_equal(hi_l, hi_t)
+    assert sa_probe == [int(lines.suffix_array(count=1, start=int(lo_t[j]))[0]) for j in range(0, len(ids), 100)]
+    lines.free()
