@@ -29,6 +29,6 @@ for k in $keys; do
   w=$(ls "$d"/write/*counter_collection.csv | head -1)
   r=$(ls "$d"/req/*counter_collection.csv | head -1)
   python3 tools/pmc_to_json.py --kernel "$kern" --nq $nq --fetch "$f" --write "$w" --req "$r" --out "$out/pmc_$name.json" || exit $?
-  rm -f "$d"/*/*counter_collection.csv.bak
+  rm -rf "$d/fetch" "$d/write" "$d/req"  # the per-dispatch CSVs: too big to bring back
 done
 exit 0
