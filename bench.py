@@ -155,30 +155,40 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             tail = 64
         h, c, l = _classify(sizes, node, lds_l)
         hbm, cache, lds = h + max(0.0, probes - H) * tail + (max(0.0, m - 32) / 4 if algo != "stree" else 0), c, l
+        # one request per DRAM-level node (a 64-B node is one cooperative request; a 32-B one
+        # too), per extra probe past the leaf, and the query stream
+        reqs = {"cache": c / node, "hbm": h / node + max(0.0, probes - H) + (8.0 if packed else m) / 128}
     hbm += io
     out = {"hbm": hbm, "cache": cache, "lds": lds, "section_8d_plain": P * (4 + m) + m + 8}
-    if algo in ("plain", "lcp", "inline", "llcp") and not range_flag:
+    if algo in ("plain", "lcp", "inline", "llcp", "stree", "quad", "sector") and not range_flag:
         out["requests_model"] = reqs
     return out
 
 
 def request_split(bpl: dict, pmc, lookups: int, kernel_ms: float):
-    """A PLAIN-family kernel's measured L2->fabric requests split by where they are served:
-    `hbm` = the model's HBM-level requests (bytes_per_lookup's requests_model), `cache` = the
-    rest of the PMC count (the cache-resident pivot levels' L2 misses, served by the Infinity
-    Cache).  Each share is priced at its own measured random-request ceiling; `frac` = that
-    floor over the kernel's time (<= 1 when the model holds)."""
+    """A kernel's measured L2->fabric requests split by where they are served: `hbm` = the
+    model's DRAM-level requests (bytes_per_lookup's requests_model), `cache` = the rest of the
+    PMC count (L2 misses of arrays the 256 MiB Infinity Cache holds).  Two limits apply: every
+    request crosses the fabric (at most the best measured random-request rate, 5.73e10/s, the
+    cache-resident one), and the DRAM share also needs DRAM (5.08e10/s); `floor_ms` is the larger
+    of the two times and `frac` = floor / kernel time (<= 1).  (Adding the two shares' times
+    instead is not a bound: PLAIN's mixed stream ran at 5.56e10 requests/s, above the DRAM rate,
+    because its cache hits never reach DRAM.)"""
     if not pmc or not pmc.get("rdreq_per_launch") or "requests_model" not in bpl:
         return None
     total = pmc["rdreq_per_launch"] / lookups
     hbm = min(total, bpl["requests_model"]["hbm"])
     cache = total - hbm
-    floor_s = lookups * (hbm / RANDOM_REQ_CEILING + cache / CACHE_REQ_CEILING)
+    t_dram = lookups * hbm / RANDOM_REQ_CEILING
+    t_fabric = lookups * total / CACHE_REQ_CEILING
+    floor_s = max(t_dram, t_fabric)
     return {"per_lookup": total, "hbm_per_lookup": hbm, "cache_per_lookup": cache,
-            "hbm_ceiling_per_s": RANDOM_REQ_CEILING, "cache_ceiling_per_s": CACHE_REQ_CEILING,
-            "floor_ms": floor_s * 1e3, "frac": floor_s / (kernel_ms * 1e-3),
-            "basis": "hbm = model (pivot levels past the cache-resident ones: 1 each; SA probes: SA word + text "
-                     "window; query stream m/128), cache = PMC TCC_EA0_RDREQ minus hbm"}
+            "hbm_ceiling_per_s": RANDOM_REQ_CEILING, "fabric_ceiling_per_s": CACHE_REQ_CEILING,
+            "dram_ms": t_dram * 1e3, "fabric_ms": t_fabric * 1e3, "floor_ms": floor_s * 1e3,
+            "frac": floor_s / (kernel_ms * 1e-3),
+            "basis": "hbm = model (DRAM-level tree nodes / pivot levels: 1 each; SA probes: SA word + text window; "
+                     "the query stream m/128), cache = PMC TCC_EA0_RDREQ minus hbm; floor = max(hbm / DRAM rate, "
+                     "all / fabric rate)"}
 
 
 # ---------------------------------------------------------------- harness

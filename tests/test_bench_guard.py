@@ -95,8 +95,15 @@ def test_byte_model_hbm_pivot_levels():
     nq, kms = 10_000_000, 5.0
     sp = bench.request_split(bpl, {"rdreq_per_launch": 20.0 * nq}, nq, kms)
     assert abs(sp["hbm_per_lookup"] - 16.25) < 1e-9 and abs(sp["cache_per_lookup"] - 3.75) < 1e-9
-    floor = nq * (16.25 / bench.RANDOM_REQ_CEILING + 3.75 / bench.CACHE_REQ_CEILING)
+    floor = max(nq * 16.25 / bench.RANDOM_REQ_CEILING, nq * 20.0 / bench.CACHE_REQ_CEILING)
     assert abs(sp["frac"] - floor / (kms * 1e-3)) < 1e-12 and sp["frac"] < 1
+    # round 3's measured PLAIN (23 levels): 22.74 requests at 4.089 ms per 10^7 is under both limits
+    sp = bench.request_split(bpl, {"rdreq_per_launch": 22.74 * nq}, nq, 4.089)
+    assert sp["frac"] <= 1
+    # a tree: QUAD at n = 2^30 (3 LDS layers, 3 cache-resident, the 1 GB layer and the leaves in DRAM)
+    st = {"sa_width": 4, "quad_layers": 8, "quad_lds_layers": 3, "quad_fan": 17, "quad_entry_bytes": 16}
+    q = bench.bytes_per_lookup("quad", st, n, m, 8.0)
+    assert q["requests_model"] == {"cache": 3.0, "hbm": 2.0 + m / 128}
     assert bench.request_split(bench.bytes_per_lookup("prefix", {"sa_width": 4, "prefix_bytes": (4 ** 16 + 1) * 32,
                                                                   "prefix_chars": 16, "quad_entry_bytes": 16},
                                                       n, m, 1.0), {"rdreq_per_launch": 1.0}, nq, kms) is None
