@@ -129,16 +129,19 @@ typedef struct sas_index sas_index;
                                         count; results never depend on L                   */
 #define SAS_BUILD_TAG_LINES (1u << 24) /* with SAS_BUILD_TAGGED: the tagged entries as one
                                         128-B line per p-char bucket {overflow offset 40 bits
-                                        | count 24 bits, first rank, the 14 entries of ranks
-                                        first .. first + 13} (slots past the bucket's count hold
-                                        the next buckets' first suffixes, so the line ends with
+                                        | count 24 bits, the 20 entries of ranks first ..
+                                        first + 19 as 48-bit {SA | tag} split into u16 high and
+                                        u32 low halves} (slots past the bucket's count hold the
+                                        next buckets' first suffixes, so the line ends with
                                         the answer to "every suffix of the bucket is < q") plus
-                                        an overflow array with ranks first + 14 .. first + count
-                                        of the larger buckets.  A lookup reads its line as one
-                                        request of an 8-lane group: bucket and first entries
-                                        together.  p = SAS_BUILD_PREFIX_P or ceil(log4 n) - 2
-                                        (15 at n = 2^34: 128 GiB of lines, ~16 suffixes each).
-                                        No SA array: TAGGED lookups, ranges and sas_copy_sa64 */
+                                        an overflow array with ranks first + 20 .. first + count
+                                        of the larger buckets, the buckets' first ranks and a
+                                        second text copy 64 B off the 128-B line grid.  A
+                                        lookup reads its line as one request of an 8-lane
+                                        group: bucket and first entries together.  p =
+                                        SAS_BUILD_PREFIX_P or ceil(log4 n) - 2 (15 at n = 2^34:
+                                        128 GiB of lines, ~16 suffixes each).  No SA array:
+                                        TAGGED lookups, ranges and sas_copy_sa64          */
 #define SAS_BUILD_LLCP    (1u << 13) /* also build the Manber-Myers accelerant for
                                         SAS_ALGO_LLCP: per SA rank m, one 16-B entry
                                         {SA[m] 40 bits, Llcp 12 bits, Rlcp 12 bits, 16 chars
@@ -218,10 +221,14 @@ typedef struct sas_stats {
     uint64_t tag_table_bytes; /* SAS_BUILD_TAGGED bucket table, (4^p + 1) x 8 B       */
     uint64_t index_bytes;    /* every HBM array of the index together (text, SA or tagged
                                 entries, LCP, LLCP, trees, tables, top2)              */
-    uint32_t tag_line_slots; /* SAS_BUILD_TAG_LINES: entries per 128-B bucket line (14), else 0;
-                                tag_table_bytes is then the lines, sa_bytes the overflow */
-    uint32_t reserved0;
+    uint32_t tag_line_slots; /* SAS_BUILD_TAG_LINES: entries per 128-B bucket line (20), else 0;
+                                tag_table_bytes is then the lines and the first-rank
+                                table, sa_bytes the overflow                          */
+    uint32_t tag_line_tag_bits; /* SAS_BUILD_TAG_LINES: tag bits of a line entry (48 minus
+                                the SA bits: 16 below n = 2^32, 13 at n = 2^34)       */
     uint64_t tag_overflow_entries; /* SAS_BUILD_TAG_LINES: entries in the overflow array */
+    uint64_t text2_bytes;    /* SAS_BUILD_TAG_LINES: the second packed-text copy (64 B off
+                                the 128-B line grid, so a tie's compare reads one line) */
 } sas_stats;
 
 const char* sas_last_error(void);

@@ -135,13 +135,19 @@ struct sas_index {
     // min(rank count of key x, 2^24 - 1) << 40} for x in [0, 4^tag_p]
     uint64_t* tag_table = nullptr;
     uint32_t tag_p = 0;
-    // SAS_BUILD_TAG_LINES (no SA, no tag_table): line b = 16 u64 {overflow offset | min(count,
-    // 2^24 - 1) << 40, first rank, entries of ranks first .. first + SAS_TL_SLOTS - 1}
-    // (an entry past sa_n is SAS_TL_END); tag_ovf holds ranks first + SAS_TL_SLOTS .. first +
-    // count of every bucket with count >= SAS_TL_SLOTS, bucket after bucket
+    // SAS_BUILD_TAG_LINES (no SA, no tag_table): line b = 128 B {header u64: overflow offset |
+    // min(count, 2^24 - 1) << 40; u16 hi[20]; u32 lo[20]}, slot j = the 48-bit entry
+    // {SA (tag_sb bits) | tag << tag_sb} of rank first + j split as hi[j] << 32 | lo[j]
+    // (tl_slot below; an SA field of all ones stands for rank sa_n); tag_ovf holds the entries
+    // of ranks first + SAS_TL_SLOTS .. first + count (u64, same format) of every bucket with
+    // count >= SAS_TL_SLOTS, bucket after bucket; tag_first[b] = bucket b's first rank
     uint64_t* tag_lines = nullptr;
     uint64_t* tag_ovf = nullptr;
     uint64_t tag_ovf_n = 0;
+    uint64_t* tag_first = nullptr;
+    uint32_t tag_sb = 40;          // SA bits of a line entry: max(32, bit length of n)
+    uint64_t* text2 = nullptr;     // SAS_BUILD_TAG_LINES: the packed text again, 64 B off the
+    void* text2_base = nullptr;    // 128-B line grid (text2 = text2_base + 64 B; tl_text)
     sas_stats stats = {};
     mutable StagePool* stage = nullptr;  // created by the first host-pointer search
     mutable hipMemPool_t route_pool = nullptr;  // stream-ordered scratch of sas_route_pack (first use)
@@ -176,9 +182,24 @@ struct sst_index {
 // W = 8: the tagged SA of SAS_BUILD_TAGGED, u64 entries {SA 40 bits | 12 chars << 40}
 // (sas_build.hip, build_tagged): the SA value is the low 40 bits.
 #define SAS_TAG_CHARS 12
-#define SAS_TL_SLOTS 14                  // entries per 128-B bucket line (SAS_BUILD_TAG_LINES)
-#define SAS_TL_END ((1ull << 40) - 1)    // SA field standing for rank sa_n (the answer is next_pos)
-#define SAS_TL_TAG_MAX (0xFFFFFFull << 40)  // the tag of a slot past its bucket's suffixes
+// Bucket lines (SAS_BUILD_TAG_LINES): 20 entries of 48 bits per 128-B line, {SA | tag << sb}
+// with sb = max(32, bit length of n) SA bits and 48 - sb tag bits (the bits of chars [p, ...)
+// after the bucket's p chars: 13 bits at n = 2^34, 16 below 2^32).  In the line the entry is
+// split: u16 hi[j] = entry >> 32 at u16 4 + j, u32 lo[j] at u32 12 + j, so an 8-lane group
+// reading 16 B per lane holds the header and hi[0..3] (lane 0), hi[4..11], hi[12..19] (lanes
+// 1, 2) and lo[4s - 12 ..] (lanes 3..7).
+#define SAS_TL_SLOTS 20
+__host__ __device__ __forceinline__ uint64_t tl_sa_mask(uint32_t sb) { return (1ull << sb) - 1; }
+__host__ __device__ __forceinline__ uint32_t tl_tag_bits(uint32_t sb) { return 48 - sb; }
+// the tag of a packed 32-char key: tb bits from char p (the bucket's p chars are the key's first)
+__host__ __device__ __forceinline__ uint32_t tl_tag_of_key(uint64_t k64, uint32_t p, uint32_t tb) {
+    return (uint32_t)((k64 << (2 * p)) >> (64 - tb));
+}
+__device__ __forceinline__ uint64_t tl_slot(const uint64_t* __restrict__ lines, uint64_t b, uint32_t j) {
+    const uint16_t* h = reinterpret_cast<const uint16_t*>(lines + b * 16);
+    const uint32_t* l = reinterpret_cast<const uint32_t*>(lines + b * 16);
+    return ((uint64_t)h[4 + j] << 32) | l[12 + j];
+}
 template <int W>
 struct SaView {
     const uint8_t* p;
@@ -428,9 +449,12 @@ __device__ __forceinline__ bool suffix_less_from_x2(const uint64_t* __restrict__
 // a positive query matches its own suffix to the end, so the compare always runs over every
 // window and the plain loop's pair loads form a dependent chain ((m - h) / 64 round trips).
 // Windows past the preloaded 2 PRE - 2 continue as suffix_less_from_x2 does.
+// tw2: the same text 64 B off the 128-B line grid (bucket lines, sas_index::text2), or tw: the
+// pairs are read from the copy in which they lie in one 128-B line when only one copy has that
+// (any run of <= 4 pairs lies in one line of one of the two copies).
 template <int PRE, class Q>
-__device__ __forceinline__ bool suffix_less_from_pre(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
-                                                     const Q& q, uint32_t h, uint32_t* lcp) {
+__device__ __forceinline__ bool suffix_less_from_pre(const uint64_t* __restrict__ tw, const uint64_t* __restrict__ tw2,
+                                                     uint64_t n, uint64_t p, const Q& q, uint32_t h, uint32_t* lcp) {
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     const uint64_t lenS = n - p;
     const uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
@@ -438,9 +462,11 @@ __device__ __forceinline__ bool suffix_less_from_pre(const uint64_t* __restrict_
         const uint64_t w0 = (p + h) >> 5;
         const uint32_t sh = (uint32_t)((p + h) & 31) << 1;
         const uint32_t o = (uint32_t)(w0 & 1);
-        const u64x2* tp = reinterpret_cast<const u64x2*>(tw) + (w0 >> 1);
         const uint32_t nwin = (L - h + 31) >> 5;  // windows; window r reads words w0 + r, w0 + r + 1
         const uint32_t npair = (o + nwin) / 2 + 1;  // pairs holding words w0 .. w0 + nwin
+        const uint64_t P0 = w0 >> 1, P1 = P0 + (npair < (uint32_t)PRE ? npair : (uint32_t)PRE) - 1;
+        const bool two = (P0 >> 3) != (P1 >> 3) && ((P0 + 4) >> 3) == ((P1 + 4) >> 3);
+        const u64x2* tp = reinterpret_cast<const u64x2*>(two ? tw2 : tw) + P0;
         uint64_t W[2 * PRE];
 #pragma unroll
         for (int j = 0; j < PRE; j++) {

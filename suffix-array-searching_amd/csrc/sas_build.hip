@@ -1093,7 +1093,8 @@ static int build_tagged(sas_index* x, uint32_t p) {
 static void free_index(sas_index* x) {
     if (!x) return;
     void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->scratch, x->sec_inner,
-                     x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table, x->tag_lines, x->tag_ovf};
+                     x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table, x->tag_lines, x->tag_ovf,
+                     x->tag_first, x->text2_base};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     sas_stage_pool_free(x->stage);
     if (x->route_pool) {  // its blocks were freed stream-ordered: drain before destroying
@@ -1156,24 +1157,29 @@ extern "C" int sas_verify(const sas_index* index) {
 
 // ------------------------------------------------------------------ bucket lines
 // SAS_BUILD_TAG_LINES: the tagged entries as one 128-B line per p-char bucket (common.hpp,
-// sas_index::tag_lines): {first rank | min(count, 2^24 - 1) << 40, overflow offset, entries of
-// ranks first .. first + 13}, and the overflow array with ranks first + 14 .. first + count of
-// every bucket of >= 14 suffixes.  Built from the SA: first ranks (k_tt_fill), overflow
-// offsets (a block scan of max(count - 13, 0)), then every slot and overflow entry computed
-// from SA[r] and its text.  Peak: the SA, the lines, the first-rank table, then the overflow
-// array after the table is gone.
+// sas_index::tag_lines): the header {overflow offset | min(count, 2^24 - 1) << 40} and the
+// 48-bit entries {SA | tag << sb} of ranks first .. first + 19, split into u16 high and u32
+// low halves; the overflow array with the entries of ranks first + 20 .. first + count of
+// every bucket of >= 20 suffixes; the first-rank table (range and SA-by-rank calls, saturated
+// counts); a second copy of the packed text 64 B off the 128-B line grid (tl_text).  Built
+// from the SA: first ranks (k_tt_fill), overflow offsets (a block scan of max(count - 19,
+// 0)), then every slot and overflow entry from SA[r] and its text.  Peak: the SA, the lines
+// and the first-rank table.
 #define TL_BLOCK 1024
 #define TL_PER 4  // buckets per thread in the offset scan
 
+// the entry of rank r: {SA | tag << sb}; rank sa_n (past the index): every bit set, the SA
+// field standing for next_pos and the tag the maximum
 template <int W>
 __device__ __forceinline__ uint64_t tl_make(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint64_t r,
-                                            uint32_t p) {
-    if (r >= sa_n) return SAS_TL_END;
+                                            uint32_t p, uint32_t sb) {
+    if (r >= sa_n) return (1ull << 48) - 1;
     const uint64_t s = sa[r];
-    return s | (((text_chars32(tw, s) << (2 * p)) >> 40) << 40);
+    return s | ((uint64_t)tl_tag_of_key(text_chars32(tw, s), p, tl_tag_bits(sb)) << sb);
 }
+__device__ __forceinline__ uint64_t tl_tag_max(uint64_t e, uint32_t sb) { return e | (((1ull << 48) - 1) & ~tl_sa_mask(sb)); }
 
-// overflow entries of bucket b: ranks first + 14 .. first + count (the last, rank first + count,
+// overflow entries of bucket b: ranks first + 20 .. first + count (the last, rank first + count,
 // is the next bucket's first suffix)
 __device__ __forceinline__ uint64_t tl_ovf_need(const uint64_t* __restrict__ t, uint64_t b) {
     const uint64_t c = t[b + 1] - t[b];
@@ -1216,9 +1222,7 @@ __global__ __launch_bounds__(TL_BLOCK) void k_tl_sums(const uint64_t* __restrict
     if (threadIdx.x == 0) bsum[blockIdx.x] = tot;
 }
 
-// headers: line b's {overflow offset | count << 40, first rank} (bsum: exclusive block
-// offsets; the word a lookup needs first holds all it needs of the header); line `keys` is a
-// terminal header {0, sa_n} so a saturated count reads the next line's first rank
+// headers: line b's {overflow offset | count << 40} (bsum: exclusive block offsets)
 __global__ __launch_bounds__(TL_BLOCK) void k_tl_hdr(const uint64_t* __restrict__ t, uint64_t keys,
                                                      const uint64_t* __restrict__ bsum, uint64_t* __restrict__ lines) {
     __shared__ uint64_t lds[TL_BLOCK / 64 + 1];
@@ -1233,47 +1237,50 @@ __global__ __launch_bounds__(TL_BLOCK) void k_tl_hdr(const uint64_t* __restrict_
     for (int k = 0; k < TL_PER; k++) {
         const uint64_t b = b0 + k;
         if (b < keys) {
-            const uint64_t first = t[b], c = t[b + 1] - first;
+            const uint64_t c = t[b + 1] - t[b];
             lines[b * 16] = off | ((c < 0xFFFFFFull ? c : 0xFFFFFFull) << 40);
-            lines[b * 16 + 1] = first;
             off += need[k];
-        } else if (b == keys) {
-            lines[b * 16] = 0;
-            lines[b * 16 + 1] = t[b];
         }
     }
 }
 
 // slot j of line b: rank first + j; a slot past the bucket's count (a later bucket's suffix,
-// > every query routed to b) carries the tag 0xFFFFFF, so a lookup's "first slot whose tag is
-// >= q's" never passes it and needs no count
+// > every query routed to b) carries the maximal tag, so a lookup's count of the slots whose
+// tag is < q's never passes it and needs no count
 template <int W>
-__global__ void k_tl_slots(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint64_t keys,
-                           uint64_t* __restrict__ lines) {
+__global__ void k_tl_slots(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint32_t sb,
+                           uint64_t keys, const uint64_t* __restrict__ t, uint64_t* __restrict__ lines) {
     GRID_STRIDE(k, keys * SAS_TL_SLOTS) {
         const uint64_t b = k / SAS_TL_SLOTS, j = k - b * SAS_TL_SLOTS;
-        const uint64_t h = lines[b * 16], first = lines[b * 16 + 1];
-        const uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p);
-        lines[b * 16 + 2 + j] = j < (h >> 40) ? e : (e | SAS_TL_TAG_MAX);
+        const uint64_t first = t[b], c = t[b + 1] - first;
+        uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p, sb);
+        if (j >= c) e = tl_tag_max(e, sb);
+        reinterpret_cast<uint16_t*>(lines + b * 16)[4 + j] = (uint16_t)(e >> 32);
+        reinterpret_cast<uint32_t*>(lines + b * 16)[12 + j] = (uint32_t)e;
     }
 }
 
 template <int W>
-__global__ void k_tl_ovf(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint64_t keys,
-                         const uint64_t* __restrict__ lines, uint64_t* __restrict__ ovf) {
+__global__ void k_tl_ovf(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint32_t sb,
+                         uint64_t keys, const uint64_t* __restrict__ t, const uint64_t* __restrict__ lines,
+                         uint64_t* __restrict__ ovf) {
     GRID_STRIDE(b, keys) {
-        const uint64_t first = lines[b * 16 + 1];
-        const uint64_t c = lines[(b + 1) * 16 + 1] - first;
+        const uint64_t first = t[b], c = t[b + 1] - first;
         if (c < SAS_TL_SLOTS) continue;
         const uint64_t o = lines[b * 16] & (SAS_SA40_MAX - 1);
-        for (uint64_t j = SAS_TL_SLOTS; j <= c; j++)
-            ovf[o + j - SAS_TL_SLOTS] = tl_make<W>(tw, sa, sa_n, first + j, p) | (j == c ? SAS_TL_TAG_MAX : 0ull);
+        for (uint64_t j = SAS_TL_SLOTS; j <= c; j++) {
+            const uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p, sb);
+            ovf[o + j - SAS_TL_SLOTS] = j == c ? tl_tag_max(e, sb) : e;
+        }
     }
 }
 
 template <int W>
 static int build_tag_lines_w(sas_index* x, uint32_t p) {
     const uint64_t sa_n = x->sa_n, keys = 1ull << (2 * p);
+    uint32_t sb = 32;  // SA bits: the all-ones field (rank sa_n) must exceed every position < n
+    while (sb < 40 && (x->n >> sb) != 0) sb++;
+    if ((x->n >> sb) != 0) SAS_FAIL(ENOTSUP, "SAS_BUILD_TAG_LINES: n >= 2^40");
     const dim3 b(256);
     // 1. first rank of every bucket (the tagged table's fill, from the SA)
     const uint64_t cap = (keys + 1) / (PT_SMALL + 1) + 2;
@@ -1293,7 +1300,7 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
     big.alloc(0, "free");
     // 2. overflow offsets: block sums, their exclusive scan, the headers
     const uint64_t per_blk = (uint64_t)TL_BLOCK * TL_PER;
-    const uint64_t nblk = (keys + 1 + per_blk - 1) / per_blk;
+    const uint64_t nblk = (keys + per_blk - 1) / per_blk;
     DevBuf bsum, tmp, lines;
     TRY(bsum.alloc(nblk * 8, "bucket lines block sums"));
     hipLaunchKernelGGL(k_tl_sums, dim3((unsigned)nblk), dim3(TL_BLOCK), 0, 0, t.as<uint64_t>(), keys,
@@ -1310,12 +1317,11 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
     uint64_t lastx = 0;
     HIP_TRY(hipMemcpy(&lastx, bsum.as<uint64_t>() + nblk - 1, 8, hipMemcpyDeviceToHost));
     const uint64_t novf = lastx + last;
-    TRY(lines.alloc((keys + 1) * 128, "bucket lines"));
+    TRY(lines.alloc(keys * 128, "bucket lines"));
     hipLaunchKernelGGL(k_tl_hdr, dim3((unsigned)nblk), dim3(TL_BLOCK), 0, 0, t.as<uint64_t>(), keys,
                        bsum.as<uint64_t>(), lines.as<uint64_t>());
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipDeviceSynchronize());
-    t.alloc(0, "free");
     bsum.alloc(0, "free");
     tmp.alloc(0, "free");
     // 3. the slots and the overflow entries, from the SA and the text
@@ -1323,9 +1329,9 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
     TRY(ovf.alloc(novf * 8 + 32, "bucket lines overflow"));
     HIP_TRY(hipMemset(ovf.as<uint8_t>() + novf * 8, 0, 32));  // pair loads may read 2 entries past the end
     hipLaunchKernelGGL(k_tl_slots<W>, dim3(grid_for(keys * SAS_TL_SLOTS)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n,
-                       p, keys, lines.as<uint64_t>());
-    hipLaunchKernelGGL(k_tl_ovf<W>, dim3(grid_for(keys)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, keys,
-                       lines.as<uint64_t>(), ovf.as<uint64_t>());
+                       p, sb, keys, t.as<uint64_t>(), lines.as<uint64_t>());
+    hipLaunchKernelGGL(k_tl_ovf<W>, dim3(grid_for(keys)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, sb, keys,
+                       t.as<uint64_t>(), lines.as<uint64_t>(), ovf.as<uint64_t>());
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipDeviceSynchronize());
     // the lines and the overflow hold every SA value: the plain SA goes
@@ -1336,8 +1342,17 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
     lines.release();
     x->tag_ovf = ovf.as<uint64_t>();
     ovf.release();
+    x->tag_first = t.as<uint64_t>();
+    t.release();
     x->tag_ovf_n = novf;
     x->tag_p = p;
+    x->tag_sb = sb;
+    // 4. the second text copy, its word 0 at byte 64 of a 128-B line
+    DevBuf t2;
+    TRY(t2.alloc(x->text_words * 8 + 128, "packed text, second copy"));
+    HIP_TRY(hipMemcpy(t2.as<uint8_t>() + 64, x->text_w, x->text_words * 8, hipMemcpyDeviceToDevice));
+    x->text2_base = t2.release();
+    x->text2 = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(x->text2_base) + 64);
     return 0;
 }
 
@@ -1632,11 +1647,14 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.top2_levels = x->top2_levels;
     st.tag_chars = x->tag_p;
     st.tag_table_bytes = x->tag_table   ? ((1ull << (2 * x->tag_p)) + 1) * 8
-                         : x->tag_lines ? ((1ull << (2 * x->tag_p)) + 1) * 128 : 0;
+                         : x->tag_lines ? (1ull << (2 * x->tag_p)) * 128 + ((1ull << (2 * x->tag_p)) + 1) * 8 : 0;
     st.tag_line_slots = x->tag_lines ? SAS_TL_SLOTS : 0;
+    st.tag_line_tag_bits = x->tag_lines ? tl_tag_bits(x->tag_sb) : 0;
+    st.text2_bytes = x->text2 ? x->text_words * 8 : 0;
     st.tag_overflow_entries = x->tag_ovf_n;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
-                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + ((uint64_t)16 << x->top2_levels);
+                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes +
+                     ((uint64_t)16 << x->top2_levels);
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard
@@ -1721,22 +1739,23 @@ __global__ void k_widen_sa(SaView<W> sa, uint64_t start, uint64_t count, uint64_
     GRID_STRIDE(i, count) out[i] = sa[start + i];
 }
 
-// SAS_BUILD_TAG_LINES: SA[r] from the line of r's bucket (the last line whose first rank is
-// <= r: a binary search over the line headers), its slot or its overflow entry
-__global__ void k_tl_sa(const uint64_t* __restrict__ lines, const uint64_t* __restrict__ ovf, uint64_t keys,
-                        uint64_t start, uint64_t count, uint64_t* __restrict__ out) {
+// SAS_BUILD_TAG_LINES: SA[r] from the line of r's bucket (the last bucket whose first rank is
+// <= r: a binary search over the first-rank table), its slot or its overflow entry
+__global__ void k_tl_sa(const uint64_t* __restrict__ lines, const uint64_t* __restrict__ ovf,
+                        const uint64_t* __restrict__ first, uint64_t keys, uint32_t sb, uint64_t start, uint64_t count,
+                        uint64_t* __restrict__ out) {
     GRID_STRIDE(i, count) {
         const uint64_t r = start + i;
         uint64_t lo = 0, hi = keys;
         while (lo < hi) {
             const uint64_t mid = (lo + hi) >> 1;
-            if (lines[mid * 16 + 1] > r) hi = mid;
+            if (first[mid] > r) hi = mid;
             else lo = mid + 1;
         }
-        const uint64_t b = lo - 1, j = r - lines[b * 16 + 1];
-        const uint64_t e = j < SAS_TL_SLOTS ? lines[b * 16 + 2 + j]
+        const uint64_t b = lo - 1, j = r - first[b];
+        const uint64_t e = j < SAS_TL_SLOTS ? tl_slot(lines, b, (uint32_t)j)
                                             : ovf[(lines[b * 16] & (SAS_SA40_MAX - 1)) + j - SAS_TL_SLOTS];
-        out[i] = e & (SAS_SA40_MAX - 1);
+        out[i] = e & tl_sa_mask(sb);
     }
 }
 
@@ -1755,7 +1774,7 @@ extern "C" int sas_copy_sa64(const sas_index* index, uint64_t start, uint64_t co
     uint64_t s0 = start - index->rank_lo;
     if (index->tag_lines)
         hipLaunchKernelGGL(k_tl_sa, dim3(grid_for(count)), dim3(256), 0, 0, index->tag_lines, index->tag_ovf,
-                           1ull << (2 * index->tag_p), s0, count, out);
+                           index->tag_first, 1ull << (2 * index->tag_p), index->tag_sb, s0, count, out);
     else if (index->sa_w == 8)
         hipLaunchKernelGGL(k_widen_sa<8>, dim3(grid_for(count)), dim3(256), 0, 0, SaView<8>{index->sa}, s0, count, out);
     else if (index->sa_w == 5)

@@ -82,6 +82,9 @@ struct SearchArgs {
     uint32_t tag_p;
     const uint64_t* tag_lines;  // SAS_BUILD_TAG_LINES: 128-B bucket lines (common.hpp)
     const uint64_t* tag_ovf;    // and their overflow entries
+    const uint64_t* tag_first;  // and the buckets' first ranks
+    const uint64_t* tw2;        // and the second text copy (tl_text)
+    uint32_t tag_sb;            // SA bits of a line entry
     const uint8_t* qbytes;
     const uint64_t* qwords;  // sas_search_packed: 2-bit packed fixed-length queries (PREFIX)
     const uint64_t* qoff;
@@ -1709,7 +1712,7 @@ __device__ __forceinline__ bool tag_ge(uint64_t e, uint32_t Q12, const SearchArg
     if (q.m <= L) return (a.n - p) >= (uint64_t)q.m;  // equal padded keys: a shorter suffix is a prefix of q
     uint32_t lcp;
 #if SAS_TAG_PRE
-    return !suffix_less_from_pre<SAS_TAG_PRE>(a.tw, a.n, p, q, L, &lcp);
+    return !suffix_less_from_pre<SAS_TAG_PRE>(a.tw, a.tw, a.n, p, q, L, &lcp);
 #else
     return !suffix_less_from_x2<QW>(a.tw, a.n, p, q, L, &lcp);
 #endif
@@ -1951,15 +1954,18 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_range(SearchArgs 
 
 // ------------------------------------------------------------------ TAGGED on bucket lines
 // SAS_BUILD_TAG_LINES (sas_build.hip, build_tag_lines): line b holds bucket b's header
-// {first rank | count, overflow offset} and the entries of ranks first .. first + 13, so the
-// bucket word and the first window of the tagged lookup above are one 128-B request.  An
-// 8-lane group reads the lines of its 8 queries (one per lane) together, 16 B per lane
-// (lane 0 the header, lane s the slots 2s - 2 and 2s - 1), finds in each the first slot of
-// the bucket whose tag is >= the query's (group ballot), and hands it to the query's lane;
-// the rest -- the tie's text compare, a larger bucket's overflow window -- is per lane.
-// Slots past the bucket's count hold the next buckets' first suffixes, so "every suffix of
-// the bucket is < q" finds its answer (the first suffix after the bucket, rank first + count)
-// in the same line whenever count < 14 (and at overflow index count - 14 otherwise).
+// {overflow offset | count} and the 48-bit entries {SA | tag << sb} of ranks first .. first +
+// 19 (common.hpp: u16 high halves, then u32 low halves), so the bucket word and the first
+// window of the tagged lookup above are one 128-B request, and 20 slots keep 98% of the
+// positive lookups at ~16 suffixes per bucket inside it.  An 8-lane group reads the lines of
+// its 8 queries (one per lane) together, 16 B per lane (lane 0 the header and hi[0..3], lanes
+// 1 and 2 hi[4..19], lanes 3..7 lo[0..19]); per line lanes 0-2 count the slots whose tag is
+// below the query's, the group sums the counts, and the lanes holding that slot's halves
+// hand them to the query's lane; the rest -- the tie's text compare, a larger bucket's
+// overflow window -- is per lane.  Slots past the bucket's count hold the next buckets' first
+// suffixes with the maximal tag, so "every suffix of the bucket is < q" finds its answer (the
+// first suffix after the bucket, rank first + count) in the same line whenever count < 20
+// (and at overflow index count - 20 otherwise).
 #define TL_G 8
 // waves per SIMD the line kernels are built for: the 8 line loads a lane keeps in flight take
 // 32 VGPRs (at 5 waves the kernel spills)
@@ -1970,57 +1976,77 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_range(SearchArgs 
 #define SAS_TL_WIN 8  // overflow entries a lane reads before bisecting the rest
 #endif
 
+// entry j of bucket b: line slot j (j < 20) or overflow entry j - 20
 __device__ __forceinline__ uint64_t tl_entry(const SearchArgs& a, uint64_t b, uint64_t ovf, uint64_t j) {
-    return j < SAS_TL_SLOTS ? __builtin_nontemporal_load(a.tag_lines + b * 16 + 2 + j)
+    return j < SAS_TL_SLOTS ? tl_slot(a.tag_lines, b, (uint32_t)j)
                             : __builtin_nontemporal_load(a.tag_ovf + ovf + (j - SAS_TL_SLOTS));
 }
 
-// bucket b's suffix count from its header word (a saturated count reads the next line's rank)
+// bucket b's suffix count from its header word (a saturated count reads the first-rank table)
 __device__ __forceinline__ uint64_t tl_count(const SearchArgs& a, uint64_t b, uint64_t h0) {
     const uint64_t c = h0 >> 40;
-    return c == 0xFFFFFFull ? a.tag_lines[(b + 1) * 16 + 1] - a.tag_lines[b * 16 + 1] : c;
+    return c == 0xFFFFFFull ? a.tag_first[b + 1] - a.tag_first[b] : c;
 }
+
+// chars known equal to q's when an entry's tag ties with q's: the bucket's p and the tag's whole chars
+__device__ __forceinline__ uint32_t tl_known(const SearchArgs& a) { return a.tag_p + (tl_tag_bits(a.tag_sb) >> 1); }
 
 // text word pairs a bucket-line lookup loads together for its tie's compare: 5 pairs (80 B)
 // cover chars [p + 12, 256) of any suffix, so no compare of a query of <= 256 chars waits for a
 // second round trip (loaded lazily they are ~3 dependent round trips of the whole wave).  Same
 // box, 2*10^7 ragged 8..256 at n = 2^34: 5 pairs 1.91 ms, 4 pairs 1.99, 3 pairs 2.05-2.07
-// (gpurun_out A/B, profiles/r3/); 0: the lazy pair loop (suffix_less_from_x2)
+// (gpurun_out A/B, profiles/r3/); 0: the lazy pair loop (suffix_less_from_x2).  The pairs come
+// from the text copy in which they lie in one 128-B line (sas_index::text2).
 #ifndef SAS_TL_PRE
 #define SAS_TL_PRE 5
 #endif
 
-// suffix(e) >= q for an entry of q's bucket (tag_ge), the tie's text compare preloading
-template <int QW, class Q>
-__device__ __forceinline__ bool tl_ge(uint64_t e, uint32_t Q12, const SearchArgs& a, const Q& q) {
-    const uint32_t T = (uint32_t)(e >> 40);
-    if (T != Q12) return T > Q12;
-    const uint64_t p = e & TAG_M40;
-    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+// suffix(e) >= q for an entry of q's bucket (Qt: q's tag), the tie's text compare preloading
+// (PRE) or pair by pair (the rare bisection and the range kernel)
+template <int QW, bool PRE, class Q>
+__device__ __forceinline__ bool tl_ge(uint64_t e, uint32_t Qt, const SearchArgs& a, const Q& q) {
+    const uint32_t T = (uint32_t)(e >> a.tag_sb);
+    if (T != Qt) return T > Qt;
+    const uint64_t p = e & tl_sa_mask(a.tag_sb);
+    const uint32_t L = tl_known(a);
     if (q.m <= L) return (a.n - p) >= (uint64_t)q.m;
     const uint64_t src = query_source(q);  // a text-slice query's own suffix starts with q
     if (src != ~0ull && src + q.m <= a.n && p == src) return true;
     uint32_t lcp;
 #if SAS_TL_PRE
-    return !suffix_less_from_pre<SAS_TL_PRE>(a.tw, a.n, p, q, L, &lcp);
-#else
-    return !suffix_less_from_x2<QW>(a.tw, a.n, p, q, L, &lcp);
+    if (PRE) return !suffix_less_from_pre<SAS_TL_PRE>(a.tw, a.tw2, a.n, p, q, L, &lcp);
 #endif
+    return !suffix_less_from_x2<QW>(a.tw, a.n, p, q, L, &lcp);
 }
 
-// The lookup after the line: f = the first slot j < 14 whose tag is >= q's (14 if none), ef =
-// slot f's entry when f < 14, h0 = the line's header word {overflow offset | count}.  Slots past the bucket's count
-// carry the tag 0xFFFFFF, so f <= count when count < 14, and f == count finds the first suffix
-// after the bucket.  The answer is entry j of the bucket for the first j in [0, count] whose
-// suffix is >= q (j = count: the next bucket's first suffix).  A wave waits for its slowest
-// lane at every step, so the loads of the lanes that need the overflow window are issued
-// before the other lanes' text compares wait for theirs: one round trip serves both.
+// the first min(m, len) chars of suffix(e) are > q, for an entry of the bucket of q's routing
+// key (Q3t: the tag of q padded with 3s; as tag_gt_prefix)
+template <int QW, class Q>
+__device__ __forceinline__ bool tl_gt_prefix(uint64_t e, uint32_t Qt, uint32_t Q3t, const SearchArgs& a, const Q& q) {
+    const uint32_t T = (uint32_t)(e >> a.tag_sb);
+    const uint32_t L = tl_known(a);
+    if (q.m <= L) return T > Q3t;
+    if (T != Qt) return T > Qt;
+    uint32_t lcp;
+    const bool lt = suffix_less_from_x2<QW>(a.tw, a.n, e & tl_sa_mask(a.tag_sb), q, L, &lcp);
+    return !lt && lcp < q.m;
+}
+
+// The lookup after the line: f = the number of the bucket's first 20 suffixes whose tag is
+// below q's (20: all of them), ef = slot f's entry when f < 20, h0 = the line's header word
+// {overflow offset | count}.  Slots past the bucket's count carry the maximal tag, so f <=
+// count when count < 20, and f == count finds the first suffix after the bucket.  The answer
+// is entry j of the bucket for the first j in [0, count] whose suffix is >= q (j = count: the
+// next bucket's first suffix).  A wave waits for its slowest lane at every step, so the loads
+// of the lanes that need the overflow window are issued before the other lanes' text compares
+// wait for theirs: one round trip serves both.
 template <int QW, class Q>
 __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint64_t i, uint64_t b, uint64_t h0,
-                                          uint32_t f, uint64_t ef, uint32_t Q12) {
+                                          uint32_t f, uint64_t ef, uint32_t Qt) {
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const uint32_t sb = a.tag_sb;
     const uint64_t cnt = tl_count(a, b, h0), ovf = h0 & TAG_M40;
-    // the overflow window [14, cnt] (entry cnt is >= q whatever its tag), as 16-B aligned pairs
+    // the overflow window [20, cnt] (entry cnt is >= q whatever its tag), as 16-B aligned pairs
     const bool ovfl = f >= SAS_TL_SLOTS && cnt > SAS_TL_SLOTS;
     const uint64_t rest = ovfl ? cnt + 1 - SAS_TL_SLOTS : 0;
     const uint32_t nw = rest < SAS_TL_WIN ? (uint32_t)rest : (uint32_t)SAS_TL_WIN;
@@ -2035,13 +2061,17 @@ __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint6
             w2[2 * k + 1] = v.y;
         }
     }
-    uint64_t j = 0, e = 0, start = SAS_TL_SLOTS;
-    bool done = false;
+    uint64_t j = 0, e = 0, start = SAS_TL_SLOTS, cj = 0, ce = 0;
+    bool done = false, cand = false;  // cand: entry ce (index cj) needs the compare
     if (f < SAS_TL_SLOTS) {
-        if (f >= cnt || tl_ge<QW>(ef, Q12, a, q)) {  // f == cnt: the first suffix after the bucket
+        if (f >= cnt) {  // the first suffix after the bucket
             j = f;
             e = ef;
             done = true;
+        } else {
+            cand = true;
+            cj = f;
+            ce = ef;
         }
         start = (uint64_t)f + 1;  // a tie whose suffix is < q: the search goes on
     } else if (cnt == SAS_TL_SLOTS) {  // every suffix of the bucket is < q: the next one's first
@@ -2055,21 +2085,30 @@ __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint6
         uint32_t k0 = nw;
 #pragma unroll
         for (int k = SAS_TL_WIN - 1; k >= 0; k--)
-            if ((uint32_t)k < nw && (SAS_TL_SLOTS + k == cnt || (uint32_t)(ew[k] >> 40) >= Q12)) k0 = (uint32_t)k;
+            if ((uint32_t)k < nw && (SAS_TL_SLOTS + k == cnt || (uint32_t)(ew[k] >> sb) >= Qt)) k0 = (uint32_t)k;
         uint64_t ek0 = ew[0];
 #pragma unroll
         for (int k = 1; k < SAS_TL_WIN; k++) ek0 = (k0 == (uint32_t)k) ? ew[k] : ek0;
         if (k0 < nw) {
             const uint64_t r = SAS_TL_SLOTS + k0;
-            if (r == cnt || tl_ge<QW>(ek0, Q12, a, q)) {
+            if (r == cnt) {
                 j = r;
                 e = ek0;
                 done = true;
+            } else {
+                cand = true;
+                cj = r;
+                ce = ek0;
             }
             start = r + 1;
         } else {
             start = SAS_TL_SLOTS + nw;
         }
+    }
+    if (cand && tl_ge<QW, true>(ce, Qt, a, q)) {  // one compare site: a slot's or the window's
+        j = cj;
+        e = ce;
+        done = true;
     }
     if (!done && start == cnt) {  // the first suffix after the bucket
         j = cnt;
@@ -2082,7 +2121,7 @@ __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint6
         while (l2 < h2) {
             const uint64_t mid = (l2 + h2) >> 1;
             const uint64_t fm = tl_entry(a, b, ovf, mid);
-            if (tag_ge<QW>(fm, Q12, a, q)) {
+            if (tl_ge<QW, false>(fm, Qt, a, q)) {
                 h2 = mid;
                 pe = fm;
                 have = true;
@@ -2093,8 +2132,8 @@ __device__ __forceinline__ void tl_finish(const SearchArgs& a, const Q& q, uint6
         j = l2;
         e = (have && l2 < cnt) ? pe : tl_entry(a, b, ovf, l2);
     }
-    const uint64_t s = e & TAG_M40;
-    a.out_pos[i] = s == SAS_TL_END ? a.next_pos : s;
+    const uint64_t s = e & tl_sa_mask(sb);
+    a.out_pos[i] = s == tl_sa_mask(sb) ? a.next_pos : s;
     if (a.out_probes) {  // the reference's cnt: the table, then binary_search over [first, first + cnt)
         uint32_t probes = 1;
         for (uint64_t l2 = 0, h2 = cnt; l2 < h2; probes++) {
@@ -2120,29 +2159,30 @@ __device__ __forceinline__ uint32_t g8_swz(uint32_t v, int pattern_k) {
         default: return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, 0x18 | (7 << 5));
     }
 }
-__device__ __forceinline__ uint32_t g8_min(uint32_t c) {
-    uint32_t t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);  // lane ^ 1
-    c = t < c ? t : c;
-    t = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);  // lane ^ 2
-    c = t < c ? t : c;
-    t = (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x1F | (4 << 10));  // lane ^ 4
-    return t < c ? t : c;
+// sum over the group of 8 (every lane gets it)
+__device__ __forceinline__ uint32_t g8_sum(uint32_t c) {
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0xB1, 0xF, 0xF, false);  // lane ^ 1
+    c += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)c, 0x4E, 0xF, 0xF, false);  // lane ^ 2
+    return c + (uint32_t)__builtin_amdgcn_ds_swizzle((int)c, 0x1F | (4 << 10));    // lane ^ 4
+}
+__device__ __forceinline__ uint32_t sel4(const uint4& v, uint32_t k) {
+    const uint32_t lo = (k & 1) ? v.y : v.x, hi = (k & 1) ? v.w : v.z;
+    return (k & 2) ? hi : lo;
 }
 
 // The cooperative part: every lane of the wave calls it together (act: the lane holds query
-// i).  Lane s of a group holds 16 B of each of the group's 8 lines (s = 0: the header; s >= 1:
-// slots 2s - 2, 2s - 1); per line the group finds the first slot of the bucket whose tag is >=
-// the line's query's tag (a min over the group), and hands that slot's entry and the header
-// word {overflow offset | count} to the query's lane.  (Measured slower, same box: each lane
-// loading its own line's header as a ninth 16-B load, and ballots in place of the min:
-// 2.04-2.07 vs 1.90-1.92 ms per 2*10^7, profiles/r3/ab_lines_v2_vs_v1.txt.)
+// i).  Lane s of a group holds 16 B of each of the group's 8 lines (common.hpp); per line
+// lanes 0-2 count the slots whose tag is below the line's query's (the tag halves are the
+// high bits of the u16 fields: h < Qt << (sb - 32)), the group sums the counts into f, and the
+// lanes holding hi[f] ((f + 4) / 8) and lo[f] (3 + f / 4) hand them, with the header word, to
+// the query's lane.
 template <int QW, class Q>
 __device__ __forceinline__ void tl_lookup(const SearchArgs& a, const Q& q, bool act, uint64_t i) {
     const uint32_t lane = threadIdx.x & 63, sub = lane & (TL_G - 1), g0 = lane & ~(uint32_t)(TL_G - 1);
-    const uint32_t sh = 64 - 2 * a.tag_p;
+    const uint32_t sh = 64 - 2 * a.tag_p, hs = a.tag_sb - 32;
     const uint64_t K64 = act ? q.w[0] : 0ull;
     const uint64_t b = K64 >> sh;
-    const uint32_t Q12 = tag_of_key(K64, a.tag_p);
+    const uint32_t Qt = tl_tag_of_key(K64, a.tag_p, tl_tag_bits(a.tag_sb));
     const uint4* L4 = reinterpret_cast<const uint4*>(a.tag_lines);
     uint4 v[TL_G];
 #pragma unroll
@@ -2150,31 +2190,39 @@ __device__ __forceinline__ void tl_lookup(const SearchArgs& a, const Q& q, bool 
         const uint64_t bk = ((uint64_t)g8_swz((uint32_t)(b >> 32), k) << 32) | g8_swz((uint32_t)b, k);
         v[k] = nt_load4(L4 + bk * 8 + sub);
     }
+    // tag fields of this lane's 16 B: lane 0 the upper 8 B (hi[0..3]), lanes 1 and 2 all of it;
+    // a field h counts when h < Qt << (sb - 32), two fields per packed saturating subtract
+    typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+    const u16x2 one = {1, 1};
+    const bool lo_tags = sub == 1 || sub == 2, hi_tags = sub <= 2;
     uint64_t my_h0 = 0, my_ef = 0;
     uint32_t my_f = 0;
 #pragma unroll
     for (int k = 0; k < TL_G; k++) {
-        const uint64_t lo64 = ((uint64_t)v[k].y << 32) | v[k].x, hi64 = ((uint64_t)v[k].w << 32) | v[k].z;
-        const uint32_t c32 = g8_swz(v[k].y, 0);  // the header word's high half: count << 8 | offset bits
-        const uint64_t h0 = ((uint64_t)c32 << 32) | g8_swz(v[k].x, 0);
-        const uint32_t c = c32 >> 8;  // a saturated count is >= 14 as well
-        const uint32_t lim = c < SAS_TL_SLOTS ? c : (uint32_t)SAS_TL_SLOTS;
-        const uint32_t Qk = g8_swz(Q12, k);
-        const uint32_t j0 = 2 * sub - 2;  // slots of this lane (lane 0: the header)
-        const bool ge0 = sub != 0 && j0 < lim && (uint32_t)(lo64 >> 40) >= Qk;
-        const bool ge1 = sub != 0 && j0 + 1 < lim && (uint32_t)(hi64 >> 40) >= Qk;
-        const uint32_t cand = g8_min(ge0 ? j0 : (ge1 ? j0 + 1 : 64u));
-        const uint32_t f = cand == 64u ? lim : cand;
-        const uint64_t mine = (f & 1) ? hi64 : lo64;
-        const int src = (int)g0 + (f < SAS_TL_SLOTS ? (int)(f >> 1) + 1 : 0);
-        const uint64_t ef = (uint64_t)__shfl((long long)mine, src, 64);
+        const uint32_t Qs = g8_swz(Qt, k) << hs;  // (h >> hs) < Qt  <=>  h < Qt << hs
+        const uint32_t Qp = Qs | (Qs << 16);
+        const u16x2 Qlo = __builtin_bit_cast(u16x2, lo_tags ? Qp : 0u), Qhi = __builtin_bit_cast(u16x2, hi_tags ? Qp : 0u);
+        const u16x2 acc =
+            __builtin_elementwise_min(__builtin_elementwise_sub_sat(Qlo, __builtin_bit_cast(u16x2, v[k].x)), one) +
+            __builtin_elementwise_min(__builtin_elementwise_sub_sat(Qlo, __builtin_bit_cast(u16x2, v[k].y)), one) +
+            __builtin_elementwise_min(__builtin_elementwise_sub_sat(Qhi, __builtin_bit_cast(u16x2, v[k].z)), one) +
+            __builtin_elementwise_min(__builtin_elementwise_sub_sat(Qhi, __builtin_bit_cast(u16x2, v[k].w)), one);
+        const uint32_t f = g8_sum((uint32_t)acc.x + acc.y);
+        const uint32_t fe = (f + 4) & 7;
+        const uint32_t hw = (sel4(v[k], fe >> 1) >> ((fe & 1) * 16)) & 0xFFFFu;
+        const uint32_t mine = sub < 3 ? hw : sel4(v[k], f & 3);
+        const uint32_t hl = (f + 4) >> 3, ll = 3 + (f >> 2);
+        const uint32_t hiv = (uint32_t)__shfl((int)mine, (int)(g0 + (hl < 2 ? hl : 2u)), 64);
+        const uint32_t lov = (uint32_t)__shfl((int)mine, (int)(g0 + (ll < 7 ? ll : 7u)), 64);
+        const uint64_t h0 = ((uint64_t)g8_swz(v[k].y, 0) << 32) | g8_swz(v[k].x, 0);
         if (sub == (uint32_t)k) {
             my_h0 = h0;
             my_f = f;
-            my_ef = ef;
+            my_ef = ((uint64_t)hiv << 32) | lov;
         }
+        __builtin_amdgcn_sched_barrier(0);  // one line at a time: interleaved, the 8 spill
     }
-    if (act) tl_finish<QW>(a, q, i, b, my_h0, my_f, my_ef, Q12);
+    if (act) tl_finish<QW>(a, q, i, b, my_h0, my_f, my_ef, Qt);
 }
 
 template <int QW>
@@ -2224,8 +2272,8 @@ __global__ __launch_bounds__(SAS_TAG_BLOCK, SAS_TL_LB) void k_sa_tagged_lines_sl
 template <int QW>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_lines_range(SearchArgs a, uint64_t* out_hi) {
     uint32_t bad = 0;
-    const uint32_t sh = 64 - 2 * a.tag_p;
-    const uint32_t L = a.tag_p + SAS_TAG_CHARS;
+    const uint32_t sh = 64 - 2 * a.tag_p, tb = tl_tag_bits(a.tag_sb);
+    const uint32_t L = tl_known(a);
     for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
          i += (uint64_t)gridDim.x * blockDim.x) {
         const uint8_t* qb;
@@ -2235,7 +2283,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_lines_range(Searc
         q.load(qb, m, &bad);
         const uint64_t K64 = q.w[0];
         const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
-        const uint32_t Q12 = tag_of_key(K64, a.tag_p), Q3t = tag_of_key(Q3, a.tag_p);
+        const uint32_t Qt = tl_tag_of_key(K64, a.tag_p, tb), Q3t = tl_tag_of_key(Q3, a.tag_p, tb);
         const uint64_t b0 = K64 >> sh, b1 = (m <= L ? Q3 : K64) >> sh;
         const uint64_t h00 = a.tag_lines[b0 * 16], h10 = a.tag_lines[b1 * 16];
         const uint64_t o0 = h00 & TAG_M40, o1 = h10 & TAG_M40;
@@ -2246,15 +2294,15 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_tagged_lines_range(Searc
             const uint64_t e0 = g0 ? tl_entry(a, b0, o0, m0) : 0;
             const uint64_t e1 = g1 ? tl_entry(a, b1, o1, m1) : 0;
             if (g0) {
-                if (tag_ge<QW>(e0, Q12, a, q)) l1 = m0;
+                if (tl_ge<QW, false>(e0, Qt, a, q)) l1 = m0;
                 else lo = m0 + 1;
             }
             if (g1) {
-                if (tag_gt_prefix<QW>(e1, Q12, Q3t, a, q)) h1 = m1;
+                if (tl_gt_prefix<QW>(e1, Qt, Q3t, a, q)) h1 = m1;
                 else hi = m1 + 1;
             }
         }
-        uint64_t rlo = a.tag_lines[b0 * 16 + 1] + lo, rhi = a.tag_lines[b1 * 16 + 1] + hi;
+        uint64_t rlo = a.tag_first[b0] + lo, rhi = a.tag_first[b1] + hi;
         if (rhi < rlo) rhi = rlo;
         a.out_pos[i] = a.rank_lo + rlo;
         out_hi[i] = a.rank_lo + rhi;
@@ -2519,6 +2567,9 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.tag_p = x->tag_p;
     a.tag_lines = x->tag_lines;
     a.tag_ovf = x->tag_ovf;
+    a.tag_first = x->tag_first;
+    a.tw2 = x->text2 ? x->text2 : x->text_w;
+    a.tag_sb = x->tag_sb;
 }
 
 // Algorithm / index / flag compatibility, shared by the search entry points.

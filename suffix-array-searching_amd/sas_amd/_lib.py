@@ -79,7 +79,8 @@ class SasStats(C.Structure):
         ("quad_fan", C.c_uint32), ("top2_levels", C.c_uint32), ("llcp_bytes", C.c_uint64),
         ("prefix_bytes", C.c_uint64), ("prefix_chars", C.c_uint32), ("tag_chars", C.c_uint32),
         ("tag_table_bytes", C.c_uint64), ("index_bytes", C.c_uint64),
-        ("tag_line_slots", C.c_uint32), ("reserved0", C.c_uint32), ("tag_overflow_entries", C.c_uint64),
+        ("tag_line_slots", C.c_uint32), ("tag_line_tag_bits", C.c_uint32), ("tag_overflow_entries", C.c_uint64),
+        ("text2_bytes", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -124,7 +124,7 @@ def test_c3_full_size():
     lines = sas_amd.SaNaive.build(ht, lcp=False, verify=True, tagged=True, tag_lines=True)
     del ht
     st = lines.stats()
-    assert st["tag_chars"] == 15 and st["tag_line_slots"] == 14 and st["sa_entries"] == N
+    assert st["tag_chars"] == 15 and st["tag_line_slots"] == 20 and st["tag_line_tag_bits"] == 13 and st["sa_entries"] == N
     r = lines.search_batch(qb, qoff, qlen, algo="tagged")
     torch.cuda.synchronize()
     assert torch.equal(r.cpu(), ref)

@@ -193,8 +193,9 @@ def test_tag_lines_match_oracle(sas, p):
                                     tag_lines=True)
             st = idx.stats()
             pp = st["tag_chars"]
-            assert st["tag_line_slots"] == 14 and st["tag_table_bytes"] == (4 ** pp + 1) * 128
-            assert st["sa_bytes"] == st["tag_overflow_entries"] * 8
+            assert st["tag_line_slots"] == 20 and st["tag_table_bytes"] == 4 ** pp * 128 + (4 ** pp + 1) * 8
+            assert st["tag_line_tag_bits"] == 48 - max(32, n.bit_length())  # 16 below 2^32
+            assert st["sa_bytes"] == st["tag_overflow_entries"] * 8 and st["text2_bytes"] == st["text_bytes"]
             assert np.array_equal(idx.suffix_array(), sa.astype(np.uint64)), name
             got, cnt = idx.search_batch(buf, off, lens, algo="tagged", probes=True)
             bad = np.nonzero(got != epos)[0]
@@ -210,13 +211,13 @@ def test_tag_lines_match_oracle(sas, p):
                     idx.search_batch(buf, off, lens, algo=algo)
             with pytest.raises(sas.SasError):
                 idx.verify()
-            # overflow entries: ranks first + 14 .. first + count of each bucket of >= 14
+            # overflow entries: ranks first + 20 .. first + count of each bucket of >= 20
             keys = np.zeros(n, np.int64)
             tpi = tp.astype(np.int64)
             for j in range(pp):
                 keys = keys * 4 + tpi[sa.astype(np.int64) + j]
             c = np.bincount(keys, minlength=4 ** pp)
-            assert st["tag_overflow_entries"] == int(np.sum(np.where(c >= 14, c - 13, 0))), name
+            assert st["tag_overflow_entries"] == int(np.sum(np.where(c >= 20, c - 19, 0))), name
             idx.free()
 
 
