@@ -108,10 +108,11 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         leaf = 16 if st["quad_entry_bytes"] == 16 else 8 + sa_w
         hbm += max(0.0, probes - 1) * leaf
     elif algo == "tagged" and st.get("tag_line_slots"):
-        # bucket lines: the 128-B line (header + 14 entries), the entries of a mean bucket past
-        # the line (overflow), the text past the (p + 12)-char key
+        # bucket lines: the 128-B line (header + 20 entries), the entries of a mean bucket past
+        # the line (overflow), the text past the bucket's p chars and the tag's whole chars
+        known = st["tag_chars"] + st.get("tag_line_tag_bits", 24) // 2
         hbm += 128 + max(0.0, n / 4 ** st["tag_chars"] + 1 - st["tag_line_slots"]) * 8 + \
-            max(0.0, m - st["tag_chars"] - 12) / 4
+            max(0.0, m - known) / 4
     elif algo == "tagged":
         hbm += 8 + min(n / 4 ** st["tag_chars"] + 1, 8) * 8 + max(0.0, m - st["tag_chars"] - 12) / 4
     elif range_flag:  # PLAIN / LCP from the prefix table's range: table entry + SA word + window per probe
@@ -473,7 +474,7 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and 10^8 positive
     queries of mixed length 8..256 (random_queries with len in [8, 257), sas/util.rs:18-26),
     ragged, through sas_search_batch on device buffers.  TAGGED on bucket lines
-    (SAS_BUILD_TAGGED | SAS_BUILD_TAG_LINES, p = 15: a bucket's header and first 14 entries in
+    (SAS_BUILD_TAGGED | SAS_BUILD_TAG_LINES, p = 15: a bucket's header and first 20 entries in
     one 128-B line) by default (--c3-layout lines); then, as the cross-check, the rank-ordered
     tagged index (8-B tagged SA entries + a p = 16 bucket table) with TAGGED and the
     extra algorithms, whose positions must be identical.  PREFIX / QUAD: compact key-only quad

@@ -117,7 +117,7 @@ class SaNaive:
         23 cache-resident levels; 30 = 16 GiB of HBM-resident pivots at n = 2^30).
         tag_lines (with tagged): the tagged entries as 128-B bucket lines + an overflow array
         (SAS_BUILD_TAG_LINES; p = ceil(log4 n) - 2 unless tagged gives it): one request gives a
-        lookup its bucket and first 14 entries; algo="tagged" only, no SA array."""
+        lookup its bucket and first 20 entries; algo="tagged" only, no SA array."""
         t = _as_u8(t)
         n = int(t.numel() if _is_cuda(t) else len(t))
         if tagged is not False:
