@@ -2267,6 +2267,15 @@ __global__ __launch_bounds__(SAS_TAG_BLOCK, SAS_TL_LB) void k_sa_tagged_lines_sl
     }
 }
 
+// Measured and not kept (profiles/r3/defer/, same box, 2*10^7 ragged 8..256 at n = 2^34):
+// * two passes: the lanes whose answer lies past the line's 20 slots (~2% of lanes, in most
+//   waves) wrote their query index into a per-wave list and a second kernel ran them whole,
+//   so no wave waited for the overflow window and its second compare: 1.67 against 1.48 ms
+//   (one list counter for the grid, claimed by an atomic per wave: 3.3 ms);
+// * the next batch's query offsets and lengths loaded a batch ahead: 1.478 against 1.462 ms.
+// The kernel is bound by the rate of its random requests (0.84 of the ceiling), not by the
+// round trips of a wave's slowest lane.
+
 // Occurrence ranges on bucket lines: both bounds bisected in their buckets (entries by
 // bucket index: slot or overflow), as k_sa_tagged_range does over rank-ordered entries.
 template <int QW>

@@ -380,3 +380,36 @@ def test_tagged_text_slices(sas, lines):
         with pytest.raises(sas.SasError):
             idx.search_slices(torch.tensor([n - 3], dtype=torch.int64, device="cuda"),
                               torch.tensor([4], dtype=torch.int32, device="cuda"))
+
+
+def test_tag_lines_overflow_heavy(sas):
+    """Bucket lines whose answers mostly lie in the overflow array: at p = 2 (~12,500
+    suffixes a bucket) every lookup's answer lies past its line's 20 slots (overflow window,
+    then the bisection); at p = 5 (~200) both kinds meet in every wave.  60,000 ragged
+    queries, byte queries and text slices equal the rank-ordered tagged index's positions,
+    and a sample equals the oracle's."""
+    import torch
+    t = O.random_string(200_003, seed=12)
+    n = len(t)
+    rng = np.random.default_rng(13)
+    nq = 60_000
+    off = rng.integers(0, n - 300, nq)
+    lens = rng.integers(1, 300, nq).astype(np.uint32)
+    qs = [t[o:o + l] for o, l in zip(off, lens)]
+    buf, qoff, qlen = pack(qs)
+    ref_idx = sas.SaNaive.build(t, tagged=True, lcp=False)
+    ref = ref_idx.search_batch(buf, qoff, qlen, algo="tagged")
+    ref_idx.free()
+    for p in (2, 5):
+        idx = sas.SaNaive.build(t, tagged=p, lcp=False, tag_lines=True)
+        got = idx.search_batch(buf, qoff, qlen, algo="tagged")
+        assert np.array_equal(got, ref), (p, np.nonzero(got != ref)[0][:5])
+        src = torch.from_numpy(off.astype(np.int64)).cuda()
+        sl = idx.search_slices(src, torch.from_numpy(qlen.astype(np.int32)).cuda())
+        torch.cuda.synchronize()
+        assert np.array_equal(sl.cpu().numpy().astype(np.uint64), ref.astype(np.uint64)), p
+        idx.free()
+    sa = O.build_sa(t)
+    tp = O.padded(t)
+    for k in range(0, nq, 97):
+        assert int(ref[k]) == O.search_one(tp, n, sa, qs[k])[0], k
