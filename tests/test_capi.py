@@ -120,3 +120,18 @@ def test_stats_struct_matches_header():
     body = hdr[hdr.index("typedef struct sas_stats {"):hdr.index("} sas_stats;")]
     fields = re.findall(r"^\s*uint(?:32|64)_t\s+(\w+);", body, re.M)
     assert fields == [f for f, _ in _lib.SasStats._fields_]
+
+
+def test_rust_stats_mirror_matches_header():
+    """INTEGRATION.md's Rust `SasStats` declares the fields of sas_stats, in order and with
+    their widths (u32 / u64), so a binding built from it reads the struct the library fills."""
+    import re
+    root = os.path.join(os.path.dirname(_lib.LIB_PATH), "..")
+    hdr = open(os.path.join(root, "include", "sas.h")).read()
+    body = hdr[hdr.index("typedef struct sas_stats {"):hdr.index("} sas_stats;")]
+    c_fields = re.findall(r"^\s*uint(32|64)_t\s+(\w+);", body, re.M)
+    doc = open(os.path.join(root, "INTEGRATION.md")).read()
+    rs = doc[doc.index("pub struct SasStats {"):]
+    rs = rs[:rs.index("\n}")]
+    rust_fields = re.findall(r"pub (\w+): u(32|64)", rs)
+    assert [(w, f) for f, w in rust_fields] == c_fields
