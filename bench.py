@@ -624,9 +624,9 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     del qbytes, qoff, qlen, lens, out, ref, src, htext
     torch.cuda.empty_cache()
     kst = stats_of[phases[0][0]]
-    return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({kst['sa_width'] * 8}-bit "
-                        f"{'tagged entries' if algo == 'tagged' else 'SA'}"
-                        f"{' in 128-B bucket lines' if lines else ''}), {nq} positive queries of length "
+    ent = (f"48-bit tagged entries ({kst['tag_line_tag_bits']}-bit tags), {kst['tag_line_slots']} per 128-B "
+           f"bucket line" if lines else f"{kst['sa_width'] * 8}-bit {'tagged entries' if algo == 'tagged' else 'SA'}")
+    return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({ent}), {nq} positive queries of length "
                         f"8..256 (mean {mean_m:.1f}), ragged",
             "algo": first, "lookups_per_s": h["lookups_per_s"], "kernel_ms": h["kernel_ms"],
             "ns_per_lookup": h["ns_per_lookup"], "index_bytes": kst["index_bytes"], "setup_s": setup,
