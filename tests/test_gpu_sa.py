@@ -730,7 +730,9 @@ def test_sa_beyond_u32(sas):
     """n > 2^32 (past the reference's u32 SA, sas/sa_search.rs:35): the 40-bit
     builder for real.  The SA is checked on the GPU (adjacency as
     sas/sa_search.rs:36-38 + permutation); every answer is then proven to be the
-    exact lower bound on the host text: SA[lo-1] < q <= SA[lo], pos = SA[lo]."""
+    exact lower bound on the host text: SA[lo-1] < q <= SA[lo], pos = SA[lo].  The
+    compact-leaf, LLCP, 40-bit prefix-table and bucket-line indexes of the same text
+    return the same positions and ranges."""
     import torch
     n = (1 << 32) + 12345
     t = sas.random_string(n, seed=321, device="cuda")
@@ -782,6 +784,20 @@ def test_sa_beyond_u32(sas):
         assert np.array_equal(cidx.search_batch(buf, off, lens, algo=algo), got["plain"]), algo
     clo, chi = cidx.search_range(buf, off, lens)
     assert np.array_equal(clo, lo) and np.array_equal(chi, hi)
+    # bucket lines above 2^32 chars: 33-bit SA fields and 15-bit tags (an odd tag: the tie's
+    # text compare starts at char p + 7); p = 14, ~16 suffixes a line
+    cidx.free()
+    torch.cuda.empty_cache()
+    lidx = sas.SaNaive.build(ht, lcp=False, tagged=14, tag_lines=True)
+    lst = lidx.stats()
+    assert lst["tag_line_tag_bits"] == 15 and lst["tag_line_slots"] == 20 and lst["tag_chars"] == 14
+    assert np.array_equal(lidx.search_batch(buf, off, lens, algo="tagged"), got["plain"])
+    llo, lhi = lidx.search_range(buf, off, lens)
+    assert np.array_equal(llo, lo) and np.array_equal(lhi, hi)
+    for k in range(0, len(qs), 211):
+        r = int(lo[k])
+        if r < n:
+            assert int(lidx.suffix_array(count=1, start=r)[0]) == int(got["plain"][k]), k
 
 
 def test_fasta_genome_like_end_to_end(sas, tmp_path):
