@@ -76,6 +76,9 @@ enum class Algo : int {
 /* build flags of SaNaive::build: the LCP array, the fused quad tree and the p = 16 prefix
  * table with two-suffix inline entries (the fastest lookup at n = 2^30) */
 constexpr uint32_t kDefaultBuild = SAS_BUILD_LCP | SAS_BUILD_QUAD | SAS_BUILD_PREFIX | SAS_BUILD_PREFIX_INLINE2;
+/* the configs[3] index (long texts, long ragged queries): tagged entries in 128-B bucket
+ * lines, no SA array; it answers Algo::Tagged lookups, ranges and sa(rank) */
+constexpr uint32_t kLinesBuild = SAS_BUILD_TAGGED | SAS_BUILD_TAG_LINES;
 
 /* GPU-resident replacement for SaNaive<'t> (sas/sa_search.rs:11-19): the packed text, the
  * SA and the search structures live in HBM; the caller keeps its text. */
@@ -86,12 +89,14 @@ class SaNaive {
         sas_index* h = nullptr;
         if (t.len >= 0xFFFFFFFFull) flags &= ~(uint32_t)SAS_BUILD_PREFIX_INLINE2;  // 40-bit SA: rank table
         check(sas_build(t.ptr, t.len, nullptr, 4, flags | SAS_BUILD_VERIFY, &h));
-        return SaNaive(h, t.len);
+        const Algo a = (flags & SAS_BUILD_TAGGED) ? Algo::Tagged : (flags & SAS_BUILD_PREFIX) ? Algo::Prefix : Algo::Plain;
+        return SaNaive(h, t.len, a);
     }
-    SaNaive(SaNaive&& o) noexcept : h_(o.h_), n_(o.n_) { o.h_ = nullptr; }
+    SaNaive(SaNaive&& o) noexcept : h_(o.h_), n_(o.n_), algo_(o.algo_) { o.h_ = nullptr; }
     SaNaive& operator=(SaNaive&& o) noexcept {
         std::swap(h_, o.h_);
         std::swap(n_, o.n_);
+        std::swap(algo_, o.algo_);
         return *this;
     }
     SaNaive(const SaNaive&) = delete;
@@ -101,6 +106,9 @@ class SaNaive {
     }
 
     size_t n() const { return n_; }
+    /* the fastest lookup the build flags made possible: Tagged (SAS_BUILD_TAGGED), Prefix
+     * (SAS_BUILD_PREFIX), else Plain; Search::search uses it */
+    Algo default_algo() const { return algo_; }
     const sas_index* raw() const { return h_; }
     sas_stats stats() const {
         sas_stats s{};
@@ -143,7 +151,7 @@ class SaNaive {
     /* Search::search (sas/util.rs:34): position of the smallest suffix >= q (n if none) */
     size_t search(Seq q) const {
         size_t c = 0;
-        return search_many({q}, Algo::Prefix, &c)[0];
+        return search_many({q}, algo_, &c)[0];
     }
 
     /* occurrence range: global SA ranks [lo, hi) of the suffixes starting with q */
@@ -185,7 +193,7 @@ class SaNaive {
     }
 
    private:
-    SaNaive(sas_index* h, size_t n) : h_(h), n_(n) {}
+    SaNaive(sas_index* h, size_t n, Algo a) : h_(h), n_(n), algo_(a) {}
     static std::vector<uint8_t> padded(Seq q) {
         std::vector<uint8_t> b(q.ptr, q.ptr + q.len);
         b.resize(q.len + 64, 0);
@@ -193,6 +201,7 @@ class SaNaive {
     }
     sas_index* h_ = nullptr;
     size_t n_ = 0;
+    Algo algo_ = Algo::Prefix;
 };
 
 /* type F1 (sas/sa_search.rs:453): binary_search (:98-112), the canonical lookup: the

@@ -119,6 +119,25 @@ static void test_sa() {
         for (size_t i = 0; i < some.size(); i++) EXPECT(rs[i].second >= rs[i].first, "range order %zu", i);
     }
     EXPECT(sa.search(qs[0]) == all[0], "Search::search");
+    {  // the configs[3] index (bucket lines, no SA array): the same positions, ranges and SA
+        const sas::SaNaive lines = sas::SaNaive::build(t, sas::kLinesBuild);
+        EXPECT(lines.default_algo() == sas::Algo::Tagged, "bucket lines default to TAGGED");
+        EXPECT(lines.stats().tag_line_slots == 20, "20 slots a line");
+        const std::vector<size_t> plain = sa.search_many(qs, sas::Algo::Plain);
+        size_t lc = 0;
+        EXPECT(lines.search_many(qs, sas::Algo::Tagged, &lc) == plain, "TAGGED on bucket lines != PLAIN");
+        EXPECT(lines.search(qs[1]) == plain[1], "Search::search on bucket lines");
+        const std::vector<sas::Seq> some(qs.begin(), qs.begin() + 300);
+        EXPECT(lines.search_ranges(some) == sa.search_ranges(some), "bucket-line ranges");
+        for (size_t r : {size_t(0), size_t(1), n / 3, n - 1}) EXPECT(lines.sa(r) == osa[r], "lines sa[%zu]", r);
+        bool threw = false;
+        try {
+            lines.search_many(some, sas::Algo::Plain);
+        } catch (const sas::Panic& e) {
+            threw = e.code == ENOTSUP;
+        }
+        EXPECT(threw, "PLAIN on an index without an SA array must panic with ENOTSUP");
+    }
     std::fprintf(stderr, "SA: %zu queries, cnt plain %zu (oracle %zu), interp %zu (oracle %zu), prefix %zu\n",
                  qs.size(), cnt_plain, cnt_oracle, cnt_interp, cnt_ointerp, cnt_prefix);
     sas::bench(sa, std::vector<sas::Seq>(qs.begin(), qs.begin() + 200), "binary_search (GPU)", sas::binary_search);
