@@ -161,6 +161,17 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         reqs = {"cache": c / node, "hbm": h / node + max(0.0, probes - H) + (8.0 if packed else m) / 128}
     hbm += io
     out = {"hbm": hbm, "cache": cache, "lds": lds, "section_8d_plain": P * (4 + m) + m + 8}
+    # SURVEY §8(d)'s algorithmic bytes of this probe sequence on the reference's byte layout,
+    # every level counted wherever it is served (the roofline `achieved` of a config): the
+    # binary-search family P (4 + m) + m + 8; trees H node bytes + what the tail reads
+    if algo in ("plain", "lcp", "llcp", "inline") and not range_flag:
+        out["section_8d"] = P * (4 + m) + m + 8
+    elif algo in ("stree", "quad", "sector"):
+        node = 32 if algo == "sector" else 64
+        tail = {"stree": 4 + m, "quad": 64, "sector": 12}[algo]
+        out["section_8d"] = H * node + max(0.0, probes - H) * tail + m + 8
+    else:
+        out["section_8d"] = hbm
     if algo in ("plain", "lcp", "inline", "llcp", "stree", "quad", "sector") and not range_flag:
         out["requests_model"] = reqs
     return out
@@ -208,6 +219,80 @@ def timed_loop(step, steps: int, warmup: int, sync, barrier, reduce_max):
     barrier()
     elapsed = time.perf_counter() - t0
     return reduce_max(elapsed)
+
+
+def launch_times(torch, step, steps: int, warmup: int, stream, sync=None, barrier=None, reduce_max=None):
+    """W untimed launches, then K timed ones with a HIP event recorded on `stream` (the
+    stream the library launches on) before each and after the last: the per-launch kernel
+    times.  Returns {"mean_ms", "median_ms", "wall_s"}: the events' mean (total / K, the
+    roofline's kernel time), their median (what rocprofv3's per-dispatch statistics show
+    beside it) and the host clock over the K launches (timed_loop: barrier + sync on both
+    sides, MAX over ranks when reduce_max is given)."""
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
+    state = {"i": 0}
+
+    def timed_step():
+        i = state["i"] - warmup
+        if 0 <= i < steps:
+            evs[i].record(stream)
+        step()
+        state["i"] += 1
+        if state["i"] == warmup + steps:
+            evs[steps].record(stream)
+    el = timed_loop(timed_step, steps, warmup, sync or torch.cuda.synchronize, barrier or (lambda: None),
+                    reduce_max or (lambda x: x))
+    per = [evs[i].elapsed_time(evs[i + 1]) for i in range(steps)]
+    return {"mean_ms": evs[0].elapsed_time(evs[steps]) / steps, "median_ms": float(np.median(per)), "wall_s": el}
+
+
+# ---------------------------------------------------------------- index footprints
+def _quad_leaf_bytes(st: dict) -> int:
+    """The quad tree's leaf layer: 64-B leaves of 4 fused {key64, SA} entries (16 B) or 8
+    key-only entries (compact, 8 B)."""
+    e = st.get("quad_entry_bytes", 0)
+    return -(-st["sa_entries"] * e // 64) * 64 if e else 0
+
+
+def footprint(algo: str, st: dict) -> int:
+    """HBM bytes of the arrays one algorithm reads on this index (sas_stats fields), not the
+    combined index a bench build holds (bench.rs:526-527 records index_size per index):
+    PLAIN / LCP = SA + packed text + the pivot levels it reads (+ nothing else: mlr
+    skipping keeps its lcps in registers); LLCP = its 16-B entries + pivots + text; INLINE =
+    the fused quad leaves + pivots + text; QUAD = the quad tree (+ SA with compact leaves) +
+    text; SECTOR = the sector tree + text; STREE = the S-tree + SA + text; PREFIX = the prefix
+    table + the quad leaves (+ SA with compact leaves) + text; *_range = + the prefix table;
+    TAGGED = the tagged index (it holds nothing else)."""
+    base = algo[:-6] if algo.endswith("_range") else ("prefix" if algo == "prefix_packed" else algo)
+    text = st["text_bytes"] + st.get("text2_bytes", 0)
+    sa, t2 = st["sa_bytes"], st.get("top2_levels", 0)
+    compact_sa = sa if st.get("quad_entry_bytes") == 8 else 0
+
+    def piv(cap):
+        lv = min(t2, cap)
+        return (16 << lv) if lv else 0
+    if base == "tagged":
+        return st["index_bytes"]
+    if base in ("plain", "lcp"):
+        b = sa + text + piv(31)
+    elif base == "llcp":
+        b = st["llcp_bytes"] + text + piv(21)  # SAS_LLCP_TOP2_LEVELS
+    elif base == "inline":
+        b = _quad_leaf_bytes(st) + text + piv(TOP2_CACHE_LEVELS)  # SAS_INLINE_TOP2_LEVELS
+    elif base == "quad":
+        b = st["quad_bytes"] + compact_sa + text
+    elif base == "sector":
+        b = st["sector_bytes"] + text
+    elif base == "stree":
+        b = st["stree_bytes"] + sa + text
+    elif base == "prefix":
+        b = st["prefix_bytes"] + _quad_leaf_bytes(st) + compact_sa + text
+    elif base == "interp":
+        b = (_quad_leaf_bytes(st) if st.get("quad_entry_bytes") == 16 else sa) + text
+    else:
+        raise ValueError(f"footprint: unknown algo {algo}")
+    if algo.endswith("_range"):
+        b += st["prefix_bytes"]
+    return int(b)
 
 
 def rank_query_offsets(n: int, nq: int, m: int, rank: int) -> np.ndarray:
@@ -347,8 +432,8 @@ def lower_bound_proof(idx, window, qwin, out, sample_ids) -> int:
         if r < idx.sa_n:
             sa2 = idx.suffix_array(count=2 if r > 0 else 1, start=r - 1 if r > 0 else 0).astype(np.int64)
             p0, prev = int(sa2[-1]), (int(sa2[0]) if r > 0 else None)
-        else:
-            p0 = n
+        else:  # past this index's range: SA[rank_lo + sa_n] (n for a whole index)
+            p0 = getattr(idx, "next_pos", n)
             prev = int(idx.suffix_array(count=1, start=r - 1)[0]) if r > 0 else None
         if p0 != int(out[j]):
             bad += 1
@@ -468,8 +553,97 @@ def c0_record(torch, sas_amd, dev, seconds: float):
             "note": "10^4 queries are ~0.1 ms of GPU work: launch-bound, a plumbing check, not a GPU benchmark"}
 
 
+# ---------------------------------------------------------------- LCP skipping on long queries
+LCP_LONG_MS = (64, 128, 256)
+LCP_LONG_ALGOS = ("plain", "lcp", "llcp")
+
+
+def cut_queries(torch, text, off_t, m: int):
+    """Fixed-length queries t[off .. off + m) as one uint8 tensor (gathered in chunks)."""
+    nq = off_t.numel()
+    q = torch.empty(nq * m, dtype=torch.uint8, device=text.device)
+    ar = torch.arange(m, device=text.device, dtype=torch.int64)
+    step = max(1, (1 << 23) // m)
+    for s0 in range(0, nq, step):
+        e0 = min(nq, s0 + step)
+        q[s0 * m:e0 * m] = text[(off_t[s0:e0, None] + ar[None, :]).reshape(-1)]
+    return q
+
+
+def repetitive_text(torch, n: int, dev, base_log2: int = 24, rate: float = 0.01):
+    """A resequencing-shaped text: one random_string base of 2^base_log2 chars (ChaCha8,
+    seed 31415 + 2) copied n / 2^base_log2 times, every copy with i.i.d. substitutions at
+    `rate` (torch's seeded device generator).  Suffixes of the same locus in two copies
+    agree for ~1/(2 rate) chars, the best of 63 other copies for a few hundred: compares
+    run long, which is where LCP skipping can pay."""
+    import sas_amd
+    base = sas_amd.random_string(1 << base_log2, seed=SEED + 2, device=dev)
+    t = base.repeat(n >> base_log2)
+    g = torch.Generator(device=dev)
+    g.manual_seed(SEED)
+    chunk = 1 << 26
+    for s0 in range(0, n, chunk):
+        e0 = min(n, s0 + chunk)
+        hit = torch.rand(e0 - s0, generator=g, device=dev) < rate
+        sub = torch.randint(1, 4, (e0 - s0,), generator=g, device=dev, dtype=torch.uint8)
+        seg = t[s0:e0]
+        seg[hit] = (seg[hit] + sub[hit]) & 3  # a different code
+    return t
+
+
+def lcp_long_runs(torch, idx, text, nq: int, steps: int, warmup: int, stream, label: str) -> dict:
+    """PLAIN, mlr LCP and Manber-Myers LLCP on the same index over positive queries of
+    m = 64, 128, 256 chars: kernel time (events), mean probes, positions identical to
+    PLAIN's and every answer an occurrence of its query."""
+    n = idx.n
+    res = {}
+    for m in LCP_LONG_MS:
+        import sas_amd
+        off = sas_amd.random_queries(n, nq, seed=SEED, word_pos=n, margin=max(256, m), len_lo=m, len_hi=m + 1)[0]
+        off_t = torch.from_numpy(off.astype(np.int64)).to(text.device)
+        qb = cut_queries(torch, text, off_t, m)
+        out = torch.empty(nq, dtype=torch.int64, device=text.device)
+        ref = None
+        row = {}
+        for a in LCP_LONG_ALGOS:
+            t = launch_times(torch, lambda: idx.search_fixed(qb, m, algo=a, out=out), steps, warmup, stream)
+            if ref is None:
+                ref = out.clone()
+                occ = cut_queries(torch, text, out.clamp(max=n - m), m)
+                if not bool(torch.equal(occ, qb)):
+                    raise SystemExit(f"bench lcp_long: {label} m={m} {a} returned a non-occurrence")
+                del occ
+            elif not bool(torch.equal(out, ref)):
+                raise SystemExit(f"bench lcp_long: {label} m={m} {a} differs from plain")
+            _, pr = idx.search_fixed(qb, m, algo=a, probes=True)
+            row[a] = {"kernel_ms": t["mean_ms"], "kernel_ms_median": t["median_ms"],
+                      "lookups_per_s": nq / (t["mean_ms"] * 1e-3), "mean_probes": float(pr.double().mean().item())}
+        row["identical"] = True
+        res[f"m{m}"] = row
+        log(f"lcp_long {label} m={m}: " + ", ".join(f"{a} {row[a]['kernel_ms']:.3f}" for a in LCP_LONG_ALGOS))
+        del qb, out, ref, off_t
+    return res
+
+
+def lcp_long_summary(rec: dict) -> dict:
+    """{text_m: [plain, lcp, llcp] kernel ms} and which skipping beats PLAIN where."""
+    s, wins = {}, []
+    for tk, rows in rec.items():
+        if not isinstance(rows, dict) or tk in ("what", "summary"):
+            continue
+        for mk, row in rows.items():
+            if not isinstance(row, dict) or "plain" not in row:
+                continue
+            ms = [_r(row[a]["kernel_ms"]) for a in LCP_LONG_ALGOS]
+            s[f"{tk}_{mk}"] = ms
+            for a in ("lcp", "llcp"):
+                if row[a]["kernel_ms"] < row["plain"]["kernel_ms"]:
+                    wins.append(f"{a}@{tk}_{mk}:{row['plain']['kernel_ms'] / row[a]['kernel_ms']:.2f}x")
+    return {"ms_plain_lcp_llcp": s, "skipping_beats_plain": wins}
+
+
 # ---------------------------------------------------------------- configs[3]
-def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plain",)):
+def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plain", "lcp")):
     """configs[3]-shaped run: n = 2^34 chars (16 GiB of byte-coded text; BASELINE's
     "64 GiB" = 2^36 chars cannot hold any SA in 288 GB) and 10^8 positive
     queries of mixed length 8..256 (random_queries with len in [8, 257), sas/util.rs:18-26),
@@ -534,19 +708,9 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
 
             def step():
                 idx.search_batch(qbytes, qoff, qlen, algo=a, out=out)
-            steps = args.c3_steps if ref is None else max(2, args.c3_steps // 2)
-            for _ in range(args.warmup):
-                step()
-            torch.cuda.synchronize()
-            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            tt = time.perf_counter()
-            ev0.record()
-            for _ in range(steps):
-                step()
-            ev1.record()
-            torch.cuda.synchronize()
-            el = time.perf_counter() - tt
-            kms = ev0.elapsed_time(ev1) / steps
+            steps = args.c3_steps
+            ct = launch_times(torch, step, steps, args.warmup, torch.cuda.current_stream(dev))
+            el, kms = ct["wall_s"], ct["mean_ms"]
             if ref is None:
                 ref = out.clone()
                 # guard 1: each answer is an occurrence of its query (positive queries)
@@ -591,8 +755,9 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
             mp = float(pr.double().mean().item())
             bpl = bytes_per_lookup(a, kst, n, mean_m, mp)
             pmc_key = f"c3_{name}_n{n}_q{nq}"
-            res[name] = record(name, nq, kms, el, bpl, kst["index_bytes"], load_pmc(pmc_key) if a == algo else None,
+            res[name] = record(name, nq, kms, el, bpl, footprint(a, kst), load_pmc(pmc_key) if a == algo else None,
                                mp, {"identical_to_first": agrees, "lookups_per_s": nq * steps / el,
+                                    "kernel_ms_median": ct["median_ms"], "timed_launches": steps,
                                     "index": "bucket lines (SAS_BUILD_TAG_LINES)" if kind == "lines" else
                                     ("rank-ordered tagged entries + bucket table" if kind == "tagged" else kind)})
             log(f"c3 {name}: {kms:.3f} ms per {nq}")
@@ -600,23 +765,16 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
                 # the same queries handed over as the slices of the text they are (random_queries
                 # returns borrowed &t[i..i+len], sas/util.rs:18-26): offsets + lengths, no query
                 # bytes; a lookup whose candidate is the query's own suffix skips its text compare
-                for _ in range(args.warmup):
-                    idx.search_slices(src, qlen, out=out)
-                torch.cuda.synchronize()
-                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                ssteps = max(2, args.c3_steps // 2)
-                ev0.record()
-                for _ in range(ssteps):
-                    idx.search_slices(src, qlen, out=out)
-                ev1.record()
-                torch.cuda.synchronize()
-                sms = ev0.elapsed_time(ev1) / ssteps
+                sl_t = launch_times(torch, lambda: idx.search_slices(src, qlen, out=out), args.c3_steps, args.warmup,
+                                    torch.cuda.current_stream(dev))
+                sms = sl_t["mean_ms"]
                 same = bool(torch.equal(out, ref))
                 if not same:
                     raise SystemExit("bench c3: text-slice queries differ from the byte queries")
                 slices = {"what": "the same queries as slices of the indexed text (sas_search_batch with "
                                   "SAS_QUERIES_ARE_SLICES: offsets + lengths, chars from the packed text)",
-                          "kernel_ms": sms, "lookups_per_s": nq / (sms * 1e-3), "identical_to_first": same}
+                          "kernel_ms": sms, "kernel_ms_median": sl_t["median_ms"], "lookups_per_s": nq / (sms * 1e-3),
+                          "identical_to_first": same}
                 log(f"c3 {name} slices: {sms:.3f} ms per {nq}")
     first = "tagged_lines" if lines else algo
     h = res[first]
@@ -629,7 +787,8 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
     return {"workload": f"configs[3]-shaped: n = 2^{int(np.log2(n))} chars ({ent}), {nq} positive queries of length "
                         f"8..256 (mean {mean_m:.1f}), ragged",
             "algo": first, "lookups_per_s": h["lookups_per_s"], "kernel_ms": h["kernel_ms"],
-            "ns_per_lookup": h["ns_per_lookup"], "index_bytes": kst["index_bytes"], "setup_s": setup,
+            "ns_per_lookup": h["ns_per_lookup"], "kernel_ms_median": h.get("kernel_ms_median"),
+            "index_bytes": kst["index_bytes"], "setup_s": setup,
             "proof_sample": args.proof_sample, "verified": True,
             "roofline": {"bound": "hbm", "achieved": h["achieved_hbm_GBps"], "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": h["achieved_hbm_GBps"] / HBM_PEAK_GBPS,
@@ -639,6 +798,44 @@ def c3_record(args, torch, sas_amd, dev, rank, algo="tagged", extra_algos=("plai
             "index": {k: kst[k] for k in ("sa_width", "sa_bytes", "quad_bytes", "prefix_chars", "prefix_bytes",
                                           "tag_chars", "tag_table_bytes", "tag_line_slots", "tag_overflow_entries",
                                           "index_bytes", "build_sa_ns", "build_total_ns")}}
+
+
+def c4_proof(torch, idx, engine, n: int, m: int, ws: int, rank: int, sample: int) -> dict:
+    """lower_bound_proof on the slots this rank received in its last sharded step
+    (ShardedSearch.last): their queries (bytes, or 2-bit words unpacked), the local
+    answers, windows of this rank's packed text."""
+    L = getattr(engine, "last", None)
+    if L is None:
+        return {"checked": 0, "failures": 0}
+    cap = int(L["cap"])
+    rc = np.minimum(L["rcounts"].cpu().numpy().astype(np.int64), cap)
+    filled = np.concatenate([b * cap + np.arange(int(c), dtype=np.int64) for b, c in enumerate(rc)] +
+                            [np.zeros(0, np.int64)])
+    if len(filled) == 0:
+        return {"checked": 0, "failures": 0}
+    rng = np.random.default_rng(101 + rank)
+    ids = np.sort(rng.choice(filled, size=min(len(filled), sample), replace=False))
+    dids = torch.from_numpy(ids).to(L["recv"].device)
+    if L["packed"]:
+        w = L["recv"][dids].cpu().numpy().view(np.uint64)
+        sh = (62 - 2 * np.arange(m, dtype=np.uint64)).astype(np.uint64)
+        qs = ((w[:, None] >> sh[None, :]) & np.uint64(3)).astype(np.uint8)
+    else:
+        qs = L["recv"].view(-1, m)[dids].cpu().numpy()
+    ans = L["local"][dids].cpu().numpy()
+    qmap = {int(i): qs[j] for j, i in enumerate(ids)}
+    dev = L["recv"].device
+
+    def window(p, ln):
+        ln = min(ln, n - p)
+        if ln <= 0:
+            return np.zeros(0, np.uint8)
+        o = torch.empty(ln, dtype=torch.uint8, device=dev)
+        idx.extract(torch.tensor([p], dtype=torch.int64, device=dev), torch.tensor([ln], dtype=torch.int32, device=dev),
+                    torch.zeros(1, dtype=torch.int64, device=dev), o)
+        return o.cpu().numpy()
+    bad = lower_bound_proof(idx, window, lambda i: qmap[i], ans, ids)
+    return {"checked": int(len(ids)), "failures": int(bad)}
 
 
 def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
@@ -667,17 +864,17 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     # collective of the step, so a failure skips the record instead of hanging the others
     err = None
     try:
-        text = sas_amd.random_string(n, seed=SEED + 1, device=dev)
-        inline = 2  # two-suffix inline table (local ranks < 2^32; SA bits 32..39 in slot 1 above 2^32 chars)
-        idx = sas_amd.SaNaive.build_part(text, rank, ws, lcp=False, stree=False, sector=False, quad=True,
-                                         llcp=False, prefix=16, prefix_inline=inline)
+        # the text is generated on the GPU straight into this rank's packed text (the whole
+        # text, n/4 bytes: compares need any suffix), never as n bytes; the part holds only
+        # its own SA rank range (sas_build_part_gen) with the two-suffix inline table
+        # (local ranks < 2^32; SA bits 32..39 in slot 1 above 2^32 chars)
+        idx = sas_amd.SaNaive.build_part_gen(n, seed=SEED + 1, part=rank, parts=ws, lcp=False, stree=False,
+                                             sector=False, quad=True, llcp=False, prefix=16, prefix_inline=2)
         st = idx.stats()
         off = torch.from_numpy(rank_query_offsets(n, nq, m, rank).astype(np.int64)).to(dev)
-        ar = torch.arange(m, device=dev, dtype=torch.int64)
         qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
-        for s0 in range(0, nq, 1 << 18):
-            e0 = min(nq, s0 + (1 << 18))
-            qbytes[s0 * m:e0 * m] = text[(off[s0:e0, None] + ar[None, :]).reshape(-1)]
+        idx.extract(off, torch.full((nq,), m, dtype=torch.int32, device=dev),
+                    torch.arange(nq, device=dev, dtype=torch.int64) * m, qbytes)
         del off
         torch.cuda.synchronize()
     except Exception as e:  # noqa: BLE001 -- reported in the record
@@ -728,11 +925,22 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
                  "lookups_per_s": nq * max(3, args.c4_steps // 2) / el3, "identical": True,
                  "what": "exchange_self: the count, query and position exchanges through the world-1 RCCL group"}
         del out3
-    occ = text[(out[:, None] + ar[None, :]).reshape(-1).clamp_(max=n - 1)]
+    # every answer an occurrence of its query (read back from this rank's packed text)
+    occ = torch.empty_like(qbytes)
+    idx.extract(out.clamp(max=n - m), torch.full((nq,), m, dtype=torch.int32, device=dev),
+                torch.arange(nq, device=dev, dtype=torch.int64) * m, occ)
     ok = torch.tensor([int(bool(torch.equal(occ, qbytes)))], dtype=torch.int32, device=dev)
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     if not int(ok.item()):
         raise SystemExit("bench c4: a sharded answer is not an occurrence of its query")
+    # and a sample of the queries this rank received proven exact lower bounds on its own
+    # part: SA[lo] = its answer, suffix(SA[lo-1]) < q <= suffix(SA[lo]) (lo past the part:
+    # the next part's first suffix, next_pos)
+    proven = c4_proof(torch, idx, engine, n, m, ws, rank, max(1, args.proof_sample // ws))
+    bad = torch.tensor([proven["failures"]], dtype=torch.int64, device=dev)
+    dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+    if int(bad.item()):
+        raise SystemExit(f"bench c4: {int(bad.item())} sampled sharded answers are not exact lower bounds")
     cap = engine.capacity(-(-nq // max(1, args.shard_chunks)))  # per piece
     rec = {"workload": f"configs[4]-shaped: text of {ws} x {args.c4_share} chars sharded by SA rank ranges over "
                        f"{ws} GPU(s) (sas_build_part), {nq} len-{m} queries per GPU routed with RCCL "
@@ -748,9 +956,11 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
                           "lookups_per_s": ws * nq * max(3, args.c4_steps // 2) / el2, "identical": True},
            "exchange_bytes_per_step_per_rank": 2 * ws * cap * 8 * args.shard_chunks if ws > 1 else 0,
            "rccl_world1": rccl1,
-           "index_bytes": st["index_bytes"], "setup_s": setup, "verified": True}
+           "index_bytes": st["index_bytes"], "setup_s": setup, "verified": True,
+           "proven": proven["checked"], "proof": "each rank: a sample of the queries it received in its last step, "
+                                                  "proven exact lower bounds on its own part's SA"}
     idx.free()
-    del text, qbytes, out, occ
+    del qbytes, out, occ
     torch.cuda.empty_cache()
     if own is not None:
         own.destroy_process_group()
@@ -948,6 +1158,115 @@ def run_sst_sweep(args, torch, sas_amd, dev):
           "sweep": rows})
 
 
+# ---------------------------------------------------------------- the result line
+LINE_LIMIT = 4096  # bytes: the driver reads the line back from the tail of stdout
+DETAIL_PATH = os.path.join("gpurun_out", "bench_detail.json")
+
+
+def _r(x, d: int = 4):
+    """x to d significant digits (the line carries measurements, not float noise)."""
+    if isinstance(x, bool) or x is None or not isinstance(x, (int, float)):
+        return x
+    if isinstance(x, int):
+        return x
+    return float(f"{x:.{d}g}") if np.isfinite(x) else None
+
+
+def config_summary(rec: dict) -> dict:
+    """One flat per-config entry of the line from a full record(): throughput, kernel time
+    (event mean and median), roofline fraction of the algorithmic HBM bytes, the PMC traffic
+    per lookup when a same-hash pass exists, and the algorithm's own index footprint."""
+    pmc = rec.get("pmc") or {}
+    return {"algo": rec.get("algo"), "lookups_per_s": _r(rec.get("kernel_lookups_per_s", rec.get("lookups_per_s"))),
+            "kernel_ms": _r(rec.get("kernel_ms")), "kernel_ms_median": _r(rec.get("kernel_ms_median")),
+            # SURVEY §8(d)'s algorithmic bytes per lookup (all levels); frac_hbm: the HBM-served share only
+            "frac": _r((rec.get("bytes_per_lookup") or {}).get("section_8d", 0.0) * rec["kernel_lookups_per_s"] / 1e9
+                       / HBM_PEAK_GBPS, 3) if rec.get("kernel_lookups_per_s") else None,
+            "frac_hbm": _r((rec.get("achieved_hbm_GBps") or 0.0) / HBM_PEAK_GBPS, 3),
+            "traffic": _r(pmc.get("fabric_bytes_per_lookup")), "index_bytes": rec.get("index_bytes")}
+
+
+def compact_line(full: dict) -> dict:
+    """The one stdout line (<= LINE_LIMIT bytes) from the full record: the contract's keys,
+    `roofline` and `cpu_baseline` of the headline, and one flat entry per BASELINE config;
+    the full record (variants with their PMC blocks, index stats, byte models) goes to the
+    detail file named in `detail` (sst/bin/bench.rs:519-545 writes one flat record per run)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data")
+    line = {k: _r(full[k]) if k in ("value", "ms_per_step") else full[k] for k in keep}
+    cfg = full["config"]
+    line["config"] = {k: cfg[k] for k in ("workload", "algo", "n", "queries_per_gpu", "m", "mode", "parallelism",
+                                          "index_bytes", "index_bytes_per_text_char") if k in cfg}
+    rf = full.get("roofline")
+    if rf:
+        req = rf.get("requests") or {}
+        line["roofline"] = {"bound": rf["bound"], "achieved": _r(rf["achieved"]), "peak": rf["peak"], "unit": rf["unit"],
+                            "frac": _r(rf["frac"], 3), "traffic": _r(rf.get("traffic")),
+                            "traffic_unit": "B/lookup" if rf.get("traffic") is not None else None,
+                            "algorithmic_bytes_per_lookup": _r(rf["bytes_per_lookup"]["hbm"]),
+                            "kernel": rf.get("kernel"), "kernel_ms": _r(rf.get("kernel_ms")),
+                            "kernel_ms_median": _r(rf.get("kernel_ms_median")),
+                            "requests_per_lookup": _r(req.get("per_lookup")), "requests_frac": _r(req.get("frac"), 3)}
+    else:
+        line["roofline"] = None
+    cpu = full.get("cpu_baseline")
+    line["cpu_baseline"] = None if not cpu else {
+        "value": _r(cpu["value"]), "unit": cpu["unit"], "cores": cpu["cores"], "kind": cpu["kind"],
+        "single_thread_value": _r(cpu.get("single_thread_value")), "agrees_with_gpu": cpu.get("agrees_with_gpu"),
+        "sample": cpu["sample"][:240]}
+    confs = full.get("configs") or {}
+    out = {}
+    if "c0" in confs:
+        c0 = confs["c0"]
+        out["c0"] = {"cpu_1thread_lookups_per_s": _r(c0["cpu_1thread_lookups_per_s"]),
+                     "cpu_all_cores_lookups_per_s": _r(c0["cpu_all_cores_lookups_per_s"]), "cpu_cores": c0["cpu_cores"],
+                     "gpu_lookups_per_s": _r(c0["gpu_lookups_per_s"]), "gpu_matches_cpu": c0["gpu_matches_cpu"]}
+    for k in ("c1", "c2"):
+        if k in confs:
+            out[k] = config_summary(confs[k])
+    if "c1" in confs and confs["c1"].get("deep_pivots"):
+        out["c1_deep_pivots"] = dict(config_summary(confs["c1"]["deep_pivots"]),
+                                     pivot_levels=confs["c1"]["deep_pivots"].get("pivot_levels"))
+    if "c3" in confs and not confs["c3"].get("skipped"):
+        c3 = confs["c3"]
+        out["c3"] = {"algo": c3["algo"], "lookups_per_s": _r(c3["lookups_per_s"]), "kernel_ms": _r(c3["kernel_ms"]),
+                     "kernel_ms_median": _r(c3.get("kernel_ms_median")), "frac": _r(c3["roofline"]["frac"], 3),
+                     "traffic": _r(c3["roofline"].get("traffic")), "index_bytes": c3["index_bytes"],
+                     "n": c3.get("n"), "cross_checks": {k: _r(v["kernel_ms"]) for k, v in c3["variants"].items()
+                                                        if k != c3["algo"]}}
+    if "c4" in confs:
+        c4 = confs["c4"]
+        out["c4"] = {"skipped": c4["skipped"]} if c4.get("skipped") else {
+            "lookups_per_s": _r(c4["lookups_per_s"]), "ms_per_step": _r(c4["ms_per_step"]), "n": c4["n"],
+            "parts": c4["parts"], "index_bytes": c4["index_bytes"], "proven": c4.get("proven")}
+    line["configs"] = out
+    if full.get("variants"):
+        line["variants_kernel_ms"] = {k: _r(v["kernel_ms"]) for k, v in full["variants"].items()}
+    if full.get("lcp_long"):
+        line["lcp_long"] = full["lcp_long"].get("summary")
+    if full.get("occurrence_ranges"):
+        line["ranges_per_s"] = _r(full["occurrence_ranges"]["ranges_per_s"])
+    if full.get("e2e_host"):
+        line["e2e_host_lookups_per_s"] = _r(full["e2e_host"]["lookups_per_s"])
+    line["verified"] = full.get("verified", False)
+    line["detail"] = full.get("detail")
+    return line
+
+
+def write_detail(full: dict, path: str) -> str | None:
+    """The full record, for the reader who wants every variant, byte model and PMC block."""
+    try:
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        with open(path, "w") as f:
+            json.dump(full, f, indent=1, default=float)
+        return path
+    except OSError as e:
+        log(f"detail not written: {e!r}")
+        return None
+
+
 # ---------------------------------------------------------------- configs[1] / [2] (headline)
 WORKLOADS = {
     "prefix": "PREFIX: p = {p}-char bucket table (the reference's prefix table, sas/sa_search.rs:59-95, "
@@ -1015,7 +1334,9 @@ def main():
                          "rank-ordered with a bucket table; with lines the rank-ordered index runs as the cross-check")
     ap.add_argument("--proof-sample", type=int, default=3000, help="queries per batch proven exact lower bounds")
     ap.add_argument("--no-c4", action="store_true", help="skip the configs[4] (sharded text) sub-record")
-    ap.add_argument("--c4-share", type=int, default=1 << 30, help="configs[4]: text chars per GPU")
+    ap.add_argument("--c4-share", type=int, default=1 << 31,
+                    help="configs[4]: text chars per GPU (2^31: at N = 8 the 2^34-char text exceeds what one GPU's "
+                         "replicated index of this shape holds)")
     ap.add_argument("--shard-chunks", type=int, default=1,
                     help="sharded step in this many pieces, exchanges overlapped with the other pieces' work")
     ap.add_argument("--c4-steps", type=int, default=10)
@@ -1027,6 +1348,9 @@ def main():
                     help="sst workload: the reference's size sweep (32 B .. 2^--sweep-to B) instead of one size")
     ap.add_argument("--sweep-to", type=int, default=30, help="sst sweep: largest size 2^k bytes")
     ap.add_argument("--sweep-dense", action="store_true", help="sst sweep: also 5/4, 3/2, 7/4 of each power")
+    ap.add_argument("--detail", default=DETAIL_PATH,
+                    help="file for the full record (every variant, byte model and PMC block); '' = none")
+    ap.add_argument("--no-lcp-long", action="store_true", help="skip the long-query LCP-skipping record")
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
@@ -1121,19 +1445,9 @@ def main():
                 idx.search_packed(packed["w"], m, out=dst)
             else:
                 idx.search_fixed(qbytes, m, algo=base, out=dst, flags=fl)
-        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        state = {"i": 0}
-
-        def timed_step():
-            # events bracket exactly the K timed launches on the launch stream
-            if state["i"] == warmup:
-                ev0.record(stream)
-            step()
-            state["i"] += 1
-            if state["i"] == warmup + steps:
-                ev1.record(stream)
-        el = timed_loop(timed_step, steps, warmup, torch.cuda.synchronize, barrier, reduce_max)
-        return el, ev0.elapsed_time(ev1) / steps
+        # events bracket each of the K timed launches on the launch stream
+        t = launch_times(torch, step, steps, warmup, stream, barrier=barrier, reduce_max=reduce_max)
+        return t["wall_s"], t["mean_ms"], t["median_ms"]
 
     def probes_of(algo):
         base, fl = algo_flags(algo)
@@ -1143,7 +1457,7 @@ def main():
             _, vp = idx.search_fixed(qbytes, m, algo=base, probes=True, flags=fl)
         return float(vp.double().mean().item())
 
-    el, kernel_ms = run_algo(args.algo, args.steps, args.warmup, out)
+    el, kernel_ms, kernel_med = run_algo(args.algo, args.steps, args.warmup, out)
     if args.mode == "shard":
         engine.assert_no_overflow()
     log(f"headline {args.algo}: {kernel_ms:.3f} ms per {nq}")
@@ -1201,8 +1515,9 @@ def main():
     variants = {}
     vout = torch.empty_like(out)
     for v in [x for x in args.variants.split(",") if x and x != args.algo and args.mode == "replicated"]:
-        vsteps = max(3, args.steps // 4)
-        vel, vk = run_algo(v, vsteps, 1, vout)
+        # every variant is timed like the headline: the driver's steps and warmup
+        vsteps = args.steps
+        vel, vk, vmed = run_algo(v, vsteps, args.warmup, vout)
         same = bool(torch.equal(vout, headline_pos))
         if not same:
             raise SystemExit(f"bench: variant {v} differs from {args.algo}")
@@ -1213,8 +1528,9 @@ def main():
         key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector"}.get(v)
         pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}" + (f"_t{stats['top2_levels']}" if key == "plain" else "")) \
             if key else None
-        variants[v] = record(v, nq, vk, vel, bpl, stats["index_bytes"], pmc, vmean,
-                             {"identical_to_headline": same, "lookups_per_s": ws * nq * vsteps / vel})
+        variants[v] = record(v, nq, vk, vel, bpl, footprint(v, stats), pmc, vmean,
+                             {"identical_to_headline": same, "lookups_per_s": ws * nq * vsteps / vel,
+                              "kernel_ms_median": vmed, "timed_launches": vsteps})
         log(f"variant {v}: {vk:.3f} ms")
 
     # configs[1]'s second figure: the same PLAIN probe sequence on an index whose pivot array
@@ -1229,33 +1545,34 @@ def main():
 
         def dstep():
             didx.search_fixed(qbytes, m, algo="plain", out=dout)
-        dsteps = max(3, args.steps // 4)
-        for _ in range(2):
-            dstep()
-        torch.cuda.synchronize()
-        d0, d1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        tt = time.perf_counter()
-        d0.record(stream)
-        for _ in range(dsteps):
-            dstep()
-        d1.record(stream)
-        torch.cuda.synchronize()
-        del_s = time.perf_counter() - tt
-        dk = d0.elapsed_time(d1) / dsteps
+        dsteps = args.steps
+        dt_ = launch_times(torch, dstep, dsteps, args.warmup, stream)
+        del_s, dk = dt_["wall_s"], dt_["mean_ms"]
         if not bool(torch.equal(dout, headline_pos)):
             raise SystemExit("bench: PLAIN on the deep pivot array differs from the headline")
         _, dpr = didx.search_fixed(qbytes, m, algo="plain", probes=True)
         dmean = float(dpr.double().mean().item())
         dbpl = bytes_per_lookup("plain", dst, n, m, dmean)
-        deep = record("plain", nq, dk, del_s, dbpl, dst["index_bytes"],
+        deep = record("plain", nq, dk, del_s, dbpl, footprint("plain", dst),
                       load_pmc(f"plain_n{n}_q{nq}_m{m}_t{dst['top2_levels']}"), dmean,
                       {"identical_to_headline": True, "lookups_per_s": ws * nq * dsteps / del_s,
+                       "kernel_ms_median": dt_["median_ms"], "timed_launches": dsteps,
                        "workload": plain_label(dst), "pivot_levels": dst["top2_levels"],
                        "pivot_bytes": 16 << dst["top2_levels"]})
         didx.free()
         del dout, dpr
         torch.cuda.empty_cache()
         log(f"c1 plain, {dst['top2_levels']} pivot levels: {dk:.3f} ms")
+
+    # LCP skipping where compares run long (sas/sa_search.rs:344-345's TODO): PLAIN / LCP /
+    # LLCP at m = 64..256 on this random text now, on a repetitive text after this index is
+    # freed (below); N = 1 only
+    lcp_long = None
+    if ws == 1 and args.mode == "replicated" and not args.no_lcp_long and stats["llcp_bytes"]:
+        lcp_long = {"what": "PLAIN vs mlr LCP vs Manber-Myers LLCP skipping, 10^7 positive len-m queries, kernel ms "
+                            "(HIP events), positions identical; random: the headline's 2^30 text; repetitive: 2^24 "
+                            "random chars x 64 copies, 1% substitutions per copy",
+                    "random": lcp_long_runs(torch, idx, text, nq, args.steps, args.warmup, stream, "random")}
 
     # occurrence ranges (Search::search_prefix / search_range, sas/util.rs:36-46): the rank
     # range [lo, hi) of each query's occurrences from the prefix table (inline slots first,
@@ -1265,17 +1582,11 @@ def main():
     ranges = None
     if args.mode == "replicated":
         def time_ranges(fl):
-            for _ in range(args.warmup):
-                idx.search_range_fixed(qbytes, m, flags=fl)
-            torch.cuda.synchronize()
-            r0, r1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            rsteps = max(3, args.steps // 4)
-            r0.record(stream)
-            for _ in range(rsteps):
-                res = idx.search_range_fixed(qbytes, m, flags=fl)
-            r1.record(stream)
-            torch.cuda.synchronize()
-            return r0.elapsed_time(r1) / rsteps, res
+            res = {}
+
+            def rstep():
+                res["r"] = idx.search_range_fixed(qbytes, m, flags=fl)
+            return launch_times(torch, rstep, args.steps, args.warmup, stream)["mean_ms"], res["r"]
         rms, (lo_d, hi_d) = time_ranges(0)
         bms, (lo_b, hi_b) = time_ranges(sas_amd._lib.SAS_RANGE_NO_INLINE)
         if not (torch.equal(lo_d, lo_b) and torch.equal(hi_d, hi_b)):
@@ -1302,7 +1613,8 @@ def main():
     pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d", 64: "q"}.get(pe, "")
     hpmc = load_pmc(f"{args.algo}{pkey if args.algo == 'prefix' else ''}_n{n}_q{nq}_m{m}")
     hbpl = bytes_per_lookup(args.algo, stats, n, m, mean_probes)
-    head = record(args.algo, nq, kernel_ms, el, hbpl, stats["index_bytes"], hpmc, mean_probes)
+    head = record(args.algo, nq, kernel_ms, el, hbpl, footprint(args.algo, stats), hpmc, mean_probes,
+                  {"kernel_ms_median": kernel_med, "timed_launches": args.steps})
     achieved = head["achieved_hbm_GBps"]
 
     cpu = None
@@ -1333,6 +1645,23 @@ def main():
                                        "iterations", "prefix_chars", "prefix_bytes", "sa_bytes", "text_bytes",
                                        "quad_bytes", "stree_bytes", "sector_bytes", "lcp_bytes", "llcp_bytes",
                                        "index_bytes", "sa_rounds", "build_sa_ns", "build_total_ns")}
+    if lcp_long is not None:
+        idx.free()
+        torch.cuda.empty_cache()
+        tb = time.perf_counter()
+        rt = repetitive_text(torch, n, dev)
+        ridx = sas_amd.SaNaive.build(rt, lcp=True, llcp=True, stree=False, sector=False, quad=False, prefix=False)
+        log(f"lcp_long repetitive index built in {time.perf_counter() - tb:.1f} s")
+        lcp_long["repetitive"] = lcp_long_runs(torch, ridx, rt, nq, args.steps, args.warmup, stream, "repetitive")
+        lc = ridx.lcp_array()
+        lcp_long["repetitive_text"] = {"mean_adjacent_lcp": float(lc.mean()), "p99_adjacent_lcp": float(np.percentile(
+            lc[:: 97], 99)), "max_adjacent_lcp": int(lc.max()), "build_s": time.perf_counter() - tb}
+        del lc
+        ridx.free()
+        del rt
+        torch.cuda.empty_cache()
+        lcp_long["summary"] = lcp_long_summary(lcp_long)
+        log("lcp_long done")
     # configs[3]: free the 2^30 index first (N = 1 only: the scaling runs time the headline)
     if ws == 1 and not args.no_c3 and args.mode == "replicated":
         idx.free()
@@ -1361,7 +1690,9 @@ def main():
                     f"substrings (sas/util.rs:9-26), per-rank query stream",
             "config": {"workload": wl, "algo": args.algo, "n": n, "queries_per_gpu": nq, "m": m,
                        "prefix_chars": stats["prefix_chars"], "prefix_entry_bytes": pe,
-                       "index_bytes": stats["index_bytes"], "prefix_bytes": stats["prefix_bytes"],
+                       "index_bytes": footprint(args.algo, stats),
+                       "index_bytes_per_text_char": _r(footprint(args.algo, stats) / n),
+                       "built_index_bytes": stats["index_bytes"], "prefix_bytes": stats["prefix_bytes"],
                        "ns_per_lookup": head["ns_per_lookup"], "mode": args.mode,
                        "parallelism": (f"replicated index x{ws}, query shards (no data-path collective)"
                                        if args.mode == "replicated" else
@@ -1378,7 +1709,8 @@ def main():
                 "traffic_source": (hpmc or {}).get("source"),
                 "kernel": "k_sa_prefix2" if args.algo == "prefix" and pe >= 32 else
                           ("k_sa_prefix" if args.algo == "prefix" else KERNELS.get(args.algo)),
-                "kernel_ms": kernel_ms, "bytes_per_lookup": hbpl, "mean_probes": mean_probes,
+                "kernel_ms": kernel_ms, "kernel_ms_median": kernel_med, "bytes_per_lookup": hbpl,
+                "mean_probes": mean_probes,
                 # what bounds this path: random 128-B-line requests (PMC L2->fabric reads of this
                 # workload, query stream included), against the measured random-request ceiling
                 "requests": None if not (head.get("pmc") or {}).get("requests_per_lookup") else {
@@ -1396,7 +1728,12 @@ def main():
                             f"index's SA; every variant bit-identical to the headline"
                             + ("; CPU restatement identical on its sample" if cpu else ""),
         }
-        emit(line)
+        if lcp_long is not None:
+            line["lcp_long"] = lcp_long
+        line["detail"] = write_detail(line, args.detail) if args.detail else None
+        short = compact_line(line)
+        log(f"result line {len(json.dumps(short))} B; full record {args.detail}")
+        emit(short)
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

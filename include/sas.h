@@ -263,6 +263,16 @@ int sas_build_shard(const uint8_t* text, uint64_t n, const void* sa_or_null, int
 int sas_build_part(const uint8_t* text, uint64_t n, uint32_t part, uint32_t parts, uint32_t flags,
                    sas_index** out);
 
+/* sas_build / sas_build_part over the text random_string(n) draws from
+ * ChaCha8Rng::seed_from_u64(seed) (sas/util.rs:9-15, sas/main.rs:38 -- the same
+ * chars sas_gen_text writes), generated on the GPU straight into the index's 2-bit
+ * packed text: no n-byte copy exists on the host or the device (a sharded rank of
+ * configs[4] holds the whole text packed, n/4 bytes, and never its bytes).  Replaces
+ * `SaNaive::build(&random_string(n))` of sas/main.rs:53-65. */
+int sas_build_gen(uint64_t seed, uint64_t n, uint32_t flags, sas_index** out);
+int sas_build_part_gen(uint64_t seed, uint64_t n, uint32_t part, uint32_t parts, uint32_t flags,
+                       sas_index** out);
+
 /* Query routing for the sharded mode: out_shard[k] = number of splitter
  * suffixes (text positions splitter_pos[0..nsplit), in increasing suffix
  * order: the first suffix of shards 1..W-1) that are < query k.  Fixed-length

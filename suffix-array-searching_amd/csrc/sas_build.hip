@@ -67,22 +67,28 @@ __device__ __forceinline__ uint32_t rotl32d(uint32_t x, int r) { return (x << r)
 
 struct ChaKey { uint32_t k[8]; };
 
+// keystream block `blk`: x[i] = the state after the 8 rounds, s[i] = the input state (the
+// output word is x[i] + s[i])
+__device__ __forceinline__ void chacha8_block(const ChaKey& key, uint64_t blk, uint32_t (&s)[16], uint32_t (&x)[16]) {
+    const uint32_t in[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                             key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
+                             (uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 16; i++) s[i] = x[i] = in[i];
+#pragma unroll
+    for (int r = 0; r < 8; r += 2) {
+        DQR(x[0], x[4], x[8], x[12]) DQR(x[1], x[5], x[9], x[13])
+        DQR(x[2], x[6], x[10], x[14]) DQR(x[3], x[7], x[11], x[15])
+        DQR(x[0], x[5], x[10], x[15]) DQR(x[1], x[6], x[11], x[12])
+        DQR(x[2], x[7], x[8], x[13]) DQR(x[3], x[4], x[9], x[14])
+    }
+}
+
 __global__ void k_gen_text(ChaKey key, uint64_t n, uint8_t* __restrict__ out) {
     uint64_t blocks = (n + 15) / 16;
     GRID_STRIDE(blk, blocks) {
-        uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
-                          key.k[0], key.k[1], key.k[2], key.k[3], key.k[4], key.k[5], key.k[6], key.k[7],
-                          (uint32_t)blk, (uint32_t)(blk >> 32), 0u, 0u};
-        uint32_t x[16];
-#pragma unroll
-        for (int i = 0; i < 16; i++) x[i] = s[i];
-#pragma unroll
-        for (int r = 0; r < 8; r += 2) {
-            DQR(x[0], x[4], x[8], x[12]) DQR(x[1], x[5], x[9], x[13])
-            DQR(x[2], x[6], x[10], x[14]) DQR(x[3], x[7], x[11], x[15])
-            DQR(x[0], x[5], x[10], x[15]) DQR(x[1], x[6], x[11], x[12])
-            DQR(x[2], x[7], x[8], x[13]) DQR(x[3], x[4], x[9], x[14])
-        }
+        uint32_t s[16], x[16];
+        chacha8_block(key, blk, s, x);
         uint64_t base = blk * 16;
         if (base + 16 <= n && (((uintptr_t)(out + base)) & 15) == 0) {
             uint32_t wv[4];
@@ -187,6 +193,30 @@ extern "C" int sas_gen_queries(uint64_t seed, uint64_t word_pos, uint64_t n, uin
     }
     if (next_word) *next_word = r.pos;
     return 0;
+}
+
+// random_string straight into the index's packed layout (sas_build_gen): text word w holds
+// chars [32w, 32w + 32), i.e. keystream blocks 2w and 2w + 1, first char in bits 63..62,
+// zero past n (the words k_pack_text would make of k_gen_text's bytes), so a sharded
+// rank never holds the n-byte text.
+__global__ void k_gen_packed(ChaKey key, uint64_t n, uint64_t* __restrict__ tw, uint64_t words) {
+    GRID_STRIDE(w, words) {
+        uint64_t v = 0;
+        const uint64_t base = w * 32;
+        if (base < n) {
+#pragma unroll
+            for (int h = 0; h < 2; h++) {
+                uint32_t s[16], x[16];
+                chacha8_block(key, 2 * w + h, s, x);
+#pragma unroll
+                for (int i = 0; i < 16; i++) {
+                    const uint32_t c = 16 * h + i;
+                    if (base + c < n) v |= (uint64_t)((x[i] + s[i]) >> 30) << (62 - 2 * c);
+                }
+            }
+        }
+        tw[w] = v;
+    }
 }
 
 // ------------------------------------------------------------------ SA construction
@@ -1444,11 +1474,12 @@ static int load_sa(const void* src, uint64_t n, int wi, bool dev, uint8_t* dst, 
 // Common builder.  [rank_lo, rank_hi) = the SA ranks this index holds
 // (the whole SA for sas_build, a shard's range for sas_build_shard).
 static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, int sa_width, uint32_t flags,
-                      uint64_t rank_lo, uint64_t rank_hi, sas_index** out, uint32_t part = 0, uint32_t parts = 0) {
+                      uint64_t rank_lo, uint64_t rank_hi, sas_index** out, uint32_t part = 0, uint32_t parts = 0,
+                      const ChaKey* gen = nullptr) {
     if (!out) SAS_FAIL(EINVAL, "sas_build: null out");
     *out = nullptr;
     if (n == 0) SAS_FAIL(EINVAL, "sas_build: empty text");
-    if (!text) SAS_FAIL(EINVAL, "sas_build: null text");
+    if (!text && !gen) SAS_FAIL(EINVAL, "sas_build: null text");
     if (n >= SAS_SA40_MAX - 64) SAS_FAIL(ENOTSUP, "sas_build: n >= 2^40 - 64");
     const bool w5 = (flags & SAS_BUILD_SA40) || n >= (1ull << 32) - 64 || parts > 0;
     const uint32_t W = w5 ? 5 : 4;
@@ -1461,6 +1492,12 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
                   SAS_BUILD_PREFIX | SAS_BUILD_PREFIX_INLINE | SAS_BUILD_PREFIX_INLINE2 | SAS_BUILD_PREFIX_INLINE4)))
         SAS_FAIL(ENOTSUP, "SAS_BUILD_TAGGED replaces the SA: it combines with SAS_BUILD_LCP only, not with the "
                           "trees, LLCP or the prefix tables");
+    // a bucket-line index serves SAS_ALGO_TAGGED only (no SA array): an LCP array, or the
+    // binary-search pivot array, would be HBM nothing reads (64 GiB of LCP at n = 2^34)
+    if ((flags & SAS_BUILD_TAG_LINES) && !(flags & SAS_BUILD_TAGGED))
+        SAS_FAIL(EINVAL, "SAS_BUILD_TAG_LINES needs SAS_BUILD_TAGGED");
+    if ((flags & SAS_BUILD_TAG_LINES) && (flags & (SAS_BUILD_LCP | SAS_BUILD_LLCP)))
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_TAG_LINES serves SAS_ALGO_TAGGED only: no LCP array");
     uint64_t t0 = now_ns();
     sas_index* x = new sas_index();
     x->n = n;
@@ -1473,25 +1510,31 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     struct Guard { sas_index*& p; ~Guard() { if (p) free_index(p); } } guard{x};
     bool dev = flags & SAS_DEVICE_PTRS;
 
-    // text -> packed words
+    // text -> packed words (or random_string generated straight into them: sas_build_gen)
     DevBuf tbytes, bad, tw;
-    const uint8_t* dtext = text;
-    if (!dev) {
-        TRY(tbytes.alloc(n, "text bytes"));
-        HIP_TRY(hipMemcpy(tbytes.p, text, n, hipMemcpyHostToDevice));
-        dtext = tbytes.as<uint8_t>();
-    }
     x->text_words = (n + 31) / 32 + SAS_TEXT_PAD_WORDS;
     TRY(tw.alloc(x->text_words * 8, "packed text"));
-    TRY(bad.alloc(4, "flag"));
-    HIP_TRY(hipMemset(bad.p, 0, 4));
-    hipLaunchKernelGGL(k_pack_text, dim3(grid_for(x->text_words)), dim3(256), 0, 0, dtext, n, tw.as<uint64_t>(),
-                       x->text_words, bad.as<uint32_t>());
-    HIP_TRY(hipGetLastError());
-    uint32_t hbad = 0;
-    HIP_TRY(hipMemcpy(&hbad, bad.p, 4, hipMemcpyDeviceToHost));
-    if (hbad) SAS_FAIL(EINVAL, "sas_build: text bytes must be DNA codes 0..3");
-    tbytes.alloc(0, "free");
+    if (gen) {
+        hipLaunchKernelGGL(k_gen_packed, dim3(grid_for(x->text_words)), dim3(256), 0, 0, *gen, n, tw.as<uint64_t>(),
+                           x->text_words);
+        HIP_TRY(hipGetLastError());
+    } else {
+        const uint8_t* dtext = text;
+        if (!dev) {
+            TRY(tbytes.alloc(n, "text bytes"));
+            HIP_TRY(hipMemcpy(tbytes.p, text, n, hipMemcpyHostToDevice));
+            dtext = tbytes.as<uint8_t>();
+        }
+        TRY(bad.alloc(4, "flag"));
+        HIP_TRY(hipMemset(bad.p, 0, 4));
+        hipLaunchKernelGGL(k_pack_text, dim3(grid_for(x->text_words)), dim3(256), 0, 0, dtext, n, tw.as<uint64_t>(),
+                           x->text_words, bad.as<uint32_t>());
+        HIP_TRY(hipGetLastError());
+        uint32_t hbad = 0;
+        HIP_TRY(hipMemcpy(&hbad, bad.p, 4, hipMemcpyDeviceToHost));
+        if (hbad) SAS_FAIL(EINVAL, "sas_build: text bytes must be DNA codes 0..3");
+        tbytes.alloc(0, "free");
+    }
     x->text_w = tw.as<uint64_t>();
     tw.release();
 
@@ -1588,10 +1631,10 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
                          : (flags & SAS_BUILD_PREFIX_INLINE2) ? 2u
                          : (flags & SAS_BUILD_PREFIX_INLINE)  ? 1u : 0u));
 
-    // binary-search top in LDS
-    {
-        uint32_t iters = 64 - __builtin_clzll(sa_n);  // ilog2(len) + 1 (sas/sa_search.rs:171)
-        x->iters = iters;
+    // binary-search top in LDS (not for a bucket-line index: TAGGED never reads it)
+    const uint32_t iters = 64 - __builtin_clzll(sa_n);  // ilog2(len) + 1 (sas/sa_search.rs:171)
+    x->iters = iters;
+    if (!(flags & SAS_BUILD_TAG_LINES)) {
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
         // the pivots of the first top2_levels iterations, 2^top2_levels 16-B entries: the
         // SAS_TOP2_CACHE_LEVELS that stay inside the 256 MiB Infinity Cache (128 MiB) unless
@@ -1675,6 +1718,20 @@ extern "C" int sas_build_part(const uint8_t* text, uint64_t n, uint32_t part, ui
                               sas_index** out) {
     if (parts == 0 || part >= parts) SAS_FAIL(EINVAL, "sas_build_part: need part < parts");
     return build_impl(text, n, nullptr, 5, flags, 0, n, out, part, parts);
+}
+
+extern "C" int sas_build_gen(uint64_t seed, uint64_t n, uint32_t flags, sas_index** out) {
+    ChaKey key;
+    h_seed_from_u64(seed, key.k);
+    return build_impl(nullptr, n, nullptr, 4, flags & ~SAS_DEVICE_PTRS, 0, n, out, 0, 0, &key);
+}
+
+extern "C" int sas_build_part_gen(uint64_t seed, uint64_t n, uint32_t part, uint32_t parts, uint32_t flags,
+                                  sas_index** out) {
+    if (parts == 0 || part >= parts) SAS_FAIL(EINVAL, "sas_build_part_gen: need part < parts");
+    ChaKey key;
+    h_seed_from_u64(seed, key.k);
+    return build_impl(nullptr, n, nullptr, 5, flags & ~SAS_DEVICE_PTRS, 0, n, out, part, parts, &key);
 }
 
 extern "C" int sas_get_stats(const sas_index* index, sas_stats* out) {

@@ -92,6 +92,7 @@ class SaNaive:
         self.n = n  # text length
         self.sa_n = self.stats()["sa_entries"]  # SA entries held (n, or a shard's rank range)
         self.rank_lo = self.stats()["rank_lo"]
+        self.next_pos = self.stats()["next_pos"]  # SA value of the rank after this index's range
 
     @classmethod
     def build(cls, t, sa=None, lcp: bool = True, stree: bool | None = None, verify: bool = False,
@@ -125,6 +126,7 @@ class SaNaive:
             llcp = bool(llcp)
             flags |= _lib.SAS_BUILD_TAGGED | (0 if tagged is True else _lib.SAS_BUILD_PREFIX_P(int(tagged)))
             flags |= _lib.SAS_BUILD_TAG_LINES if tag_lines else 0
+            lcp = lcp and not tag_lines  # a bucket-line index serves TAGGED only: no LCP array
         stree = True if stree is None else stree
         sector = True if sector is None else sector
         quad = True if quad is None else quad
@@ -179,6 +181,37 @@ class SaNaive:
         h = C.c_void_p()
         check(lib().sas_build_part(_ptr(t), n, int(part), int(parts), flags, C.byref(h)))
         return cls(h, n)
+
+    @classmethod
+    def build_gen(cls, n: int, seed: int = 31415, part: int | None = None, parts: int | None = None,
+                  flags: int = 0, **kw) -> "SaNaive":
+        """The index over random_string(n, seed) (sas/util.rs:9-15) generated on the GPU
+        straight into the packed text (sas_build_gen / sas_build_part_gen): no n-byte text
+        exists anywhere.  part/parts: a build_part index; the keyword flags are build's
+        (lcp, stree, sector, quad, llcp, prefix, prefix_inline, top2_levels, verify)."""
+        lcp, stree = kw.pop("lcp", True), kw.pop("stree", True)
+        sector, quad = kw.pop("sector", True), kw.pop("quad", True)
+        verify, top2 = kw.pop("verify", False), kw.pop("top2_levels", 0)
+        prefix, inline = kw.pop("prefix", None), kw.pop("prefix_inline", False)
+        llcp = kw.pop("llcp", None)
+        if kw:
+            raise TypeError(f"build_gen: unexpected {sorted(kw)}")
+        llcp = (n < (1 << 31)) if llcp is None else llcp
+        flags |= (_lib.SAS_BUILD_LCP if lcp else 0) | (_lib.SAS_BUILD_STREE if stree else 0)
+        flags |= (_lib.SAS_BUILD_VERIFY if verify else 0) | (_lib.SAS_BUILD_SECTOR if sector else 0)
+        flags |= _quad_flags(quad) | (_lib.SAS_BUILD_LLCP if llcp else 0) | _prefix_flags(prefix, quad, n, inline)
+        flags |= _lib.SAS_BUILD_TOP2_LEVELS(top2)
+        h = C.c_void_p()
+        if part is None:
+            check(lib().sas_build_gen(seed, n, flags, C.byref(h)))
+        else:
+            check(lib().sas_build_part_gen(seed, n, int(part), int(parts), flags, C.byref(h)))
+        return cls(h, n)
+
+    @classmethod
+    def build_part_gen(cls, n: int, seed: int = 31415, part: int = 0, parts: int = 1, **kw) -> "SaNaive":
+        """build_part over random_string(n, seed) generated on the GPU (sas_build_part_gen)."""
+        return cls.build_gen(n, seed=seed, part=part, parts=parts, **kw)
 
     def free(self):
         if self._h:
@@ -267,6 +300,10 @@ class SaNaive:
         for PREFIX with m <= 32), bucket b's first counts[b] slots are queries; only those
         are searched and written into `out` (int64, one per slot).  torch CUDA tensors."""
         import torch
+        dev = queries.device
+        for name, tns in (("queries", queries), ("counts", counts)) + ((("out", out),) if out is not None else ()):
+            if not tns.is_cuda or tns.device != dev:
+                raise ValueError(f"search_buckets: {name} must be a CUDA tensor on {dev}, not {tns.device}")
         nb = int(counts.numel())
         packed = queries.dtype == torch.int64
         need = nb * cap * (1 if packed else m)

@@ -67,6 +67,7 @@ class ShardedSearch:
         self.slack = self.SLACK if slack is None else slack
         self.min_cap = min_cap
         self.exchange = world > 1 or exchange_self
+        self._sa_width = index.stats().get("sa_width", 4) if hasattr(index, "stats") else 4
         first = torch.tensor([int(index.suffix_array(1)[0])], dtype=torch.int64, device=device)
         firsts = [torch.empty_like(first) for _ in range(world)]
         dist.all_gather(firsts, first, group=group)
@@ -99,8 +100,11 @@ class ShardedSearch:
         (no collective); otherwise the MAX over ranks of each rank's own need, agreed now --
         every rank runs this collective at the start of every step, whatever its nq."""
         if self._cap_fixed is not None:
-            if nq > -(-self.max_nq // self.chunks):
-                raise ValueError(f"ShardedSearch: a piece of {nq} queries exceeds max_nq={self.max_nq}")
+            # a piece larger than max_nq declared is not refused here: raising on one rank
+            # would leave the others blocked in the exchange.  It runs with the agreed
+            # capacity; a bucket it overfills raises the device overflow flag, which every
+            # rank sees (check=True redoes the step with exact exchanges, check=False fails
+            # in assert_no_overflow on every rank)
             return self._cap_fixed
         return self._agree(self._local_cap(nq))
 
@@ -135,10 +139,23 @@ class ShardedSearch:
         w2 = self.dist.all_to_all_single(buf["recv"], send, group=self.group, async_op=async_op)
         return buf["recv"], buf["rcounts"], [w for w in (w1, w2) if w is not None]
 
+    # the algorithms sas_search_buckets takes (csrc/sas_search.hip, sas_search_buckets):
+    # PLAIN / LCP / LLCP / PREFIX, and QUAD for m <= 32
+    BUCKET_ALGOS = ("plain", "lcp", "llcp", "prefix")
+
+    def bucket_lookup(self, m: int) -> bool:
+        """The bounded lookup (only the filled slots) applies to this algo and m."""
+        if not hasattr(self.index, "search_buckets") or self._sa_width == 8:
+            return False
+        return self.packed(m) or self.algo in self.BUCKET_ALGOS or (self.algo == "quad" and m <= 32)
+
     def _lookup(self, buf, recv, rcounts, m: int, cap: int):
-        """The local lookup of the filled received slots (positions into buf["local"])."""
+        """The local lookup of the filled received slots (positions into buf["local"]).
+        Algorithms without a bounded lookup (STREE, SECTOR, INLINE, INTERP, QUAD past 32
+        chars) search every slot: an unfilled slot holds zero bytes (a valid query whose
+        answer nobody gathers)."""
         pk = self.packed(m)
-        if hasattr(self.index, "search_buckets"):
+        if self.bucket_lookup(m):
             return self.index.search_buckets(recv, m, cap, rcounts, algo="prefix" if pk else self.algo,
                                              out=buf["local"])
         if pk:  # without the bounded lookup every slot is searched
@@ -167,6 +184,9 @@ class ShardedSearch:
                                                    **({"packed": True} if pk else {}))
         recv, rcounts, _ = self._forward(buf, send, counts)
         local = self._lookup(buf, recv, rcounts, m, cap)
+        # what this rank received and answered in its last step (device tensors, no sync):
+        # the bench proves a sample of them exact lower bounds on this part's own SA
+        self.last = {"recv": recv, "rcounts": rcounts, "local": local, "cap": cap, "m": m, "packed": pk}
         back, _ = self._backward(buf, local)
         # one flag per step (check) or the sticky one (deferred to assert_no_overflow)
         flag = torch.zeros(1, dtype=torch.int32, device=self.device) if check else self.overflow

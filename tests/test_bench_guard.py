@@ -135,3 +135,70 @@ def test_reference_sweep_sizes():
     assert bench.ref_sizes(5, 8) == [32, 64, 128, 256]
     assert bench.ref_sizes(5, 7, dense=True) == [32, 40, 48, 56, 64, 80, 96, 112, 128]
     assert bench.ref_sizes()[-1] == 1 << 30 and len(bench.ref_sizes()) == 26
+
+
+def _stats_2e30():
+    """sas_stats of the default bench index at n = 2^30 (text 2-bit packed + 4 pad words,
+    u32 SA, 23 pivot levels, fused quad leaves, p = 16 two-suffix inline table)."""
+    n = 1 << 30
+    return {"n": n, "sa_entries": n, "text_bytes": (n // 32 + 4) * 8, "sa_bytes": 4 * n, "sa_width": 4,
+            "top2_levels": 23, "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
+            "quad_bytes": 18_325_000_000, "sector_bytes": 19_400_000_000, "stree_bytes": 4_563_402_752,
+            "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "index_bytes": 205_755_777_696}
+
+
+def test_footprint_per_algorithm():
+    """Each config reports the arrays its own algorithm reads (bench.rs:526-527's
+    index_size per index), not the combined index the bench build holds."""
+    st = _stats_2e30()
+    gib = 1 << 30
+    text = st["text_bytes"]
+    assert bench.footprint("plain", st) == 4 * gib + text + (16 << 23)  # ~4.4 GiB
+    assert 4.3 * gib < bench.footprint("plain", st) < 4.5 * gib
+    assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * gib
+    assert bench.footprint("llcp", st) == 16 * gib + text + (16 << 21)
+    assert bench.footprint("quad", st) == st["quad_bytes"] + text  # ~17 GiB
+    assert bench.footprint("prefix", st) == 128 * gib + 32 + 16 * gib + text  # table + fused leaves + text
+    assert bench.footprint("prefix_packed", st) == bench.footprint("prefix", st)
+    assert bench.footprint("plain_range", st) == bench.footprint("plain", st) + st["prefix_bytes"]
+    assert bench.footprint("stree", st) == st["stree_bytes"] + 4 * gib + text
+    # compact (key-only) leaves need the SA beside them
+    cst = dict(st, quad_entry_bytes=8)
+    assert bench.footprint("quad", cst) == st["quad_bytes"] + 4 * gib + text
+    assert bench.footprint("prefix", cst) == st["prefix_bytes"] + 8 * gib + 4 * gib + text
+    assert bench.footprint("tagged", st) == st["index_bytes"]
+    for a in ("plain", "lcp", "llcp", "inline", "quad", "sector", "stree", "prefix", "interp"):
+        assert bench.footprint(a, st) < st["index_bytes"], a
+
+
+REQUIRED = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline")
+
+
+def test_result_line_is_compact_and_complete():
+    """The stdout line the driver parses stays under LINE_LIMIT (round 3's 20.9 KB line went
+    unrecorded) with every contract key, the roofline and CPU baseline, and one flat entry
+    per config; the full record is the detail file's."""
+    import json
+    import os
+    full = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_record_r3.json")))
+    full["lcp_long"] = {"summary": {"ms_plain_lcp_llcp": {f"{t}_m{m}": [4.1, 4.6, 3.1] for t in ("random", "repetitive")
+                                                          for m in (64, 128, 256)},
+                                    "skipping_beats_plain": ["llcp@random_m64:1.32x"] * 6}}
+    full["detail"] = "gpurun_out/bench_detail.json"
+    line = bench.compact_line(full)
+    text = json.dumps(line)
+    assert len(text) <= bench.LINE_LIMIT < 8192, len(text)
+    for k in REQUIRED:
+        assert k in line, k
+    assert isinstance(line["value"], float) and line["value"] > 0
+    for k in ("bound", "achieved", "peak", "unit", "frac", "traffic", "kernel", "kernel_ms"):
+        assert k in line["roofline"], k
+    for k in ("value", "unit", "cores", "kind", "sample"):
+        assert k in line["cpu_baseline"], k
+    for c in ("c0", "c1", "c2", "c3", "c4"):
+        assert c in line["configs"], c
+    for c in ("c1", "c2"):
+        assert set(line["configs"][c]) >= {"lookups_per_s", "kernel_ms", "frac", "index_bytes"}
+    assert "variants" not in line and "index" not in line
+    assert json.loads(text) == line

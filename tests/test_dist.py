@@ -216,7 +216,7 @@ def shard_worker(rank, ws, port, res):
     # with the per-step capacity agreement and with a declared max_nq
     for mx in (None, nq):
         shard = OracleShard(t, sa, lo, hi)
-        eng2 = ShardedSearch(shard, dist, ws, rank, "cpu", max_nq=mx)
+        eng2 = ShardedSearch(shard, dist, ws, rank, "cpu", algo="plain", max_nq=mx)
         total = 0
         for step in range(3):
             k = nq - 17 * ((rank + step) % 3)  # differs across ranks and steps
@@ -226,8 +226,16 @@ def shard_worker(rank, ws, port, res):
         both = torch.tensor([shard.searched, total], dtype=torch.int64)
         dist.all_reduce(both)
         assert both[0] == both[1], (int(both[0]), int(both[1]))
-    with pytest.raises(ValueError):
-        ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", max_nq=10).search_fixed(dq, m)
+    # a batch past the declared max_nq is not refused on one rank (the others would hang in
+    # the exchange): it runs with the agreed capacity, and a bucket it overfills is redone
+    # exactly by the step every rank agrees on
+    for mc in (256, 0):
+        big = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu", algo="plain", max_nq=10, min_cap=mc)
+        assert big.search_fixed(dq, m).tolist() == exact.tolist()
+    # STREE (the constructor's default) has no bounded lookup: every slot is searched
+    dflt = ShardedSearch(OracleShard(t, sa, lo, hi), dist, ws, rank, "cpu")
+    assert dflt.algo == "stree" and not dflt.bucket_lookup(m)
+    assert dflt.search_fixed(dq, m).tolist() == exact.tolist()
     res[rank] = (qs.tolist(), pos.tolist())
     dist.destroy_process_group()
 

@@ -68,6 +68,25 @@ def test_sharded_nccl_world1(sas):
             torch.cuda.synchronize()
             for g in (got, got2, exact):
                 assert np.array_equal(g.cpu().numpy().astype(np.uint64), expect), algo
+        # algorithms sas_search_buckets does not take (the constructor's default STREE,
+        # SECTOR, QUAD past 32 chars) search every slot instead of failing with ENOTSUP
+        for algo, mm in (("stree", 32), ("sector", 32), ("quad", 64), ("stree", 64)):
+            qb2 = qb if mm == m else queries(t, nq, mm, 2)
+            exp2 = expect if mm == m else full.search_fixed(qb2, mm, algo="plain")
+            eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo, exchange_self=True, max_nq=nq)
+            assert not eng.bucket_lookup(mm), (algo, mm)
+            got = eng.search_fixed(torch.from_numpy(qb2).cuda(), mm)
+            torch.cuda.synchronize()
+            assert np.array_equal(got.cpu().numpy().astype(np.uint64), exp2), (algo, mm)
+        eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), exchange_self=True, max_nq=nq)
+        assert eng.algo == "stree"
+        # a batch larger than the declared max_nq is not refused (a local raise would hang
+        # the other ranks in the exchange): with the agreed capacity it is still exact
+        eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo="plain", exchange_self=True,
+                            max_nq=nq // 4)
+        got = eng.search_fixed(dq, m)
+        torch.cuda.synchronize()
+        assert np.array_equal(got.cpu().numpy().astype(np.uint64), expect)
     finally:
         dist.destroy_process_group()
 
@@ -400,3 +419,97 @@ def test_inline_slots_above_2e32(sas):
         torch.cuda.synchronize()
         assert torch.equal(lo, lo2) and torch.equal(hi, hi2), inl
         part.free()
+
+
+def test_build_gen_equals_byte_build(sas):
+    """sas_build_gen / sas_build_part_gen generate random_string(n, seed) on the GPU straight
+    into the packed text: the text (read back through sas_extract), the SA and the part
+    ranges equal those of the same index built from sas_gen_text's bytes, for an n that is
+    not a multiple of the 32-char word, and the searches agree."""
+    import torch
+    n, seed, W = 3_000_017, 77, 3
+    t = sas.random_string(n, seed=seed)
+    a = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, prefix=10, prefix_inline=2)
+    b = sas.SaNaive.build_gen(n, seed=seed, lcp=False, stree=False, sector=False, llcp=False, prefix=10,
+                              prefix_inline=2)
+    assert np.array_equal(a.suffix_array(), b.suffix_array())
+    got = torch.empty(n, dtype=torch.uint8, device="cuda")
+    b.extract(torch.zeros(1, dtype=torch.int64, device="cuda"), torch.tensor([n], dtype=torch.int32, device="cuda"),
+              torch.zeros(1, dtype=torch.int64, device="cuda"), got)
+    torch.cuda.synchronize()
+    assert np.array_equal(got.cpu().numpy(), t)
+    qb = queries(t, 20_000, 32, 3)
+    assert np.array_equal(a.search_fixed(qb, 32, algo="prefix"), b.search_fixed(qb, 32, algo="prefix"))
+    dt = torch.from_numpy(t).cuda()
+    for g in range(W):
+        p = sas.SaNaive.build_part(dt, g, W, lcp=False, stree=False, sector=False, llcp=False, prefix=10,
+                                   prefix_inline=2)
+        q = sas.SaNaive.build_part_gen(n, seed=seed, part=g, parts=W, lcp=False, stree=False, sector=False,
+                                       llcp=False, prefix=10, prefix_inline=2)
+        assert (p.rank_lo, p.sa_n, p.next_pos) == (q.rank_lo, q.sa_n, q.next_pos), g
+        assert np.array_equal(p.suffix_array(), q.suffix_array()), g
+        p.free()
+        q.free()
+
+
+@pytest.mark.timeout(600)
+def test_c4_shape_w8_loopback_past_2e32(sas):
+    """configs[4]'s step at W = 8 on one GPU (loopback exchange, one thread per rank) over a
+    2^32-char text: each rank's part from sas_build_part_gen (generated packed text, 40-bit
+    SA, fused quad leaves, two-suffix inline table; p = 13 instead of the bench's 16 so that
+    eight parts fit one GPU), PREFIX queries crossing as 8-B words into fixed-capacity
+    buckets (max_nq, check=False + assert_no_overflow), positions equal to the whole index's
+    PLAIN search, and the bench's per-rank lower-bound proof (bench.c4_proof) on every rank."""
+    import torch
+    import bench
+    from sas_amd.shard import ShardedSearch
+    n, W, m, nq, seed = 1 << 32, 8, 32, 200_000, 4242
+    whole = sas.SaNaive.build_gen(n, seed=seed, lcp=False, stree=False, sector=False, quad=False, llcp=False,
+                                  prefix=False)
+    qbs, expect = [], []
+    for r in range(W):
+        off = torch.from_numpy(bench.rank_query_offsets(n, nq, m, r).astype(np.int64)).cuda()
+        q = torch.empty(nq * m, dtype=torch.uint8, device="cuda")
+        whole.extract(off, torch.full((nq,), m, dtype=torch.int32, device="cuda"),
+                      torch.arange(nq, device="cuda", dtype=torch.int64) * m, q)
+        q[: 1000 * m] = torch.from_numpy(np.random.default_rng(r).integers(0, 4, 1000 * m, dtype=np.uint8)).cuda()
+        qbs.append(q)
+        expect.append(whole.search_fixed(q, m, algo="plain"))
+    torch.cuda.synchronize()
+    whole.free()
+    torch.cuda.empty_cache()
+    parts = [sas.SaNaive.build_part_gen(n, seed=seed, part=g, parts=W, lcp=False, stree=False, sector=False,
+                                        quad=True, llcp=False, prefix=13, prefix_inline=2) for g in range(W)]
+    assert sum(p.sa_n for p in parts) == n
+    assert max(p.next_pos for p in parts) == n or parts[-1].next_pos == n
+    lb = Loopback(W)
+    res, errs = {}, []
+
+    def rank_main(r):
+        try:
+            d = lb.rank(r)
+            eng = ShardedSearch(parts[r], d, W, r, torch.device("cuda"), algo="prefix", max_nq=nq)
+            assert eng.packed(m) and eng.bucket_lookup(m)
+            out = torch.empty(nq, dtype=torch.int64, device="cuda")
+            eng.search_fixed(qbs[r], m, check=False, out=out)
+            eng.assert_no_overflow()
+            torch.cuda.synchronize()
+            pr = bench.c4_proof(torch, parts[r], eng, n, m, W, r, 200)
+            res[r] = (out.cpu().numpy(), pr)
+        except Exception as e:  # surfaced below
+            errs.append((r, repr(e)))
+            lb.bar.abort()
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not errs, errs
+    for r in range(W):
+        out, pr = res[r]
+        assert np.array_equal(out, expect[r].cpu().numpy()), r
+        assert pr["checked"] > 0 and pr["failures"] == 0, (r, pr)
+    assert sum(int((e >= (1 << 32) - (1 << 30)).sum().item()) for e in expect) > 0
+    for p in parts:
+        p.free()

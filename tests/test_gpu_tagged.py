@@ -413,3 +413,22 @@ def test_tag_lines_overflow_heavy(sas):
     tp = O.padded(t)
     for k in range(0, nq, 97):
         assert int(ref[k]) == O.search_one(tp, n, sa, qs[k])[0], k
+
+
+def test_tag_lines_build_holds_only_what_tagged_reads(sas):
+    """A bucket-line index serves SAS_ALGO_TAGGED only: the build asks for no LCP array and
+    builds no binary-search pivot array (Python turns lcp off; the C ABI refuses LCP / LLCP
+    with ENOTSUP and TAG_LINES without TAGGED with EINVAL)."""
+    import ctypes as C
+    from sas_amd import _lib
+    t = sas.random_string(100_003, seed=5)
+    idx = sas.SaNaive.build(t, tagged=6, tag_lines=True)  # lcp defaults to True: ignored
+    st = idx.stats()
+    assert st["lcp_bytes"] == 0 and st["llcp_bytes"] == 0 and st["top2_levels"] == 0
+    idx.free()
+    h = C.c_void_p()
+    base = _lib.SAS_BUILD_TAGGED | _lib.SAS_BUILD_TAG_LINES | _lib.SAS_BUILD_PREFIX_P(6)
+    import errno
+    for fl, err in ((base | _lib.SAS_BUILD_LCP, errno.ENOTSUP), (_lib.SAS_BUILD_TAG_LINES, errno.EINVAL)):
+        rc = _lib.lib().sas_build(t.ctypes.data, len(t), None, 4, fl, C.byref(h))
+        assert rc == err, (fl, rc)
