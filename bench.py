@@ -132,11 +132,12 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             cache += max(0.0, min(probes, tc) - t1) * 16
             hbm += max(0.0, min(probes, t2) - tc) * 16  # deeper pivot levels: one 16-B HBM entry each
             hbm += max(0.0, probes - t2) * per
-            # random 128-B-line requests per lookup by where they are served: one per
-            # cache-resident pivot level; one per HBM pivot level; two per SA probe (the SA
-            # word, then the text window: PLAIN / LCP) or one (a 16-B entry); the query stream
-            reqs = {"cache": max(0.0, min(probes, tc) - t1),
-                    "hbm": max(0.0, min(probes, t2) - tc) + max(0.0, probes - t2) * (2 if per != 16 else 1)
+            # random 128-B-line requests per lookup by where they are served: one per pivot
+            # block entered (up to 3 levels a line, common.hpp top2_layout) in the cache part
+            # and in the HBM part; two per SA probe (the SA word, then the text window: PLAIN
+            # / LCP) or one (a 16-B entry); the query stream
+            pc, ph = pivot_requests(t1, t2, probes)
+            reqs = {"cache": pc, "hbm": ph + max(0.0, probes - t2) * (2 if per != 16 else 1)
                     + (8.0 if packed else m) / 128}
         else:
             hbm += probes * per
@@ -245,6 +246,47 @@ def launch_times(torch, step, steps: int, warmup: int, stream, sync=None, barrie
     return {"mean_ms": evs[0].elapsed_time(evs[steps]) / steps, "median_ms": float(np.median(per)), "wall_s": el}
 
 
+# ---------------------------------------------------------------- the pivot array
+def top2_entries(D: int, L: int, C: int = TOP2_CACHE_LEVELS, G: int = 3):
+    """common.hpp top2_layout: (entries, groups) of the pivot array for L levels above D LDS
+    levels: levels [D, L) in groups of up to G levels, a group rooted at level d0 storing
+    2^d0 blocks of 2^h 16-B slots (one slot per node for h = 1); the cache part [D, C) puts
+    its short group first, the HBM part [C, L) last."""
+    e = 1 << D
+    groups = []
+    c = min(L, C)
+    d = D
+    if c > D:
+        r = (c - D) % G
+        if r:
+            groups.append((d, r))
+            d += r
+        while d < c:
+            groups.append((d, G))
+            d += G
+    d = max(d, c)
+    while d < L:
+        groups.append((d, min(G, L - d)))
+        d += G
+    for d0, h in groups:
+        e += (1 << d0) << (0 if h == 1 else h)
+    return e, groups
+
+
+def pivot_requests(D: int, L: int, probes: float):
+    """(cache, hbm) fabric requests of the pivot levels a lookup of `probes` probes reads: one
+    per block it enters (the block's further levels hit L2)."""
+    _, groups = top2_entries(D, L)
+    cache = hbm = 0.0
+    for d0, h in groups:
+        if probes > d0:
+            if d0 < TOP2_CACHE_LEVELS:
+                cache += 1
+            else:
+                hbm += 1
+    return cache, hbm
+
+
 # ---------------------------------------------------------------- index footprints
 def _quad_leaf_bytes(st: dict) -> int:
     """The quad tree's leaf layer: 64-B leaves of 4 fused {key64, SA} entries (16 B) or 8
@@ -269,7 +311,10 @@ def footprint(algo: str, st: dict) -> int:
 
     def piv(cap):
         lv = min(t2, cap)
-        return (16 << lv) if lv else 0
+        if not lv:
+            return 0
+        # the levels this algorithm reads of the built array (LLCP / INLINE stop early)
+        return 16 * top2_entries(min(st.get("top_levels", TOP_LDS_LEVELS), lv), lv)[0]
     if base == "tagged":
         return st["index_bytes"]
     if base in ("plain", "lcp"):
@@ -1008,6 +1053,10 @@ def run_sst(args, torch, sas_amd, dev, ws, rank):
         "STree15": lambda: sas_amd.STree15.new(vals),
         "PartitionedSTree16M_b16": lambda: sas_amd.PartitionedSTree16M.new(vals, 16),
         "PartitionedSTree16M_b20": lambda: sas_amd.PartitionedSTree16M.new(vals, 20),
+        "PartitionedSTree16_b16": lambda: sas_amd.PartitionedSTree16.new(vals, 16),
+        "PartitionedSTree16C_b16": lambda: sas_amd.PartitionedSTree16C.new(vals, 16),
+        "PartitionedSTree16L_b16": lambda: sas_amd.PartitionedSTree16L.new(vals, 16),
+        "PartitionedSTree16O_b16": lambda: sas_amd.PartitionedSTree16O.new(vals, 16),
         "DirectMap": lambda: sas_amd.DirectMap.new(vals),
     }
     res, ref = {}, None
@@ -1240,6 +1289,8 @@ def compact_line(full: dict) -> dict:
             "lookups_per_s": _r(c4["lookups_per_s"]), "ms_per_step": _r(c4["ms_per_step"]), "n": c4["n"],
             "parts": c4["parts"], "index_bytes": c4["index_bytes"], "proven": c4.get("proven")}
     line["configs"] = out
+    line["configs_frac_basis"] = ("frac: SURVEY 8(d) algorithmic bytes per lookup (every level, wherever served) / "
+                                  "kernel time / 8 TB/s; frac_hbm: the HBM-served bytes only")
     if full.get("variants"):
         line["variants_kernel_ms"] = {k: _r(v["kernel_ms"]) for k, v in full["variants"].items()}
     if full.get("lcp_long"):
@@ -1291,10 +1342,11 @@ def plain_label(st: dict) -> str:
     """configs[1]'s workload text from the index's own pivot depth (sas_stats.top2_levels)."""
     t1, t2 = st["top_levels"], st["top2_levels"]
     hbm = t2 > TOP2_CACHE_LEVELS
+    pb = st.get("top2_bytes") or (16 << t2)
     return WORKLOADS["plain"].format(
-        t1=t1, t1p=t1 + 1, t2=t2, pb=(f"{(16 << t2) >> 30} GiB" if (16 << t2) >= 1 << 30 else f"{(16 << t2) >> 20} MiB"),
-        where=(f"levels {t1 + 1}-{TOP2_CACHE_LEVELS} cache-resident, {TOP2_CACHE_LEVELS + 1}-{t2} one 16-B HBM entry "
-               f"each" if hbm else "cache-resident"))
+        t1=t1, t1p=t1 + 1, t2=t2, pb=(f"{pb / 2 ** 30:.1f} GiB" if pb >= 1 << 30 else f"{pb >> 20} MiB"),
+        where=(f"levels {t1 + 1}-{TOP2_CACHE_LEVELS} cache-resident, {TOP2_CACHE_LEVELS + 1}-{t2} from HBM; "
+               f"up to 3 levels per 128-B line" if hbm else "cache-resident, up to 3 levels per 128-B line"))
 
 
 def main():
@@ -1308,8 +1360,9 @@ def main():
     ap.add_argument("--algo", default=None, choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
                                                      "prefix", "tagged", "interp"])
     ap.add_argument("--variants",
-                    default="plain,plain_range,lcp,llcp,stree,sector,quad,inline,interp,interp_range,prefix_packed",
-                    help="other algos timed beside the headline one")
+                    default="plain,plain_range,llcp,stree,sector,quad,inline,interp,interp_range,prefix_packed",
+                    help="other algos timed beside the headline one (mlr LCP skipping, 'lcp', lost to PLAIN at every "
+                         "m and on both texts of the lcp_long record: it runs there and in configs[3] only)")
     ap.add_argument("--prefix-chars", type=int, default=16,
                     help="p of the prefix table in chars (the reference's main.rs intends -p 20 key BITS)")
     ap.add_argument("--prefix-table", default="inline2", choices=["inline2", "inline4", "inline", "ranks"],
@@ -1558,7 +1611,7 @@ def main():
                       {"identical_to_headline": True, "lookups_per_s": ws * nq * dsteps / del_s,
                        "kernel_ms_median": dt_["median_ms"], "timed_launches": dsteps,
                        "workload": plain_label(dst), "pivot_levels": dst["top2_levels"],
-                       "pivot_bytes": 16 << dst["top2_levels"]})
+                       "pivot_bytes": dst["top2_bytes"]})
         didx.free()
         del dout, dpr
         torch.cuda.empty_cache()
@@ -1631,7 +1684,7 @@ def main():
     if args.mode == "replicated":
         if "plain" in variants:
             configs["c1"] = dict(variants["plain"], workload=plain_label(stats),
-                                 pivot_levels=stats["top2_levels"], pivot_bytes=16 << stats["top2_levels"])
+                                 pivot_levels=stats["top2_levels"], pivot_bytes=stats["top2_bytes"])
             if deep is not None:
                 configs["c1"]["deep_pivots"] = deep
         best2 = max((v for v in ("quad", "sector", "stree") if v in variants),

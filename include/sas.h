@@ -229,6 +229,8 @@ typedef struct sas_stats {
     uint64_t tag_overflow_entries; /* SAS_BUILD_TAG_LINES: entries in the overflow array */
     uint64_t text2_bytes;    /* SAS_BUILD_TAG_LINES: the second packed-text copy (64 B off
                                 the 128-B line grid, so a tie's compare reads one line) */
+    uint64_t top2_bytes;     /* the binary-search pivot array: the LDS levels, then blocks of
+                                up to 3 levels in one 128-B line each (0 for bucket lines) */
 } sas_stats;
 
 const char* sas_last_error(void);

@@ -45,12 +45,21 @@ enum sst_layout {
     SST_PARTITIONED_MAP = 4, /* PartitionedSTree16M: prefix map on the top b key bits
                                + S-tree (sst/partitioned_s_tree.rs:111-190,364-648);
                                b = SST_PART_BITS(b) in flags                         */
-    SST_DIRECT_MAP = 5 /* the prefix map taken to its limit: a direct-address table on
+    SST_DIRECT_MAP = 5, /* the prefix map taken to its limit: a direct-address table on
                           the top b of the 31 key bits (b = SST_PART_BITS(b), 0 = ceil(
                           log2 n) + 1, at most 30), 16-B entries {first index whose key
                           is >= the bucket start, that key and the next two}: a lookup
                           is one read unless three keys of its bucket are < q (then a
                           binary search over the sorted keys of the bucket)          */
+    /* PartitionedSTree<16,16,Tp>::new(vals, b) (sst/partitioned_s_tree.rs:111-648,
+       searches :654-831) for the other four markers the reference's differential test
+       runs (sst/test.rs:222-246); b = SST_PART_BITS(b).  Leaves are padded per part, so
+       these layouts return values only (out_rank: EINVAL) */
+    SST_PARTITIONED = 6,         /* Simple: (B+1)^h-node layers per part, layer by layer  */
+    SST_PARTITIONED_COMPACT = 7, /* Compact: one packed tree per part (bpp nodes each)   */
+    SST_PARTITIONED_L1 = 8,      /* L1: the root's fan-out cut to what the parts need    */
+    SST_PARTITIONED_OVERLAP = 9  /* Overlapping: parts share root windows (16 - overlap
+                                    new subtrees per part)                               */
 };
 
 /* layout flags (STree::new_params arguments) */

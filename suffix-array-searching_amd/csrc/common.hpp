@@ -38,6 +38,50 @@
 // caller's explicit choice (and an ENOMEM if they do not fit).
 #define SAS_TOP2_CACHE_LEVELS 23
 #define SAS_TOP2_MAX_LEVELS 31
+// The pivot array past the LDS levels is blocked (round 4): levels [SAS_TOP_LEVELS, L) are
+// cut into groups of at most SAS_TOP2_GROUP consecutive levels.  A group rooted at level d0
+// holds, for each of its 2^d0 root nodes, that root's h-level subtree as one block of 2^h
+// 16-B slots in local Eytzinger order (slot 0 unused; h = 3: 128 B, one line), or one slot
+// per node for h = 1.  A lookup's h probes in a group read one line: the first is a fabric
+// request, the next h - 1 hit L2.  Groups end at SAS_TOP2_CACHE_LEVELS, so no block mixes
+// the cache-resident levels with the HBM ones; in the cache part the first group is the
+// short one (its blocks are the fewest), in the HBM part the last.
+#define SAS_TOP2_GROUP 3
+struct Top2Layout {
+    uint64_t base[SAS_TOP2_MAX_LEVELS];  // entry offset of the level's group
+    uint8_t t[SAS_TOP2_MAX_LEVELS];      // level - the group's root level
+    uint8_t lg[SAS_TOP2_MAX_LEVELS];     // log2 slots per block (0: one slot per node)
+};
+// entry index of Eytzinger node k of level d (d >= SAS_TOP_LEVELS; below: k itself)
+__host__ __device__ __forceinline__ uint64_t top2_slot(const Top2Layout& y, uint32_t d, uint32_t k) {
+    const uint32_t t = y.t[d], lg = y.lg[d];
+    const uint64_t blk = (uint64_t)(k >> t) - (1ull << (d - t));
+    const uint32_t j = lg ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
+    return y.base[d] + (blk << lg) + j;
+}
+// fill the layout for L levels above D LDS levels; returns the array's entries
+static inline uint64_t top2_layout(uint32_t D, uint32_t L, Top2Layout* y) {
+    uint64_t entries = 1ull << D;
+    auto group = [&](uint32_t d0, uint32_t h) {
+        const uint32_t lg = h == 1 ? 0u : h;
+        for (uint32_t t = 0; t < h; t++) {
+            y->base[d0 + t] = entries;
+            y->t[d0 + t] = (uint8_t)t;
+            y->lg[d0 + t] = (uint8_t)lg;
+        }
+        entries += (1ull << d0) << lg;
+    };
+    const uint32_t C = L < SAS_TOP2_CACHE_LEVELS ? L : SAS_TOP2_CACHE_LEVELS;
+    uint32_t d = D;
+    if (C > D) {  // cache part: the short group first
+        const uint32_t r = (C - D) % SAS_TOP2_GROUP;
+        if (r) { group(d, r); d += r; }
+        for (; d < C; d += SAS_TOP2_GROUP) group(d, SAS_TOP2_GROUP);
+    }
+    for (d = d > C ? d : C; d < L; d += SAS_TOP2_GROUP)  // HBM part: the short group last
+        group(d, L - d < SAS_TOP2_GROUP ? L - d : SAS_TOP2_GROUP);
+    return entries;
+}
 #define SAS_STREE_B 16                // keys per node / branching factor - 1
 #define SAS_STREE_MAX_LAYERS 16
 #define SAS_STREE_LDS_NODES 1024      // <= 64 KiB of top S-tree layers in LDS
@@ -101,8 +145,10 @@ struct sas_index {
     uint64_t stree_off[SAS_STREE_MAX_LAYERS] = {};
     uint32_t stree_lds_layers = 0;
     uint32_t stree_lds_nodes = 0;
-    uint4* top2 = nullptr;        // [2^top2_levels] Eytzinger pivots {key64 lo, hi, SA lo, hi}, index 0
-                                  // unused; the first SAS_TOP_NODES are staged in LDS
+    uint4* top2 = nullptr;        // pivots {key64 lo, hi, SA lo, hi}: Eytzinger nodes 1..2^D - 1 (staged
+                                  // in LDS), then the blocked levels (top2_layout); index 0 unused
+    Top2Layout top2_lay{};
+    uint64_t top2_entries = 0;
     uint32_t top_levels = 0;      // levels served from LDS
     uint32_t top2_levels = 0;     // levels served from LDS or top2
     uint32_t iters = 0;           // ilog2(n) + 1
@@ -171,6 +217,10 @@ struct sst_index {
     uint64_t pmap_words = 0;
     uint32_t shift = 0;
     uint32_t parts = 0;
+    // SST_PARTITIONED*: the root window's element stride per part and the first step's
+    // multiplier (sst/partitioned_s_tree.rs:654-831), nodes per part (Compact)
+    uint64_t root_stride = 16, l1_mul = 17;
+    uint64_t bpp = 0;
 };
 
 // ---------------------------------------------------------------- suffix-array element access

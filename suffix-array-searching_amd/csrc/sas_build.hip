@@ -845,11 +845,12 @@ static int build_quad(sas_index* x, bool compact, uint32_t mode) {
 
 // ------------------------------------------------------------------ top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
-// the leading one (0 = went left: r = mid, 1 = right: l = mid + 1); entry k =
-// {32-char key, SA value} of that state's pivot SA[(l + r) / 2].
+// the leading one (0 = went left: r = mid, 1 = right: l = mid + 1); its entry =
+// {32-char key, SA value} of that state's pivot SA[(l + r) / 2], at index k for the D
+// LDS levels and at top2_slot (the blocked layout, common.hpp) below them.
 template <int W>
 __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint4* __restrict__ top2,
-                      uint32_t nodes) {
+                      uint32_t nodes, uint32_t D, Top2Layout lay) {
     GRID_STRIDE(k, nodes) {
         uint64_t l = 0, r = sa_n, p = 0xFFFFFFFFu, key = 0;
         int depth = k ? 63 - __clzll(k) : 0;
@@ -862,7 +863,8 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
             p = sa[(l + r) >> 1];
             key = text_chars32(tw, p);
         }
-        top2[k] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
+        const uint64_t at = depth < (int)D ? k : top2_slot(lay, (uint32_t)depth, (uint32_t)k);
+        top2[at] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
     }
 }
 
@@ -1290,15 +1292,44 @@ __global__ void k_tl_slots(const uint64_t* __restrict__ tw, SaView<W> sa, uint64
     }
 }
 
+// A bucket's overflow entries, ranks first + 20 .. first + count (the last one the next
+// bucket's first suffix with the maximal tag).  One thread per bucket writes up to
+// TL_OVF_SMALL of them; a longer bucket (a low-complexity text: a poly-A run at p = 15 is
+// millions of suffixes) goes to a list whose buckets whole workgroups fill (k_tl_ovf_big),
+// so no bucket waits on one thread's serial tail.
+#define TL_OVF_SMALL 256
 template <int W>
 __global__ void k_tl_ovf(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint32_t sb,
                          uint64_t keys, const uint64_t* __restrict__ t, const uint64_t* __restrict__ lines,
-                         uint64_t* __restrict__ ovf) {
+                         uint64_t* __restrict__ ovf, uint64_t* __restrict__ big, unsigned long long* __restrict__ nbig,
+                         uint64_t cap) {
     GRID_STRIDE(b, keys) {
         const uint64_t first = t[b], c = t[b + 1] - first;
         if (c < SAS_TL_SLOTS) continue;
+        if (c - SAS_TL_SLOTS >= TL_OVF_SMALL) {
+            const unsigned long long k = atomicAdd(nbig, 1ull);
+            if (k < cap) big[k] = b;
+            continue;
+        }
         const uint64_t o = lines[b * 16] & (SAS_SA40_MAX - 1);
         for (uint64_t j = SAS_TL_SLOTS; j <= c; j++) {
+            const uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p, sb);
+            ovf[o + j - SAS_TL_SLOTS] = j == c ? tl_tag_max(e, sb) : e;
+        }
+    }
+}
+
+template <int W>
+__global__ void k_tl_ovf_big(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint32_t sb,
+                             const uint64_t* __restrict__ t, const uint64_t* __restrict__ lines,
+                             uint64_t* __restrict__ ovf, const uint64_t* __restrict__ big,
+                             const unsigned long long* __restrict__ nbig) {
+    const uint64_t nb = *nbig;
+    for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
+        const uint64_t b = big[k];
+        const uint64_t first = t[b], c = t[b + 1] - first;
+        const uint64_t o = lines[b * 16] & (SAS_SA40_MAX - 1);
+        for (uint64_t j = SAS_TL_SLOTS + threadIdx.x; j <= c; j += blockDim.x) {
             const uint64_t e = tl_make<W>(tw, sa, sa_n, first + j, p, sb);
             ovf[o + j - SAS_TL_SLOTS] = j == c ? tl_tag_max(e, sb) : e;
         }
@@ -1360,10 +1391,25 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
     HIP_TRY(hipMemset(ovf.as<uint8_t>() + novf * 8, 0, 32));  // pair loads may read 2 entries past the end
     hipLaunchKernelGGL(k_tl_slots<W>, dim3(grid_for(keys * SAS_TL_SLOTS)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n,
                        p, sb, keys, t.as<uint64_t>(), lines.as<uint64_t>());
-    hipLaunchKernelGGL(k_tl_ovf<W>, dim3(grid_for(keys)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, sb, keys,
-                       t.as<uint64_t>(), lines.as<uint64_t>(), ovf.as<uint64_t>());
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipDeviceSynchronize());
+    {
+        // buckets of > TL_OVF_SMALL overflow entries: at most novf / TL_OVF_SMALL of them
+        const uint64_t bcap = novf / TL_OVF_SMALL + 2;
+        DevBuf bl, nbl;
+        TRY(bl.alloc(bcap * 8, "overflow big-bucket list"));
+        TRY(nbl.alloc(8, "overflow big-bucket count"));
+        HIP_TRY(hipMemset(nbl.p, 0, 8));
+        hipLaunchKernelGGL(k_tl_ovf<W>, dim3(grid_for(keys)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, sb,
+                           keys, t.as<uint64_t>(), lines.as<uint64_t>(), ovf.as<uint64_t>(), bl.as<uint64_t>(),
+                           nbl.as<unsigned long long>(), bcap);
+        hipLaunchKernelGGL(k_tl_ovf_big<W>, dim3(4096), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, sb,
+                           t.as<uint64_t>(), lines.as<uint64_t>(), ovf.as<uint64_t>(), bl.as<uint64_t>(),
+                           nbl.as<unsigned long long>());
+        HIP_TRY(hipGetLastError());
+        uint64_t nb = 0;
+        HIP_TRY(hipMemcpy(&nb, nbl.p, 8, hipMemcpyDeviceToHost));
+        if (nb > bcap) SAS_FAIL(EFAULT, "bucket lines: overflow big-bucket list overflow");
+        HIP_TRY(hipDeviceSynchronize());
+    }
     // the lines and the overflow hold every SA value: the plain SA goes
     (void)hipFree(x->sa);
     x->sa = nullptr;
@@ -1646,13 +1692,17 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         const uint32_t lv = iters < want ? iters : want;
         x->top2_levels = lv;
         const uint32_t nodes = 1u << x->top2_levels;
+        x->top2_entries = top2_layout(x->top_levels, x->top2_levels, &x->top2_lay);
         DevBuf t2;
-        TRY(t2.alloc((uint64_t)nodes * 16, "top2"));
+        TRY(t2.alloc(x->top2_entries * 16, "top2"));
+        HIP_TRY(hipMemset(t2.p, 0, x->top2_entries * 16));  // unused block slots
         const dim3 tg(grid_for(nodes)), tb(256);
         if (W == 5)
-            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes);
+            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes,
+                               x->top_levels, x->top2_lay);
         else
-            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes);
+            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes,
+                               x->top_levels, x->top2_lay);
         HIP_TRY(hipGetLastError());
         x->top2 = static_cast<uint4*>(t2.release());
     }
@@ -1696,8 +1746,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.text2_bytes = x->text2 ? x->text_words * 8 : 0;
     st.tag_overflow_entries = x->tag_ovf_n;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
-                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes +
-                     ((uint64_t)16 << x->top2_levels);
+                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes + x->top2_entries * 16;
+    st.top2_bytes = x->top2_entries * 16;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

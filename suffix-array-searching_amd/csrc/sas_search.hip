@@ -53,6 +53,7 @@ struct SearchArgs {
     uint32_t prefix_w;       // bytes per table entry (4 or 5)
     uint32_t prefix_hi40;    // inline slots: SA bits 32..39 in slot 1's rank word
     const uint4* top2;
+    Top2Layout top2_lay;     // the blocked levels' addresses (common.hpp)
     uint32_t top_levels;
     uint32_t top2_levels;
     uint32_t iters;
@@ -216,9 +217,10 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
                     k = 2 * k + (lt ? 1u : 0u);
                 } else if (TOP && it < a.top2_levels) {
-                    // the next levels' pivots from the L2-resident top2 array: one 16-B read
-                    // instead of an SA word and a text window
-                    const uint4 e = a.top2[k];
+                    // the next levels' pivots from the cache-resident (or, deeper, HBM) pivot
+                    // array: one 16-B read instead of an SA word and a text window, and the
+                    // levels of one block share its line (one fabric request per block)
+                    const uint4 e = a.top2[top2_slot(a.top2_lay, it, k)];
                     p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
                     lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
                     k = 2 * k + (lt ? 1u : 0u);
@@ -1164,7 +1166,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                     key = s_key[k];
                     p = s_sa[k];
                 } else if (TOP && it < a.top2_levels) {
-                    const uint4 e = a.top2[k];
+                    const uint4 e = a.top2[top2_slot(a.top2_lay, it, k)];
                     key = (uint64_t)e.x | ((uint64_t)e.y << 32);
                     p = (uint64_t)e.z | ((uint64_t)e.w << 32);
                 } else if (KO) {
@@ -2537,6 +2539,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.prefix_w = x->prefix_w;
     a.prefix_hi40 = x->prefix_hi40;
     a.top2 = x->top2;
+    a.top2_lay = x->top2_lay;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;
     a.iters = x->iters;

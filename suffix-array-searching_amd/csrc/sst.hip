@@ -15,7 +15,6 @@
 #define SST_BLOCK 1024
 #define SST_EYT_LDS 8192  // first 13 Eytzinger levels (32 KiB) in LDS
 
-static constexpr uint32_t SST_MAX = 0x7fffffffu;  // sst/node.rs:5
 
 struct SstArgs {
     const uint32_t* nodes;
@@ -36,6 +35,9 @@ struct SstArgs {
     uint32_t parts;
     uint32_t leaf_nt;  // leaf layer read non-temporal (> SAS_NT_BYTES)
     const uint4* direct;  // SST_DIRECT_MAP: [2^b + 1] entries {index, key, next key, next-but-one}
+    uint64_t root_stride;  // SST_PARTITIONED*: elements between two parts' root windows
+    uint64_t l1_mul;       // and the first step's multiplier (k_sst_part4)
+    uint64_t bpp;          // Compact: nodes per part (0 otherwise)
 };
 
 // count of keys < q under SIGNED compare (find_popcnt, sst/node.rs:93-109)
@@ -201,6 +203,48 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_pmap4(SstArgs a) {
     }
 }
 
+// PartitionedSTree<16,16,{Simple,Compact,L1,Overlapping}>::search (sst/partitioned_s_tree.rs:
+// 654-831), one 4-lane group per query (lane j: keys 4j..4j+3 of each 16-key window).  In
+// elements of the node array: the root window of part P starts at off[0]*16 + P*root_stride
+// (Simple / L1: one node per part; Compact: the part's packed tree, bpp nodes; Overlapping:
+// 16 - overlap keys per part, read unaligned); the first step goes to node
+// P*root_stride*l1_mul/16 + c of layer 1 (Compact: c inside the part), then k*17 + c; the
+// answer is key idx of the leaf window (idx = 16: the next window's first key).
+__global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_part4(SstArgs a) {
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
+    const bool compact = a.bpp != 0;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
+        const int32_t q = (int32_t)a.qs[i];
+        uint64_t part = (uint32_t)q >> a.shift;
+        if (part >= a.parts) part = a.parts - 1;  // q above every key's prefix (UB in the reference)
+        auto cnt4 = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) -> uint32_t {
+            return quad_sum((q > (int32_t)w0) + (q > (int32_t)w1) + (q > (int32_t)w2) + (q > (int32_t)w3));
+        };
+        const uint64_t cbase = compact ? part * a.bpp : 0;
+        uint64_t e = a.off[0] * 16 + part * a.root_stride;  // the window read now (elements)
+        const uint32_t* r0 = a.nodes + e + 4 * sub;  // any alignment (Overlapping)
+        uint32_t w0 = r0[0], w1 = r0[1], w2 = r0[2], w3 = r0[3];
+        uint32_t c = cnt4(w0, w1, w2, w3);
+        if (a.height >= 2) {
+            uint64_t k = compact ? c : part * a.root_stride * a.l1_mul / 16 + c;
+            const uint4* g = reinterpret_cast<const uint4*>(a.nodes);
+            for (uint32_t h = 1; h < a.height; h++) {
+                e = (a.off[h] + cbase + k) * 16;
+                const uint4 v = (h + 1 == a.height) ? load4(g + e / 4 + sub, a.leaf_nt) : g[e / 4 + sub];
+                w0 = v.x; w1 = v.y; w2 = v.z; w3 = v.w;
+                c = cnt4(w0, w1, w2, w3);
+                k = k * 17 + c;
+            }
+        }
+        const uint32_t r = c & 3;
+        const uint32_t mine = r == 0 ? w0 : r == 1 ? w1 : r == 2 ? w2 : w3;
+        uint32_t val = (uint32_t)__shfl((int)mine, (int)((threadIdx.x & 63) & ~3u) + (int)((c >> 2) & 3), 64);
+        if (c >= 16) val = a.nodes[e + 16];
+        if (sub == 0) a.out[i] = val;
+    }
+}
+
 __global__ __launch_bounds__(SST_BLOCK) void k_sst_eytzinger(SstArgs a) {
     __shared__ uint32_t s_e[SST_EYT_LDS];
     uint64_t len = a.n + 1;
@@ -310,187 +354,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_direct(SstArgs a) {
     }
 }
 
-// ------------------------------------------------------------------ host builders
-// TreeBase<B> (sst/s_tree.rs:22-45)
-static uint64_t blocks_of(uint64_t n, uint64_t B) { return (n + B - 1) / B; }
-static uint64_t prev_keys(uint64_t n, uint64_t B) { return (blocks_of(n, B) + B) / (B + 1) * B; }
-static uint32_t height_of(uint64_t n, uint64_t B) { return n <= B ? 1 : height_of(prev_keys(n, B), B) + 1; }
-static uint64_t layer_size(uint64_t n, uint32_t h, uint32_t height, uint64_t B) {
-    for (uint32_t i = h; i + 1 < height; i++) n = prev_keys(n, B);
-    return n;
-}
-
-// STree::new_params (sst/s_tree.rs:72-176).  The node array starts zeroed
-// like the reference's fresh hugepage allocation (:125-129).
-static int build_stree_host(const uint32_t* vals, uint64_t n, uint32_t B, bool left_max, bool reverse, bool full,
-                            std::vector<uint32_t>& tree, sst_index* x) {
-    const uint32_t N = 16;
-    if (full && reverse) SAS_FAIL(EINVAL, "sst_build: full array only makes sense in forward layout");
-    for (uint64_t i = 0; i < n; i++)
-        if (vals[i] > SST_MAX) SAS_FAIL(EINVAL, "sst_build: S-tree keys must be <= i32::MAX (sst/node.rs:5)");
-    uint32_t height = height_of(n, B);
-    if (height > SAS_STREE_MAX_LAYERS) SAS_FAIL(ENOTSUP, "sst_build: tree too high");
-    uint64_t ls[SAS_STREE_MAX_LAYERS], nb = 0;
-    for (uint32_t h = 0; h < height; h++) {
-        if (full) {
-            uint64_t s = 1;
-            for (uint32_t k = 0; k < h; k++) s *= (B + 1);
-            ls[h] = s;
-        } else {
-            ls[h] = (layer_size(n, h, height, B) + B - 1) / B;
-        }
-        nb += ls[h];
-    }
-    uint64_t sum = 0;
-    for (uint32_t h = 0; h < height; h++) {
-        if (!reverse) { x->off[h] = sum; sum += ls[h]; }
-        else { sum += ls[h]; x->off[h] = nb - sum; }
-        x->layer_nodes[h] = ls[h];
-    }
-    tree.assign(nb * N, 0u);
-    auto node = [&](uint64_t b) { return tree.data() + b * N; };
-    uint64_t ol = x->off[height - 1];
-    for (uint64_t i = 0; i < n; i++) {
-        node(ol + i / B)[i % B] = vals[i];
-        if (B < N && i % B == 0 && i > 0) node(ol + i / B - 1)[B] = vals[i];
-    }
-    if (n / B < ls[height - 1])
-        for (uint64_t j = n % B; j < N; j++) node(ol + n / B)[j] = SST_MAX;
-    for (int h = (int)height - 2; h >= 0; h--) {
-        uint64_t oh = x->off[h];
-        std::fill(tree.begin() + oh * N, tree.begin() + (oh + ls[h]) * N, SST_MAX);
-        for (uint64_t i = 0; i < (uint64_t)B * ls[h]; i++) {
-            uint64_t k = i / B, j = i % B;
-            k = k * (B + 1) + j + 1;
-            for (uint32_t l = (uint32_t)h; l + 2 < height; l++) k *= (B + 1);
-            node(oh + i / B)[i % B] =
-                k * B < n ? (!left_max ? node(ol + k)[0] : node(ol + k - 1)[B - 1]) : SST_MAX;
-        }
-    }
-    x->height = height;
-    x->B = B;
-    x->N = N;
-    // LDS-staged top layers
-    uint32_t L = 0, nodes = 0;
-    for (uint32_t h = 0; h + 1 < height; h++) {
-        if (nodes + ls[h] > SAS_STREE_LDS_NODES) break;
-        nodes += (uint32_t)ls[h];
-        L++;
-    }
-    x->lds_layers = L;
-    x->lds_nodes = nodes;
-    return 0;
-}
-
-// PartitionedSTree<16,16,Map>::get_part_size + try_new
-// (sst/partitioned_s_tree.rs:111-190, 364-648 with Tp = Map: not compact, L1,
-// overlap Some(0), prefix map).
-static int build_pmap_host(const uint32_t* vals, uint64_t n, uint32_t b, std::vector<uint32_t>& tree,
-                           std::vector<uint32_t>& pmap, sst_index* x) {
-    const uint64_t B = 16;
-    if (vals[n - 1] > SST_MAX) SAS_FAIL(EINVAL, "sst_build: keys must be <= i32::MAX (sst/node.rs:5)");
-    // get_part_size (:111-190)
-    uint32_t bits = 1 + (31 - __builtin_clz(vals[n - 1] ? vals[n - 1] : 1));
-    if (vals[n - 1] == 0) bits = 1;  // ilog2(0) panics in the reference; treat as 1 bit
-    auto part_sizes = [&](uint32_t shift, uint64_t parts, uint64_t* maxb) {
-        std::vector<uint64_t> bs(parts, 0);
-        for (uint64_t i = 0; i < n; i++) bs[vals[i] >> shift]++;
-        uint64_t m = 0;
-        for (uint64_t v : bs) m = v > m ? v : m;
-        *maxb = m;
-    };
-    auto get_height = [&](uint64_t xx) { return height_of((xx * 17 + 15) / 16, B); };  // MAP: x*17/16
-    uint32_t shift = bits > b ? bits - b : 0;
-    uint64_t parts = 1ull << (bits - shift);
-    uint64_t max_bucket;
-    part_sizes(shift, parts, &max_bucket);
-    uint32_t height = get_height(max_bucket);
-    uint32_t b2 = b;
-    for (;;) {
-        if (b2 == 0) break;
-        b2 -= 1;
-        if (b2 > bits) break;
-        uint32_t shift2 = bits > b2 ? bits - b2 : 0;
-        uint64_t parts2 = 1ull << (bits - shift2);
-        uint64_t mb2;
-        part_sizes(shift2, parts2, &mb2);
-        uint32_t h2 = get_height(mb2);
-        if (h2 > height) break;
-        shift = shift2;
-        parts = parts2;
-        max_bucket = mb2;
-        height = h2;
-    }
-    // try_new (:364-648), Map
-    uint64_t ls[SAS_STREE_MAX_LAYERS];
-    if (height > SAS_STREE_MAX_LAYERS) SAS_FAIL(ENOTSUP, "sst_build: tree too high");
-    for (uint32_t h = 0; h < height; h++) ls[h] = (layer_size(n, h, height, B) + B - 1) / B;
-    if (height > 1) ls[0] = ((layer_size(n, 1, height, B) + B - 1) / B + B - 1) / B;
-    uint64_t nb = 0;
-    for (uint32_t h = 0; h < height; h++) {
-        x->off[h] = nb;
-        x->layer_nodes[h] = ls[h];
-        nb += ls[h];
-    }
-    if (nb * 64 > (32ull << 30)) SAS_FAIL(ENOMEM, "sst_build: PartitionedSTree16M overhead too large (try_new -> None)");
-    tree.assign(nb * 16, SST_MAX);
-    uint64_t ol = x->off[height - 1];
-    for (uint64_t i = 0; i < n; i++) tree[(ol + i / B) * 16 + i % B] = vals[i];
-    uint64_t subtree = height == 1 ? 1 : B;
-    for (uint32_t k = 0; k + 2 < height; k++) subtree *= (B + 1);
-    for (int h = (int)height - 2; h >= 0; h--) {
-        uint64_t oh = x->off[h];
-        if (h == 0) {  // overlap Some(0): layer 0 holds the max of every layer-1 subtree
-            for (uint64_t i = 0; i + 1 < ls[1]; i++) {
-                uint64_t j = (i + 1) * subtree - 1;
-                tree[(oh + i / B) * 16 + i % B] = tree[(ol + j / B) * 16 + j % B];
-            }
-            break;
-        }
-        for (uint64_t i = 0; i < B * ls[h]; i++) {
-            uint64_t k = i / B, j = i % B;
-            k = k * (B + 1) + j + 1;
-            for (uint32_t l = (uint32_t)h; l + 2 < height; l++) k *= (B + 1);
-            tree[(oh + i / B) * 16 + i % B] = k * B < n ? tree[(ol + k - 1) * 16 + B - 1] : SST_MAX;
-        }
-    }
-    // prefix map (:605-627)
-    pmap.assign(parts, 0);
-    uint64_t max_idx = ls[0] * B - B;
-    uint64_t p = 0;
-    for (uint64_t i = 0; i < ls[0] * B; i++) {
-        uint64_t pi = tree[x->off[0] * 16 + i] >> shift;
-        while (p < pi && p + 1 < parts) {
-            p++;
-            pmap[p] = (uint32_t)(i < max_idx ? i : max_idx);
-        }
-    }
-    while (p + 1 < parts) {
-        p++;
-        pmap[p] = (uint32_t)max_idx;
-    }
-    x->height = height;
-    x->B = 16;
-    x->N = 16;
-    x->shift = shift;
-    x->parts = (uint32_t)parts;
-    return 0;
-}
-
-// Eytzinger::new (sst/eytzinger.rs:37-63), iterative in-order fill.
-static void build_eytzinger_host(const uint32_t* vals, uint64_t n, std::vector<uint32_t>& e) {
-    e.assign(n + 1, 0);
-    e[0] = 0xFFFFFFFFu;
-    uint64_t i = 0, k = 1;
-    std::vector<uint64_t> stack;
-    while (k <= n || !stack.empty()) {
-        while (k <= n) { stack.push_back(k); k *= 2; }
-        k = stack.back();
-        stack.pop_back();
-        e[k] = vals[i++];
-        k = 2 * k + 1;
-    }
-}
+#include "sst_host.hpp"
 
 // ------------------------------------------------------------------ C ABI
 extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, uint32_t flags, sst_index** out) {
@@ -530,6 +394,12 @@ extern "C" int sst_build(const uint32_t* sorted_vals, uint64_t n, int layout, ui
             break;
         case SST_PARTITIONED_MAP:
             rc = build_pmap_host(sorted_vals, n, SST_PART_BITS_OF(flags), host, pmap, x);
+            break;
+        case SST_PARTITIONED:
+        case SST_PARTITIONED_COMPACT:
+        case SST_PARTITIONED_L1:
+        case SST_PARTITIONED_OVERLAP:
+            rc = build_part_host(sorted_vals, n, SST_PART_BITS_OF(flags), layout, host, x);
             break;
         case SST_DIRECT_MAP:
             host.assign(sorted_vals, sorted_vals + n);  // the sorted keys (the fallback search)
@@ -647,6 +517,7 @@ static int sst_launch(const sst_index* x, SstArgs& a, uint32_t flags, hipStream_
         uint64_t b4 = (a.nq * QUAD_G + SST_BLOCK - 1) / SST_BLOCK;
         dim3 grid4((unsigned)(b4 < cap ? b4 : cap));
         if (x->layout == SST_PARTITIONED_MAP) hipLaunchKernelGGL(k_sst_pmap4, grid4, block, 0, st, a);
+        else if (x->layout >= SST_PARTITIONED) hipLaunchKernelGGL(k_sst_part4, grid4, block, 0, st, a);
         else if (flags & SST_NO_LDS_TOP) hipLaunchKernelGGL(k_sst_stree4<false>, grid4, block, 0, st, a);
         else hipLaunchKernelGGL(k_sst_stree4<true>, grid4, block, 0, st, a);
     }
@@ -673,6 +544,9 @@ static void sst_fill(const sst_index* x, SstArgs& a) {
     a.parts = x->parts;
     a.leaf_nt = x->height > 0 && x->layer_nodes[x->height - 1] * 64 > SAS_NT_BYTES;
     a.direct = x->direct;
+    a.root_stride = x->root_stride;
+    a.l1_mul = x->l1_mul;
+    a.bpp = x->bpp;
 }
 
 extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, uint32_t* out_val, uint64_t* out_rank,
@@ -681,6 +555,8 @@ extern "C" int sst_query(const sst_index* x, const uint32_t* qs, uint64_t nq, ui
     if (nq == 0) return 0;
     if (!qs || !out_val) SAS_FAIL(EINVAL, "sst_query: null qs/out_val");
     if (out_rank && x->layout == SST_EYTZINGER) SAS_FAIL(EINVAL, "sst_query: Eytzinger layout has no rank output");
+    if (out_rank && x->layout >= SST_PARTITIONED)
+        SAS_FAIL(EINVAL, "sst_query: partitioned layouts pad every part's leaves: no rank output");
     hipStream_t st = static_cast<hipStream_t>(stream);
     SstArgs a{};
     sst_fill(x, a);

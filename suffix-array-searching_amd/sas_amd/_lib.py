@@ -59,6 +59,7 @@ ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, 
          "interp": 8, "tagged": 9}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP, SST_DIRECT_MAP = 0, 1, 2, 3, 4, 5
+SST_PARTITIONED, SST_PARTITIONED_COMPACT, SST_PARTITIONED_L1, SST_PARTITIONED_OVERLAP = 6, 7, 8, 9
 SST_LEFT_MAX = 1 << 0
 SST_REVERSE = 1 << 1
 SST_FULL = 1 << 2
@@ -80,7 +81,7 @@ class SasStats(C.Structure):
         ("prefix_bytes", C.c_uint64), ("prefix_chars", C.c_uint32), ("tag_chars", C.c_uint32),
         ("tag_table_bytes", C.c_uint64), ("index_bytes", C.c_uint64),
         ("tag_line_slots", C.c_uint32), ("tag_line_tag_bits", C.c_uint32), ("tag_overflow_entries", C.c_uint64),
-        ("text2_bytes", C.c_uint64),
+        ("text2_bytes", C.c_uint64), ("top2_bytes", C.c_uint64),
     ]
 
     def as_dict(self):

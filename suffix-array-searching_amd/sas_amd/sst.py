@@ -128,6 +128,36 @@ class PartitionedSTree16M(_Index):
         return cls._build(vals, cls.LAYOUT, (b & 0xFF) << 16)
 
 
+class _Partitioned(_Index):
+    """PartitionedSTree<16,16,Tp>::new(vals, b) (sst/partitioned_s_tree.rs:111-648) for the
+    markers the reference's differential test runs beside Map (sst/test.rs:222-246).  The
+    leaves are padded per part: query() returns values only."""
+
+    @classmethod
+    def new(cls, vals, b: int = 16):
+        return cls._build(vals, cls.LAYOUT, (b & 0xFF) << 16)
+
+
+class PartitionedSTree16(_Partitioned):
+    """Simple: every part a full (B+1)^h tree, layer by layer."""
+    LAYOUT = _lib.SST_PARTITIONED
+
+
+class PartitionedSTree16C(_Partitioned):
+    """Compact: each part's tree packed on its own (bpp nodes per part)."""
+    LAYOUT = _lib.SST_PARTITIONED_COMPACT
+
+
+class PartitionedSTree16L(_Partitioned):
+    """L1: the root's fan-out reduced to what the largest part needs."""
+    LAYOUT = _lib.SST_PARTITIONED_L1
+
+
+class PartitionedSTree16O(_Partitioned):
+    """Overlapping: consecutive parts share root windows (16 - overlap new subtrees each)."""
+    LAYOUT = _lib.SST_PARTITIONED_OVERLAP
+
+
 class DirectMap(_Index):
     """SST_DIRECT_MAP: the prefix map of PartitionedSTree16M taken to its limit, a
     direct-address table on the top b of the 31 key bits whose 16-B entries inline

@@ -82,13 +82,16 @@ def test_byte_model_hbm_pivot_levels():
     p30 = bench.bytes_per_lookup("plain", st, n, m, 31.0)
     assert p30["lds"] == 12 * 12 and p30["cache"] == 11 * 16
     assert p30["hbm"] == 7 * 16 + 1 * (4 + m / 4) + m + 8
-    assert p30["requests_model"] == {"cache": 11.0, "hbm": 7 + 2 * 1 + m / 128}
+    # blocked pivots: one request per block entered (blocks of levels 13-14, 15-17, 18-20,
+    # 21-23 in the cache; 24-26, 27-29, 30 from HBM), then level 31's SA word + text window
+    assert p30["requests_model"] == {"cache": 4.0, "hbm": 3 + 2 * 1 + m / 128}
     # fewer probes than the pivot levels (a short range): no SA-level term
     p20 = bench.bytes_per_lookup("plain", st, n, m, 20.0)
     assert p20["hbm"] == m + 8 and p20["cache"] == 8 * 16
     # INLINE stays on the cache-resident 23 levels whatever the array holds (launch_search)
     pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
     assert pin["hbm"] == 8 * 16 + m + 8 and pin["requests_model"]["hbm"] == 8 + m / 128
+    assert pin["requests_model"]["cache"] == 4.0
     # the split: model HBM requests first, the rest of the PMC count is cache-served
     bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
     assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
@@ -153,10 +156,12 @@ def test_footprint_per_algorithm():
     st = _stats_2e30()
     gib = 1 << 30
     text = st["text_bytes"]
-    assert bench.footprint("plain", st) == 4 * gib + text + (16 << 23)  # ~4.4 GiB
+    piv23 = 16 * bench.top2_entries(12, 23)[0]  # the blocked pivot array, ~146 MiB
+    assert 128 << 20 < piv23 < 150 << 20
+    assert bench.footprint("plain", st) == 4 * gib + text + piv23  # ~4.4 GiB
     assert 4.3 * gib < bench.footprint("plain", st) < 4.5 * gib
-    assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * gib
-    assert bench.footprint("llcp", st) == 16 * gib + text + (16 << 21)
+    assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * bench.top2_entries(12, 30)[0]
+    assert bench.footprint("llcp", st) == 16 * gib + text + 16 * bench.top2_entries(12, 21)[0]
     assert bench.footprint("quad", st) == st["quad_bytes"] + text  # ~17 GiB
     assert bench.footprint("prefix", st) == 128 * gib + 32 + 16 * gib + text  # table + fused leaves + text
     assert bench.footprint("prefix_packed", st) == bench.footprint("prefix", st)

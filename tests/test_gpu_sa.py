@@ -1070,3 +1070,42 @@ def test_occurrence_ranges_inline_slots(sas):
             assert np.array_equal(lo, lo2) and np.array_equal(hi, hi2), (n, p, inl)
             for k in range(0, len(qs), 7):
                 assert (int(lo[k]), int(hi[k])) == O.prefix_range(tp, n, sa, qs[k]), (n, p, inl, k)
+
+
+def test_blocked_pivot_levels(sas):
+    """The pivot array's blocked layout (levels past the 12 LDS levels in blocks of up to 3
+    levels per 128-B line, cache part and HBM part grouped apart): every depth 13..25 on an
+    n = 3 x 2^23 text (25 iterations) gives PLAIN, LCP, LLCP and INLINE the positions and
+    probe counts of the oracle's binary_search (sas/sa_search.rs:98-112) -- groups of 1, 2
+    and 3 levels in both parts -- and sas_stats.top2_bytes is the layout's size."""
+    import bench
+    n = 3 << 23
+    t = sas.random_string(n, seed=123)
+    rng = np.random.default_rng(9)
+    nq, m = 20_000, 40
+    offs = rng.integers(0, n - m, nq)
+    qs = np.stack([t[o:o + m] for o in offs])
+    qs[: nq // 4] = rng.integers(0, 4, (nq // 4, m))
+    qb = qs.reshape(-1).copy()
+    ref = None
+    for L in (0, 13, 14, 15, 16, 21, 24, 25):
+        idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False,
+                                top2_levels=L)
+        st = idx.stats()
+        lv = st["top2_levels"]
+        assert lv == (23 if L == 0 else L)
+        assert st["top2_bytes"] == 16 * bench.top2_entries(12, lv)[0], L
+        if ref is None:
+            sa = idx.suffix_array()
+            tp = O.padded(t)
+            ref = np.array([O.search_one(tp, n, sa, q)[0] for q in qs[::50]], np.uint64)
+            ref_all, ref_pr = idx.search_fixed(qb, m, algo="plain", probes=True)
+            assert np.array_equal(ref_all[::50], ref)
+        for algo in ("plain", "lcp", "llcp", "inline"):
+            got, pr = idx.search_fixed(qb, m, algo=algo, probes=True)
+            assert np.array_equal(got, ref_all), (L, algo)
+            assert np.array_equal(pr, ref_pr), (L, algo)
+        idx.free()
+    # the layout itself: the cache part's short group first, the HBM part's last
+    assert bench.top2_entries(12, 23)[1] == [(12, 2), (14, 3), (17, 3), (20, 3)]
+    assert bench.top2_entries(12, 30)[1] == [(12, 2), (14, 3), (17, 3), (20, 3), (23, 3), (26, 3), (29, 1)]

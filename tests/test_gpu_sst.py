@@ -76,6 +76,14 @@ def test_differential(sas, size):
         assert np.array_equal(v, ref), (size, b)
         assert np.array_equal(vals[np.minimum(r, len(vals) - 1)], ref)
         assert pm.layers() >= 1 and pm.size() >= len(vals) * 4
+    # the other PartitionedSTree16 markers of sst/test.rs:222-246 (Simple, Compact, L1,
+    # Overlapping), each for b in {0, 4, 8, 16, 20}: values equal SortedVec's
+    for cls in (sas.PartitionedSTree16, sas.PartitionedSTree16C, sas.PartitionedSTree16L, sas.PartitionedSTree16O):
+        for b in (0, 4, 8, 16, 20):
+            idx = cls.new(vals, b)
+            assert np.array_equal(idx.query(qs), ref), (cls.__name__, size, b)
+            assert idx.layers() >= 1 and idx.size() >= len(vals) * 4
+            idx.free()
     # SST_DIRECT_MAP: same values and ranks as SortedVec, for the automatic and forced b
     for b in (0, 1, 5, 12, 24):
         dm = sas.DirectMap.new(vals, b)
@@ -114,6 +122,28 @@ def test_no_lds_and_device_path(sas):
     out = idx.query(dq)
     torch.cuda.synchronize()
     assert np.array_equal(out.cpu().numpy().view(np.uint32), ref)
+
+
+def test_partitioned_variants_edges(sas):
+    """The four partitioned markers on skewed keys (one part holding most keys, empty
+    parts, runs of equal keys across part boundaries), a single key, and queries at every
+    part boundary and above every key: values equal SortedVec's; no rank output."""
+    rng = np.random.default_rng(12)
+    skew = np.sort(np.concatenate([rng.integers(0, 1 << 12, 30_000), rng.integers(1 << 30, (1 << 30) + 5, 500),
+                                   np.full(3000, 1 << 25), [O.MAX]]).astype(np.uint32))
+    for vals in (skew, np.array([O.MAX], np.uint32), np.array([5, 5, 5, O.MAX], np.uint32)):
+        qs = np.concatenate([rng.integers(0, O.MAX, 4096, dtype=np.uint64).astype(np.uint32),
+                             vals[:: max(1, len(vals) // 512)], vals[:: max(1, len(vals) // 512)] + 1,
+                             np.array([0, 1, 1 << 25, (1 << 25) + 1, O.MAX - 1, O.MAX], np.uint32)])
+        ref = O.SortedVec(vals).query(qs)
+        for cls in (sas.PartitionedSTree16, sas.PartitionedSTree16C, sas.PartitionedSTree16L,
+                    sas.PartitionedSTree16O):
+            for b in (0, 4, 8, 16, 20):
+                idx = cls.new(vals, b)
+                assert np.array_equal(idx.query(qs), ref), (cls.__name__, len(vals), b)
+                with pytest.raises(sas.SasError):
+                    idx.query(qs[:4], want_rank=True)
+                idx.free()
 
 
 def test_build_assertions(sas):
