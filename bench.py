@@ -1578,7 +1578,7 @@ def main():
         vbase, vfl = algo_flags(v)
         bpl = bytes_per_lookup("prefix" if v == "prefix_packed" else vbase, stats, n, m, vmean,
                                range_flag=bool(vfl), packed=v == "prefix_packed")
-        key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector"}.get(v)
+        key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector", "llcp": "llcp"}.get(v)
         pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}" + (f"_t{stats['top2_levels']}" if key == "plain" else "")) \
             if key else None
         variants[v] = record(v, nq, vk, vel, bpl, footprint(v, stats), pmc, vmean,

@@ -10,7 +10,8 @@
  *   SaNaive::search / search_prefix       Search::search/_prefix      sas/util.rs:29-47
  *   sas::random_string / random_queries   util.rs:9-26 (ChaCha8Rng::seed_from_u64(31415), main.rs:38)
  *   sas::read_fasta_file                  util.rs:144-169
- *   sst::SortedVec / Eytzinger / STree16 / STree15 / PartitionedSTree16M / DirectMap
+ *   sst::SortedVec / Eytzinger / STree16 / STree15 / PartitionedSTree16M / DirectMap /
+ *   PartitionedSTree16 / 16C / 16L / 16O
  *                                         SearchIndex::new/size/layers + SearchScheme::query
  *                                         sst/lib.rs:30-57, s_tree.rs:72-176, eytzinger.rs, binary_search.rs
  *
@@ -358,6 +359,19 @@ struct PartitionedSTree16M : SearchIndex {  // sst/partitioned_s_tree.rs:98
     }
     using SearchIndex::SearchIndex;
 };
+/* PartitionedSTree<16,16,Tp>::new(vals, b) for Tp = Simple, Compact, L1, Overlapping
+   (sst/partitioned_s_tree.rs:86-94 type aliases; values only: the leaves are padded) */
+template <int LAYOUT>
+struct PartitionedSTree : SearchIndex {
+    static PartitionedSTree new_(const std::vector<uint32_t>& v, uint32_t b) {
+        return PartitionedSTree(make(v, LAYOUT, SST_PART_BITS(b)));
+    }
+    using SearchIndex::SearchIndex;
+};
+using PartitionedSTree16 = PartitionedSTree<SST_PARTITIONED>;
+using PartitionedSTree16C = PartitionedSTree<SST_PARTITIONED_COMPACT>;
+using PartitionedSTree16L = PartitionedSTree<SST_PARTITIONED_L1>;
+using PartitionedSTree16O = PartitionedSTree<SST_PARTITIONED_OVERLAP>;
 struct DirectMap : SearchIndex {  // the prefix map taken to its limit (sst.h SST_DIRECT_MAP)
     static DirectMap new_(const std::vector<uint32_t>& v) { return DirectMap(make(v, SST_DIRECT_MAP, 0)); }
     using SearchIndex::SearchIndex;

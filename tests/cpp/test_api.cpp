@@ -185,6 +185,13 @@ static void test_sst() {
             same(sst::STree16::new_params(vals, false, false, true), qs, expect, "STree16 full", n);
             same(sst::STree15::new_(vals), qs, expect, "STree15", n);
             if (n >= 4096) same(sst::PartitionedSTree16M::new_(vals, 8), qs, expect, "PartitionedSTree16M", n);
+            // sst/test.rs:222-246: the other partitioned markers
+            for (uint32_t b : {0u, 8u, 16u}) {
+                same(sst::PartitionedSTree16::new_(vals, b), qs, expect, "PartitionedSTree16", n);
+                same(sst::PartitionedSTree16C::new_(vals, b), qs, expect, "PartitionedSTree16C", n);
+                same(sst::PartitionedSTree16L::new_(vals, b), qs, expect, "PartitionedSTree16L", n);
+                same(sst::PartitionedSTree16O::new_(vals, b), qs, expect, "PartitionedSTree16O", n);
+            }
             same(sst::DirectMap::new_(vals), qs, expect, "DirectMap", n);
         }
     }

@@ -135,6 +135,7 @@ def test_partitioned_variants_edges(sas):
         qs = np.concatenate([rng.integers(0, O.MAX, 4096, dtype=np.uint64).astype(np.uint32),
                              vals[:: max(1, len(vals) // 512)], vals[:: max(1, len(vals) // 512)] + 1,
                              np.array([0, 1, 1 << 25, (1 << 25) + 1, O.MAX - 1, O.MAX], np.uint32)])
+        qs = np.minimum(qs, O.MAX)  # the trees compare signed: queries live in [0, i32::MAX] (sst/node.rs:5)
         ref = O.SortedVec(vals).query(qs)
         for cls in (sas.PartitionedSTree16, sas.PartitionedSTree16C, sas.PartitionedSTree16L,
                     sas.PartitionedSTree16O):

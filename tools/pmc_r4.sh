@@ -1,0 +1,38 @@
+#!/bin/bash
+# Round-4 PMC passes (GPU box): separate rocprofv3 --pmc runs (FETCH_SIZE; WRITE_SIZE;
+# TCC_EA0_RDREQ + 32B + hit/miss) over bench.py for each record whose traffic bench.py
+# reports, summarised into gpurun_out/pmc_r3/pmc_<key>.json stamped with the library's
+# source hash (copy them into profiles/ to have bench.py attach them).
+# usage: tools/pmc_r4.sh [keys...]   keys: prefix plain23 plain30 quad stree sector llcp c3 (bucket lines) c3tagged
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
+out=gpurun_out/pmc_r4
+mkdir -p "$out"
+keys=${*:-prefix plain23 plain30 quad stree sector llcp c3 c3tagged}
+base="--no-cpu --no-c3 --no-c4 --no-e2e --no-lcp-long --variants= --c1-deep-levels 0 --steps 3 --warmup 1 --detail="
+for k in $keys; do
+  case $k in
+    prefix)  args="$base --algo prefix"; kern=k_sa_prefix2; nq=10000000; name=prefix16d_n1073741824_q10000000_m32 ;;
+    plain23) args="$base --algo plain"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t23 ;;
+    plain30) args="$base --algo plain --top2-levels 30"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t30 ;;
+    quad)    args="$base --algo quad"; kern=k_sa_quad; nq=10000000; name=quad_n1073741824_q10000000_m32 ;;
+    stree)   args="$base --algo stree"; kern=k_sa_stree; nq=10000000; name=stree_n1073741824_q10000000_m32 ;;
+    sector)  args="$base --algo sector"; kern=k_sa_sector; nq=10000000; name=sector_n1073741824_q10000000_m32 ;;
+    llcp)    args="$base --algo llcp"; kern=k_sa_binary; nq=10000000; name=llcp_n1073741824_q10000000_m32 ;;
+    c3)      args="--workload c3 --c3-steps 2 --warmup 1 --c3-no-cross --detail="; kern=k_sa_tagged_lines; nq=100000000; name=c3_tagged_lines_n17179869184_q100000000 ;;
+    c3tagged) args="--workload c3 --c3-steps 2 --warmup 1 --c3-no-cross --c3-layout tagged --detail="; kern=k_sa_tagged; nq=100000000; name=c3_tagged_n17179869184_q100000000 ;;
+    *) echo "unknown key $k"; exit 2 ;;
+  esac
+  d=$out/$k
+  mkdir -p "$d"
+  echo "[pmc_r4] $k: $args"
+  timeout -s KILL 420 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$d/fetch" -o run -- python3 bench.py $args > "$d/fetch.log" 2>&1 || exit $?
+  timeout -s KILL 420 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$d/write" -o run -- python3 bench.py $args > "$d/write.log" 2>&1 || exit $?
+  timeout -s KILL 420 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_HIT_sum TCC_MISS_sum --output-format csv -d "$d/req" -o run -- python3 bench.py $args > "$d/req.log" 2>&1 || exit $?
+  f=$(ls "$d"/fetch/*counter_collection.csv | head -1)
+  w=$(ls "$d"/write/*counter_collection.csv | head -1)
+  r=$(ls "$d"/req/*counter_collection.csv | head -1)
+  python3 tools/pmc_to_json.py --kernel "$kern" --nq $nq --fetch "$f" --write "$w" --req "$r" --out "$out/pmc_$name.json" || exit $?
+  rm -rf "$d/fetch" "$d/write" "$d/req"  # the per-dispatch CSVs: too big to bring back
+done
+exit 0
