@@ -126,7 +126,7 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             if algo == "inline":
                 t2 = min(t2, TOP2_CACHE_LEVELS)  # launch_search caps INLINE's pivot levels
             elif algo == "llcp":
-                t2 = min(t2, 21)  # and LLCP's (SAS_LLCP_TOP2_LEVELS)
+                t2 = min(t2, 23)  # and LLCP's (SAS_LLCP_TOP2_LEVELS)
             tc = min(t2, TOP2_CACHE_LEVELS)  # the array's first 2^23 entries (128 MiB) stay in cache
             lds += min(probes, t1) * 12
             cache += max(0.0, min(probes, tc) - t1) * 16
@@ -136,7 +136,7 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             # block entered (up to 3 levels a line, common.hpp top2_layout) in the cache part
             # and in the HBM part; two per SA probe (the SA word, then the text window: PLAIN
             # / LCP) or one (a 16-B entry); the query stream
-            pc, ph = pivot_requests(t1, t2, probes)
+            pc, ph = pivot_requests(t1, t2, probes, blocked=algo in ("plain", "inline"))
             reqs = {"cache": pc, "hbm": ph + max(0.0, probes - t2) * (2 if per != 16 else 1)
                     + (8.0 if packed else m) / 128}
         else:
@@ -273,17 +273,22 @@ def top2_entries(D: int, L: int, C: int = TOP2_CACHE_LEVELS, G: int = 3):
     return e, groups
 
 
-def pivot_requests(D: int, L: int, probes: float):
-    """(cache, hbm) fabric requests of the pivot levels a lookup of `probes` probes reads: one
-    per block it enters (the block's further levels hit L2)."""
+def pivot_requests(D: int, L: int, probes: float, blocked: bool = True):
+    """(cache, hbm) requests of the pivot levels a lookup of `probes` probes reads.  PLAIN
+    (`blocked`) reads a block's 16-char keys with loads issued together: one request per block
+    it enters; LCP / LLCP / INLINE need every pivot's whole key and SA value (exact lcps), one
+    request per level."""
     _, groups = top2_entries(D, L)
     cache = hbm = 0.0
     for d0, h in groups:
-        if probes > d0:
-            if d0 < TOP2_CACHE_LEVELS:
-                cache += 1
-            else:
-                hbm += 1
+        lv = max(0.0, min(float(h), probes - d0))
+        if lv <= 0:
+            continue
+        c = 1.0 if blocked else lv
+        if d0 < TOP2_CACHE_LEVELS:
+            cache += c
+        else:
+            hbm += c
     return cache, hbm
 
 
@@ -320,7 +325,7 @@ def footprint(algo: str, st: dict) -> int:
     if base in ("plain", "lcp"):
         b = sa + text + piv(31)
     elif base == "llcp":
-        b = st["llcp_bytes"] + text + piv(21)  # SAS_LLCP_TOP2_LEVELS
+        b = st["llcp_bytes"] + text + piv(23)  # SAS_LLCP_TOP2_LEVELS
     elif base == "inline":
         b = _quad_leaf_bytes(st) + text + piv(TOP2_CACHE_LEVELS)  # SAS_INLINE_TOP2_LEVELS
     elif base == "quad":

@@ -42,8 +42,7 @@
 // cut into groups of at most SAS_TOP2_GROUP consecutive levels.  A group rooted at level d0
 // holds, for each of its 2^d0 root nodes, that root's h-level subtree as one block of 2^h
 // 16-B slots in local Eytzinger order (slot 0 unused; h = 3: 128 B, one line), or one slot
-// per node for h = 1.  A lookup's h probes in a group read one line: the first is a fabric
-// request, the next h - 1 hit L2.  Groups end at SAS_TOP2_CACHE_LEVELS, so no block mixes
+// per node for h = 1.  A lookup's h probes in a group read one line.  Groups end at SAS_TOP2_CACHE_LEVELS, so no block mixes
 // the cache-resident levels with the HBM ones; in the cache part the first group is the
 // short one (its blocks are the fewest), in the HBM part the last.
 #define SAS_TOP2_GROUP 3
@@ -52,12 +51,28 @@ struct Top2Layout {
     uint8_t t[SAS_TOP2_MAX_LEVELS];      // level - the group's root level
     uint8_t lg[SAS_TOP2_MAX_LEVELS];     // log2 slots per block (0: one slot per node)
 };
-// entry index of Eytzinger node k of level d (d >= SAS_TOP_LEVELS; below: k itself)
-__host__ __device__ __forceinline__ uint64_t top2_slot(const Top2Layout& y, uint32_t d, uint32_t k) {
+// Inside a block of S = 2^lg slots (lg >= 2) the slots' keys come first, split into their
+// high halves (chars 0..15, u32 x S) and low halves (chars 16..31, u32 x S), then their SA
+// values (u64 x S); a 1-slot block is {key u64, SA u64}.  One lane reads a 3-level block's
+// seven 16-char keys with two 16-B loads of one line issued together (one request), and
+// the rest of a key or an SA value only when it needs them (k_sa_binary, PLAIN).
+// the first byte of Eytzinger node k's block at level d (d >= SAS_TOP_LEVELS)
+__host__ __device__ __forceinline__ uint64_t top2_block_byte(const Top2Layout& y, uint32_t d, uint32_t k) {
     const uint32_t t = y.t[d], lg = y.lg[d];
     const uint64_t blk = (uint64_t)(k >> t) - (1ull << (d - t));
-    const uint32_t j = lg ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
-    return y.base[d] + (blk << lg) + j;
+    return 16 * (y.base[d] + (blk << lg));
+}
+// node k's slot in its block
+__host__ __device__ __forceinline__ uint32_t top2_j(const Top2Layout& y, uint32_t d, uint32_t k) {
+    const uint32_t t = y.t[d];
+    return y.lg[d] ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
+}
+// byte offsets in the block of slot j's key halves and SA value
+struct Top2Slot { uint32_t hi, lo, sa; };
+__host__ __device__ __forceinline__ Top2Slot top2_slot_at(uint32_t lg, uint32_t j) {
+    if (!lg) return Top2Slot{4, 0, 8};  // {key u64 (low word first), SA}
+    const uint32_t S = 1u << lg;
+    return Top2Slot{4 * j, 4 * S + 4 * j, 8 * S + 8 * j};
 }
 // fill the layout for L levels above D LDS levels; returns the array's entries
 static inline uint64_t top2_layout(uint32_t D, uint32_t L, Top2Layout* y) {

@@ -863,8 +863,15 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
             p = sa[(l + r) >> 1];
             key = text_chars32(tw, p);
         }
-        const uint64_t at = depth < (int)D ? k : top2_slot(lay, (uint32_t)depth, (uint32_t)k);
-        top2[at] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
+        if (depth < (int)D) {
+            top2[k] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
+        } else {
+            uint8_t* b = reinterpret_cast<uint8_t*>(top2) + top2_block_byte(lay, (uint32_t)depth, (uint32_t)k);
+            const Top2Slot o = top2_slot_at(lay.lg[depth], top2_j(lay, (uint32_t)depth, (uint32_t)k));
+            *reinterpret_cast<uint32_t*>(b + o.hi) = (uint32_t)(key >> 32);
+            *reinterpret_cast<uint32_t*>(b + o.lo) = (uint32_t)key;
+            *reinterpret_cast<uint64_t*>(b + o.sa) = p;
+        }
     }
 }
 

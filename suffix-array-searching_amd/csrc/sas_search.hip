@@ -197,34 +197,104 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         QueryRegs<QW> q;
         q.load(qb, m, &bad);
 
-        uint64_t l = 0, r = a.sa_n;
+        // ranks fit 32 bits beside a u32 SA (sa_n < 2^32): fewer registers for l, r, mid
+        using rank_t = sa_val_t<W>;
+        rank_t l = 0, r = (rank_t)a.sa_n;
         uint32_t k = 1, probes = 0, llcp = 0, rlcp = 0;
-        sa_val_t<W> pr = 0;  // SA[r] once r has moved
-        bool rmoved = false;
+        sa_val_t<W> pr = 0;  // SA[r] while prv
+        bool prv = false;
         if (RANGE) {
-            prefix_range(a, q.w[0] >> (64 - 2 * a.prefix_chars), &l, &r);
+            uint64_t l64, r64;
+            prefix_range(a, q.w[0] >> (64 - 2 * a.prefix_chars), &l64, &r64);
+            l = (rank_t)l64;
+            r = (rank_t)r64;
             probes = 1;  // the reference's cnt counts the table read (:87-89)
         }
-        for (uint32_t it = 0; it < a.iters; ++it) {
+        // one probe's outcome: the reference's l / r update (sas/sa_search.rs:102-110); pk:
+        // p is known (PLAIN's blocked pivot levels may decide from the key alone)
+        auto take = [&](rank_t mid, bool lt, uint32_t lcp, sa_val_t<W> p, bool pk) {
+            probes++;
+            if (lt) {
+                l = mid + 1;
+                llcp = lcp;
+            } else {
+                r = mid;
+                rlcp = lcp;
+                pr = p;
+                prv = pk;
+            }
+        };
+        uint32_t it = 0;
+        if (TOP) {
+            for (; it < D; ++it) {  // the LDS levels
+                if (l < r) {
+                    const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
+                    const uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
+                    uint32_t lcp;
+                    const sa_val_t<W> p = s_sa[k];
+                    const bool lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
+                    k = 2 * k + (lt ? 1u : 0u);
+                    take(mid, lt, lcp, p, true);
+                }
+            }
+            // the pivot array (cache-resident; deeper, HBM) instead of an SA word and a text
+            // window, block by block: a group's levels share one line (common.hpp top2_layout)
+            const uint8_t* t2 = reinterpret_cast<const uint8_t*>(a.top2);
+            while (it < a.top2_levels) {
+                const uint32_t lg = a.top2_lay.lg[it];
+                const uint32_t levels = lg ? lg : 1u;
+                const uint8_t* blk = t2 + top2_block_byte(a.top2_lay, it, k);  // k: the group's root node
+                uint4 kh0 = make_uint4(0, 0, 0, 0), kh1 = kh0;
+                if (MODE == BS_PLAIN && lg >= 2 && l < r) {
+                    // PLAIN (no lcps to keep exact): the high halves of all of the block's
+                    // keys at once -- two (one) 16-B loads of one line, one request
+                    kh0 = *reinterpret_cast<const uint4*>(blk);
+                    if (lg == 3) kh1 = *reinterpret_cast<const uint4*>(blk + 16);
+                }
+                for (uint32_t t = 0; t < levels && it < a.top2_levels; ++t, ++it) {
+                    if (!(l < r)) continue;
+                    const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
+                    const uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
+                    const uint32_t j = lg ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
+                    const Top2Slot o = top2_slot_at(lg, j);
+                    sa_val_t<W> p = 0;
+                    uint32_t lcp = 0;
+                    bool lt = false, pk = true, done = false;
+                    if (MODE == BS_PLAIN && lg >= 2) {
+                        // decide from the key's first 16 chars when they differ from q's first
+                        // min(m, 16); a difference only past the suffix's end (zero padding)
+                        // makes it a proper prefix of q: key < q there, as slice order has it.
+                        // Else the rest of the key and the SA value (one more request)
+                        const uint4 v = (j >> 2) ? kh1 : kh0;
+                        const uint32_t khi = (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
+                        const uint32_t c = q.m < 16 ? q.m : 16;
+                        const uint32_t mk = c ? ~0u << (32 - 2 * c) : 0u;
+                        const uint32_t av = khi & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
+                        if (av != bv) {
+                            lt = av < bv;
+                            pk = false;
+                            done = true;
+                        }
+                    }
+                    if (!done) {  // the whole key and the SA value (one line)
+                        const uint64_t key = ((uint64_t)*reinterpret_cast<const uint32_t*>(blk + o.hi) << 32) |
+                                             *reinterpret_cast<const uint32_t*>(blk + o.lo);
+                        p = (sa_val_t<W>)*reinterpret_cast<const uint64_t*>(blk + o.sa);
+                        lt = suffix_less_key<QW>(a.tw, n, p, key, q, h, &lcp);
+                    }
+                    k = 2 * k + (lt ? 1u : 0u);
+                    take(mid, lt, lcp, p, pk);
+                }
+            }
+        }
+        for (; it < a.iters; ++it) {
             if (l < r) {
-                uint64_t mid = (l + r) >> 1;
-                uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
+                const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
+                const uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
                 sa_val_t<W> p;
                 uint32_t lcp;
                 bool lt;
-                if (TOP && it < D) {
-                    p = s_sa[k];
-                    lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
-                    k = 2 * k + (lt ? 1u : 0u);
-                } else if (TOP && it < a.top2_levels) {
-                    // the next levels' pivots from the cache-resident (or, deeper, HBM) pivot
-                    // array: one 16-B read instead of an SA word and a text window, and the
-                    // levels of one block share its line (one fabric request per block)
-                    const uint4 e = a.top2[top2_slot(a.top2_lay, it, k)];
-                    p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
-                    lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
-                    k = 2 * k + (lt ? 1u : 0u);
-                } else if (MODE == BS_LLCP) {
+                if (MODE == BS_LLCP) {
                     // one 16-B read: SA[mid], the lcps of the pivot with the interval's
                     // bounds L = SA[l-1] (< q) and R = SA[r] (>= q), and 16 pivot chars
                     // after each.  Manber-Myers: with llcp >= rlcp, Llcp > llcp puts the
@@ -252,19 +322,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     p = (sa_val_t<W>)sa[mid];
                     lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
                 }
-                probes++;
-                if (lt) {
-                    l = mid + 1;
-                    llcp = lcp;
-                } else {
-                    r = mid;
-                    rlcp = lcp;
-                    pr = p;
-                    rmoved = true;
-                }
+                take(mid, lt, lcp, p, true);
             }
         }
-        if (RANGE && !rmoved && r < a.sa_n) pr = (sa_val_t<W>)sa[r];
+        // SA[r] not seen yet: r never moved (RANGE: the table's range end) or moved last on a
+        // pivot decided from its key alone (rare below a 23-level array: a right move on
+        // every one of the last levels' SA probes would have to be missing)
+        if (!prv && r < a.sa_n) pr = (sa_val_t<W>)sa[r];
         a.out_pos[i] = (r >= a.sa_n) ? a.next_pos : (uint64_t)pr;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1158,18 +1222,65 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
         const uint64_t K64 = q.w[0];
         uint64_t l = 0, r = a.sa_n, pr = QUAD_NO_SA;
         uint32_t k = 1, probes = 0;
-        for (uint32_t it = 0; it < a.iters; ++it) {
+        auto take = [&](uint64_t mid, bool ge, uint64_t p) {
+            probes++;
+            if (ge) {
+                r = mid;
+                pr = p;
+            } else {
+                l = mid + 1;
+            }
+        };
+        uint32_t it = 0;
+        if (TOP) {
+            for (; it < D; ++it) {  // the LDS levels
+                if (l < r) {
+                    const uint64_t mid = (l + r) >> 1;
+                    const bool ge = sector_ge<QW>(s_key[k], s_sa[k], K64, a, q);
+                    k = 2 * k + (ge ? 0u : 1u);
+                    take(mid, ge, s_sa[k >> 1]);
+                }
+            }
+            // the pivot array block by block, as PLAIN: a block's 16-char key halves in one
+            // request; the rest of a key and its SA value only on a tie of the first 16 chars
+            // (key != K64 decides key > K64, the sector predicate)
+            const uint8_t* t2 = reinterpret_cast<const uint8_t*>(a.top2);
+            while (it < a.top2_levels) {
+                const uint32_t lg = a.top2_lay.lg[it];
+                const uint32_t levels = lg ? lg : 1u;
+                const uint8_t* blk = t2 + top2_block_byte(a.top2_lay, it, k);
+                uint4 kh0 = make_uint4(0, 0, 0, 0), kh1 = kh0;
+                if (lg >= 2 && l < r) {
+                    kh0 = *reinterpret_cast<const uint4*>(blk);
+                    if (lg == 3) kh1 = *reinterpret_cast<const uint4*>(blk + 16);
+                }
+                for (uint32_t t = 0; t < levels && it < a.top2_levels; ++t, ++it) {
+                    if (!(l < r)) continue;
+                    const uint64_t mid = (l + r) >> 1;
+                    const uint32_t j = lg ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
+                    const Top2Slot o = top2_slot_at(lg, j);
+                    bool ge;
+                    uint64_t p = QUAD_NO_SA;
+                    const uint4 v = (j >> 2) ? kh1 : kh0;
+                    const uint32_t khi = (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
+                    if (lg >= 2 && khi != (uint32_t)(K64 >> 32)) {
+                        ge = khi > (uint32_t)(K64 >> 32);
+                    } else {
+                        const uint64_t key = ((uint64_t)*reinterpret_cast<const uint32_t*>(blk + o.hi) << 32) |
+                                             *reinterpret_cast<const uint32_t*>(blk + o.lo);
+                        p = *reinterpret_cast<const uint64_t*>(blk + o.sa);
+                        ge = sector_ge<QW>(key, p, K64, a, q);
+                    }
+                    k = 2 * k + (ge ? 0u : 1u);
+                    take(mid, ge, p);
+                }
+            }
+        }
+        for (; it < a.iters; ++it) {
             if (l < r) {
                 const uint64_t mid = (l + r) >> 1;
                 uint64_t key, p;
-                if (TOP && it < D) {
-                    key = s_key[k];
-                    p = s_sa[k];
-                } else if (TOP && it < a.top2_levels) {
-                    const uint4 e = a.top2[top2_slot(a.top2_lay, it, k)];
-                    key = (uint64_t)e.x | ((uint64_t)e.y << 32);
-                    p = (uint64_t)e.z | ((uint64_t)e.w << 32);
-                } else if (KO) {
+                if (KO) {
                     key = quad_entry_key<true>(a, mid);
                     p = key == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
                 } else {
@@ -1177,19 +1288,12 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                     key = (uint64_t)e.x | ((uint64_t)e.y << 32);
                     p = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
                 }
-                const bool ge = sector_ge<QW>(key, p, K64, a, q);
-                if (TOP && it < a.top2_levels) k = 2 * k + (ge ? 0u : 1u);
-                probes++;
-                if (ge) {
-                    r = mid;
-                    pr = p;
-                } else {
-                    l = mid + 1;
-                }
+                take(mid, sector_ge<QW>(key, p, K64, a, q), p);
             }
         }
+        // SA[r] not seen yet (a compact leaf's key, or a pivot decided by its first 16 chars)
         if (r >= a.sa_n) pr = a.next_pos;
-        else if (KO && pr == QUAD_NO_SA) pr = quad_entry_sa<true, W>(a, r);
+        else if (pr == QUAD_NO_SA) pr = KO ? quad_entry_sa<true, W>(a, r) : quad_entry_sa<false, W>(a, r);
         a.out_pos[i] = pr;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1671,7 +1775,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 // pairs, suffix_less_from_x2), and its position straight from the entry.  Larger buckets
 // continue with a binary search over the rest.
 #ifndef SAS_LLCP_TOP2_LEVELS
-#define SAS_LLCP_TOP2_LEVELS 21
+#define SAS_LLCP_TOP2_LEVELS 23
 #endif
 #ifndef SAS_INLINE_TOP2_LEVELS
 #define SAS_INLINE_TOP2_LEVELS 23
@@ -2453,9 +2557,9 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     // LLCP reads one 16-B entry per probe either way, and its own entries carry the interval
-    // lcps that spare text reads: pivot-array levels past SAS_LLCP_TOP2_LEVELS cost it time
-    // (3.08 ms with 21 levels, 3.29 ms with 23; PLAIN and LCP gain from 23, two requests per
-    // probe there)
+    // lcps that spare text reads: pivot-array levels past the cache-resident ones cost it
+    // time (round 3, unblocked array: 3.08 ms with 21 levels, 3.29 with 23; round 4, blocked:
+    // 2.80 with 23 against 2.93 with 21, profiles/r4/ab_pivots/)
     if (algo == SAS_ALGO_LLCP && a.top2_levels > SAS_LLCP_TOP2_LEVELS) a.top2_levels = SAS_LLCP_TOP2_LEVELS;
     // INLINE's own probes read one 16-B fused entry in rank order, whose last levels share
     // lines; the pivot array past its cache-resident levels only moves them apart

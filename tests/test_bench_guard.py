@@ -91,7 +91,7 @@ def test_byte_model_hbm_pivot_levels():
     # INLINE stays on the cache-resident 23 levels whatever the array holds (launch_search)
     pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
     assert pin["hbm"] == 8 * 16 + m + 8 and pin["requests_model"]["hbm"] == 8 + m / 128
-    assert pin["requests_model"]["cache"] == 4.0
+    assert pin["requests_model"]["cache"] == 4.0  # INLINE reads a block's 16-char keys at once, as PLAIN
     # the split: model HBM requests first, the rest of the PMC count is cache-served
     bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
     assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
@@ -161,7 +161,7 @@ def test_footprint_per_algorithm():
     assert bench.footprint("plain", st) == 4 * gib + text + piv23  # ~4.4 GiB
     assert 4.3 * gib < bench.footprint("plain", st) < 4.5 * gib
     assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * bench.top2_entries(12, 30)[0]
-    assert bench.footprint("llcp", st) == 16 * gib + text + 16 * bench.top2_entries(12, 21)[0]
+    assert bench.footprint("llcp", st) == 16 * gib + text + 16 * bench.top2_entries(12, 23)[0]
     assert bench.footprint("quad", st) == st["quad_bytes"] + text  # ~17 GiB
     assert bench.footprint("prefix", st) == 128 * gib + 32 + 16 * gib + text  # table + fused leaves + text
     assert bench.footprint("prefix_packed", st) == bench.footprint("prefix", st)

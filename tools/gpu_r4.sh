@@ -4,7 +4,7 @@
 #   suite  pytest -m gpu          smoke  __graft_entry__.smoke()
 #   bench  the default bench line quick  the c1/c2 lineup only (no c0/c3/c4/CPU/e2e/lcp_long)
 #   lcp    the lcp_long record (c1 lineup + lcp_long)
-#   kt     the default bench under rocprofv3 --kernel-trace --stats
+#   kt     the bench under rocprofv3 --kernel-trace --stats, by grid (tools/prof_r4.sh)
 set -o pipefail
 out=gpurun_out/$1
 shift
@@ -20,9 +20,7 @@ for s in "$@"; do
                    --detail "$out/quick_detail.json" > "$out/quick.json" 2> "$out/quick.err" || exit $? ;;
         lcp) timeout -k 10 300 python -u bench.py --no-c3 --no-c4 --no-cpu --no-e2e \
                    --detail "$out/lcp_detail.json" > "$out/lcp.json" 2> "$out/lcp.err" || exit $? ;;
-        kt) (cd /tmp && export TMPDIR=/tmp; true) && timeout -k 10 900 rocprofv3 --kernel-trace --stats \
-                   -d "$out/kt" -o kt -- python3 bench.py --detail "$out/kt_detail.json" > "$out/kt_bench.json" \
-                   2> "$out/kt_bench.err" || exit $? ;;
+        kt) bash tools/prof_r4.sh "$out/prof" > "$out/prof.log" 2>&1 || exit $? ;;
         *) echo "unknown step $s" >&2; exit 2 ;;
     esac
 done

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-4 PMC passes (GPU box): separate rocprofv3 --pmc runs (FETCH_SIZE; WRITE_SIZE;
 # TCC_EA0_RDREQ + 32B + hit/miss) over bench.py for each record whose traffic bench.py
-# reports, summarised into gpurun_out/pmc_r3/pmc_<key>.json stamped with the library's
+# reports, summarised into gpurun_out/pmc_r4/pmc_<key>.json stamped with the library's
 # source hash (copy them into profiles/ to have bench.py attach them).
 # usage: tools/pmc_r4.sh [keys...]   keys: prefix plain23 plain30 quad stree sector llcp c3 (bucket lines) c3tagged
 set -o pipefail
