@@ -55,7 +55,8 @@ SEED = 31415  # sas/main.rs:38
 # binary-search levels served from LDS / the pivot array (the index's stats win): the library
 # default builds the 23 cache-resident levels (SAS_TOP2_CACHE_LEVELS, 128 MiB); deeper levels
 # (SAS_BUILD_TOP2_LEVELS, e.g. 30 = 16 GiB) are HBM reads
-TOP_LDS_LEVELS, TOP2_LEVELS = 12, 23
+TOP_LDS_LEVELS, TOP2_LEVELS = 14, 23
+TOP_FULL_LDS_LEVELS = 12  # LCP / LLCP: whole keys + SA values in LDS (common.hpp SAS_TOP_FULL_LEVELS)
 TOP2_CACHE_LEVELS = 23
 C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: pivots of levels 24-30 from HBM
 
@@ -127,16 +128,23 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
                 t2 = min(t2, TOP2_CACHE_LEVELS)  # launch_search caps INLINE's pivot levels
             elif algo == "llcp":
                 t2 = min(t2, 23)  # and LLCP's (SAS_LLCP_TOP2_LEVELS)
-            tc = min(t2, TOP2_CACHE_LEVELS)  # the array's first 2^23 entries (128 MiB) stay in cache
-            lds += min(probes, t1) * 12
-            cache += max(0.0, min(probes, tc) - t1) * 16
+            tc = min(t2, TOP2_CACHE_LEVELS)  # the array's first 23 levels stay in cache
+            # LDS: PLAIN / INLINE stage the plain levels' 16-char keys (4 B), LCP / LLCP the
+            # first TOP_FULL_LDS_LEVELS' whole keys and SA values (12 B) and read the rest of
+            # the plain levels from the array (common.hpp SAS_TOP_LEVELS)
+            k16 = algo in ("plain", "inline")
+            tl = t1 if k16 else min(t1, TOP_FULL_LDS_LEVELS)
+            lds += min(probes, tl) * (4 if k16 else 12)
+            cache += max(0.0, min(probes, tc) - tl) * 16
             hbm += max(0.0, min(probes, t2) - tc) * 16  # deeper pivot levels: one 16-B HBM entry each
             hbm += max(0.0, probes - t2) * per
             # random 128-B-line requests per lookup by where they are served: one per pivot
             # block entered (up to 3 levels a line, common.hpp top2_layout) in the cache part
-            # and in the HBM part; two per SA probe (the SA word, then the text window: PLAIN
-            # / LCP) or one (a 16-B entry); the query stream
-            pc, ph = pivot_requests(t1, t2, probes, blocked=algo in ("plain", "inline"))
+            # and in the HBM part (LCP / LLCP: one per level, and one per plain level past
+            # their LDS ones); two per SA probe (the SA word, then the text window: PLAIN /
+            # LCP) or one (a 16-B entry); the query stream
+            pc, ph = pivot_requests(t1, t2, probes, blocked=k16)
+            pc += max(0.0, min(probes, t1) - tl)
             reqs = {"cache": pc, "hbm": ph + max(0.0, probes - t2) * (2 if per != 16 else 1)
                     + (8.0 if packed else m) / 128}
         else:

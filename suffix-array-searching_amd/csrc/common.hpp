@@ -24,8 +24,15 @@
 #include "../../include/sst.h"
 
 #define SAS_TEXT_PAD_WORDS 4
-#define SAS_TOP_LEVELS 12             // 4095 pivots: 32 KiB keys + 16 KiB SA in LDS
+// The pivot array's first SAS_TOP_LEVELS levels are plain Eytzinger entries, staged in LDS:
+// PLAIN and INLINE stage their 16-char keys (4 B each: 16383 pivots, 64 KiB a workgroup)
+// and read a whole entry only on a 16-char tie; LCP and LLCP, which keep exact lcps, stage
+// SAS_TOP_FULL_LEVELS levels of whole keys and SA values (4095 pivots, 48 KiB) and read the
+// next levels' entries from the array.
+#define SAS_TOP_LEVELS 14
 #define SAS_TOP_NODES (1u << SAS_TOP_LEVELS)
+#define SAS_TOP_FULL_LEVELS 12
+#define SAS_TOP_FULL_NODES (1u << SAS_TOP_FULL_LEVELS)
 // Levels 13.. of the lockstep binary search (PLAIN, LCP, INLINE) read their pivot
 // (32-char key, SA value) from one 16-B entry of the top2 array instead of an SA word and a
 // text window.  Same-box: PLAIN 7.15 ms without it, 5.4-5.7 with 17 levels, 5.0-5.2 with

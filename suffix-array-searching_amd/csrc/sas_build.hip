@@ -1698,6 +1698,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         const uint32_t want = req ? req : SAS_TOP2_CACHE_LEVELS;
         const uint32_t lv = iters < want ? iters : want;
         x->top2_levels = lv;
+        // the plain (LDS-staged) levels are part of the array: never more than it holds
+        if (x->top_levels > lv) x->top_levels = lv;
         const uint32_t nodes = 1u << x->top2_levels;
         x->top2_entries = top2_layout(x->top_levels, x->top2_levels, &x->top2_lay);
         DevBuf t2;

@@ -172,17 +172,26 @@ __device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, ui
 #define BS_LLCP 2
 template <int QW, int MODE, bool TOP, int W, bool RANGE = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
-    __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
-    __shared__ sa_val_t<W> s_sa[TOP ? SAS_TOP_NODES : 1];
+    // PLAIN: the 16-char keys of the top SAS_TOP_LEVELS levels; LCP / LLCP: whole keys and
+    // SA values of the top SAS_TOP_FULL_LEVELS (common.hpp)
+    constexpr bool K16 = MODE == BS_PLAIN;
+    __shared__ uint32_t s_k16[TOP && K16 ? SAS_TOP_NODES : 1];
+    __shared__ uint64_t s_key[TOP && !K16 ? SAS_TOP_FULL_NODES : 1];
+    __shared__ sa_val_t<W> s_sa[TOP && !K16 ? SAS_TOP_FULL_NODES : 1];
     const SaView<W> sa{a.sa};
-    uint32_t D = 0;
+    uint32_t D = 0, DL = 0;  // plain levels of the pivot array; those staged in LDS
     if (TOP) {
         D = a.top_levels;
-        uint32_t nodes = 1u << D;
+        DL = K16 ? D : (D < SAS_TOP_FULL_LEVELS ? D : SAS_TOP_FULL_LEVELS);
+        const uint32_t nodes = 1u << DL;
         for (uint32_t k = threadIdx.x; k < nodes; k += blockDim.x) {
             const uint4 e = a.top2[k];
-            s_key[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
-            s_sa[k] = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
+            if (K16) {
+                s_k16[k] = e.y;
+            } else {
+                s_key[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                s_sa[k] = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
+            }
         }
         __syncthreads();
     }
@@ -226,15 +235,38 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         };
         uint32_t it = 0;
         if (TOP) {
-            for (; it < D; ++it) {  // the LDS levels
+            // the plain levels: from LDS (PLAIN: decided by the 16-char key unless it ties with
+            // q's first min(m, 16) chars, as on the blocked levels below), then -- LCP / LLCP
+            // past their SAS_TOP_FULL_LEVELS -- one whole entry each from the array
+            for (; it < D; ++it) {
                 if (l < r) {
                     const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
                     const uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
-                    uint32_t lcp;
-                    const sa_val_t<W> p = s_sa[k];
-                    const bool lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
+                    uint32_t lcp = 0;
+                    sa_val_t<W> p = 0;
+                    bool lt, pk = true;
+                    if (K16) {
+                        const uint32_t c = q.m < 16 ? q.m : 16;
+                        const uint32_t mk = c ? ~0u << (32 - 2 * c) : 0u;
+                        const uint32_t av = s_k16[k] & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
+                        if (av != bv) {
+                            lt = av < bv;
+                            pk = false;
+                        } else {
+                            const uint4 e = a.top2[k];
+                            p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
+                            lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
+                        }
+                    } else if (it < DL) {
+                        p = s_sa[k];
+                        lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
+                    } else {
+                        const uint4 e = a.top2[k];
+                        p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
+                        lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
+                    }
                     k = 2 * k + (lt ? 1u : 0u);
-                    take(mid, lt, lcp, p, true);
+                    take(mid, lt, lcp, p, pk);
                 }
             }
             // the pivot array (cache-resident; deeper, HBM) instead of an SA word and a text
@@ -1199,16 +1231,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a,
 // word + two text words.
 template <int QW, bool TOP, bool KO, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
-    __shared__ uint64_t s_key[TOP ? SAS_TOP_NODES : 1];
-    __shared__ uint64_t s_sa[TOP ? SAS_TOP_NODES : 1];
+    __shared__ uint32_t s_k16[TOP ? SAS_TOP_NODES : 1];  // the top levels' 16-char keys
     uint32_t D = 0;
     if (TOP) {
         D = a.top_levels;
-        for (uint32_t k = threadIdx.x; k < (1u << D); k += blockDim.x) {
-            const uint4 e = a.top2[k];
-            s_key[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
-            s_sa[k] = (uint64_t)e.z | ((uint64_t)e.w << 32);
-        }
+        for (uint32_t k = threadIdx.x; k < (1u << D); k += blockDim.x) s_k16[k] = a.top2[k].y;
         __syncthreads();
     }
     uint32_t bad = 0;
@@ -1233,12 +1260,20 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
         };
         uint32_t it = 0;
         if (TOP) {
-            for (; it < D; ++it) {  // the LDS levels
+            for (; it < D; ++it) {  // the LDS levels: the 16-char key, a whole entry on a tie
                 if (l < r) {
                     const uint64_t mid = (l + r) >> 1;
-                    const bool ge = sector_ge<QW>(s_key[k], s_sa[k], K64, a, q);
+                    bool ge;
+                    uint64_t p = QUAD_NO_SA;
+                    if (s_k16[k] != (uint32_t)(K64 >> 32)) {
+                        ge = s_k16[k] > (uint32_t)(K64 >> 32);
+                    } else {
+                        const uint4 e = a.top2[k];
+                        p = (uint64_t)e.z | ((uint64_t)e.w << 32);
+                        ge = sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), p, K64, a, q);
+                    }
                     k = 2 * k + (ge ? 0u : 1u);
-                    take(mid, ge, s_sa[k >> 1]);
+                    take(mid, ge, p);
                 }
             }
             // the pivot array block by block, as PLAIN: a block's 16-char key halves in one

@@ -60,15 +60,19 @@ def test_lower_bound_proof_accepts_and_rejects():
 def test_byte_model_splits_served_levels():
     st = {"sa_width": 4, "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "quad_entry_bytes": 16,
           "stree_layers": 8, "stree_lds_layers": 2, "sector_layers": 12, "sector_lds_layers": 3, "quad_layers": 8,
-          "quad_lds_layers": 3, "quad_fan": 17, "tag_chars": 16, "top_levels": 12, "top2_levels": 21}
+          "quad_lds_layers": 3, "quad_fan": 17, "tag_chars": 16, "top_levels": 14, "top2_levels": 21}
     n, m = 1 << 30, 32
     q = bench.bytes_per_lookup("quad", st, n, m, 8.0)
     # quad at 2^30: 3 LDS layers, the 206 KB / 3.5 MB / 59 MB layers in cache, 1 GB + leaves in HBM
     assert q["lds"] == 3 * 64 and q["cache"] == 3 * 64 and q["hbm"] == 2 * 64 + m + 8
+    # PLAIN: the 14 plain levels' 16-char keys in LDS (4 B), then the pivot array
     p = bench.bytes_per_lookup("plain", st, n, m, 31.0)
-    assert p["lds"] == 12 * 12 and p["cache"] == 9 * 16 and p["hbm"] == 10 * (4 + m / 4) + m + 8
+    assert p["lds"] == 14 * 4 and p["cache"] == 7 * 16 and p["hbm"] == 10 * (4 + m / 4) + m + 8
     p23 = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
-    assert p23["cache"] == 11 * 16 and p23["hbm"] == 8 * (4 + m / 4) + m + 8
+    assert p23["cache"] == 9 * 16 and p23["hbm"] == 8 * (4 + m / 4) + m + 8
+    # LLCP: whole keys + SA values of 12 levels in LDS, levels 13-14 read from the array
+    ll = bench.bytes_per_lookup("llcp", dict(st, top2_levels=23), n, m, 31.0)
+    assert ll["lds"] == 12 * 12 and ll["cache"] == 11 * 16 and ll["requests_model"]["cache"] == 2 + 9
     h = bench.bytes_per_lookup("prefix", st, n, m, 1.0)
     assert h["hbm"] == 32 + m + 8 and h["cache"] == 0 and h["lds"] == 0
     assert bench._tree_layers(n, 4, 64, 17, 64, 8)[-1] == n // 4 * 64
@@ -77,21 +81,21 @@ def test_byte_model_splits_served_levels():
 def test_byte_model_hbm_pivot_levels():
     """The deep pivot array (SAS_BUILD_TOP2_LEVELS = 30): levels 13-23 cache-resident, 24-30
     one 16-B HBM entry each, level 31 an SA word + a text window; requests by tier."""
-    st = {"sa_width": 4, "top_levels": 12, "top2_levels": 30}
+    st = {"sa_width": 4, "top_levels": 14, "top2_levels": 30}
     n, m = 1 << 30, 32
     p30 = bench.bytes_per_lookup("plain", st, n, m, 31.0)
-    assert p30["lds"] == 12 * 12 and p30["cache"] == 11 * 16
+    assert p30["lds"] == 14 * 4 and p30["cache"] == 9 * 16
     assert p30["hbm"] == 7 * 16 + 1 * (4 + m / 4) + m + 8
-    # blocked pivots: one request per block entered (blocks of levels 13-14, 15-17, 18-20,
-    # 21-23 in the cache; 24-26, 27-29, 30 from HBM), then level 31's SA word + text window
-    assert p30["requests_model"] == {"cache": 4.0, "hbm": 3 + 2 * 1 + m / 128}
+    # blocked pivots: one request per block entered (blocks of levels 15-17, 18-20, 21-23 in
+    # the cache; 24-26, 27-29, 30 from HBM), then level 31's SA word + text window
+    assert p30["requests_model"] == {"cache": 3.0, "hbm": 3 + 2 * 1 + m / 128}
     # fewer probes than the pivot levels (a short range): no SA-level term
     p20 = bench.bytes_per_lookup("plain", st, n, m, 20.0)
-    assert p20["hbm"] == m + 8 and p20["cache"] == 8 * 16
+    assert p20["hbm"] == m + 8 and p20["cache"] == 6 * 16
     # INLINE stays on the cache-resident 23 levels whatever the array holds (launch_search)
     pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
     assert pin["hbm"] == 8 * 16 + m + 8 and pin["requests_model"]["hbm"] == 8 + m / 128
-    assert pin["requests_model"]["cache"] == 4.0  # INLINE reads a block's 16-char keys at once, as PLAIN
+    assert pin["requests_model"]["cache"] == 3.0  # INLINE reads a block's 16-char keys at once, as PLAIN
     # the split: model HBM requests first, the rest of the PMC count is cache-served
     bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
     assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
@@ -145,7 +149,7 @@ def _stats_2e30():
     u32 SA, 23 pivot levels, fused quad leaves, p = 16 two-suffix inline table)."""
     n = 1 << 30
     return {"n": n, "sa_entries": n, "text_bytes": (n // 32 + 4) * 8, "sa_bytes": 4 * n, "sa_width": 4,
-            "top2_levels": 23, "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
+            "top_levels": 14, "top2_levels": 23, "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
             "quad_bytes": 18_325_000_000, "sector_bytes": 19_400_000_000, "stree_bytes": 4_563_402_752,
             "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "index_bytes": 205_755_777_696}
 
@@ -156,12 +160,12 @@ def test_footprint_per_algorithm():
     st = _stats_2e30()
     gib = 1 << 30
     text = st["text_bytes"]
-    piv23 = 16 * bench.top2_entries(12, 23)[0]  # the blocked pivot array, ~146 MiB
+    piv23 = 16 * bench.top2_entries(14, 23)[0]  # the blocked pivot array, ~146 MiB
     assert 128 << 20 < piv23 < 150 << 20
     assert bench.footprint("plain", st) == 4 * gib + text + piv23  # ~4.4 GiB
     assert 4.3 * gib < bench.footprint("plain", st) < 4.5 * gib
-    assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * bench.top2_entries(12, 30)[0]
-    assert bench.footprint("llcp", st) == 16 * gib + text + 16 * bench.top2_entries(12, 23)[0]
+    assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * bench.top2_entries(14, 30)[0]
+    assert bench.footprint("llcp", st) == 16 * gib + text + 16 * bench.top2_entries(14, 23)[0]
     assert bench.footprint("quad", st) == st["quad_bytes"] + text  # ~17 GiB
     assert bench.footprint("prefix", st) == 128 * gib + 32 + 16 * gib + text  # table + fused leaves + text
     assert bench.footprint("prefix_packed", st) == bench.footprint("prefix", st)

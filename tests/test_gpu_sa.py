@@ -1088,13 +1088,13 @@ def test_blocked_pivot_levels(sas):
     qs[: nq // 4] = rng.integers(0, 4, (nq // 4, m))
     qb = qs.reshape(-1).copy()
     ref = None
-    for L in (0, 13, 14, 15, 16, 21, 24, 25):
+    for L in (0, 5, 13, 15, 16, 17, 18, 21, 24, 25):
         idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False,
                                 top2_levels=L)
         st = idx.stats()
         lv = st["top2_levels"]
-        assert lv == (23 if L == 0 else L)
-        assert st["top2_bytes"] == 16 * bench.top2_entries(12, lv)[0], L
+        assert lv == (23 if L == 0 else L) and st["top_levels"] == min(lv, 14)
+        assert st["top2_bytes"] == 16 * bench.top2_entries(st["top_levels"], lv)[0], L
         if ref is None:
             sa = idx.suffix_array()
             tp = O.padded(t)
@@ -1107,5 +1107,6 @@ def test_blocked_pivot_levels(sas):
             assert np.array_equal(pr, ref_pr), (L, algo)
         idx.free()
     # the layout itself: the cache part's short group first, the HBM part's last
-    assert bench.top2_entries(12, 23)[1] == [(12, 2), (14, 3), (17, 3), (20, 3)]
-    assert bench.top2_entries(12, 30)[1] == [(12, 2), (14, 3), (17, 3), (20, 3), (23, 3), (26, 3), (29, 1)]
+    assert bench.top2_entries(14, 23)[1] == [(14, 3), (17, 3), (20, 3)]
+    assert bench.top2_entries(14, 30)[1] == [(14, 3), (17, 3), (20, 3), (23, 3), (26, 3), (29, 1)]
+    assert bench.top2_entries(14, 22)[1] == [(14, 2), (16, 3), (19, 3)]
