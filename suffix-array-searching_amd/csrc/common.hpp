@@ -81,6 +81,17 @@ __host__ __device__ __forceinline__ Top2Slot top2_slot_at(uint32_t lg, uint32_t 
     const uint32_t S = 1u << lg;
     return Top2Slot{4 * j, 4 * S + 4 * j, 8 * S + 8 * j};
 }
+// LDS staging of the plain levels' 16-char keys from their contiguous copy: 16-B loads, four
+// keys each (a workgroup's staging decides the time of small batches: configs[0]'s 10^4
+// queries)
+__device__ __forceinline__ void stage_k16(uint32_t* s, const uint32_t* __restrict__ g, uint32_t nodes) {
+    const uint32_t nw = nodes / 4;
+    const uint4* src = reinterpret_cast<const uint4*>(g);
+    uint4* dst = reinterpret_cast<uint4*>(s);
+    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) dst[w] = src[w];
+    for (uint32_t x = nw * 4 + threadIdx.x; x < nodes; x += blockDim.x) s[x] = g[x];
+}
+
 // fill the layout for L levels above D LDS levels; returns the array's entries
 static inline uint64_t top2_layout(uint32_t D, uint32_t L, Top2Layout* y) {
     uint64_t entries = 1ull << D;
@@ -171,6 +182,7 @@ struct sas_index {
                                   // in LDS), then the blocked levels (top2_layout); index 0 unused
     Top2Layout top2_lay{};
     uint64_t top2_entries = 0;
+    uint32_t* top_k16 = nullptr;  // the plain levels' 16-char keys, contiguous (inside top2's allocation)
     uint32_t top_levels = 0;      // levels served from LDS
     uint32_t top2_levels = 0;     // levels served from LDS or top2
     uint32_t iters = 0;           // ilog2(n) + 1

@@ -849,8 +849,8 @@ static int build_quad(sas_index* x, bool compact, uint32_t mode) {
 // {32-char key, SA value} of that state's pivot SA[(l + r) / 2], at index k for the D
 // LDS levels and at top2_slot (the blocked layout, common.hpp) below them.
 template <int W>
-__global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint4* __restrict__ top2,
-                      uint32_t nodes, uint32_t D, Top2Layout lay) {
+__global__ void k_top(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa, uint64_t sa_n,
+                      uint4* __restrict__ top2, uint32_t nodes, uint32_t D, Top2Layout lay) {
     GRID_STRIDE(k, nodes) {
         uint64_t l = 0, r = sa_n, p = 0xFFFFFFFFu, key = 0;
         int depth = k ? 63 - __clzll(k) : 0;
@@ -871,8 +871,17 @@ __global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa
             *reinterpret_cast<uint32_t*>(b + o.hi) = (uint32_t)(key >> 32);
             *reinterpret_cast<uint32_t*>(b + o.lo) = (uint32_t)key;
             *reinterpret_cast<uint64_t*>(b + o.sa) = p;
+            // slot 0's high word (no node) flags the block's suffixes of fewer than 32 chars,
+            // whose keys end in padding: an lcp read off their key would not be exact
+            const uint32_t j = top2_j(lay, (uint32_t)depth, (uint32_t)k);
+            if (lay.lg[depth] && !(l < r && p + 32 <= (uint64_t)n))
+                atomicOr(reinterpret_cast<uint32_t*>(b), 1u << j);
         }
     }
+}
+
+__global__ void k_top_k16(const uint4* __restrict__ top2, uint32_t nodes, uint32_t* __restrict__ k16) {
+    GRID_STRIDE(k, nodes) k16[k] = top2[k].y;
 }
 
 // ------------------------------------------------------------------ prefix table
@@ -1703,17 +1712,23 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         const uint32_t nodes = 1u << x->top2_levels;
         x->top2_entries = top2_layout(x->top_levels, x->top2_levels, &x->top2_lay);
         DevBuf t2;
-        TRY(t2.alloc(x->top2_entries * 16, "top2"));
-        HIP_TRY(hipMemset(t2.p, 0, x->top2_entries * 16));  // unused block slots
+        const uint64_t k16_bytes = ((4ull << x->top_levels) + 15) & ~15ull;
+        TRY(t2.alloc(x->top2_entries * 16 + k16_bytes, "top2"));
+        HIP_TRY(hipMemset(t2.p, 0, x->top2_entries * 16 + k16_bytes));  // unused block slots
         const dim3 tg(grid_for(nodes)), tb(256);
         if (W == 5)
-            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes,
+            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, n, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes,
                                x->top_levels, x->top2_lay);
         else
-            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes,
+            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, n, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes,
                                x->top_levels, x->top2_lay);
         HIP_TRY(hipGetLastError());
         x->top2 = static_cast<uint4*>(t2.release());
+        // the plain levels' 16-char keys again, contiguous, for the LDS staging (stage_k16)
+        x->top_k16 = reinterpret_cast<uint32_t*>(x->top2 + x->top2_entries);
+        hipLaunchKernelGGL(k_top_k16, dim3(grid_for(1ull << x->top_levels)), tb, 0, 0, x->top2, 1u << x->top_levels,
+                           x->top_k16);
+        HIP_TRY(hipGetLastError());
     }
     if ((flags & SAS_BUILD_TAGGED) && (flags & SAS_BUILD_TAG_LINES)) TRY(build_tag_lines(x, (flags >> 16) & 31));
     else if (flags & SAS_BUILD_TAGGED) TRY(build_tagged(x, (flags >> 16) & 31));
@@ -1754,9 +1769,9 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.tag_line_tag_bits = x->tag_lines ? tl_tag_bits(x->tag_sb) : 0;
     st.text2_bytes = x->text2 ? x->text_words * 8 : 0;
     st.tag_overflow_entries = x->tag_ovf_n;
+    st.top2_bytes = x->top2 ? x->top2_entries * 16 + (((4ull << x->top_levels) + 15) & ~15ull) : 0;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
-                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes + x->top2_entries * 16;
-    st.top2_bytes = x->top2_entries * 16;
+                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes + st.top2_bytes;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -53,6 +53,7 @@ struct SearchArgs {
     uint32_t prefix_w;       // bytes per table entry (4 or 5)
     uint32_t prefix_hi40;    // inline slots: SA bits 32..39 in slot 1's rank word
     const uint4* top2;
+    const uint32_t* top_k16;  // the plain levels' 16-char keys, contiguous (LDS staging)
     Top2Layout top2_lay;     // the blocked levels' addresses (common.hpp)
     uint32_t top_levels;
     uint32_t top2_levels;
@@ -167,6 +168,11 @@ __device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, ui
 // RANGE (SAS_PREFIX_RANGE, PLAIN / LCP without the LDS top): start from the prefix
 // table's range for q's first p chars instead of [0, sa_n), exactly as the reference's
 // binary_search does (sas/sa_search.rs:98-101) once its p is not 0
+// LCP / LLCP read a pivot block's whole keys at its root (4 loads, one request) and take
+// exact lcps from them (0: one whole entry per level, as before round 4's A/B)
+#ifndef SAS_LCP_BLOCK_KEYS
+#define SAS_LCP_BLOCK_KEYS 1
+#endif
 #define BS_PLAIN 0
 #define BS_MLR 1
 #define BS_LLCP 2
@@ -184,13 +190,24 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         D = a.top_levels;
         DL = K16 ? D : (D < SAS_TOP_FULL_LEVELS ? D : SAS_TOP_FULL_LEVELS);
         const uint32_t nodes = 1u << DL;
-        for (uint32_t k = threadIdx.x; k < nodes; k += blockDim.x) {
-            const uint4 e = a.top2[k];
-            if (K16) {
-                s_k16[k] = e.y;
-            } else {
-                s_key[k] = (uint64_t)e.x | ((uint64_t)e.y << 32);
-                s_sa[k] = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
+        if (K16) {
+            stage_k16(s_k16, a.top_k16, nodes);
+        } else {  // whole entries: four loads in flight per thread before the stores
+            for (uint32_t k0 = threadIdx.x; k0 < nodes; k0 += 4 * blockDim.x) {
+                uint4 e[4];
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t k = k0 + u * blockDim.x;
+                    if (k < nodes) e[u] = a.top2[k];
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t k = k0 + u * blockDim.x;
+                    if (k < nodes) {
+                        s_key[k] = (uint64_t)e[u].x | ((uint64_t)e[u].y << 32);
+                        s_sa[k] = (sa_val_t<W>)((uint64_t)e[u].z | ((uint64_t)e[u].w << 32));
+                    }
+                }
             }
         }
         __syncthreads();
@@ -276,12 +293,17 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                 const uint32_t lg = a.top2_lay.lg[it];
                 const uint32_t levels = lg ? lg : 1u;
                 const uint8_t* blk = t2 + top2_block_byte(a.top2_lay, it, k);  // k: the group's root node
-                uint4 kh0 = make_uint4(0, 0, 0, 0), kh1 = kh0;
-                if (MODE == BS_PLAIN && lg >= 2 && l < r) {
-                    // PLAIN (no lcps to keep exact): the high halves of all of the block's
-                    // keys at once -- two (one) 16-B loads of one line, one request
+                uint4 kh0 = make_uint4(0, 0, 0, 0), kh1 = kh0, kl0 = kh0, kl1 = kh0;
+                if (lg >= 2 && l < r) {
+                    // the high halves of all of the block's keys at once -- two (one) 16-B loads
+                    // of one line, one request; LCP / LLCP also the low halves (exact lcps
+                    // need all 32 chars), two (one) more loads of the same line
                     kh0 = *reinterpret_cast<const uint4*>(blk);
                     if (lg == 3) kh1 = *reinterpret_cast<const uint4*>(blk + 16);
+                    if (MODE != BS_PLAIN && SAS_LCP_BLOCK_KEYS) {
+                        kl0 = *reinterpret_cast<const uint4*>(blk + (4u << lg));
+                        if (lg == 3) kl1 = *reinterpret_cast<const uint4*>(blk + (4u << lg) + 16);
+                    }
                 }
                 for (uint32_t t = 0; t < levels && it < a.top2_levels; ++t, ++it) {
                     if (!(l < r)) continue;
@@ -304,6 +326,30 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                         const uint32_t av = khi & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
                         if (av != bv) {
                             lt = av < bv;
+                            pk = false;
+                            done = true;
+                        }
+                    } else if (MODE != BS_PLAIN && SAS_LCP_BLOCK_KEYS && lg >= 2 && h < 32 && !((kh0.x >> j) & 1u)) {
+                        // LCP / LLCP: the whole 32-char key of a suffix of >= 32 chars (slot 0's
+                        // high word flags the block's shorter ones) gives the exact lcp when it
+                        // differs from q's first min(m, 32) chars, and for m <= 32 when it does
+                        // not (then lcp = m and suffix >= q); else the SA value and the text
+                        const uint4 vh = (j >> 2) ? kh1 : kh0, vl = (j >> 2) ? kl1 : kl0;
+                        const uint32_t jj = j & 3;
+                        const uint64_t key =
+                            ((uint64_t)(jj == 0 ? vh.x : jj == 1 ? vh.y : jj == 2 ? vh.z : vh.w) << 32) |
+                            (jj == 0 ? vl.x : jj == 1 ? vl.y : jj == 2 ? vl.z : vl.w);
+                        const uint32_t c = q.m < 32 ? q.m : 32;
+                        const uint64_t mk = chars_mask(c);
+                        const uint64_t av = key & mk, bv = q.w[0] & mk;
+                        if (av != bv) {
+                            lt = av < bv;
+                            lcp = (uint32_t)(__clzll(av ^ bv) >> 1);
+                            pk = false;
+                            done = true;
+                        } else if (q.m <= 32) {
+                            lt = false;
+                            lcp = q.m;
                             pk = false;
                             done = true;
                         }
@@ -1235,7 +1281,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
     uint32_t D = 0;
     if (TOP) {
         D = a.top_levels;
-        for (uint32_t k = threadIdx.x; k < (1u << D); k += blockDim.x) s_k16[k] = a.top2[k].y;
+        stage_k16(s_k16, a.top_k16, 1u << D);
         __syncthreads();
     }
     uint32_t bad = 0;
@@ -2678,6 +2724,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.prefix_w = x->prefix_w;
     a.prefix_hi40 = x->prefix_hi40;
     a.top2 = x->top2;
+    a.top_k16 = x->top_k16;
     a.top2_lay = x->top2_lay;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;
