@@ -124,10 +124,6 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         per = {"plain": sa_w + win, "lcp": sa_w + win, "inline": 16, "llcp": 16, "interp": 16}[algo]
         if algo in ("plain", "lcp", "inline", "llcp"):
             t1, t2 = st.get("top_levels", TOP_LDS_LEVELS), st.get("top2_levels", TOP2_LEVELS)
-            if algo == "inline":
-                t2 = min(t2, TOP2_CACHE_LEVELS)  # launch_search caps INLINE's pivot levels
-            elif algo == "llcp":
-                t2 = min(t2, 23)  # and LLCP's (SAS_LLCP_TOP2_LEVELS)
             tc = min(t2, TOP2_CACHE_LEVELS)  # the array's first 23 levels stay in cache
             # LDS: PLAIN / INLINE stage the plain levels' 16-char keys (4 B), LCP / LLCP the
             # first TOP_FULL_LDS_LEVELS' whole keys and SA values (12 B) and read the rest of
@@ -333,9 +329,9 @@ def footprint(algo: str, st: dict) -> int:
     if base in ("plain", "lcp"):
         b = sa + text + piv(31)
     elif base == "llcp":
-        b = st["llcp_bytes"] + text + piv(23)  # SAS_LLCP_TOP2_LEVELS
+        b = st["llcp_bytes"] + text + piv(31)
     elif base == "inline":
-        b = _quad_leaf_bytes(st) + text + piv(TOP2_CACHE_LEVELS)  # SAS_INLINE_TOP2_LEVELS
+        b = _quad_leaf_bytes(st) + text + piv(31)
     elif base == "quad":
         b = st["quad_bytes"] + compact_sa + text
     elif base == "sector":

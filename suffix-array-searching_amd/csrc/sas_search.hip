@@ -1856,10 +1856,10 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 // pairs, suffix_less_from_x2), and its position straight from the entry.  Larger buckets
 // continue with a binary search over the rest.
 #ifndef SAS_LLCP_TOP2_LEVELS
-#define SAS_LLCP_TOP2_LEVELS 23
+#define SAS_LLCP_TOP2_LEVELS 31
 #endif
 #ifndef SAS_INLINE_TOP2_LEVELS
-#define SAS_INLINE_TOP2_LEVELS 23
+#define SAS_INLINE_TOP2_LEVELS 31
 #endif
 #ifndef SAS_TAG_WIN
 #define SAS_TAG_WIN 8
@@ -2637,10 +2637,10 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    // LLCP reads one 16-B entry per probe either way, and its own entries carry the interval
-    // lcps that spare text reads: pivot-array levels past the cache-resident ones cost it
-    // time (round 3, unblocked array: 3.08 ms with 21 levels, 3.29 with 23; round 4, blocked:
-    // 2.80 with 23 against 2.93 with 21, profiles/r4/ab_pivots/)
+    // LLCP and INLINE read every level of the pivot array the index holds (31 = no cap): a
+    // blocked level costs them a third of a request against one request for their own entry
+    // (round 3, unblocked: pivot levels past the cache-resident ones cost LLCP time, 3.08 ms
+    // with 21 levels, 3.29 with 23)
     if (algo == SAS_ALGO_LLCP && a.top2_levels > SAS_LLCP_TOP2_LEVELS) a.top2_levels = SAS_LLCP_TOP2_LEVELS;
     // INLINE's own probes read one 16-B fused entry in rank order, whose last levels share
     // lines; the pivot array past its cache-resident levels only moves them apart

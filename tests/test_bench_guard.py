@@ -92,9 +92,10 @@ def test_byte_model_hbm_pivot_levels():
     # fewer probes than the pivot levels (a short range): no SA-level term
     p20 = bench.bytes_per_lookup("plain", st, n, m, 20.0)
     assert p20["hbm"] == m + 8 and p20["cache"] == 6 * 16
-    # INLINE stays on the cache-resident 23 levels whatever the array holds (launch_search)
+    # INLINE reads every pivot level the array holds (round 4: blocked levels cost it less than
+    # its own rank-ordered entries): levels 24-30 in 3 blocks, then level 31's fused entry
     pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
-    assert pin["hbm"] == 8 * 16 + m + 8 and pin["requests_model"]["hbm"] == 8 + m / 128
+    assert pin["hbm"] == 7 * 16 + 16 + m + 8 and pin["requests_model"]["hbm"] == 3 + 1 + m / 128
     assert pin["requests_model"]["cache"] == 3.0  # INLINE reads a block's 16-char keys at once, as PLAIN
     # the split: model HBM requests first, the rest of the PMC count is cache-served
     bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
