@@ -170,6 +170,12 @@ __device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, ui
 // binary_search does (sas/sa_search.rs:98-101) once its p is not 0
 // LCP / LLCP read a pivot block's whole keys at its root (4 loads, one request) and take
 // exact lcps from them (0: one whole entry per level, as before round 4's A/B)
+// PLAIN over a u32 SA: a range of at most this many ranks (4 or 8; 0: off) has its SA words
+// loaded together for the remaining probes
+#ifndef SAS_PLAIN_SA_RUN
+#define SAS_PLAIN_SA_RUN 8
+#endif
+static_assert(SAS_PLAIN_SA_RUN == 0 || SAS_PLAIN_SA_RUN == 4 || SAS_PLAIN_SA_RUN == 8, "SAS_PLAIN_SA_RUN: 0, 4 or 8");
 #ifndef SAS_LCP_BLOCK_KEYS
 #define SAS_LCP_BLOCK_KEYS 1
 #endif
@@ -365,6 +371,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                 }
             }
         }
+        bool run = false;  // PLAIN, u32 SA: the range's SA words are in sc0..sc2 (from rank rb)
+        uint32_t rb = 0;
+        uint4 sc0 = make_uint4(0, 0, 0, 0), sc1 = sc0, sc2 = sc0;
         for (; it < a.iters; ++it) {
             if (l < r) {
                 const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
@@ -396,6 +405,27 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     if (!decided) {
                         lt = llcp_tie_less<QW>(a.tw, n, p, q, hh, inl, &lcp);
                     }
+                } else if (MODE == BS_PLAIN && W == 4 && SAS_PLAIN_SA_RUN) {
+                    // the last probes' SA words: once the range holds <= SAS_PLAIN_SA_RUN ranks,
+                    // the 16-B chunks covering it are loaded together (one request) and the
+                    // remaining probes take their SA values from registers
+                    if (!run && r - l <= SAS_PLAIN_SA_RUN) {
+                        run = true;
+                        rb = l & ~3u;
+                        const uint4* c = reinterpret_cast<const uint4*>(a.sa) + (rb >> 2);
+                        sc0 = c[0];
+                        if (((uint32_t)r - 1) - rb >= 4) sc1 = c[1];
+                        if (SAS_PLAIN_SA_RUN > 4 && ((uint32_t)r - 1) - rb >= 8) sc2 = c[2];
+                    }
+                    if (run) {
+                        const uint32_t o = (uint32_t)mid - rb;
+                        const uint4 v = o < 4 ? sc0 : (SAS_PLAIN_SA_RUN > 4 && o >= 8 ? sc2 : sc1);
+                        const uint32_t oo = o & 3;
+                        p = (sa_val_t<W>)(oo == 0 ? v.x : oo == 1 ? v.y : oo == 2 ? v.z : v.w);
+                    } else {
+                        p = (sa_val_t<W>)sa[mid];
+                    }
+                    lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
                 } else {
                     p = (sa_val_t<W>)sa[mid];
                     lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
