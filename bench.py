@@ -52,13 +52,11 @@ RANDOM_REQ_CEILING = 5.084e10
 CACHE_REQ_CEILING = 5.731e10
 CACHE_BYTES = 256 << 20  # Infinity Cache (MALL): arrays at most this large count as cache-served
 SEED = 31415  # sas/main.rs:38
-# binary-search levels served from LDS / the pivot array (the index's stats win): the library
-# default builds the 23 cache-resident levels (SAS_TOP2_CACHE_LEVELS, 128 MiB); deeper levels
-# (SAS_BUILD_TOP2_LEVELS, e.g. 30 = 16 GiB) are HBM reads
-TOP_LDS_LEVELS, TOP2_LEVELS = 14, 23
-TOP_FULL_LDS_LEVELS = 12  # LCP / LLCP: whole keys + SA values in LDS (common.hpp SAS_TOP_FULL_LEVELS)
-TOP2_CACHE_LEVELS = 23
-C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: pivots of levels 24-30 from HBM
+# binary-search levels served from LDS (16-char keys) / the prefix-relative pivot blocks (the
+# index's stats win): the library default reaches 26 levels (SAS_TOP2_CACHE_LEVELS, 136 MiB of
+# blocks, cache-resident); deeper ones (SAS_BUILD_TOP2_LEVELS, e.g. 30 = 2.1 GiB) are HBM reads
+TOP_LDS_LEVELS = 14
+C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: pivot blocks of levels 27-30 from HBM
 
 KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
@@ -120,31 +118,31 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)  # (INTERP: a fused 16-B entry per probe)
         per = 16 if (algo == "interp" and st["quad_entry_bytes"] == 16) else sa_w + win
         hbm += entry + max(0.0, probes - 1) * per
-    elif algo in ("plain", "lcp", "inline", "llcp", "interp"):
-        per = {"plain": sa_w + win, "lcp": sa_w + win, "inline": 16, "llcp": 16, "interp": 16}[algo]
-        if algo in ("plain", "lcp", "inline", "llcp"):
-            t1, t2 = st.get("top_levels", TOP_LDS_LEVELS), st.get("top2_levels", TOP2_LEVELS)
-            tc = min(t2, TOP2_CACHE_LEVELS)  # the array's first 23 levels stay in cache
-            # LDS: PLAIN / INLINE stage the plain levels' 16-char keys (4 B), LCP / LLCP the
-            # first TOP_FULL_LDS_LEVELS' whole keys and SA values (12 B) and read the rest of
-            # the plain levels from the array (common.hpp SAS_TOP_LEVELS)
-            k16 = algo in ("plain", "inline")
-            tl = t1 if k16 else min(t1, TOP_FULL_LDS_LEVELS)
-            lds += min(probes, tl) * (4 if k16 else 12)
-            cache += max(0.0, min(probes, tc) - tl) * 16
-            hbm += max(0.0, min(probes, t2) - tc) * 16  # deeper pivot levels: one 16-B HBM entry each
-            hbm += max(0.0, probes - t2) * per
-            # random 128-B-line requests per lookup by where they are served: one per pivot
-            # block entered (up to 3 levels a line, common.hpp top2_layout) in the cache part
-            # and in the HBM part (LCP / LLCP: one per level, and one per plain level past
-            # their LDS ones); two per SA probe (the SA word, then the text window: PLAIN /
-            # LCP) or one (a 16-B entry); the query stream
-            pc, ph = pivot_requests(t1, t2, probes, blocked=k16)
-            pc += max(0.0, min(probes, t1) - tl)
-            reqs = {"cache": pc, "hbm": ph + max(0.0, probes - t2) * (2 if per != 16 else 1)
-                    + (8.0 if packed else m) / 128}
-        else:
-            hbm += probes * per
+    elif algo in ("plain", "lcp", "inline", "llcp"):
+        # the LDS levels' 16-char keys (4 B), one 32-B prefix-relative block per 4 levels (one
+        # request, cache or HBM by where its group's array ends; common.hpp SAS_REL_GROUP),
+        # then per probe: SA word + text window (PLAIN / LCP, two requests) or one 16-B entry
+        # (INLINE / LLCP, one request); a lookup decided by keys alone reads SA[r] at the end
+        per, rq = (sa_w + win, 2) if algo in ("plain", "lcp") else (16, 1)
+        t1 = st.get("top_levels", TOP_LDS_LEVELS)
+        R = st.get("rel_levels") or t1
+        lds += min(probes, t1) * 4
+        rc = rh = 0.0
+        for d0, h, cached in rel_groups(t1, R):
+            if probes - d0 <= 0:
+                continue
+            if cached:
+                cache += 32
+                rc += 1
+            else:
+                hbm += 32
+                rh += 1
+        hbm += max(0.0, probes - R) * per
+        fin = 1.0 if probes <= R else 0.0
+        hbm += fin * (sa_w if algo in ("plain", "lcp") else 16)
+        reqs = {"cache": rc, "hbm": rh + max(0.0, probes - R) * rq + fin + (8.0 if packed else m) / 128}
+    elif algo == "interp":
+        hbm += probes * 16
     elif algo in ("stree", "quad", "sector"):
         if algo == "stree":
             H, node, lds_l = st["stree_layers"], 64, st["stree_lds_layers"]
@@ -251,49 +249,19 @@ def launch_times(torch, step, steps: int, warmup: int, stream, sync=None, barrie
 
 
 # ---------------------------------------------------------------- the pivot array
-def top2_entries(D: int, L: int, C: int = TOP2_CACHE_LEVELS, G: int = 3):
-    """common.hpp top2_layout: (entries, groups) of the pivot array for L levels above D LDS
-    levels: levels [D, L) in groups of up to G levels, a group rooted at level d0 storing
-    2^d0 blocks of 2^h 16-B slots (one slot per node for h = 1); the cache part [D, C) puts
-    its short group first, the HBM part [C, L) last."""
-    e = 1 << D
-    groups = []
-    c = min(L, C)
-    d = D
-    if c > D:
-        r = (c - D) % G
-        if r:
-            groups.append((d, r))
-            d += r
-        while d < c:
-            groups.append((d, G))
-            d += G
-    d = max(d, c)
-    while d < L:
-        groups.append((d, min(G, L - d)))
-        d += G
-    for d0, h in groups:
-        e += (1 << d0) << (0 if h == 1 else h)
-    return e, groups
+def rel_groups(D: int, R: int, G: int = 4):
+    """common.hpp rel_layout: the prefix-relative pivot blocks for levels [D, R), groups of G
+    levels rooted at D, D + G, ..., one 32-B block per root node; (d0, h, cached) per group,
+    cached = the array up to and including the group fits the 256 MiB Infinity Cache."""
+    out, tot = [], 0
+    for d0 in range(D, R, G):
+        tot += 32 << d0
+        out.append((d0, min(G, R - d0), tot <= CACHE_BYTES))
+    return out
 
 
-def pivot_requests(D: int, L: int, probes: float, blocked: bool = True):
-    """(cache, hbm) requests of the pivot levels a lookup of `probes` probes reads.  PLAIN
-    (`blocked`) reads a block's 16-char keys with loads issued together: one request per block
-    it enters; LCP / LLCP / INLINE need every pivot's whole key and SA value (exact lcps), one
-    request per level."""
-    _, groups = top2_entries(D, L)
-    cache = hbm = 0.0
-    for d0, h in groups:
-        lv = max(0.0, min(float(h), probes - d0))
-        if lv <= 0:
-            continue
-        c = 1.0 if blocked else lv
-        if d0 < TOP2_CACHE_LEVELS:
-            cache += c
-        else:
-            hbm += c
-    return cache, hbm
+def rel_bytes(D: int, R: int) -> int:
+    return sum(32 << d0 for d0, _, _ in rel_groups(D, R))
 
 
 # ---------------------------------------------------------------- index footprints
@@ -315,23 +283,18 @@ def footprint(algo: str, st: dict) -> int:
     TAGGED = the tagged index (it holds nothing else)."""
     base = algo[:-6] if algo.endswith("_range") else ("prefix" if algo == "prefix_packed" else algo)
     text = st["text_bytes"] + st.get("text2_bytes", 0)
-    sa, t2 = st["sa_bytes"], st.get("top2_levels", 0)
+    sa = st["sa_bytes"]
     compact_sa = sa if st.get("quad_entry_bytes") == 8 else 0
-
-    def piv(cap):
-        lv = min(t2, cap)
-        if not lv:
-            return 0
-        # the levels this algorithm reads of the built array (LLCP / INLINE stop early)
-        return 16 * top2_entries(min(st.get("top_levels", TOP_LDS_LEVELS), lv), lv)[0]
+    # the pivots: the LDS levels' entries and 16-char keys, then the prefix-relative blocks
+    piv = (20 << st.get("top_levels", TOP_LDS_LEVELS)) + st.get("rel_bytes", 0) if st.get("top_levels") else 0
     if base == "tagged":
         return st["index_bytes"]
     if base in ("plain", "lcp"):
-        b = sa + text + piv(31)
+        b = sa + text + piv
     elif base == "llcp":
-        b = st["llcp_bytes"] + text + piv(31)
+        b = st["llcp_bytes"] + text + piv
     elif base == "inline":
-        b = _quad_leaf_bytes(st) + text + piv(31)
+        b = _quad_leaf_bytes(st) + text + piv
     elif base == "quad":
         b = st["quad_bytes"] + compact_sa + text
     elif base == "sector":
@@ -1333,8 +1296,10 @@ WORKLOADS = {
               "with p live) of {e}-B inline entries holding each bucket's first {k} suffixes "
               "({tb:.0f} GiB), then binary search over the fused {{32-char key, SA}} quad-leaf entries "
               "of the bucket; 2^30 text in HBM, 10^7 len-32 queries",
-    "plain": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112): levels 1-{t1} from LDS, "
-             "levels {t1p}-{t2} from the {pb} pivot array ({where}), the rest read SA[mid] and a text window",
+    "plain_rel": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112): levels 1-{t1} from LDS "
+                 "(16-char keys), levels {t1p}-{R} from the {rb} prefix-relative pivot blocks ({where}; 4 levels "
+                 "per 32-B block: the 8 chars after the block bounds' common prefix), the rest read SA[mid] and a "
+                 "text window",
     "lcp": "configs[1] + mlr LCP skipping",
     "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (16-B {SA, Llcp, Rlcp, chars} entries)",
     "inline": "configs[1] probe sequence over fused {32-char key, SA} entries",
@@ -1348,14 +1313,15 @@ WORKLOADS = {
 
 
 def plain_label(st: dict) -> str:
-    """configs[1]'s workload text from the index's own pivot depth (sas_stats.top2_levels)."""
-    t1, t2 = st["top_levels"], st["top2_levels"]
-    hbm = t2 > TOP2_CACHE_LEVELS
-    pb = st.get("top2_bytes") or (16 << t2)
-    return WORKLOADS["plain"].format(
-        t1=t1, t1p=t1 + 1, t2=t2, pb=(f"{pb / 2 ** 30:.1f} GiB" if pb >= 1 << 30 else f"{pb >> 20} MiB"),
-        where=(f"levels {t1 + 1}-{TOP2_CACHE_LEVELS} cache-resident, {TOP2_CACHE_LEVELS + 1}-{t2} from HBM; "
-               f"up to 3 levels per 128-B line" if hbm else "cache-resident, up to 3 levels per 128-B line"))
+    """configs[1]'s workload text from the index's own pivot depth (sas_stats.rel_levels)."""
+    t1, R = st["top_levels"], st.get("rel_levels", 0)
+    if R:
+        rb = st["rel_bytes"]
+        hb = [d0 for d0, _, c in rel_groups(t1, R) if not c]
+        return WORKLOADS["plain_rel"].format(
+            t1=t1, t1p=t1 + 1, R=R, rb=(f"{rb / 2 ** 30:.2f} GiB" if rb >= 1 << 30 else f"{rb >> 20} MiB"),
+            where=(f"levels {t1 + 1}-{hb[0]} cache-resident, {hb[0] + 1}-{R} from HBM" if hb else "cache-resident"))
+    return WORKLOADS["plain_rel"].format(t1=t1, t1p=t1 + 1, R=t1, rb="0 MiB", where="none")
 
 
 def main():
@@ -1381,7 +1347,7 @@ def main():
     ap.add_argument("--c1-deep-levels", type=int, default=C1_DEEP_TOP2_LEVELS,
                     help="configs[1]'s second figure: PLAIN with this many pivot-array levels (0: skip)")
     ap.add_argument("--top2-levels", type=int, default=0,
-                    help="pivot-array depth of the headline index (SAS_BUILD_TOP2_LEVELS; 0 = library default 23)")
+                    help="pivot-array depth of the headline index (SAS_BUILD_TOP2_LEVELS; 0 = library default 26)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the configs[3] sub-record")
@@ -1595,9 +1561,9 @@ def main():
                               "kernel_ms_median": vmed, "timed_launches": vsteps})
         log(f"variant {v}: {vk:.3f} ms")
 
-    # configs[1]'s second figure: the same PLAIN probe sequence on an index whose pivot array
-    # holds C1_DEEP_TOP2_LEVELS levels (SAS_BUILD_TOP2_LEVELS; 16 GiB at 30): levels past the
-    # cache-resident 23 read one 16-B HBM entry instead of an SA word and a text window
+    # configs[1]'s second figure: the same PLAIN probe sequence on an index whose pivots reach
+    # C1_DEEP_TOP2_LEVELS levels (SAS_BUILD_TOP2_LEVELS; 2.1 GiB of blocks at 30): the block of
+    # levels 27-30 is one HBM request instead of four SA words and text windows
     deep = None
     if args.mode == "replicated" and "plain" in variants and args.c1_deep_levels:
         didx = sas_amd.SaNaive.build(text, lcp=False, stree=False, sector=False, quad=False, llcp=False,
@@ -1620,7 +1586,7 @@ def main():
                       {"identical_to_headline": True, "lookups_per_s": ws * nq * dsteps / del_s,
                        "kernel_ms_median": dt_["median_ms"], "timed_launches": dsteps,
                        "workload": plain_label(dst), "pivot_levels": dst["top2_levels"],
-                       "pivot_bytes": dst["top2_bytes"]})
+                       "pivot_bytes": dst["rel_bytes"] + dst["top2_bytes"]})
         didx.free()
         del dout, dpr
         torch.cuda.empty_cache()
@@ -1693,7 +1659,8 @@ def main():
     if args.mode == "replicated":
         if "plain" in variants:
             configs["c1"] = dict(variants["plain"], workload=plain_label(stats),
-                                 pivot_levels=stats["top2_levels"], pivot_bytes=stats["top2_bytes"])
+                                 pivot_levels=stats["top2_levels"],
+                                 pivot_bytes=stats["rel_bytes"] + stats["top2_bytes"])
             if deep is not None:
                 configs["c1"]["deep_pivots"] = deep
         best2 = max((v for v in ("quad", "sector", "stree") if v in variants),
@@ -1703,10 +1670,10 @@ def main():
                                  lds_layers={"quad": stats["quad_lds_layers"], "sector": stats["sector_lds_layers"],
                                              "stree": stats["stree_lds_layers"]}[best2])
     idx_stats = {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
-                                       "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels",
+                                       "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "rel_levels",
                                        "iterations", "prefix_chars", "prefix_bytes", "sa_bytes", "text_bytes",
                                        "quad_bytes", "stree_bytes", "sector_bytes", "lcp_bytes", "llcp_bytes",
-                                       "index_bytes", "sa_rounds", "build_sa_ns", "build_total_ns")}
+                                       "rel_bytes", "index_bytes", "sa_rounds", "build_sa_ns", "build_total_ns")}
     if lcp_long is not None:
         idx.free()
         torch.cuda.empty_cache()

@@ -119,14 +119,17 @@ typedef struct sas_index sas_index;
                                         replace the SA (sa_width 8).  Combines with LCP;
                                         not with the trees, LLCP or SAS_BUILD_PREFIX*  */
 #define SAS_BUILD_TOP2_LEVELS(L) ((uint32_t)(L) << 27) /* bits 27..31: depth L (1..31) of
-                                        the binary-search pivot array (PLAIN / LCP / INLINE /
-                                        LLCP): the pivots of the first L lockstep iterations,
-                                        one 16-B {32-char key, SA} entry each, 2^L x 16 B.
-                                        0 = the default, 23 levels (128 MiB, resident in the
-                                        256 MiB Infinity Cache); deeper levels are HBM reads
-                                        (one request instead of an SA word and a text window)
-                                        and cost 16 GiB at L = 30.  Clamped to the iteration
-                                        count; results never depend on L                   */
+                                        the binary-search pivots (PLAIN / LCP / LLCP / INLINE):
+                                        the first 14 levels' 16-B {32-char key, SA} entries
+                                        (their 16-char keys staged in LDS), then levels 15..L
+                                        as prefix-relative blocks of 4 levels (32 B each: the
+                                        lcp P of the block's bounds and the 8 chars after P of
+                                        15 pivots), L rounded up to that grid.  0 = the default,
+                                        26 levels (136 MiB, resident in the 256 MiB Infinity
+                                        Cache); L = 30 costs 2.1 GiB.  One request per block
+                                        instead of an SA word and a text window per level.
+                                        Clamped to the iteration count; results never depend
+                                        on L                                               */
 #define SAS_BUILD_TAG_LINES (1u << 24) /* with SAS_BUILD_TAGGED: the tagged entries as one
                                         128-B line per p-char bucket {overflow offset 40 bits
                                         | count 24 bits, the 20 entries of ranks first ..
@@ -212,7 +215,7 @@ typedef struct sas_stats {
     uint32_t quad_fan;       /* quad inner-node fan-out: 31 (prefix-relative nodes) or
                                 17 (SAS_BUILD_QUAD_ABS), 0 if not built              */
     uint32_t top2_levels;    /* binary-search levels whose pivots come from LDS or the
-                                cache-resident pivot array (PLAIN/LCP/INLINE)        */
+                                prefix-relative blocks (PLAIN/LCP/LLCP/INLINE)       */
     uint64_t llcp_bytes;     /* SAS_BUILD_LLCP entries (16 B per suffix), 0 if not built */
     uint64_t prefix_bytes;   /* SAS_BUILD_PREFIX table, 0 if not built                */
     uint32_t prefix_chars;   /* its p (chars per table key)                           */
@@ -229,8 +232,14 @@ typedef struct sas_stats {
     uint64_t tag_overflow_entries; /* SAS_BUILD_TAG_LINES: entries in the overflow array */
     uint64_t text2_bytes;    /* SAS_BUILD_TAG_LINES: the second packed-text copy (64 B off
                                 the 128-B line grid, so a tie's compare reads one line) */
-    uint64_t top2_bytes;     /* the binary-search pivot array: the LDS levels, then blocks of
-                                up to 3 levels in one 128-B line each (0 for bucket lines) */
+    uint64_t top2_bytes;     /* the LDS levels' pivot entries and their 16-char keys (0 for
+                                bucket lines)                                        */
+    uint32_t rel_levels;     /* the prefix-relative pivot blocks: the levels they reach
+                                (the pivot depth rounded up to 4-level blocks past the
+                                LDS levels, clamped to the iterations; 0 if none)    */
+    uint32_t rel_pad;        /* 0 */
+    uint64_t rel_bytes;      /* their array: one 32-B block {lcp of the block's bounds, the
+                                8 chars after it of each of 15 pivots} per 4-level subtree */
 } sas_stats;
 
 const char* sas_last_error(void);

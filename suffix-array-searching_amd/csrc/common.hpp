@@ -24,63 +24,21 @@
 #include "../../include/sst.h"
 
 #define SAS_TEXT_PAD_WORDS 4
-// The pivot array's first SAS_TOP_LEVELS levels are plain Eytzinger entries, staged in LDS:
-// PLAIN and INLINE stage their 16-char keys (4 B each: 16383 pivots, 64 KiB a workgroup)
-// and read a whole entry only on a 16-char tie; LCP and LLCP, which keep exact lcps, stage
-// SAS_TOP_FULL_LEVELS levels of whole keys and SA values (4095 pivots, 48 KiB) and read the
-// next levels' entries from the array.
+// The binary search's first SAS_TOP_LEVELS levels are plain Eytzinger entries whose 16-char
+// keys are staged in LDS (4 B each: 16383 pivots, 64 KiB a workgroup); a 16-char tie (or, for
+// the exact lcps of LCP / LLCP, a key that may end in padding) reads the whole entry.
 #define SAS_TOP_LEVELS 14
 #define SAS_TOP_NODES (1u << SAS_TOP_LEVELS)
-#define SAS_TOP_FULL_LEVELS 12
-#define SAS_TOP_FULL_NODES (1u << SAS_TOP_FULL_LEVELS)
-// Levels 13.. of the lockstep binary search (PLAIN, LCP, INLINE) read their pivot
-// (32-char key, SA value) from one 16-B entry of the top2 array instead of an SA word and a
-// text window.  Same-box: PLAIN 7.15 ms without it, 5.4-5.7 with 17 levels, 5.0-5.2 with
-// 19, 4.70 with 21, 4.50 with 22, 4.27 with 23 (128 MiB, the levels that stay inside the
-// Infinity Cache; profiles/r2/ab_top2_depth.txt).  Past those, a level from HBM is still
-// one request instead of two: 3.81 ms with 25 levels, 3.58 with 26, 3.11 with 28, 2.71
-// with 30 (16 GiB at n = 2^30) and 31 (profiles/r2/ab_top2_deeper*.txt).  The depth is a
-// build parameter (SAS_BUILD_TOP2_LEVELS(L) in sas.h), never derived from free memory:
-// the default is the SAS_TOP2_CACHE_LEVELS cache-resident levels, deeper levels are the
-// caller's explicit choice (and an ENOMEM if they do not fit).
-#define SAS_TOP2_CACHE_LEVELS 23
+// Past the LDS levels the pivots come from the prefix-relative blocks below ("rel"): an
+// SA word and a text window replaced by one request per 4 levels.  History: round 2 read a
+// 16-B {32-char key, SA} entry per level (PLAIN 7.15 ms per 10^7 without pivots, 4.27 with 23
+// levels, 2.71 with 30; profiles/r2/ab_top2_*.txt), round 4 first a 128-B line of 3 levels
+// of 16-char keys (2.97 ms at 23 levels), then the rel blocks (1.66 ms at 26 levels in the
+// same 136 MiB).  The depth is a build parameter (SAS_BUILD_TOP2_LEVELS(L) in sas.h, rounded
+// up to the block grid), never derived from free memory: the default is the
+// SAS_TOP2_CACHE_LEVELS levels that stay inside the 256 MiB Infinity Cache.
+#define SAS_TOP2_CACHE_LEVELS 26
 #define SAS_TOP2_MAX_LEVELS 31
-// The pivot array past the LDS levels is blocked (round 4): levels [SAS_TOP_LEVELS, L) are
-// cut into groups of at most SAS_TOP2_GROUP consecutive levels.  A group rooted at level d0
-// holds, for each of its 2^d0 root nodes, that root's h-level subtree as one block of 2^h
-// 16-B slots in local Eytzinger order (slot 0 unused; h = 3: 128 B, one line), or one slot
-// per node for h = 1.  A lookup's h probes in a group read one line.  Groups end at SAS_TOP2_CACHE_LEVELS, so no block mixes
-// the cache-resident levels with the HBM ones; in the cache part the first group is the
-// short one (its blocks are the fewest), in the HBM part the last.
-#define SAS_TOP2_GROUP 3
-struct Top2Layout {
-    uint64_t base[SAS_TOP2_MAX_LEVELS];  // entry offset of the level's group
-    uint8_t t[SAS_TOP2_MAX_LEVELS];      // level - the group's root level
-    uint8_t lg[SAS_TOP2_MAX_LEVELS];     // log2 slots per block (0: one slot per node)
-};
-// Inside a block of S = 2^lg slots (lg >= 2) the slots' keys come first, split into their
-// high halves (chars 0..15, u32 x S) and low halves (chars 16..31, u32 x S), then their SA
-// values (u64 x S); a 1-slot block is {key u64, SA u64}.  One lane reads a 3-level block's
-// seven 16-char keys with two 16-B loads of one line issued together (one request), and
-// the rest of a key or an SA value only when it needs them (k_sa_binary, PLAIN).
-// the first byte of Eytzinger node k's block at level d (d >= SAS_TOP_LEVELS)
-__host__ __device__ __forceinline__ uint64_t top2_block_byte(const Top2Layout& y, uint32_t d, uint32_t k) {
-    const uint32_t t = y.t[d], lg = y.lg[d];
-    const uint64_t blk = (uint64_t)(k >> t) - (1ull << (d - t));
-    return 16 * (y.base[d] + (blk << lg));
-}
-// node k's slot in its block
-__host__ __device__ __forceinline__ uint32_t top2_j(const Top2Layout& y, uint32_t d, uint32_t k) {
-    const uint32_t t = y.t[d];
-    return y.lg[d] ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
-}
-// byte offsets in the block of slot j's key halves and SA value
-struct Top2Slot { uint32_t hi, lo, sa; };
-__host__ __device__ __forceinline__ Top2Slot top2_slot_at(uint32_t lg, uint32_t j) {
-    if (!lg) return Top2Slot{4, 0, 8};  // {key u64 (low word first), SA}
-    const uint32_t S = 1u << lg;
-    return Top2Slot{4 * j, 4 * S + 4 * j, 8 * S + 8 * j};
-}
 // LDS staging of the plain levels' 16-char keys from their contiguous copy: 16-B loads, four
 // keys each (a workgroup's staging decides the time of small batches: configs[0]'s 10^4
 // queries)
@@ -92,28 +50,38 @@ __device__ __forceinline__ void stage_k16(uint32_t* s, const uint32_t* __restric
     for (uint32_t x = nw * 4 + threadIdx.x; x < nodes; x += blockDim.x) s[x] = g[x];
 }
 
-// fill the layout for L levels above D LDS levels; returns the array's entries
-static inline uint64_t top2_layout(uint32_t D, uint32_t L, Top2Layout* y) {
-    uint64_t entries = 1ull << D;
-    auto group = [&](uint32_t d0, uint32_t h) {
-        const uint32_t lg = h == 1 ? 0u : h;
-        for (uint32_t t = 0; t < h; t++) {
-            y->base[d0 + t] = entries;
-            y->t[d0 + t] = (uint8_t)t;
-            y->lg[d0 + t] = (uint8_t)lg;
-        }
-        entries += (1ull << d0) << lg;
-    };
-    const uint32_t C = L < SAS_TOP2_CACHE_LEVELS ? L : SAS_TOP2_CACHE_LEVELS;
-    uint32_t d = D;
-    if (C > D) {  // cache part: the short group first
-        const uint32_t r = (C - D) % SAS_TOP2_GROUP;
-        if (r) { group(d, r); d += r; }
-        for (; d < C; d += SAS_TOP2_GROUP) group(d, SAS_TOP2_GROUP);
+// The prefix-relative pivot blocks (round 4): levels [D, R) in groups of SAS_REL_GROUP; a
+// group rooted at level d0 holds one 32-B block per root node, 16 u16
+// slots: slot 0 = P, the lcp (capped at SAS_REL_PMAX) of the block interval's bounds
+// SA[l - 1] and SA[r] (0 at the array's ends), slots 1..15 = chars [P, P + 8) of the
+// pivots of its 4-level subtree in local Eytzinger order.  Every suffix strictly inside the
+// interval, and every query q with SA[l - 1] < q <= SA[r], starts with those P chars, so
+// chars [P, P + 8) decide key < q unless they tie (then the SA value and the text).  A 16-B
+// pair read of one block is one request for 4 levels, where a 128-B block of 16-char keys
+// held 3: at the same array size (136 MiB) 26 levels instead of 23.  PLAIN, LCP, LLCP and
+// INLINE all read them (LCP / LLCP take exact lcps off the keys, common.hpp callers).
+#define SAS_REL_GROUP 4
+#define SAS_REL_PMAX 24      // P + 8 <= 32: q's chars [P, P + 8) come from its first word
+#define SAS_REL_MAX_GROUPS 5  // (SAS_TOP2_MAX_LEVELS - SAS_TOP_LEVELS + 3) / 4
+static_assert((SAS_TOP2_MAX_LEVELS - SAS_TOP_LEVELS + SAS_REL_GROUP - 1) / SAS_REL_GROUP <= SAS_REL_MAX_GROUPS,
+              "rel groups");
+// the rel array's depth for a pivot array of L levels above D LDS levels: L rounded up to
+// the group grid, clamped to the iteration count (no rel levels when iters <= D)
+static inline uint32_t rel_levels_for(uint32_t D, uint32_t L, uint32_t iters) {
+    if (iters <= D || L <= D) return D;
+    const uint32_t R = D + (L - D + SAS_REL_GROUP - 1) / SAS_REL_GROUP * SAS_REL_GROUP;
+    return R < iters ? R : iters;
+}
+struct RelBase { uint64_t b[SAS_REL_MAX_GROUPS]; };  // byte offset of each group (root level D + 4g)
+// fill the groups' offsets; returns the array's bytes
+static inline uint64_t rel_layout(uint32_t D, uint32_t R, uint64_t* base) {
+    uint64_t b = 0;
+    for (uint32_t g = 0; g < SAS_REL_MAX_GROUPS; g++) {
+        base[g] = b;
+        const uint32_t d0 = D + SAS_REL_GROUP * g;
+        if (d0 < R) b += 32ull << d0;
     }
-    for (d = d > C ? d : C; d < L; d += SAS_TOP2_GROUP)  // HBM part: the short group last
-        group(d, L - d < SAS_TOP2_GROUP ? L - d : SAS_TOP2_GROUP);
-    return entries;
+    return b;
 }
 #define SAS_STREE_B 16                // keys per node / branching factor - 1
 #define SAS_STREE_MAX_LAYERS 16
@@ -178,13 +146,16 @@ struct sas_index {
     uint64_t stree_off[SAS_STREE_MAX_LAYERS] = {};
     uint32_t stree_lds_layers = 0;
     uint32_t stree_lds_nodes = 0;
-    uint4* top2 = nullptr;        // pivots {key64 lo, hi, SA lo, hi}: Eytzinger nodes 1..2^D - 1 (staged
-                                  // in LDS), then the blocked levels (top2_layout); index 0 unused
-    Top2Layout top2_lay{};
+    uint4* top2 = nullptr;        // the LDS levels' pivots {key64 lo, hi, SA lo, hi}: Eytzinger nodes
+                                  // 1..2^D - 1 (their 16-char keys are staged in LDS); index 0 unused
     uint64_t top2_entries = 0;
     uint32_t* top_k16 = nullptr;  // the plain levels' 16-char keys, contiguous (inside top2's allocation)
     uint32_t top_levels = 0;      // levels served from LDS
-    uint32_t top2_levels = 0;     // levels served from LDS or top2
+    uint32_t top2_levels = 0;     // levels served from LDS or the rel blocks
+    uint8_t* rel = nullptr;       // the prefix-relative pivot blocks (SAS_REL_GROUP), levels [top_levels, rel_levels)
+    RelBase rel_base{};
+    uint64_t rel_bytes = 0;
+    uint32_t rel_levels = 0;
     uint32_t iters = 0;           // ilog2(n) + 1
     uint32_t* scratch = nullptr;  // device flag word(s) for kernels (invalid query codes)
     // sector tree (SAS_ALGO_SECTOR): 32-B nodes

@@ -846,11 +846,10 @@ static int build_quad(sas_index* x, bool compact, uint32_t mode) {
 // ------------------------------------------------------------------ top of the binary search
 // Node k (1-based Eytzinger) = state after the path given by k's bits below
 // the leading one (0 = went left: r = mid, 1 = right: l = mid + 1); its entry =
-// {32-char key, SA value} of that state's pivot SA[(l + r) / 2], at index k for the D
-// LDS levels and at top2_slot (the blocked layout, common.hpp) below them.
+// {32-char key, SA value} of that state's pivot SA[(l + r) / 2], for the D LDS levels.
 template <int W>
-__global__ void k_top(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa, uint64_t sa_n,
-                      uint4* __restrict__ top2, uint32_t nodes, uint32_t D, Top2Layout lay) {
+__global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint4* __restrict__ top2,
+                      uint32_t nodes) {
     GRID_STRIDE(k, nodes) {
         uint64_t l = 0, r = sa_n, p = 0xFFFFFFFFu, key = 0;
         int depth = k ? 63 - __clzll(k) : 0;
@@ -863,25 +862,58 @@ __global__ void k_top(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa,
             p = sa[(l + r) >> 1];
             key = text_chars32(tw, p);
         }
-        if (depth < (int)D) {
-            top2[k] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
-        } else {
-            uint8_t* b = reinterpret_cast<uint8_t*>(top2) + top2_block_byte(lay, (uint32_t)depth, (uint32_t)k);
-            const Top2Slot o = top2_slot_at(lay.lg[depth], top2_j(lay, (uint32_t)depth, (uint32_t)k));
-            *reinterpret_cast<uint32_t*>(b + o.hi) = (uint32_t)(key >> 32);
-            *reinterpret_cast<uint32_t*>(b + o.lo) = (uint32_t)key;
-            *reinterpret_cast<uint64_t*>(b + o.sa) = p;
-            // slot 0's high word (no node) flags the block's suffixes of fewer than 32 chars,
-            // whose keys end in padding: an lcp read off their key would not be exact
-            const uint32_t j = top2_j(lay, (uint32_t)depth, (uint32_t)k);
-            if (lay.lg[depth] && !(l < r && p + 32 <= (uint64_t)n))
-                atomicOr(reinterpret_cast<uint32_t*>(b), 1u << j);
-        }
+        top2[k] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
     }
 }
 
 __global__ void k_top_k16(const uint4* __restrict__ top2, uint32_t nodes, uint32_t* __restrict__ k16) {
     GRID_STRIDE(k, nodes) k16[k] = top2[k].y;
+}
+
+// PLAIN's prefix-relative blocks (common.hpp SAS_REL_GROUP): node k at level d in [D, R),
+// t = (d - D) % 4 levels below its block's root.  The root's interval [l0, r0) gives P =
+// lcp(SA[l0 - 1], SA[r0]) (whole suffixes: never past either one's end; capped), the node's
+// pivot SA[(l + r) / 2] its chars [P, P + 8) (zero past the text's end) in slot
+// (1 << t) | (k's low t bits); the root thread writes P to slot 0.  Nodes whose interval is
+// empty keep 0 (never read: the search stops probing there).
+template <int W>
+__global__ void k_rel(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa, uint64_t sa_n,
+                      uint8_t* __restrict__ rel, uint64_t first, uint64_t nodes, uint32_t D,
+                      const RelBase base) {
+    GRID_STRIDE(i, nodes) {
+        const uint64_t k = first + i;
+        const int depth = 63 - __clzll(k);
+        const uint32_t t = (uint32_t)(depth - (int)D) % SAS_REL_GROUP;
+        const int d0 = depth - (int)t;
+        uint64_t l = 0, r = sa_n, l0 = 0, r0 = sa_n;
+        bool live = true;
+        for (int b = depth - 1; b >= 0; b--) {
+            if (depth - 1 - b == d0) { l0 = l; r0 = r; }
+            const uint64_t mid = (l + r) >> 1;
+            if (l >= r) { live = false; break; }
+            if ((k >> b) & 1) l = mid + 1; else r = mid;
+        }
+        if (depth == d0) { l0 = l; r0 = r; }
+        if (!(l < r)) live = false;
+        if (!(l0 < r0)) continue;  // the whole block is empty
+        uint32_t P = 0;
+        if (l0 > 0 && r0 < sa_n) {
+            const uint64_t a = sa[l0 - 1], c = sa[r0];
+            const uint64_t x = text_chars32(tw, a) ^ text_chars32(tw, c);
+            uint64_t lc = x ? (uint64_t)(__clzll(x) >> 1) : 32;
+            if (lc > n - a) lc = n - a;
+            if (lc > n - c) lc = n - c;
+            P = lc < SAS_REL_PMAX ? (uint32_t)lc : SAS_REL_PMAX;
+        }
+        const uint64_t k0 = k >> t;
+        uint16_t* blk = reinterpret_cast<uint16_t*>(rel + base.b[(d0 - (int)D) / SAS_REL_GROUP] +
+                                                    32 * (k0 - (1ull << d0)));
+        if (t == 0) blk[0] = (uint16_t)P;
+        if (live) {
+            const uint64_t p = sa[(l + r) >> 1];
+            blk[(1u << t) | (uint32_t)(k & ((1ull << t) - 1))] = (uint16_t)(text_chars32(tw, p + P) >> 48);
+        }
+    }
 }
 
 // ------------------------------------------------------------------ prefix table
@@ -1140,8 +1172,8 @@ static int build_tagged(sas_index* x, uint32_t p) {
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
-    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->scratch, x->sec_inner,
-                     x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table, x->tag_lines, x->tag_ovf,
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->rel, x->scratch,
+                     x->sec_inner, x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table, x->tag_lines, x->tag_ovf,
                      x->tag_first, x->text2_base};
     for (void* p : ptrs) if (p) (void)hipFree(p);
     sas_stage_pool_free(x->stage);
@@ -1698,30 +1730,26 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     x->iters = iters;
     if (!(flags & SAS_BUILD_TAG_LINES)) {
         x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
-        // the pivots of the first top2_levels iterations, 2^top2_levels 16-B entries: the
-        // SAS_TOP2_CACHE_LEVELS that stay inside the 256 MiB Infinity Cache (128 MiB) unless
-        // the caller asks for another depth (SAS_BUILD_TOP2_LEVELS).  The depth is never
-        // taken from free memory, so a text always gets the same index.  The probe sequence,
-        // and so every result, is the same at any depth.
+        // the pivots of the first L iterations: SAS_TOP2_CACHE_LEVELS (26: 136 MiB of rel
+        // blocks, inside the 256 MiB Infinity Cache) unless the caller asks for another depth
+        // (SAS_BUILD_TOP2_LEVELS), rounded up to the rel blocks' 4-level grid.  The depth is
+        // never taken from free memory, so a text always gets the same index.  The probe
+        // sequence, and so every result, is the same at any depth.
         const uint32_t req = (flags >> 27) & 31u;
         const uint32_t want = req ? req : SAS_TOP2_CACHE_LEVELS;
         const uint32_t lv = iters < want ? iters : want;
-        x->top2_levels = lv;
-        // the plain (LDS-staged) levels are part of the array: never more than it holds
+        // the plain (LDS-staged) levels are part of the depth: never more than it holds
         if (x->top_levels > lv) x->top_levels = lv;
-        const uint32_t nodes = 1u << x->top2_levels;
-        x->top2_entries = top2_layout(x->top_levels, x->top2_levels, &x->top2_lay);
+        const uint32_t nodes = 1u << x->top_levels;
+        x->top2_entries = nodes;
         DevBuf t2;
         const uint64_t k16_bytes = ((4ull << x->top_levels) + 15) & ~15ull;
         TRY(t2.alloc(x->top2_entries * 16 + k16_bytes, "top2"));
-        HIP_TRY(hipMemset(t2.p, 0, x->top2_entries * 16 + k16_bytes));  // unused block slots
         const dim3 tg(grid_for(nodes)), tb(256);
         if (W == 5)
-            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, n, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes,
-                               x->top_levels, x->top2_lay);
+            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes);
         else
-            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, n, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes,
-                               x->top_levels, x->top2_lay);
+            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes);
         HIP_TRY(hipGetLastError());
         x->top2 = static_cast<uint4*>(t2.release());
         // the plain levels' 16-char keys again, contiguous, for the LDS staging (stage_k16)
@@ -1729,6 +1757,28 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         hipLaunchKernelGGL(k_top_k16, dim3(grid_for(1ull << x->top_levels)), tb, 0, 0, x->top2, 1u << x->top_levels,
                            x->top_k16);
         HIP_TRY(hipGetLastError());
+        // the levels past the LDS ones: prefix-relative blocks, 4 levels a block (common.hpp)
+        x->rel_levels = rel_levels_for(x->top_levels, lv, iters);
+        if (x->rel_levels > x->top_levels) {
+            RelBase& rb = x->rel_base;
+            x->rel_bytes = rel_layout(x->top_levels, x->rel_levels, rb.b);
+            DevBuf rl;
+            TRY(rl.alloc(x->rel_bytes, "rel"));
+            HIP_TRY(hipMemset(rl.p, 0, x->rel_bytes));
+            const uint64_t first = 1ull << x->top_levels, cnt = (1ull << x->rel_levels) - first;
+            if (W == 5)
+                hipLaunchKernelGGL(k_rel<5>, dim3(grid_for(cnt)), tb, 0, 0, x->text_w, n, SaView<5>{x->sa}, sa_n,
+                                   rl.as<uint8_t>(), first, cnt, x->top_levels, rb);
+            else
+                hipLaunchKernelGGL(k_rel<4>, dim3(grid_for(cnt)), tb, 0, 0, x->text_w, n, SaView<4>{x->sa}, sa_n,
+                                   rl.as<uint8_t>(), first, cnt, x->top_levels, rb);
+            HIP_TRY(hipGetLastError());
+            x->rel = static_cast<uint8_t*>(rl.release());
+            x->top2_levels = x->rel_levels;
+        } else {
+            x->rel_levels = 0;
+            x->top2_levels = x->top_levels;
+        }
     }
     if ((flags & SAS_BUILD_TAGGED) && (flags & SAS_BUILD_TAG_LINES)) TRY(build_tag_lines(x, (flags >> 16) & 31));
     else if (flags & SAS_BUILD_TAGGED) TRY(build_tagged(x, (flags >> 16) & 31));
@@ -1770,8 +1820,11 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.text2_bytes = x->text2 ? x->text_words * 8 : 0;
     st.tag_overflow_entries = x->tag_ovf_n;
     st.top2_bytes = x->top2 ? x->top2_entries * 16 + (((4ull << x->top_levels) + 15) & ~15ull) : 0;
+    st.rel_levels = x->rel ? x->rel_levels : 0;
+    st.rel_bytes = x->rel ? x->rel_bytes : 0;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
-                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes + st.top2_bytes;
+                     st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes + st.top2_bytes +
+                     st.rel_bytes;
     st.build_total_ns = now_ns() - t0;
     *out = x;
     x = nullptr;  // disarm guard

@@ -54,9 +54,11 @@ struct SearchArgs {
     uint32_t prefix_hi40;    // inline slots: SA bits 32..39 in slot 1's rank word
     const uint4* top2;
     const uint32_t* top_k16;  // the plain levels' 16-char keys, contiguous (LDS staging)
-    Top2Layout top2_lay;     // the blocked levels' addresses (common.hpp)
     uint32_t top_levels;
     uint32_t top2_levels;
+    const uint8_t* rel;      // PLAIN's prefix-relative pivot blocks (common.hpp SAS_REL_GROUP)
+    RelBase rel_base;
+    uint32_t rel_levels;
     uint32_t iters;
     const uint32_t* stree;
     uint64_t stree_off[SAS_STREE_MAX_LAYERS];
@@ -168,54 +170,25 @@ __device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, ui
 // RANGE (SAS_PREFIX_RANGE, PLAIN / LCP without the LDS top): start from the prefix
 // table's range for q's first p chars instead of [0, sa_n), exactly as the reference's
 // binary_search does (sas/sa_search.rs:98-101) once its p is not 0
-// LCP / LLCP read a pivot block's whole keys at its root (4 loads, one request) and take
-// exact lcps from them (0: one whole entry per level, as before round 4's A/B)
 // PLAIN over a u32 SA: a range of at most this many ranks (4 or 8; 0: off) has its SA words
 // loaded together for the remaining probes
 #ifndef SAS_PLAIN_SA_RUN
 #define SAS_PLAIN_SA_RUN 8
 #endif
 static_assert(SAS_PLAIN_SA_RUN == 0 || SAS_PLAIN_SA_RUN == 4 || SAS_PLAIN_SA_RUN == 8, "SAS_PLAIN_SA_RUN: 0, 4 or 8");
-#ifndef SAS_LCP_BLOCK_KEYS
-#define SAS_LCP_BLOCK_KEYS 1
-#endif
 #define BS_PLAIN 0
 #define BS_MLR 1
 #define BS_LLCP 2
 template <int QW, int MODE, bool TOP, int W, bool RANGE = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
-    // PLAIN: the 16-char keys of the top SAS_TOP_LEVELS levels; LCP / LLCP: whole keys and
-    // SA values of the top SAS_TOP_FULL_LEVELS (common.hpp)
-    constexpr bool K16 = MODE == BS_PLAIN;
-    __shared__ uint32_t s_k16[TOP && K16 ? SAS_TOP_NODES : 1];
-    __shared__ uint64_t s_key[TOP && !K16 ? SAS_TOP_FULL_NODES : 1];
-    __shared__ sa_val_t<W> s_sa[TOP && !K16 ? SAS_TOP_FULL_NODES : 1];
+    // the 16-char keys of the top SAS_TOP_LEVELS levels in LDS, then the prefix-relative
+    // blocks (common.hpp)
+    __shared__ uint32_t s_k16[TOP ? SAS_TOP_NODES : 1];
     const SaView<W> sa{a.sa};
-    uint32_t D = 0, DL = 0;  // plain levels of the pivot array; those staged in LDS
+    uint32_t D = 0;  // the pivot array's plain levels, staged in LDS
     if (TOP) {
         D = a.top_levels;
-        DL = K16 ? D : (D < SAS_TOP_FULL_LEVELS ? D : SAS_TOP_FULL_LEVELS);
-        const uint32_t nodes = 1u << DL;
-        if (K16) {
-            stage_k16(s_k16, a.top_k16, nodes);
-        } else {  // whole entries: four loads in flight per thread before the stores
-            for (uint32_t k0 = threadIdx.x; k0 < nodes; k0 += 4 * blockDim.x) {
-                uint4 e[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t k = k0 + u * blockDim.x;
-                    if (k < nodes) e[u] = a.top2[k];
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t k = k0 + u * blockDim.x;
-                    if (k < nodes) {
-                        s_key[k] = (uint64_t)e[u].x | ((uint64_t)e[u].y << 32);
-                        s_sa[k] = (sa_val_t<W>)((uint64_t)e[u].z | ((uint64_t)e[u].w << 32));
-                    }
-                }
-            }
-        }
+        stage_k16(s_k16, a.top_k16, 1u << D);
         __syncthreads();
     }
     uint32_t bad = 0;
@@ -258,9 +231,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         };
         uint32_t it = 0;
         if (TOP) {
-            // the plain levels: from LDS (PLAIN: decided by the 16-char key unless it ties with
-            // q's first min(m, 16) chars, as on the blocked levels below), then -- LCP / LLCP
-            // past their SAS_TOP_FULL_LEVELS -- one whole entry each from the array
+            // the plain levels from LDS: decided by the 16-char key unless it ties with q's
+            // first min(m, 16) chars (then the whole entry from the array)
             for (; it < D; ++it) {
                 if (l < r) {
                     const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
@@ -268,21 +240,18 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     uint32_t lcp = 0;
                     sa_val_t<W> p = 0;
                     bool lt, pk = true;
-                    if (K16) {
-                        const uint32_t c = q.m < 16 ? q.m : 16;
-                        const uint32_t mk = c ? ~0u << (32 - 2 * c) : 0u;
-                        const uint32_t av = s_k16[k] & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
-                        if (av != bv) {
-                            lt = av < bv;
-                            pk = false;
-                        } else {
-                            const uint4 e = a.top2[k];
-                            p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
-                            lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
-                        }
-                    } else if (it < DL) {
-                        p = s_sa[k];
-                        lt = suffix_less_key<QW>(a.tw, n, p, s_key[k], q, h, &lcp);
+                    // LCP / LLCP also need the exact lcp: the first differing char, unless the
+                    // key is below q there and zero from there on (maybe the zero padding of a
+                    // suffix shorter than 16 chars: then the whole entry)
+                    const uint32_t c = q.m < 16 ? q.m : 16;
+                    const uint32_t mk = c ? ~0u << (32 - 2 * c) : 0u;
+                    const uint32_t kk = s_k16[k];
+                    const uint32_t av = kk & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
+                    const uint32_t dc = av != bv ? (uint32_t)__clz(av ^ bv) >> 1 : 16u;
+                    if (av != bv && (MODE == BS_PLAIN || !(av < bv && (kk << (2 * dc)) == 0))) {
+                        lt = av < bv;
+                        lcp = dc;
+                        pk = false;
                     } else {
                         const uint4 e = a.top2[k];
                         p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
@@ -292,79 +261,53 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                     take(mid, lt, lcp, p, pk);
                 }
             }
-            // the pivot array (cache-resident; deeper, HBM) instead of an SA word and a text
-            // window, block by block: a group's levels share one line (common.hpp top2_layout)
-            const uint8_t* t2 = reinterpret_cast<const uint8_t*>(a.top2);
-            while (it < a.top2_levels) {
-                const uint32_t lg = a.top2_lay.lg[it];
-                const uint32_t levels = lg ? lg : 1u;
-                const uint8_t* blk = t2 + top2_block_byte(a.top2_lay, it, k);  // k: the group's root node
-                uint4 kh0 = make_uint4(0, 0, 0, 0), kh1 = kh0, kl0 = kh0, kl1 = kh0;
-                if (lg >= 2 && l < r) {
-                    // the high halves of all of the block's keys at once -- two (one) 16-B loads
-                    // of one line, one request; LCP / LLCP also the low halves (exact lcps
-                    // need all 32 chars), two (one) more loads of the same line
-                    kh0 = *reinterpret_cast<const uint4*>(blk);
-                    if (lg == 3) kh1 = *reinterpret_cast<const uint4*>(blk + 16);
-                    if (MODE != BS_PLAIN && SAS_LCP_BLOCK_KEYS) {
-                        kl0 = *reinterpret_cast<const uint4*>(blk + (4u << lg));
-                        if (lg == 3) kl1 = *reinterpret_cast<const uint4*>(blk + (4u << lg) + 16);
-                    }
+            // the prefix-relative blocks, 4 levels from one 32-B read (two 16-B loads of one
+            // line, one request): the 8 chars after the block bounds' common prefix of P chars
+            // decide each probe unless they tie with q's (then the SA value -- LLCP: from its
+            // entry -- and the text from char P + c).  q starts with those P chars (common.hpp),
+            // and a key padded past its suffix's end that differs from q there is a proper
+            // prefix of q (key < q)
+            while (it < a.rel_levels) {
+                const uint32_t hh = a.rel_levels - it < SAS_REL_GROUP ? a.rel_levels - it : SAS_REL_GROUP;
+                uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0;
+                if (l < r) {
+                    const uint8_t* blk = a.rel + a.rel_base.b[(it - D) / SAS_REL_GROUP] + 32ull * (k - (1u << it));
+                    b0 = *reinterpret_cast<const uint4*>(blk);
+                    if (hh == SAS_REL_GROUP) b1 = *reinterpret_cast<const uint4*>(blk + 16);
                 }
-                for (uint32_t t = 0; t < levels && it < a.top2_levels; ++t, ++it) {
+                const uint32_t P = b0.x & 0xFFFFu;
+                const uint32_t c0 = q.m > P ? q.m - P : 0u;
+                const uint32_t c = c0 < 8 ? c0 : 8u;
+                const uint32_t mk = c ? (0xFFFFu << (16 - 2 * c)) & 0xFFFFu : 0u;
+                const uint32_t qk = (uint32_t)((q.w[0] << (2 * P)) >> 48) & mk;
+                for (uint32_t t = 0; t < hh; ++t, ++it) {
                     if (!(l < r)) continue;
                     const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
-                    const uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
-                    const uint32_t j = lg ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
-                    const Top2Slot o = top2_slot_at(lg, j);
+                    const uint32_t j = (1u << t) | (k & ((1u << t) - 1u));
+                    const uint4 v = j >= 8 ? b1 : b0;
+                    const uint32_t cw = (j >> 1) & 3u;
+                    const uint32_t wv = cw == 0 ? v.x : cw == 1 ? v.y : cw == 2 ? v.z : v.w;
+                    const uint32_t kr = ((j & 1u) ? (wv >> 16) : wv) & 0xFFFFu;
+                    const uint32_t key = kr & mk;
+                    // LCP / LLCP: lcp = P + the first differing char, unless the key is below q
+                    // there and zero from there on (maybe padding past its suffix's end)
+                    const uint32_t dc = key != qk ? ((uint32_t)__clz(key ^ qk) - 16u) >> 1 : 8u;
                     sa_val_t<W> p = 0;
-                    uint32_t lcp = 0;
-                    bool lt = false, pk = true, done = false;
-                    if (MODE == BS_PLAIN && lg >= 2) {
-                        // decide from the key's first 16 chars when they differ from q's first
-                        // min(m, 16); a difference only past the suffix's end (zero padding)
-                        // makes it a proper prefix of q: key < q there, as slice order has it.
-                        // Else the rest of the key and the SA value (one more request)
-                        const uint4 v = (j >> 2) ? kh1 : kh0;
-                        const uint32_t khi = (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
-                        const uint32_t c = q.m < 16 ? q.m : 16;
-                        const uint32_t mk = c ? ~0u << (32 - 2 * c) : 0u;
-                        const uint32_t av = khi & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
-                        if (av != bv) {
-                            lt = av < bv;
-                            pk = false;
-                            done = true;
+                    uint32_t lcp = P + dc;
+                    bool lt, pk = false;
+                    if (key != qk && (MODE == BS_PLAIN || !(key < qk && ((kr << (2 * dc)) & 0xFFFFu) == 0))) {
+                        lt = key < qk;
+                    } else {
+                        if (MODE == BS_LLCP) {
+                            const uint4 e = a.llcp[mid];
+                            p = (sa_val_t<W>)((uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32));
+                        } else {
+                            p = (sa_val_t<W>)sa[mid];
                         }
-                    } else if (MODE != BS_PLAIN && SAS_LCP_BLOCK_KEYS && lg >= 2 && h < 32 && !((kh0.x >> j) & 1u)) {
-                        // LCP / LLCP: the whole 32-char key of a suffix of >= 32 chars (slot 0's
-                        // high word flags the block's shorter ones) gives the exact lcp when it
-                        // differs from q's first min(m, 32) chars, and for m <= 32 when it does
-                        // not (then lcp = m and suffix >= q); else the SA value and the text
-                        const uint4 vh = (j >> 2) ? kh1 : kh0, vl = (j >> 2) ? kl1 : kl0;
-                        const uint32_t jj = j & 3;
-                        const uint64_t key =
-                            ((uint64_t)(jj == 0 ? vh.x : jj == 1 ? vh.y : jj == 2 ? vh.z : vh.w) << 32) |
-                            (jj == 0 ? vl.x : jj == 1 ? vl.y : jj == 2 ? vl.z : vl.w);
-                        const uint32_t c = q.m < 32 ? q.m : 32;
-                        const uint64_t mk = chars_mask(c);
-                        const uint64_t av = key & mk, bv = q.w[0] & mk;
-                        if (av != bv) {
-                            lt = av < bv;
-                            lcp = (uint32_t)(__clzll(av ^ bv) >> 1);
-                            pk = false;
-                            done = true;
-                        } else if (q.m <= 32) {
-                            lt = false;
-                            lcp = q.m;
-                            pk = false;
-                            done = true;
-                        }
-                    }
-                    if (!done) {  // the whole key and the SA value (one line)
-                        const uint64_t key = ((uint64_t)*reinterpret_cast<const uint32_t*>(blk + o.hi) << 32) |
-                                             *reinterpret_cast<const uint32_t*>(blk + o.lo);
-                        p = (sa_val_t<W>)*reinterpret_cast<const uint64_t*>(blk + o.sa);
-                        lt = suffix_less_key<QW>(a.tw, n, p, key, q, h, &lcp);
+                        // chars [0, P + c) are known equal unless the keys differ (LLCP's
+                        // padding case): then from P
+                        lt = suffix_less_from<QW>(a.tw, n, p, q, key != qk ? P : P + c, &lcp);
+                        pk = true;
                     }
                     k = 2 * k + (lt ? 1u : 0u);
                     take(mid, lt, lcp, p, pk);
@@ -436,7 +379,14 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         // SA[r] not seen yet: r never moved (RANGE: the table's range end) or moved last on a
         // pivot decided from its key alone (rare below a 23-level array: a right move on
         // every one of the last levels' SA probes would have to be missing)
-        if (!prv && r < a.sa_n) pr = (sa_val_t<W>)sa[r];
+        if (!prv && r < a.sa_n) {
+            if (MODE == BS_LLCP) {  // LLCP reads its own entries only
+                const uint4 e = a.llcp[r];
+                pr = (sa_val_t<W>)((uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32));
+            } else {
+                pr = (sa_val_t<W>)sa[r];
+            }
+        }
         a.out_pos[i] = (r >= a.sa_n) ? a.next_pos : (uint64_t)pr;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1352,35 +1302,44 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                     take(mid, ge, p);
                 }
             }
-            // the pivot array block by block, as PLAIN: a block's 16-char key halves in one
-            // request; the rest of a key and its SA value only on a tie of the first 16 chars
-            // (key != K64 decides key > K64, the sector predicate)
-            const uint8_t* t2 = reinterpret_cast<const uint8_t*>(a.top2);
-            while (it < a.top2_levels) {
-                const uint32_t lg = a.top2_lay.lg[it];
-                const uint32_t levels = lg ? lg : 1u;
-                const uint8_t* blk = t2 + top2_block_byte(a.top2_lay, it, k);
-                uint4 kh0 = make_uint4(0, 0, 0, 0), kh1 = kh0;
-                if (lg >= 2 && l < r) {
-                    kh0 = *reinterpret_cast<const uint4*>(blk);
-                    if (lg == 3) kh1 = *reinterpret_cast<const uint4*>(blk + 16);
+            // the prefix-relative blocks, as PLAIN: 4 levels from one 32-B read; an 8-char tie
+            // reads the probe's own entry (key != K64 decides key > K64, the sector predicate)
+            while (it < a.rel_levels) {
+                const uint32_t hh = a.rel_levels - it < SAS_REL_GROUP ? a.rel_levels - it : SAS_REL_GROUP;
+                uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0;
+                if (l < r) {
+                    const uint8_t* blk = a.rel + a.rel_base.b[(it - D) / SAS_REL_GROUP] + 32ull * (k - (1u << it));
+                    b0 = *reinterpret_cast<const uint4*>(blk);
+                    if (hh == SAS_REL_GROUP) b1 = *reinterpret_cast<const uint4*>(blk + 16);
                 }
-                for (uint32_t t = 0; t < levels && it < a.top2_levels; ++t, ++it) {
+                const uint32_t P = b0.x & 0xFFFFu;
+                const uint32_t c0 = q.m > P ? q.m - P : 0u;
+                const uint32_t c = c0 < 8 ? c0 : 8u;
+                const uint32_t mk = c ? (0xFFFFu << (16 - 2 * c)) & 0xFFFFu : 0u;
+                const uint32_t qk = (uint32_t)((K64 << (2 * P)) >> 48) & mk;
+                for (uint32_t t = 0; t < hh; ++t, ++it) {
                     if (!(l < r)) continue;
                     const uint64_t mid = (l + r) >> 1;
-                    const uint32_t j = lg ? ((1u << t) | (k & ((1u << t) - 1u))) : 0u;
-                    const Top2Slot o = top2_slot_at(lg, j);
+                    const uint32_t j = (1u << t) | (k & ((1u << t) - 1u));
+                    const uint4 v = j >= 8 ? b1 : b0;
+                    const uint32_t cw = (j >> 1) & 3u;
+                    const uint32_t wv = cw == 0 ? v.x : cw == 1 ? v.y : cw == 2 ? v.z : v.w;
+                    const uint32_t key = ((j & 1u) ? (wv >> 16) : wv) & mk;
                     bool ge;
                     uint64_t p = QUAD_NO_SA;
-                    const uint4 v = (j >> 2) ? kh1 : kh0;
-                    const uint32_t khi = (j & 3) == 0 ? v.x : (j & 3) == 1 ? v.y : (j & 3) == 2 ? v.z : v.w;
-                    if (lg >= 2 && khi != (uint32_t)(K64 >> 32)) {
-                        ge = khi > (uint32_t)(K64 >> 32);
+                    if (key != qk) {
+                        ge = key > qk;
                     } else {
-                        const uint64_t key = ((uint64_t)*reinterpret_cast<const uint32_t*>(blk + o.hi) << 32) |
-                                             *reinterpret_cast<const uint32_t*>(blk + o.lo);
-                        p = *reinterpret_cast<const uint64_t*>(blk + o.sa);
-                        ge = sector_ge<QW>(key, p, K64, a, q);
+                        uint64_t ek;
+                        if (KO) {
+                            ek = quad_entry_key<true>(a, mid);
+                            p = ek == K64 ? quad_entry_sa<true, W>(a, mid) : QUAD_NO_SA;
+                        } else {
+                            const uint4 e = a.quad_leaves[mid];
+                            ek = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                            p = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+                        }
+                        ge = sector_ge<QW>(ek, p, K64, a, q);
                     }
                     k = 2 * k + (ge ? 0u : 1u);
                     take(mid, ge, p);
@@ -1885,12 +1844,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_interp(SearchArgs a, uin
 // single candidate whose tag ties q's (a positive query's own suffix; read as 16-B word
 // pairs, suffix_less_from_x2), and its position straight from the entry.  Larger buckets
 // continue with a binary search over the rest.
-#ifndef SAS_LLCP_TOP2_LEVELS
-#define SAS_LLCP_TOP2_LEVELS 31
-#endif
-#ifndef SAS_INLINE_TOP2_LEVELS
-#define SAS_INLINE_TOP2_LEVELS 31
-#endif
 #ifndef SAS_TAG_WIN
 #define SAS_TAG_WIN 8
 #endif
@@ -2667,14 +2620,8 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
-    // LLCP and INLINE read every level of the pivot array the index holds (31 = no cap): a
-    // blocked level costs them a third of a request against one request for their own entry
-    // (round 3, unblocked: pivot levels past the cache-resident ones cost LLCP time, 3.08 ms
-    // with 21 levels, 3.29 with 23)
-    if (algo == SAS_ALGO_LLCP && a.top2_levels > SAS_LLCP_TOP2_LEVELS) a.top2_levels = SAS_LLCP_TOP2_LEVELS;
-    // INLINE's own probes read one 16-B fused entry in rank order, whose last levels share
-    // lines; the pivot array past its cache-resident levels only moves them apart
-    if (algo == SAS_ALGO_INLINE && a.top2_levels > SAS_INLINE_TOP2_LEVELS) a.top2_levels = SAS_INLINE_TOP2_LEVELS;
+    // PLAIN, LLCP and INLINE read the pivot levels past the LDS ones from the prefix-relative
+    // blocks, which the build makes wherever the array has such levels
     const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
@@ -2755,9 +2702,11 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.prefix_hi40 = x->prefix_hi40;
     a.top2 = x->top2;
     a.top_k16 = x->top_k16;
-    a.top2_lay = x->top2_lay;
     a.top_levels = x->top_levels;
     a.top2_levels = x->top2_levels;
+    a.rel = x->rel;
+    a.rel_base = x->rel_base;
+    a.rel_levels = x->rel ? x->rel_levels : 0;
     a.iters = x->iters;
     a.stree = x->stree;
     for (int h = 0; h < SAS_STREE_MAX_LAYERS; h++) a.stree_off[h] = x->stree_off[h];

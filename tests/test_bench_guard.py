@@ -65,40 +65,44 @@ def test_byte_model_splits_served_levels():
     q = bench.bytes_per_lookup("quad", st, n, m, 8.0)
     # quad at 2^30: 3 LDS layers, the 206 KB / 3.5 MB / 59 MB layers in cache, 1 GB + leaves in HBM
     assert q["lds"] == 3 * 64 and q["cache"] == 3 * 64 and q["hbm"] == 2 * 64 + m + 8
-    # PLAIN: the 14 plain levels' 16-char keys in LDS (4 B), then the pivot array
-    p = bench.bytes_per_lookup("plain", st, n, m, 31.0)
-    assert p["lds"] == 14 * 4 and p["cache"] == 7 * 16 and p["hbm"] == 10 * (4 + m / 4) + m + 8
-    p23 = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
-    assert p23["cache"] == 9 * 16 and p23["hbm"] == 8 * (4 + m / 4) + m + 8
-    # LLCP: whole keys + SA values of 12 levels in LDS, levels 13-14 read from the array
-    ll = bench.bytes_per_lookup("llcp", dict(st, top2_levels=23), n, m, 31.0)
-    assert ll["lds"] == 12 * 12 and ll["cache"] == 11 * 16 and ll["requests_model"]["cache"] == 2 + 9
+    # PLAIN: the 14 plain levels' 16-char keys in LDS (4 B), then one 32-B prefix-relative block
+    # per 4 levels (26 levels: 3 blocks, cache-resident), then SA word + text window per probe
+    st26 = dict(st, top2_levels=26, rel_levels=26, rel_bytes=bench.rel_bytes(14, 26))
+    p = bench.bytes_per_lookup("plain", st26, n, m, 31.0)
+    assert p["lds"] == 14 * 4 and p["cache"] == 3 * 32 and p["hbm"] == 5 * (4 + m / 4) + m + 8
+    assert p["requests_model"] == {"cache": 3.0, "hbm": 5 * 2 + m / 128}
+    # LLCP: the same pivots (exact lcps off the keys), then one 16-B entry per probe
+    ll = bench.bytes_per_lookup("llcp", st26, n, m, 31.0)
+    assert ll["lds"] == 14 * 4 and ll["cache"] == 3 * 32 and ll["hbm"] == 5 * 16 + m + 8
+    assert ll["requests_model"] == {"cache": 3.0, "hbm": 5 + m / 128}
     h = bench.bytes_per_lookup("prefix", st, n, m, 1.0)
     assert h["hbm"] == 32 + m + 8 and h["cache"] == 0 and h["lds"] == 0
     assert bench._tree_layers(n, 4, 64, 17, 64, 8)[-1] == n // 4 * 64
 
 
 def test_byte_model_hbm_pivot_levels():
-    """The deep pivot array (SAS_BUILD_TOP2_LEVELS = 30): levels 13-23 cache-resident, 24-30
-    one 16-B HBM entry each, level 31 an SA word + a text window; requests by tier."""
-    st = {"sa_width": 4, "top_levels": 14, "top2_levels": 30}
+    """Deep pivots (SAS_BUILD_TOP2_LEVELS = 30): blocks of levels 15-18, 19-22, 23-26
+    cache-resident (136 MiB), 27-30 from HBM (the 2 GiB group), level 31 an SA word + a text
+    window; requests by tier."""
+    assert bench.rel_bytes(14, 26) == 32 * ((1 << 14) + (1 << 18) + (1 << 22))
+    assert [c for _, _, c in bench.rel_groups(14, 30)] == [True, True, True, False]
+    st = {"sa_width": 4, "top_levels": 14, "top2_levels": 30, "rel_levels": 30, "rel_bytes": bench.rel_bytes(14, 30)}
     n, m = 1 << 30, 32
     p30 = bench.bytes_per_lookup("plain", st, n, m, 31.0)
-    assert p30["lds"] == 14 * 4 and p30["cache"] == 9 * 16
-    assert p30["hbm"] == 7 * 16 + 1 * (4 + m / 4) + m + 8
-    # blocked pivots: one request per block entered (blocks of levels 15-17, 18-20, 21-23 in
-    # the cache; 24-26, 27-29, 30 from HBM), then level 31's SA word + text window
-    assert p30["requests_model"] == {"cache": 3.0, "hbm": 3 + 2 * 1 + m / 128}
-    # fewer probes than the pivot levels (a short range): no SA-level term
+    assert p30["lds"] == 14 * 4 and p30["cache"] == 3 * 32
+    assert p30["hbm"] == 32 + 1 * (4 + m / 4) + m + 8
+    assert p30["requests_model"] == {"cache": 3.0, "hbm": 1 + 2 * 1 + m / 128}
+    # fewer probes than the pivot levels (a short range): blocks entered only, SA[r] at the end
     p20 = bench.bytes_per_lookup("plain", st, n, m, 20.0)
-    assert p20["hbm"] == m + 8 and p20["cache"] == 6 * 16
-    # INLINE reads every pivot level the array holds (round 4: blocked levels cost it less than
-    # its own rank-ordered entries): levels 24-30 in 3 blocks, then level 31's fused entry
+    assert p20["hbm"] == 4 + m + 8 and p20["cache"] == 2 * 32
+    assert p20["requests_model"] == {"cache": 2.0, "hbm": 1 + m / 128}
+    # INLINE: the same blocks, then level 31's fused entry
     pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
-    assert pin["hbm"] == 7 * 16 + 16 + m + 8 and pin["requests_model"]["hbm"] == 3 + 1 + m / 128
-    assert pin["requests_model"]["cache"] == 3.0  # INLINE reads a block's 16-char keys at once, as PLAIN
+    assert pin["hbm"] == 32 + 16 + m + 8 and pin["requests_model"]["hbm"] == 1 + 1 + m / 128
+    assert pin["requests_model"]["cache"] == 3.0
     # the split: model HBM requests first, the rest of the PMC count is cache-served
-    bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23), n, m, 31.0)
+    bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23, rel_levels=23, rel_bytes=bench.rel_bytes(14, 23)),
+                                 n, m, 31.0)
     assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
     nq, kms = 10_000_000, 5.0
     sp = bench.request_split(bpl, {"rdreq_per_launch": 20.0 * nq}, nq, kms)
@@ -147,10 +151,11 @@ def test_reference_sweep_sizes():
 
 def _stats_2e30():
     """sas_stats of the default bench index at n = 2^30 (text 2-bit packed + 4 pad words,
-    u32 SA, 23 pivot levels, fused quad leaves, p = 16 two-suffix inline table)."""
+    u32 SA, 26 pivot levels, fused quad leaves, p = 16 two-suffix inline table)."""
     n = 1 << 30
     return {"n": n, "sa_entries": n, "text_bytes": (n // 32 + 4) * 8, "sa_bytes": 4 * n, "sa_width": 4,
-            "top_levels": 14, "top2_levels": 23, "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
+            "top_levels": 14, "top2_levels": 26, "rel_levels": 26, "rel_bytes": 32 * ((1 << 14) + (1 << 18) + (1 << 22)),
+            "top2_bytes": (16 << 14) + (4 << 14), "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
             "quad_bytes": 18_325_000_000, "sector_bytes": 19_400_000_000, "stree_bytes": 4_563_402_752,
             "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "index_bytes": 205_755_777_696}
 
@@ -161,12 +166,13 @@ def test_footprint_per_algorithm():
     st = _stats_2e30()
     gib = 1 << 30
     text = st["text_bytes"]
-    piv23 = 16 * bench.top2_entries(14, 23)[0]  # the blocked pivot array, ~146 MiB
-    assert 128 << 20 < piv23 < 150 << 20
-    assert bench.footprint("plain", st) == 4 * gib + text + piv23  # ~4.4 GiB
+    piv = (20 << 14) + st["rel_bytes"]  # the LDS levels' entries + keys, the 136 MiB of rel blocks
+    assert 136 << 20 < piv < 137 << 20
+    assert bench.footprint("plain", st) == 4 * gib + text + piv  # ~4.4 GiB
     assert 4.3 * gib < bench.footprint("plain", st) < 4.5 * gib
-    assert bench.footprint("plain", dict(st, top2_levels=30)) == 4 * gib + text + 16 * bench.top2_entries(14, 30)[0]
-    assert bench.footprint("llcp", st) == 16 * gib + text + 16 * bench.top2_entries(14, 23)[0]
+    st30 = dict(st, top2_levels=30, rel_levels=30, rel_bytes=bench.rel_bytes(14, 30))
+    assert bench.footprint("plain", st30) == 4 * gib + text + (20 << 14) + bench.rel_bytes(14, 30)
+    assert bench.footprint("llcp", st) == 16 * gib + text + piv
     assert bench.footprint("quad", st) == st["quad_bytes"] + text  # ~17 GiB
     assert bench.footprint("prefix", st) == 128 * gib + 32 + 16 * gib + text  # table + fused leaves + text
     assert bench.footprint("prefix_packed", st) == bench.footprint("prefix", st)

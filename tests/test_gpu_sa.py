@@ -1073,11 +1073,12 @@ def test_occurrence_ranges_inline_slots(sas):
 
 
 def test_blocked_pivot_levels(sas):
-    """The pivot array's blocked layout (levels past the 12 LDS levels in blocks of up to 3
-    levels per 128-B line, cache part and HBM part grouped apart): every depth 13..25 on an
-    n = 3 x 2^23 text (25 iterations) gives PLAIN, LCP, LLCP and INLINE the positions and
-    probe counts of the oracle's binary_search (sas/sa_search.rs:98-112) -- groups of 1, 2
-    and 3 levels in both parts -- and sas_stats.top2_bytes is the layout's size."""
+    """The pivot depth (SAS_BUILD_TOP2_LEVELS): the LDS levels' entries (16-char keys in LDS),
+    then prefix-relative blocks of 4 levels, the depth rounded up to that grid and clamped to
+    the 25 iterations of an n = 3 x 2^23 text.  Every depth (blocks of 1..4 levels, none at
+    all) gives PLAIN, LCP, LLCP and INLINE the positions and probe counts of the oracle's
+    binary_search (sas/sa_search.rs:98-112), and sas_stats top2_bytes / rel_bytes are the
+    layout's sizes."""
     import bench
     n = 3 << 23
     t = sas.random_string(n, seed=123)
@@ -1088,15 +1089,18 @@ def test_blocked_pivot_levels(sas):
     qs[: nq // 4] = rng.integers(0, 4, (nq // 4, m))
     qb = qs.reshape(-1).copy()
     ref = None
-    for L in (0, 5, 13, 15, 16, 17, 18, 21, 24, 25):
+    for L in (0, 5, 13, 14, 15, 16, 17, 18, 21, 24, 25):
         idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False,
                                 top2_levels=L)
         st = idx.stats()
-        lv = st["top2_levels"]
-        assert lv == (23 if L == 0 else L) and st["top_levels"] == min(lv, 14)
-        # the array, and the plain levels' 16-char keys again, contiguous (LDS staging)
-        assert st["top2_bytes"] == 16 * bench.top2_entries(st["top_levels"], lv)[0] + \
-            (((4 << st["top_levels"]) + 15) & ~15), L
+        lv = min(26 if L == 0 else L, st["iterations"])
+        D = min(lv, 14)
+        R = min(D + -(-(lv - D) // 4) * 4, st["iterations"]) if lv > D else 0
+        assert st["top_levels"] == D and st["rel_levels"] == R, (L, st["top_levels"], st["rel_levels"])
+        assert st["top2_levels"] == (R or D), L
+        # the LDS levels' entries, and their 16-char keys again, contiguous (LDS staging)
+        assert st["top2_bytes"] == (16 << D) + (((4 << D) + 15) & ~15), L
+        assert st["rel_bytes"] == (bench.rel_bytes(D, R) if R else 0), L
         if ref is None:
             sa = idx.suffix_array()
             tp = O.padded(t)
@@ -1108,7 +1112,61 @@ def test_blocked_pivot_levels(sas):
             assert np.array_equal(got, ref_all), (L, algo)
             assert np.array_equal(pr, ref_pr), (L, algo)
         idx.free()
-    # the layout itself: the cache part's short group first, the HBM part's last
-    assert bench.top2_entries(14, 23)[1] == [(14, 3), (17, 3), (20, 3)]
-    assert bench.top2_entries(14, 30)[1] == [(14, 3), (17, 3), (20, 3), (23, 3), (26, 3), (29, 1)]
-    assert bench.top2_entries(14, 22)[1] == [(14, 2), (16, 3), (19, 3)]
+    # the groups: 4 levels each from the LDS levels on, the last one clamped
+    assert [(d, h) for d, h, _ in bench.rel_groups(14, 26)] == [(14, 4), (18, 4), (22, 4)]
+    assert [(d, h) for d, h, _ in bench.rel_groups(14, 25)] == [(14, 4), (18, 4), (22, 3)]
+
+
+def test_rel_pivot_blocks(sas):
+    """The prefix-relative pivot blocks (common.hpp SAS_REL_GROUP): a block decides its 4
+    levels from the 8 chars after its bounds' common prefix P (capped at 24).  Texts with
+    planted repeats of 10..45 chars (P near and past the cap, 8-char ties) and a periodic text
+    (every P capped, every key a tie), queries of every length 0..40 plus 64 and 100 (m < P + 8
+    included), one-char mutations at every offset, negatives and text-end suffixes: PLAIN,
+    LCP, LLCP and INLINE equal the oracle's binary_search (sas/sa_search.rs:98-112) and PLAIN
+    without the pivot levels, positions (and probe counts, where they follow it)."""
+    from sas_amd import _lib
+    rng = np.random.default_rng(21)
+    base = sas.random_string(3 << 20, seed=99)
+    planted = base.copy()
+    n0 = len(planted)
+    for a, b, ln in zip(rng.integers(0, n0 - 64, 60_000), rng.integers(0, n0 - 64, 60_000),
+                        rng.integers(10, 46, 60_000)):
+        planted[b:b + ln] = planted[a:a + ln]
+    texts = {"planted": planted, "period_9": np.tile(rng.integers(0, 4, 9, dtype=np.uint8), (1 << 17) // 9 + 5)}
+    for name, t in texts.items():
+        n = len(t)
+        idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False)
+        st = idx.stats()
+        assert st["rel_levels"] == min(26, st["iterations"]) and st["rel_bytes"] > 0, (name, st["rel_levels"])
+        sa = idx.suffix_array()
+        qs = []
+        for m in list(range(0, 41)) + [64, 100]:
+            for o in rng.integers(0, n - m - 1, 60):
+                q = t[o:o + m].copy()
+                qs.append(q)
+                if m:
+                    k = int(rng.integers(0, m))
+                    mq = q.copy()
+                    mq[k] = (mq[k] + 1 + rng.integers(0, 3)) % 4
+                    qs.append(mq)
+        qs += [rng.integers(0, 4, l, dtype=np.uint8) for l in rng.integers(0, 40, 300)]
+        qs += [t[n - k:] for k in (1, 2, 7, 8, 9, 24, 31, 32, 33)]
+        qs += [np.concatenate([t[n - k:], np.zeros(j, np.uint8)]) for k in (3, 20, 30) for j in (1, 5, 12)]
+        buf, qo, ql = pack(qs)
+        expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+        got, pr = idx.search_batch(buf, qo, ql, algo="plain", probes=True)
+        bad = np.nonzero(got != expect)[0]
+        assert len(bad) == 0, (name, bad[:5], [qs[i] for i in bad[:2]])
+        got0, pr0 = idx.search_batch(buf, qo, ql, algo="plain", probes=True, flags=_lib.SAS_NO_LDS_TOP)
+        assert np.array_equal(got0, expect), name
+        assert np.array_equal(pr, pr0), name
+        # LCP / LLCP take exact lcps off the same keys (a key below q that may end in padding
+        # reads the whole entry); INLINE decides on them with the sector predicate
+        for algo in ("lcp", "llcp", "inline"):
+            ga, pa = idx.search_batch(buf, qo, ql, algo=algo, probes=True)
+            bad = np.nonzero(ga != expect)[0]
+            assert len(bad) == 0, (name, algo, bad[:5], [qs[i] for i in bad[:2]])
+            if algo != "inline":
+                assert np.array_equal(pa, pr), (name, algo)
+        idx.free()
