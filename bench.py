@@ -1204,6 +1204,9 @@ def config_summary(rec: dict) -> dict:
             "frac": _r((rec.get("bytes_per_lookup") or {}).get("section_8d", 0.0) * rec["kernel_lookups_per_s"] / 1e9
                        / HBM_PEAK_GBPS, 3) if rec.get("kernel_lookups_per_s") else None,
             "frac_hbm": _r((rec.get("achieved_hbm_GBps") or 0.0) / HBM_PEAK_GBPS, 3),
+            # the request-rate floor over the kernel time (PMC requests; <= 1): the bound these
+            # random-access kernels run at
+            "req_frac": _r((pmc.get("requests_split") or {}).get("frac"), 3),
             "traffic": _r(pmc.get("fabric_bytes_per_lookup")), "index_bytes": rec.get("index_bytes")}
 
 
@@ -1262,7 +1265,8 @@ def compact_line(full: dict) -> dict:
             "parts": c4["parts"], "index_bytes": c4["index_bytes"], "proven": c4.get("proven")}
     line["configs"] = out
     line["configs_frac_basis"] = ("frac: SURVEY 8(d) algorithmic bytes per lookup (every level, wherever served) / "
-                                  "kernel time / 8 TB/s; frac_hbm: the HBM-served bytes only")
+                                  "kernel time / 8 TB/s, above 1 where pivot levels come from LDS / cache-resident "
+                                  "blocks; frac_hbm: the HBM-served bytes only; req_frac: PMC request floor / time")
     if full.get("variants"):
         line["variants_kernel_ms"] = {k: _r(v["kernel_ms"]) for k, v in full["variants"].items()}
     if full.get("lcp_long"):
@@ -1273,6 +1277,11 @@ def compact_line(full: dict) -> dict:
         line["e2e_host_lookups_per_s"] = _r(full["e2e_host"]["lookups_per_s"])
     line["verified"] = full.get("verified", False)
     line["detail"] = full.get("detail")
+    # the optional summaries give way before the line outgrows LINE_LIMIT (all in the detail file)
+    for k in ("e2e_host_lookups_per_s", "ranges_per_s", "lcp_long", "variants_kernel_ms", "configs_frac_basis"):
+        if len(json.dumps(line)) <= LINE_LIMIT:
+            break
+        line.pop(k, None)
     return line
 
 

@@ -205,6 +205,11 @@ def test_result_line_is_compact_and_complete():
     line = bench.compact_line(full)
     text = json.dumps(line)
     assert len(text) <= bench.LINE_LIMIT < 8192, len(text)
+    # oversized optional summaries give way first; the contract keys stay
+    big = dict(full, lcp_long={"summary": {"x" * 40 + str(i): [1.0, 2.0, 3.0] for i in range(200)}})
+    bl = bench.compact_line(big)
+    assert len(json.dumps(bl)) <= bench.LINE_LIMIT and "lcp_long" not in bl
+    assert all(k in bl for k in REQUIRED) and "configs" in bl
     for k in REQUIRED:
         assert k in line, k
     assert isinstance(line["value"], float) and line["value"] > 0
