@@ -1717,7 +1717,7 @@ def main():
     if rank == 0:
         ms = el / args.steps * 1e3
         value = ws * nq * args.steps / el
-        wl = WORKLOADS[args.algo]
+        wl = plain_label(stats) if args.algo == "plain" else WORKLOADS[args.algo]
         if args.algo == "prefix":
             wl = wl.format(p=stats["prefix_chars"], e=pe, k=max(1, pe // 16), tb=stats["prefix_bytes"] / 2 ** 30)
         line = {

@@ -223,3 +223,18 @@ def test_result_line_is_compact_and_complete():
         assert set(line["configs"][c]) >= {"lookups_per_s", "kernel_ms", "frac", "index_bytes"}
     assert "variants" not in line and "index" not in line
     assert json.loads(text) == line
+
+
+def test_every_headline_algo_has_a_workload_label():
+    """bench.py --algo X names its workload: PLAIN from the index's pivot depth, the rest from
+    WORKLOADS (a missing label ended a PMC pass in round 4)."""
+    import re
+    src = open(bench.__file__).read()
+    choices = re.search(r'"--algo", default=None, choices=\[([^\]]*)\]', src).group(1)
+    algos = [a.strip().strip('"') for a in choices.replace("\n", " ").split(",") if a.strip()]
+    assert "plain" in algos and len(algos) >= 8
+    st = {"top_levels": 14, "rel_levels": 26, "rel_bytes": bench.rel_bytes(14, 26)}
+    assert "26" in bench.plain_label(st)
+    for a in algos:
+        if a != "plain":
+            assert a in bench.WORKLOADS, a
