@@ -52,11 +52,11 @@ RANDOM_REQ_CEILING = 5.084e10
 CACHE_REQ_CEILING = 5.731e10
 CACHE_BYTES = 256 << 20  # Infinity Cache (MALL): arrays at most this large count as cache-served
 SEED = 31415  # sas/main.rs:38
-# binary-search levels served from LDS (16-char keys) / the prefix-relative pivot blocks (the
-# index's stats win): the library default reaches 26 levels (SAS_TOP2_CACHE_LEVELS, 136 MiB of
-# blocks, cache-resident); deeper ones (SAS_BUILD_TOP2_LEVELS, e.g. 30 = 2.1 GiB) are HBM reads
-TOP_LDS_LEVELS = 14
-C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: pivot blocks of levels 27-30 from HBM
+# binary-search levels served by the prefix-relative pivot blocks (the index's stats win): the
+# library default reaches 27 levels (SAS_TOP2_CACHE_LEVELS: 15 staged in LDS, 273 MiB of blocks);
+# deeper ones (SAS_BUILD_TOP2_LEVELS, e.g. 30 -> 31 levels = 4.3 GiB) read HBM blocks
+TOP_LDS_LEVELS = 15  # common.hpp SAS_REL_LDS_LEVELS
+C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: rounded up to all 31 levels, 28-31 from HBM
 
 KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
@@ -119,23 +119,24 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         per = 16 if (algo == "interp" and st["quad_entry_bytes"] == 16) else sa_w + win
         hbm += entry + max(0.0, probes - 1) * per
     elif algo in ("plain", "lcp", "inline", "llcp"):
-        # the LDS levels' 16-char keys (4 B), one 32-B prefix-relative block per 4 levels (one
-        # request, cache or HBM by where its group's array ends; common.hpp SAS_REL_GROUP),
+        # the prefix-relative blocks (common.hpp RelLayout): one per group entered, from LDS for
+        # the first 15 levels, else one request (cache or HBM by where its group's array ends),
         # then per probe: SA word + text window (PLAIN / LCP, two requests) or one 16-B entry
         # (INLINE / LLCP, one request); a lookup decided by keys alone reads SA[r] at the end
         per, rq = (sa_w + win, 2) if algo in ("plain", "lcp") else (16, 1)
-        t1 = st.get("top_levels", TOP_LDS_LEVELS)
-        R = st.get("rel_levels") or t1
-        lds += min(probes, t1) * 4
+        R = st.get("rel_levels") or 0
         rc = rh = 0.0
-        for d0, h, cached in rel_groups(t1, R):
+        for d0, h, where in rel_groups(R):
             if probes - d0 <= 0:
                 continue
-            if cached:
-                cache += 32
+            bb = 32 if h == 4 else 16
+            if where == "lds":
+                lds += bb
+            elif where == "cache":
+                cache += bb
                 rc += 1
             else:
-                hbm += 32
+                hbm += bb
                 rh += 1
         hbm += max(0.0, probes - R) * per
         fin = 1.0 if probes <= R else 0.0
@@ -249,19 +250,37 @@ def launch_times(torch, step, steps: int, warmup: int, stream, sync=None, barrie
 
 
 # ---------------------------------------------------------------- the pivot array
-def rel_groups(D: int, R: int, G: int = 4):
-    """common.hpp rel_layout: the prefix-relative pivot blocks for levels [D, R), groups of G
-    levels rooted at D, D + G, ..., one 32-B block per root node; (d0, h, cached) per group,
-    cached = the array up to and including the group fits the 256 MiB Infinity Cache."""
-    out, tot = [], 0
-    for d0 in range(D, R, G):
-        tot += 32 << d0
-        out.append((d0, min(G, R - d0), tot <= CACHE_BYTES))
+def rel_groups(R: int, lds_levels: int = TOP_LDS_LEVELS, G: int = 4):
+    """common.hpp rel_layout: the prefix-relative pivot blocks of R levels, groups of up to G
+    levels rooted at 0, 4, 8, 12 (3 levels) in LDS, then at 15, 19, ...; one block per root
+    node (32 B at 4 levels, else 16 B).  (d0, h, where) per group: "lds", or "cache" while the
+    array past the LDS groups fits the 256 MiB Infinity Cache, else "hbm"."""
+    out, tot, d0 = [], 0, 0
+    while d0 < R:
+        h = G
+        if d0 < lds_levels < d0 + h:
+            h = lds_levels - d0
+        h = min(h, R - d0)
+        if d0 + h <= lds_levels:
+            where = "lds"
+        else:
+            tot += (32 if h == G else 16) << d0
+            where = "cache" if tot <= CACHE_BYTES else "hbm"
+        out.append((d0, h, where))
+        d0 += h
     return out
 
 
-def rel_bytes(D: int, R: int) -> int:
-    return sum(32 << d0 for d0, _, _ in rel_groups(D, R))
+def rel_levels(iters: int, L: int, lds_levels: int = TOP_LDS_LEVELS, G: int = 4) -> int:
+    """the depth rel_layout gives a requested L (clamped; rounded up to whole groups past LDS)"""
+    R = min(L, iters)
+    if R > lds_levels:
+        R = lds_levels + -(-(R - lds_levels) // G) * G
+    return min(R, iters)
+
+
+def rel_bytes(R: int) -> int:
+    return sum((32 if h == 4 else 16) << d0 for d0, h, _ in rel_groups(R))
 
 
 # ---------------------------------------------------------------- index footprints
@@ -286,7 +305,7 @@ def footprint(algo: str, st: dict) -> int:
     sa = st["sa_bytes"]
     compact_sa = sa if st.get("quad_entry_bytes") == 8 else 0
     # the pivots: the LDS levels' entries and 16-char keys, then the prefix-relative blocks
-    piv = (20 << st.get("top_levels", TOP_LDS_LEVELS)) + st.get("rel_bytes", 0) if st.get("top_levels") else 0
+    piv = st.get("rel_bytes", 0)
     if base == "tagged":
         return st["index_bytes"]
     if base in ("plain", "lcp"):
@@ -1305,10 +1324,10 @@ WORKLOADS = {
               "with p live) of {e}-B inline entries holding each bucket's first {k} suffixes "
               "({tb:.0f} GiB), then binary search over the fused {{32-char key, SA}} quad-leaf entries "
               "of the bucket; 2^30 text in HBM, 10^7 len-32 queries",
-    "plain_rel": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112): levels 1-{t1} from LDS "
-                 "(16-char keys), levels {t1p}-{R} from the {rb} prefix-relative pivot blocks ({where}; 4 levels "
-                 "per 32-B block: the 8 chars after the block bounds' common prefix), the rest read SA[mid] and a "
-                 "text window",
+    "plain_rel": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112): the pivots of levels "
+                 "1-{R} from {rb} of prefix-relative blocks (4 levels per 32-B block: the 8 chars after the block "
+                 "bounds' common prefix), levels 1-{t1} staged in LDS, {t1p}-{R} {where}; the rest read SA[mid] "
+                 "and a text window",
     "lcp": "configs[1] + mlr LCP skipping",
     "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (16-B {SA, Llcp, Rlcp, chars} entries)",
     "inline": "configs[1] probe sequence over fused {32-char key, SA} entries",
@@ -1324,13 +1343,11 @@ WORKLOADS = {
 def plain_label(st: dict) -> str:
     """configs[1]'s workload text from the index's own pivot depth (sas_stats.rel_levels)."""
     t1, R = st["top_levels"], st.get("rel_levels", 0)
-    if R:
-        rb = st["rel_bytes"]
-        hb = [d0 for d0, _, c in rel_groups(t1, R) if not c]
-        return WORKLOADS["plain_rel"].format(
-            t1=t1, t1p=t1 + 1, R=R, rb=(f"{rb / 2 ** 30:.2f} GiB" if rb >= 1 << 30 else f"{rb >> 20} MiB"),
-            where=(f"levels {t1 + 1}-{hb[0]} cache-resident, {hb[0] + 1}-{R} from HBM" if hb else "cache-resident"))
-    return WORKLOADS["plain_rel"].format(t1=t1, t1p=t1 + 1, R=t1, rb="0 MiB", where="none")
+    rb = st.get("rel_bytes", 0)
+    hb = [d0 for d0, _, w in rel_groups(R) if w == "hbm"]
+    return WORKLOADS["plain_rel"].format(
+        t1=t1, t1p=t1 + 1, R=R, rb=(f"{rb / 2 ** 30:.2f} GiB" if rb >= 1 << 30 else f"{rb >> 20} MiB"),
+        where=(f"levels {t1 + 1}-{hb[0]} cache-resident, {hb[0] + 1}-{R} from HBM" if hb else "cache-resident"))
 
 
 def main():
@@ -1356,7 +1373,7 @@ def main():
     ap.add_argument("--c1-deep-levels", type=int, default=C1_DEEP_TOP2_LEVELS,
                     help="configs[1]'s second figure: PLAIN with this many pivot-array levels (0: skip)")
     ap.add_argument("--top2-levels", type=int, default=0,
-                    help="pivot-array depth of the headline index (SAS_BUILD_TOP2_LEVELS; 0 = library default 26)")
+                    help="pivot-array depth of the headline index (SAS_BUILD_TOP2_LEVELS; 0 = library default 27)")
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-c3", action="store_true", help="skip the configs[3] sub-record")
@@ -1571,8 +1588,9 @@ def main():
         log(f"variant {v}: {vk:.3f} ms")
 
     # configs[1]'s second figure: the same PLAIN probe sequence on an index whose pivots reach
-    # C1_DEEP_TOP2_LEVELS levels (SAS_BUILD_TOP2_LEVELS; 2.1 GiB of blocks at 30): the block of
-    # levels 27-30 is one HBM request instead of four SA words and text windows
+    # C1_DEEP_TOP2_LEVELS levels (SAS_BUILD_TOP2_LEVELS, rounded up to the 4-level grid: every
+    # level of a 2^30 text, 4.3 GiB of blocks): the block of levels 28-31 is one HBM request
+    # instead of four SA words and text windows
     deep = None
     if args.mode == "replicated" and "plain" in variants and args.c1_deep_levels:
         didx = sas_amd.SaNaive.build(text, lcp=False, stree=False, sector=False, quad=False, llcp=False,
@@ -1595,7 +1613,7 @@ def main():
                       {"identical_to_headline": True, "lookups_per_s": ws * nq * dsteps / del_s,
                        "kernel_ms_median": dt_["median_ms"], "timed_launches": dsteps,
                        "workload": plain_label(dst), "pivot_levels": dst["top2_levels"],
-                       "pivot_bytes": dst["rel_bytes"] + dst["top2_bytes"]})
+                       "pivot_bytes": dst["rel_bytes"]})
         didx.free()
         del dout, dpr
         torch.cuda.empty_cache()
@@ -1669,7 +1687,7 @@ def main():
         if "plain" in variants:
             configs["c1"] = dict(variants["plain"], workload=plain_label(stats),
                                  pivot_levels=stats["top2_levels"],
-                                 pivot_bytes=stats["rel_bytes"] + stats["top2_bytes"])
+                                 pivot_bytes=stats["rel_bytes"])
             if deep is not None:
                 configs["c1"]["deep_pivots"] = deep
         best2 = max((v for v in ("quad", "sector", "stree") if v in variants),

@@ -120,14 +120,14 @@ typedef struct sas_index sas_index;
                                         not with the trees, LLCP or SAS_BUILD_PREFIX*  */
 #define SAS_BUILD_TOP2_LEVELS(L) ((uint32_t)(L) << 27) /* bits 27..31: depth L (1..31) of
                                         the binary-search pivots (PLAIN / LCP / LLCP / INLINE):
-                                        the first 14 levels' 16-B {32-char key, SA} entries
-                                        (their 16-char keys staged in LDS), then levels 15..L
-                                        as prefix-relative blocks of 4 levels (32 B each: the
-                                        lcp P of the block's bounds and the 8 chars after P of
-                                        15 pivots), L rounded up to that grid.  0 = the default,
-                                        26 levels (136 MiB, resident in the 256 MiB Infinity
-                                        Cache); L = 30 costs 2.1 GiB.  One request per block
-                                        instead of an SA word and a text window per level.
+                                        prefix-relative blocks of up to 4 levels (32 B each:
+                                        the lcp P of the block's bounds and the 8 chars after
+                                        P of 15 pivots); levels 1-15 (72.5 KiB) are staged in
+                                        each workgroup's LDS, the rest cost one request per
+                                        block instead of an SA word and a text window per
+                                        level.  L is rounded up to the 4-level grid past the
+                                        LDS levels (19, 23, 27, 31).  0 = the default, 27
+                                        levels (273 MiB); 31 levels cost 4.3 GiB at n = 2^30.
                                         Clamped to the iteration count; results never depend
                                         on L                                               */
 #define SAS_BUILD_TAG_LINES (1u << 24) /* with SAS_BUILD_TAGGED: the tagged entries as one
@@ -195,7 +195,8 @@ typedef struct sas_stats {
     uint64_t stree_bytes;    /* S-tree incl. 16-char key leaves, 0 if not built   */
     uint32_t stree_layers;   /* S-tree height (layers incl. leaves)               */
     uint32_t stree_lds_layers; /* layers served from LDS                          */
-    uint32_t top_levels;     /* binary-search levels served from LDS (PLAIN/LCP)  */
+    uint32_t top_levels;     /* binary-search levels served from LDS (15, fewer for a
+                                shallow search)                                       */
     uint32_t iterations;     /* ilog2(n)+1 lockstep iterations (sa_search.rs:171) */
     uint64_t build_sa_ns;    /* wall time of the SA construction (0 if supplied)  */
     uint64_t build_total_ns; /* wall time of sas_build                            */
@@ -232,14 +233,14 @@ typedef struct sas_stats {
     uint64_t tag_overflow_entries; /* SAS_BUILD_TAG_LINES: entries in the overflow array */
     uint64_t text2_bytes;    /* SAS_BUILD_TAG_LINES: the second packed-text copy (64 B off
                                 the 128-B line grid, so a tie's compare reads one line) */
-    uint64_t top2_bytes;     /* the LDS levels' pivot entries and their 16-char keys (0 for
-                                bucket lines)                                        */
+    uint64_t top2_bytes;     /* 0 since round 4: every pivot level is in the rel blocks */
     uint32_t rel_levels;     /* the prefix-relative pivot blocks: the levels they reach
                                 (the pivot depth rounded up to 4-level blocks past the
-                                LDS levels, clamped to the iterations; 0 if none)    */
+                                15 LDS levels, clamped to the iterations; 0 if none) */
     uint32_t rel_pad;        /* 0 */
     uint64_t rel_bytes;      /* their array: one 32-B block {lcp of the block's bounds, the
-                                8 chars after it of each of 15 pivots} per 4-level subtree */
+                                8 chars after it of each of 15 pivots} per 4-level subtree
+                                (16 B for a shorter one), the LDS levels' first    */
 } sas_stats;
 
 const char* sas_last_error(void);

@@ -24,64 +24,68 @@
 #include "../../include/sst.h"
 
 #define SAS_TEXT_PAD_WORDS 4
-// The binary search's first SAS_TOP_LEVELS levels are plain Eytzinger entries whose 16-char
-// keys are staged in LDS (4 B each: 16383 pivots, 64 KiB a workgroup); a 16-char tie (or, for
-// the exact lcps of LCP / LLCP, a key that may end in padding) reads the whole entry.
-#define SAS_TOP_LEVELS 14
-#define SAS_TOP_NODES (1u << SAS_TOP_LEVELS)
-// Past the LDS levels the pivots come from the prefix-relative blocks below ("rel"): an
-// SA word and a text window replaced by one request per 4 levels.  History: round 2 read a
-// 16-B {32-char key, SA} entry per level (PLAIN 7.15 ms per 10^7 without pivots, 4.27 with 23
-// levels, 2.71 with 30; profiles/r2/ab_top2_*.txt), round 4 first a 128-B line of 3 levels
-// of 16-char keys (2.97 ms at 23 levels), then the rel blocks (1.66 ms at 26 levels in the
-// same 136 MiB).  The depth is a build parameter (SAS_BUILD_TOP2_LEVELS(L) in sas.h, rounded
-// up to the block grid), never derived from free memory: the default is the
-// SAS_TOP2_CACHE_LEVELS levels that stay inside the 256 MiB Infinity Cache.
-#define SAS_TOP2_CACHE_LEVELS 26
+// The binary search's pivots are prefix-relative blocks ("rel", round 4): levels in groups of
+// up to 4 (SAS_REL_GROUP); a group rooted at level d0 holds one block per root node, 2^h u16
+// slots for an h-level group (32 B at h = 4, 16 B below): slot 0 = P, the lcp (capped at
+// SAS_REL_PMAX) of the block interval's bounds SA[l - 1] and SA[r] (0 at the array's ends;
+// bit 15 flags a block with a pivot whose suffix ends before char P + 8),
+// slots 1.. = chars [P, P + 8) of the pivots of its subtree in local Eytzinger order.  Every
+// suffix strictly inside the interval, and every query q with SA[l - 1] < q <= SA[r], starts
+// with those P chars, so chars [P, P + 8) decide key < q unless they tie (then the SA value
+// and the text).  Levels 0..14 (groups rooted at 0, 4, 8 and a 3-level one at 12: 72.5 KiB)
+// are staged in LDS, two workgroups a CU; past them one 16-B pair read of a block (one
+// request) serves 4 levels.  PLAIN, LCP, LLCP and INLINE all read them (LCP / LLCP take
+// exact lcps off the keys).  History: round 2 read a 16-B {32-char key, SA} entry per level
+// (PLAIN 7.15 ms per 10^7 without pivots, 4.27 with 23 levels, 2.71 with 30;
+// profiles/r2/ab_top2_*.txt), round 4 first 3 levels of 16-char keys in a 128-B line (2.97 ms
+// at 23 levels), then rel blocks past 14 LDS levels of 16-char keys (1.70 ms at 26).  The
+// depth is a build parameter (SAS_BUILD_TOP2_LEVELS(L) in sas.h, rounded up to the group
+// grid), never derived from free memory: the default SAS_TOP2_CACHE_LEVELS reach 27 levels
+// with 273 MiB of blocks.
+#define SAS_TOP2_CACHE_LEVELS 27
 #define SAS_TOP2_MAX_LEVELS 31
-// LDS staging of the plain levels' 16-char keys from their contiguous copy: 16-B loads, four
-// keys each (a workgroup's staging decides the time of small batches: configs[0]'s 10^4
-// queries)
-__device__ __forceinline__ void stage_k16(uint32_t* s, const uint32_t* __restrict__ g, uint32_t nodes) {
-    const uint32_t nw = nodes / 4;
-    const uint4* src = reinterpret_cast<const uint4*>(g);
-    uint4* dst = reinterpret_cast<uint4*>(s);
-    for (uint32_t w = threadIdx.x; w < nw; w += blockDim.x) dst[w] = src[w];
-    for (uint32_t x = nw * 4 + threadIdx.x; x < nodes; x += blockDim.x) s[x] = g[x];
-}
-
-// The prefix-relative pivot blocks (round 4): levels [D, R) in groups of SAS_REL_GROUP; a
-// group rooted at level d0 holds one 32-B block per root node, 16 u16
-// slots: slot 0 = P, the lcp (capped at SAS_REL_PMAX) of the block interval's bounds
-// SA[l - 1] and SA[r] (0 at the array's ends), slots 1..15 = chars [P, P + 8) of the
-// pivots of its 4-level subtree in local Eytzinger order.  Every suffix strictly inside the
-// interval, and every query q with SA[l - 1] < q <= SA[r], starts with those P chars, so
-// chars [P, P + 8) decide key < q unless they tie (then the SA value and the text).  A 16-B
-// pair read of one block is one request for 4 levels, where a 128-B block of 16-char keys
-// held 3: at the same array size (136 MiB) 26 levels instead of 23.  PLAIN, LCP, LLCP and
-// INLINE all read them (LCP / LLCP take exact lcps off the keys, common.hpp callers).
 #define SAS_REL_GROUP 4
-#define SAS_REL_PMAX 24      // P + 8 <= 32: q's chars [P, P + 8) come from its first word
-#define SAS_REL_MAX_GROUPS 5  // (SAS_TOP2_MAX_LEVELS - SAS_TOP_LEVELS + 3) / 4
-static_assert((SAS_TOP2_MAX_LEVELS - SAS_TOP_LEVELS + SAS_REL_GROUP - 1) / SAS_REL_GROUP <= SAS_REL_MAX_GROUPS,
-              "rel groups");
-// the rel array's depth for a pivot array of L levels above D LDS levels: L rounded up to
-// the group grid, clamped to the iteration count (no rel levels when iters <= D)
-static inline uint32_t rel_levels_for(uint32_t D, uint32_t L, uint32_t iters) {
-    if (iters <= D || L <= D) return D;
-    const uint32_t R = D + (L - D + SAS_REL_GROUP - 1) / SAS_REL_GROUP * SAS_REL_GROUP;
-    return R < iters ? R : iters;
-}
-struct RelBase { uint64_t b[SAS_REL_MAX_GROUPS]; };  // byte offset of each group (root level D + 4g)
-// fill the groups' offsets; returns the array's bytes
-static inline uint64_t rel_layout(uint32_t D, uint32_t R, uint64_t* base) {
+#define SAS_REL_PMAX 24          // P + 8 <= 32: q's chars [P, P + 8) come from its first word
+#define SAS_REL_LDS_LEVELS 15    // levels staged in LDS
+#define SAS_REL_LDS_BYTES (32 * (1 + 16 + 256) + 16 * 4096)  // their blocks: 74272 B
+#define SAS_REL_MAX_GROUPS 8     // 4 LDS groups + 4 of levels 15..30
+struct RelLayout {
+    uint64_t base[SAS_REL_MAX_GROUPS];  // byte offset of group g
+    uint8_t d0[SAS_REL_MAX_GROUPS];     // its root level
+    uint8_t h[SAS_REL_MAX_GROUPS];      // its levels (block bytes: 32 at h = 4, else 16)
+    uint32_t groups;                    // groups in all
+    uint32_t lds_groups;                // the first ones, staged in LDS
+    uint32_t levels;                    // levels the blocks serve
+    uint32_t lds_bytes;                 // bytes of the LDS groups (a multiple of 16)
+    uint64_t bytes;                     // the array's bytes
+};
+// the layout for a depth of L levels (clamped to the iteration count; past the LDS levels
+// rounded up to whole 4-level groups)
+static inline void rel_layout(uint32_t iters, uint32_t L, RelLayout* y) {
+    *y = RelLayout{};
+    uint32_t R = L < iters ? L : iters;
+    if (R > SAS_REL_LDS_LEVELS)
+        R = SAS_REL_LDS_LEVELS + (R - SAS_REL_LDS_LEVELS + SAS_REL_GROUP - 1) / SAS_REL_GROUP * SAS_REL_GROUP;
+    if (R > iters) R = iters;
     uint64_t b = 0;
-    for (uint32_t g = 0; g < SAS_REL_MAX_GROUPS; g++) {
-        base[g] = b;
-        const uint32_t d0 = D + SAS_REL_GROUP * g;
-        if (d0 < R) b += 32ull << d0;
+    uint32_t g = 0;
+    for (uint32_t d0 = 0; d0 < R; g++) {
+        uint32_t h = SAS_REL_GROUP;
+        if (d0 < SAS_REL_LDS_LEVELS && d0 + h > SAS_REL_LDS_LEVELS) h = SAS_REL_LDS_LEVELS - d0;
+        if (d0 + h > R) h = R - d0;
+        y->base[g] = b;
+        y->d0[g] = (uint8_t)d0;
+        y->h[g] = (uint8_t)h;
+        b += (uint64_t)(h == SAS_REL_GROUP ? 32 : 16) << d0;
+        d0 += h;
+        if (d0 <= SAS_REL_LDS_LEVELS) {
+            y->lds_groups = g + 1;
+            y->lds_bytes = (uint32_t)b;
+        }
     }
-    return b;
+    y->groups = g;
+    y->levels = R;
+    y->bytes = b;
 }
 #define SAS_STREE_B 16                // keys per node / branching factor - 1
 #define SAS_STREE_MAX_LAYERS 16
@@ -146,16 +150,8 @@ struct sas_index {
     uint64_t stree_off[SAS_STREE_MAX_LAYERS] = {};
     uint32_t stree_lds_layers = 0;
     uint32_t stree_lds_nodes = 0;
-    uint4* top2 = nullptr;        // the LDS levels' pivots {key64 lo, hi, SA lo, hi}: Eytzinger nodes
-                                  // 1..2^D - 1 (their 16-char keys are staged in LDS); index 0 unused
-    uint64_t top2_entries = 0;
-    uint32_t* top_k16 = nullptr;  // the plain levels' 16-char keys, contiguous (inside top2's allocation)
-    uint32_t top_levels = 0;      // levels served from LDS
-    uint32_t top2_levels = 0;     // levels served from LDS or the rel blocks
-    uint8_t* rel = nullptr;       // the prefix-relative pivot blocks (SAS_REL_GROUP), levels [top_levels, rel_levels)
-    RelBase rel_base{};
-    uint64_t rel_bytes = 0;
-    uint32_t rel_levels = 0;
+    uint8_t* rel = nullptr;       // the prefix-relative pivot blocks (rel_lay), their first groups staged in LDS
+    RelLayout rel_lay{};
     uint32_t iters = 0;           // ilog2(n) + 1
     uint32_t* scratch = nullptr;  // device flag word(s) for kernels (invalid query codes)
     // sector tree (SAS_ALGO_SECTOR): 32-B nodes

@@ -844,47 +844,23 @@ static int build_quad(sas_index* x, bool compact, uint32_t mode) {
 }
 
 // ------------------------------------------------------------------ top of the binary search
-// Node k (1-based Eytzinger) = state after the path given by k's bits below
-// the leading one (0 = went left: r = mid, 1 = right: l = mid + 1); its entry =
-// {32-char key, SA value} of that state's pivot SA[(l + r) / 2], for the D LDS levels.
-template <int W>
-__global__ void k_top(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint4* __restrict__ top2,
-                      uint32_t nodes) {
-    GRID_STRIDE(k, nodes) {
-        uint64_t l = 0, r = sa_n, p = 0xFFFFFFFFu, key = 0;
-        int depth = k ? 63 - __clzll(k) : 0;
-        for (int b = depth - 1; b >= 0; b--) {
-            uint64_t mid = (l + r) >> 1;
-            if (l >= r) break;
-            if ((k >> b) & 1) l = mid + 1; else r = mid;
-        }
-        if (k && l < r) {
-            p = sa[(l + r) >> 1];
-            key = text_chars32(tw, p);
-        }
-        top2[k] = make_uint4((uint32_t)key, (uint32_t)(key >> 32), (uint32_t)p, (uint32_t)(p >> 32));
-    }
-}
-
-__global__ void k_top_k16(const uint4* __restrict__ top2, uint32_t nodes, uint32_t* __restrict__ k16) {
-    GRID_STRIDE(k, nodes) k16[k] = top2[k].y;
-}
-
-// PLAIN's prefix-relative blocks (common.hpp SAS_REL_GROUP): node k at level d in [D, R),
-// t = (d - D) % 4 levels below its block's root.  The root's interval [l0, r0) gives P =
-// lcp(SA[l0 - 1], SA[r0]) (whole suffixes: never past either one's end; capped), the node's
-// pivot SA[(l + r) / 2] its chars [P, P + 8) (zero past the text's end) in slot
-// (1 << t) | (k's low t bits); the root thread writes P to slot 0.  Nodes whose interval is
-// empty keep 0 (never read: the search stops probing there).
+// The prefix-relative pivot blocks (common.hpp RelLayout).  Node k (1-based Eytzinger) = the
+// state after the path given by k's bits below the leading one (0 = went left: r = mid, 1 =
+// right: l = mid + 1); at level d in group g it sits t = d - d0 levels below its block's
+// root.  The root's interval [l0, r0) gives P = lcp(SA[l0 - 1], SA[r0]) (whole suffixes:
+// never past either one's end; capped), the node's pivot SA[(l + r) / 2] its chars [P, P + 8)
+// (zero past the text's end) in slot (1 << t) | (k's low t bits); the root thread writes P to
+// slot 0.  Nodes whose interval is empty keep 0 (never read: the search stops probing there).
 template <int W>
 __global__ void k_rel(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa, uint64_t sa_n,
-                      uint8_t* __restrict__ rel, uint64_t first, uint64_t nodes, uint32_t D,
-                      const RelBase base) {
+                      uint8_t* __restrict__ rel, uint64_t nodes, const RelLayout lay) {
     GRID_STRIDE(i, nodes) {
-        const uint64_t k = first + i;
+        const uint64_t k = 1 + i;
         const int depth = 63 - __clzll(k);
-        const uint32_t t = (uint32_t)(depth - (int)D) % SAS_REL_GROUP;
-        const int d0 = depth - (int)t;
+        uint32_t g = 0;
+        while (g + 1 < lay.groups && (int)lay.d0[g + 1] <= depth) g++;
+        const int d0 = lay.d0[g];
+        const uint32_t t = (uint32_t)(depth - d0);
         uint64_t l = 0, r = sa_n, l0 = 0, r0 = sa_n;
         bool live = true;
         for (int b = depth - 1; b >= 0; b--) {
@@ -906,9 +882,22 @@ __global__ void k_rel(const uint64_t* __restrict__ tw, uint64_t n, SaView<W> sa,
             P = lc < SAS_REL_PMAX ? (uint32_t)lc : SAS_REL_PMAX;
         }
         const uint64_t k0 = k >> t;
-        uint16_t* blk = reinterpret_cast<uint16_t*>(rel + base.b[(d0 - (int)D) / SAS_REL_GROUP] +
-                                                    32 * (k0 - (1ull << d0)));
-        if (t == 0) blk[0] = (uint16_t)P;
+        const uint32_t sh = lay.h[g] == SAS_REL_GROUP ? 5u : 4u;
+        uint16_t* blk = reinterpret_cast<uint16_t*>(rel + lay.base[g] + ((k0 - (1ull << d0)) << sh));
+        if (t == 0) {
+            // bit 15: a pivot of the block ends inside its key (chars [P, P + 8) padded): its
+            // first difference with q may lie in the padding, so LCP / LLCP compare the text
+            uint32_t flag = 0;
+            for (uint32_t j = 1; j < (1u << lay.h[g]) && !flag; j++) {
+                uint64_t ll = l0, rr = r0;
+                for (int bb = 30 - __clz(j); bb >= 0 && ll < rr; bb--) {
+                    const uint64_t mm = (ll + rr) >> 1;
+                    if ((j >> bb) & 1) ll = mm + 1; else rr = mm;
+                }
+                if (ll < rr && n - sa[(ll + rr) >> 1] < (uint64_t)P + 8) flag = 1;
+            }
+            blk[0] = (uint16_t)(P | (flag << 15));
+        }
         if (live) {
             const uint64_t p = sa[(l + r) >> 1];
             blk[(1u << t) | (uint32_t)(k & ((1ull << t) - 1))] = (uint16_t)(text_chars32(tw, p + P) >> 48);
@@ -1172,7 +1161,7 @@ static int build_tagged(sas_index* x, uint32_t p) {
 // ------------------------------------------------------------------ C ABI
 static void free_index(sas_index* x) {
     if (!x) return;
-    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->top2, x->rel, x->scratch,
+    void* ptrs[] = {x->text_w, x->sa, x->lcp, x->llcp, x->prefix, x->stree, x->rel, x->scratch,
                      x->sec_inner, x->sec_leaves, x->quad_inner, x->quad_leaves, x->tag_table, x->tag_lines, x->tag_ovf,
                      x->tag_first, x->text2_base};
     for (void* p : ptrs) if (p) (void)hipFree(p);
@@ -1725,60 +1714,31 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
                          : (flags & SAS_BUILD_PREFIX_INLINE2) ? 2u
                          : (flags & SAS_BUILD_PREFIX_INLINE)  ? 1u : 0u));
 
-    // binary-search top in LDS (not for a bucket-line index: TAGGED never reads it)
+    // the binary search's pivots (not for a bucket-line index: TAGGED never reads them)
     const uint32_t iters = 64 - __builtin_clzll(sa_n);  // ilog2(len) + 1 (sas/sa_search.rs:171)
     x->iters = iters;
     if (!(flags & SAS_BUILD_TAG_LINES)) {
-        x->top_levels = iters < SAS_TOP_LEVELS ? iters : SAS_TOP_LEVELS;
-        // the pivots of the first L iterations: SAS_TOP2_CACHE_LEVELS (26: 136 MiB of rel
-        // blocks, inside the 256 MiB Infinity Cache) unless the caller asks for another depth
-        // (SAS_BUILD_TOP2_LEVELS), rounded up to the rel blocks' 4-level grid.  The depth is
-        // never taken from free memory, so a text always gets the same index.  The probe
-        // sequence, and so every result, is the same at any depth.
+        // the pivots of the first L iterations: SAS_TOP2_CACHE_LEVELS (27: 273 MiB of blocks)
+        // unless the caller asks for another depth (SAS_BUILD_TOP2_LEVELS), rounded up to the
+        // 4-level grid past the LDS levels.  The depth is never taken from free memory, so a
+        // text always gets the same index.  The probe sequence, and so every result, is the
+        // same at any depth.
         const uint32_t req = (flags >> 27) & 31u;
-        const uint32_t want = req ? req : SAS_TOP2_CACHE_LEVELS;
-        const uint32_t lv = iters < want ? iters : want;
-        // the plain (LDS-staged) levels are part of the depth: never more than it holds
-        if (x->top_levels > lv) x->top_levels = lv;
-        const uint32_t nodes = 1u << x->top_levels;
-        x->top2_entries = nodes;
-        DevBuf t2;
-        const uint64_t k16_bytes = ((4ull << x->top_levels) + 15) & ~15ull;
-        TRY(t2.alloc(x->top2_entries * 16 + k16_bytes, "top2"));
-        const dim3 tg(grid_for(nodes)), tb(256);
+        rel_layout(iters, req ? req : SAS_TOP2_CACHE_LEVELS, &x->rel_lay);
+        const RelLayout& lay = x->rel_lay;
+        DevBuf rl;
+        TRY(rl.alloc(lay.bytes, "rel"));
+        HIP_TRY(hipMemset(rl.p, 0, lay.bytes));
+        const uint64_t cnt = (1ull << lay.levels) - 1;
+        const dim3 tb(256);
         if (W == 5)
-            hipLaunchKernelGGL(k_top<5>, tg, tb, 0, 0, x->text_w, SaView<5>{x->sa}, sa_n, t2.as<uint4>(), nodes);
+            hipLaunchKernelGGL(k_rel<5>, dim3(grid_for(cnt)), tb, 0, 0, x->text_w, n, SaView<5>{x->sa}, sa_n,
+                               rl.as<uint8_t>(), cnt, lay);
         else
-            hipLaunchKernelGGL(k_top<4>, tg, tb, 0, 0, x->text_w, SaView<4>{x->sa}, sa_n, t2.as<uint4>(), nodes);
+            hipLaunchKernelGGL(k_rel<4>, dim3(grid_for(cnt)), tb, 0, 0, x->text_w, n, SaView<4>{x->sa}, sa_n,
+                               rl.as<uint8_t>(), cnt, lay);
         HIP_TRY(hipGetLastError());
-        x->top2 = static_cast<uint4*>(t2.release());
-        // the plain levels' 16-char keys again, contiguous, for the LDS staging (stage_k16)
-        x->top_k16 = reinterpret_cast<uint32_t*>(x->top2 + x->top2_entries);
-        hipLaunchKernelGGL(k_top_k16, dim3(grid_for(1ull << x->top_levels)), tb, 0, 0, x->top2, 1u << x->top_levels,
-                           x->top_k16);
-        HIP_TRY(hipGetLastError());
-        // the levels past the LDS ones: prefix-relative blocks, 4 levels a block (common.hpp)
-        x->rel_levels = rel_levels_for(x->top_levels, lv, iters);
-        if (x->rel_levels > x->top_levels) {
-            RelBase& rb = x->rel_base;
-            x->rel_bytes = rel_layout(x->top_levels, x->rel_levels, rb.b);
-            DevBuf rl;
-            TRY(rl.alloc(x->rel_bytes, "rel"));
-            HIP_TRY(hipMemset(rl.p, 0, x->rel_bytes));
-            const uint64_t first = 1ull << x->top_levels, cnt = (1ull << x->rel_levels) - first;
-            if (W == 5)
-                hipLaunchKernelGGL(k_rel<5>, dim3(grid_for(cnt)), tb, 0, 0, x->text_w, n, SaView<5>{x->sa}, sa_n,
-                                   rl.as<uint8_t>(), first, cnt, x->top_levels, rb);
-            else
-                hipLaunchKernelGGL(k_rel<4>, dim3(grid_for(cnt)), tb, 0, 0, x->text_w, n, SaView<4>{x->sa}, sa_n,
-                                   rl.as<uint8_t>(), first, cnt, x->top_levels, rb);
-            HIP_TRY(hipGetLastError());
-            x->rel = static_cast<uint8_t*>(rl.release());
-            x->top2_levels = x->rel_levels;
-        } else {
-            x->rel_levels = 0;
-            x->top2_levels = x->top_levels;
-        }
+        x->rel = static_cast<uint8_t*>(rl.release());
     }
     if ((flags & SAS_BUILD_TAGGED) && (flags & SAS_BUILD_TAG_LINES)) TRY(build_tag_lines(x, (flags >> 16) & 31));
     else if (flags & SAS_BUILD_TAGGED) TRY(build_tagged(x, (flags >> 16) & 31));
@@ -1798,7 +1758,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.stree_bytes = x->stree_nodes * 64;
     st.stree_layers = x->stree_height;
     st.stree_lds_layers = x->stree_lds_layers;
-    st.top_levels = x->top_levels;
+    st.top_levels = x->rel ? x->rel_lay.levels < SAS_REL_LDS_LEVELS ? x->rel_lay.levels : SAS_REL_LDS_LEVELS : 0;
     st.iterations = x->iters;
     st.rank_lo = rank_lo;
     st.sa_entries = sa_n;
@@ -1811,7 +1771,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.quad_lds_layers = x->quad_lds_layers;
     st.quad_entry_bytes = x->quad_leaves ? (x->quad_compact ? 8 : 16) : 0;
     st.quad_fan = x->quad_leaves ? x->quad_fan : 0;
-    st.top2_levels = x->top2_levels;
+    st.top2_levels = x->rel ? x->rel_lay.levels : 0;
     st.tag_chars = x->tag_p;
     st.tag_table_bytes = x->tag_table   ? ((1ull << (2 * x->tag_p)) + 1) * 8
                          : x->tag_lines ? (1ull << (2 * x->tag_p)) * 128 + ((1ull << (2 * x->tag_p)) + 1) * 8 : 0;
@@ -1819,9 +1779,9 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.tag_line_tag_bits = x->tag_lines ? tl_tag_bits(x->tag_sb) : 0;
     st.text2_bytes = x->text2 ? x->text_words * 8 : 0;
     st.tag_overflow_entries = x->tag_ovf_n;
-    st.top2_bytes = x->top2 ? x->top2_entries * 16 + (((4ull << x->top_levels) + 15) & ~15ull) : 0;
-    st.rel_levels = x->rel ? x->rel_levels : 0;
-    st.rel_bytes = x->rel ? x->rel_bytes : 0;
+    st.top2_bytes = 0;  // round 4: every pivot level is in the rel blocks
+    st.rel_levels = x->rel ? x->rel_lay.levels : 0;
+    st.rel_bytes = x->rel ? x->rel_lay.bytes : 0;
     st.index_bytes = st.text_bytes + st.sa_bytes + st.lcp_bytes + st.llcp_bytes + st.prefix_bytes + st.stree_bytes +
                      st.sector_bytes + st.quad_bytes + st.tag_table_bytes + st.text2_bytes + st.top2_bytes +
                      st.rel_bytes;

@@ -5,11 +5,11 @@
 //
 //   PLAIN  one lane per query, the whole wave64 walks 64 queries in lockstep for
 //          ilog2(n)+1 iterations exactly like binary_search_batch<64>
-//          (sas/sa_search.rs:157-196).  The first SAS_TOP_LEVELS probes of every
-//          query hit the same 4095 pivots; they are served from LDS (pivot SA
-//          value + 32-char packed key), so those probes cost no HBM traffic.
-//          The lane remembers SA[r] of the last right move, so the final
-//          `sa[l]` (:195) needs no extra load.
+//          (sas/sa_search.rs:157-196).  The first levels' pivots come from the
+//          prefix-relative blocks (common.hpp RelLayout): 15 levels from LDS, then
+//          4 levels per request, the rest from SA words and text windows.  The
+//          lane remembers SA[r] of the last right move, so the final `sa[l]`
+//          (:195) needs no extra load unless a key decided it.
 //   LCP    PLAIN + Manber-Myers mlr skipping: chars [0, min(llcp, rlcp)) are known
 //          equal and are not compared again (sas/sa_search.rs:344-345 TODO).
 //   LLCP   PLAIN's probes with Manber-Myers' Llcp/Rlcp accelerant (SAS_BUILD_LLCP):
@@ -52,13 +52,8 @@ struct SearchArgs {
     uint32_t prefix_chars;
     uint32_t prefix_w;       // bytes per table entry (4 or 5)
     uint32_t prefix_hi40;    // inline slots: SA bits 32..39 in slot 1's rank word
-    const uint4* top2;
-    const uint32_t* top_k16;  // the plain levels' 16-char keys, contiguous (LDS staging)
-    uint32_t top_levels;
-    uint32_t top2_levels;
-    const uint8_t* rel;      // PLAIN's prefix-relative pivot blocks (common.hpp SAS_REL_GROUP)
-    RelBase rel_base;
-    uint32_t rel_levels;
+    const uint8_t* rel;      // the prefix-relative pivot blocks (common.hpp RelLayout)
+    RelLayout rel_lay;
     uint32_t iters;
     const uint32_t* stree;
     uint64_t stree_off[SAS_STREE_MAX_LAYERS];
@@ -179,16 +174,40 @@ static_assert(SAS_PLAIN_SA_RUN == 0 || SAS_PLAIN_SA_RUN == 4 || SAS_PLAIN_SA_RUN
 #define BS_PLAIN 0
 #define BS_MLR 1
 #define BS_LLCP 2
+// The rel blocks' LDS groups (common.hpp RelLayout) into a workgroup's LDS: 16-B copies
+__device__ __forceinline__ void stage_rel(uint4* s, const uint8_t* __restrict__ rel, uint32_t bytes) {
+    const uint4* src = reinterpret_cast<const uint4*>(rel);
+    for (uint32_t w = threadIdx.x; w < bytes / 16; w += blockDim.x) s[w] = src[w];
+}
+// Node k's block at level it (the root of group g, hh levels): from LDS for the staged groups,
+// else two (one) 16-B loads of one line, issued together (one request)
+__device__ __forceinline__ void rel_block(const SearchArgs& a, const uint4* s, uint32_t g, uint32_t it, uint32_t k,
+                                          uint32_t hh, uint4& b0, uint4& b1) {
+    const uint64_t off = a.rel_lay.base[g] + ((uint64_t)(k - (1u << it)) << (hh == SAS_REL_GROUP ? 5 : 4));
+    if (g < a.rel_lay.lds_groups) {
+        const uint32_t w = (uint32_t)off >> 4;
+        b0 = s[w];
+        if (hh == SAS_REL_GROUP) b1 = s[w + 1];
+    } else {
+        const uint4* p = reinterpret_cast<const uint4*>(a.rel + off);
+        b0 = p[0];
+        if (hh == SAS_REL_GROUP) b1 = p[1];
+    }
+}
+// Slot j (1..15) of a block: the pivot's chars [P, P + 8) (slot 0 = P)
+__device__ __forceinline__ uint32_t rel_slot(const uint4& b0, const uint4& b1, uint32_t j) {
+    const uint4 v = j >= 8 ? b1 : b0;
+    const uint32_t cw = (j >> 1) & 3u;
+    const uint32_t wv = cw == 0 ? v.x : cw == 1 ? v.y : cw == 2 ? v.z : v.w;
+    return ((j & 1u) ? (wv >> 16) : wv) & 0xFFFFu;
+}
 template <int QW, int MODE, bool TOP, int W, bool RANGE = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
-    // the 16-char keys of the top SAS_TOP_LEVELS levels in LDS, then the prefix-relative
-    // blocks (common.hpp)
-    __shared__ uint32_t s_k16[TOP ? SAS_TOP_NODES : 1];
+    // the prefix-relative pivot blocks, the first 15 levels' from LDS (common.hpp RelLayout)
+    __shared__ uint4 s_rel[TOP ? SAS_REL_LDS_BYTES / 16 : 1];
     const SaView<W> sa{a.sa};
-    uint32_t D = 0;  // the pivot array's plain levels, staged in LDS
     if (TOP) {
-        D = a.top_levels;
-        stage_k16(s_k16, a.top_k16, 1u << D);
+        stage_rel(s_rel, a.rel, a.rel_lay.lds_bytes);
         __syncthreads();
     }
     uint32_t bad = 0;
@@ -231,71 +250,33 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
         };
         uint32_t it = 0;
         if (TOP) {
-            // the plain levels from LDS: decided by the 16-char key unless it ties with q's
-            // first min(m, 16) chars (then the whole entry from the array)
-            for (; it < D; ++it) {
-                if (l < r) {
-                    const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
-                    const uint32_t h = MODE != BS_PLAIN ? (llcp < rlcp ? llcp : rlcp) : 0u;
-                    uint32_t lcp = 0;
-                    sa_val_t<W> p = 0;
-                    bool lt, pk = true;
-                    // LCP / LLCP also need the exact lcp: the first differing char, unless the
-                    // key is below q there and zero from there on (maybe the zero padding of a
-                    // suffix shorter than 16 chars: then the whole entry)
-                    const uint32_t c = q.m < 16 ? q.m : 16;
-                    const uint32_t mk = c ? ~0u << (32 - 2 * c) : 0u;
-                    const uint32_t kk = s_k16[k];
-                    const uint32_t av = kk & mk, bv = (uint32_t)(q.w[0] >> 32) & mk;
-                    const uint32_t dc = av != bv ? (uint32_t)__clz(av ^ bv) >> 1 : 16u;
-                    if (av != bv && (MODE == BS_PLAIN || !(av < bv && (kk << (2 * dc)) == 0))) {
-                        lt = av < bv;
-                        lcp = dc;
-                        pk = false;
-                    } else {
-                        const uint4 e = a.top2[k];
-                        p = (sa_val_t<W>)((uint64_t)e.z | ((uint64_t)e.w << 32));
-                        lt = suffix_less_key<QW>(a.tw, n, p, (uint64_t)e.x | ((uint64_t)e.y << 32), q, h, &lcp);
-                    }
-                    k = 2 * k + (lt ? 1u : 0u);
-                    take(mid, lt, lcp, p, pk);
-                }
-            }
-            // the prefix-relative blocks, 4 levels from one 32-B read (two 16-B loads of one
-            // line, one request): the 8 chars after the block bounds' common prefix of P chars
-            // decide each probe unless they tie with q's (then the SA value -- LLCP: from its
-            // entry -- and the text from char P + c).  q starts with those P chars (common.hpp),
-            // and a key padded past its suffix's end that differs from q there is a proper
-            // prefix of q (key < q)
-            while (it < a.rel_levels) {
-                const uint32_t hh = a.rel_levels - it < SAS_REL_GROUP ? a.rel_levels - it : SAS_REL_GROUP;
+            // the prefix-relative blocks, 4 levels from one 32-B block (LDS, or two 16-B loads
+            // of one line: one request): the 8 chars after the block bounds' common prefix of P
+            // chars decide each probe unless they tie with q's (then the SA value -- LLCP: from
+            // its entry -- and the text from char P + c).  q starts with those P chars
+            // (common.hpp), and a key padded past its suffix's end that differs from q there is
+            // a proper prefix of q (key < q)
+            for (uint32_t g = 0; g < a.rel_lay.groups; ++g) {
+                const uint32_t hh = a.rel_lay.h[g];
                 uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0;
-                if (l < r) {
-                    const uint8_t* blk = a.rel + a.rel_base.b[(it - D) / SAS_REL_GROUP] + 32ull * (k - (1u << it));
-                    b0 = *reinterpret_cast<const uint4*>(blk);
-                    if (hh == SAS_REL_GROUP) b1 = *reinterpret_cast<const uint4*>(blk + 16);
-                }
-                const uint32_t P = b0.x & 0xFFFFu;
+                if (l < r) rel_block(a, s_rel, g, it, k, hh, b0, b1);
+                const uint32_t P = b0.x & 0x7FFFu;
                 const uint32_t c0 = q.m > P ? q.m - P : 0u;
-                const uint32_t c = c0 < 8 ? c0 : 8u;
+                // LCP / LLCP need exact lcps: a block flagged (bit 15) as holding a pivot whose
+                // suffix ends inside its key compares no key chars (every probe: the entry and
+                // the text from P)
+                const uint32_t c = (MODE != BS_PLAIN && (b0.x & 0x8000u)) ? 0u : c0 < 8 ? c0 : 8u;
                 const uint32_t mk = c ? (0xFFFFu << (16 - 2 * c)) & 0xFFFFu : 0u;
                 const uint32_t qk = (uint32_t)((q.w[0] << (2 * P)) >> 48) & mk;
                 for (uint32_t t = 0; t < hh; ++t, ++it) {
                     if (!(l < r)) continue;
                     const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
-                    const uint32_t j = (1u << t) | (k & ((1u << t) - 1u));
-                    const uint4 v = j >= 8 ? b1 : b0;
-                    const uint32_t cw = (j >> 1) & 3u;
-                    const uint32_t wv = cw == 0 ? v.x : cw == 1 ? v.y : cw == 2 ? v.z : v.w;
-                    const uint32_t kr = ((j & 1u) ? (wv >> 16) : wv) & 0xFFFFu;
-                    const uint32_t key = kr & mk;
-                    // LCP / LLCP: lcp = P + the first differing char, unless the key is below q
-                    // there and zero from there on (maybe padding past its suffix's end)
-                    const uint32_t dc = key != qk ? ((uint32_t)__clz(key ^ qk) - 16u) >> 1 : 8u;
+                    const uint32_t key = rel_slot(b0, b1, (1u << t) | (k & ((1u << t) - 1u))) & mk;
+                    // LCP / LLCP: lcp = P + the first differing char
                     sa_val_t<W> p = 0;
-                    uint32_t lcp = P + dc;
+                    uint32_t lcp = key != qk ? P + (((uint32_t)__clz(key ^ qk) - 16u) >> 1) : 0u;
                     bool lt, pk = false;
-                    if (key != qk && (MODE == BS_PLAIN || !(key < qk && ((kr << (2 * dc)) & 0xFFFFu) == 0))) {
+                    if (key != qk) {
                         lt = key < qk;
                     } else {
                         if (MODE == BS_LLCP) {
@@ -304,9 +285,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
                         } else {
                             p = (sa_val_t<W>)sa[mid];
                         }
-                        // chars [0, P + c) are known equal unless the keys differ (LLCP's
-                        // padding case): then from P
-                        lt = suffix_less_from<QW>(a.tw, n, p, q, key != qk ? P : P + c, &lcp);
+                        // chars [0, P + c) are known equal
+                        lt = suffix_less_from<QW>(a.tw, n, p, q, P + c, &lcp);
                         pk = true;
                     }
                     k = 2 * k + (lt ? 1u : 0u);
@@ -1257,11 +1237,9 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad_range(SearchArgs a,
 // word + two text words.
 template <int QW, bool TOP, bool KO, int W>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
-    __shared__ uint32_t s_k16[TOP ? SAS_TOP_NODES : 1];  // the top levels' 16-char keys
-    uint32_t D = 0;
+    __shared__ uint4 s_rel[TOP ? SAS_REL_LDS_BYTES / 16 : 1];  // the rel blocks' LDS groups
     if (TOP) {
-        D = a.top_levels;
-        stage_k16(s_k16, a.top_k16, 1u << D);
+        stage_rel(s_rel, a.rel, a.rel_lay.lds_bytes);
         __syncthreads();
     }
     uint32_t bad = 0;
@@ -1286,33 +1264,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
         };
         uint32_t it = 0;
         if (TOP) {
-            for (; it < D; ++it) {  // the LDS levels: the 16-char key, a whole entry on a tie
-                if (l < r) {
-                    const uint64_t mid = (l + r) >> 1;
-                    bool ge;
-                    uint64_t p = QUAD_NO_SA;
-                    if (s_k16[k] != (uint32_t)(K64 >> 32)) {
-                        ge = s_k16[k] > (uint32_t)(K64 >> 32);
-                    } else {
-                        const uint4 e = a.top2[k];
-                        p = (uint64_t)e.z | ((uint64_t)e.w << 32);
-                        ge = sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), p, K64, a, q);
-                    }
-                    k = 2 * k + (ge ? 0u : 1u);
-                    take(mid, ge, p);
-                }
-            }
-            // the prefix-relative blocks, as PLAIN: 4 levels from one 32-B read; an 8-char tie
-            // reads the probe's own entry (key != K64 decides key > K64, the sector predicate)
-            while (it < a.rel_levels) {
-                const uint32_t hh = a.rel_levels - it < SAS_REL_GROUP ? a.rel_levels - it : SAS_REL_GROUP;
+            // the prefix-relative blocks, as PLAIN reads them; an 8-char tie reads the probe's
+            // own entry (key != K64 decides key > K64, the sector predicate)
+            for (uint32_t g = 0; g < a.rel_lay.groups; ++g) {
+                const uint32_t hh = a.rel_lay.h[g];
                 uint4 b0 = make_uint4(0, 0, 0, 0), b1 = b0;
-                if (l < r) {
-                    const uint8_t* blk = a.rel + a.rel_base.b[(it - D) / SAS_REL_GROUP] + 32ull * (k - (1u << it));
-                    b0 = *reinterpret_cast<const uint4*>(blk);
-                    if (hh == SAS_REL_GROUP) b1 = *reinterpret_cast<const uint4*>(blk + 16);
-                }
-                const uint32_t P = b0.x & 0xFFFFu;
+                if (l < r) rel_block(a, s_rel, g, it, (uint32_t)k, hh, b0, b1);
+                const uint32_t P = b0.x & 0x7FFFu;
                 const uint32_t c0 = q.m > P ? q.m - P : 0u;
                 const uint32_t c = c0 < 8 ? c0 : 8u;
                 const uint32_t mk = c ? (0xFFFFu << (16 - 2 * c)) & 0xFFFFu : 0u;
@@ -1320,11 +1278,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
                 for (uint32_t t = 0; t < hh; ++t, ++it) {
                     if (!(l < r)) continue;
                     const uint64_t mid = (l + r) >> 1;
-                    const uint32_t j = (1u << t) | (k & ((1u << t) - 1u));
-                    const uint4 v = j >= 8 ? b1 : b0;
-                    const uint32_t cw = (j >> 1) & 3u;
-                    const uint32_t wv = cw == 0 ? v.x : cw == 1 ? v.y : cw == 2 ? v.z : v.w;
-                    const uint32_t key = ((j & 1u) ? (wv >> 16) : wv) & mk;
+                    const uint32_t key = rel_slot(b0, b1, (1u << t) | (k & ((1u << t) - 1u))) & mk;
                     bool ge;
                     uint64_t p = QUAD_NO_SA;
                     if (key != qk) {
@@ -2700,13 +2654,8 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.prefix_chars = x->prefix_chars;
     a.prefix_w = x->prefix_w;
     a.prefix_hi40 = x->prefix_hi40;
-    a.top2 = x->top2;
-    a.top_k16 = x->top_k16;
-    a.top_levels = x->top_levels;
-    a.top2_levels = x->top2_levels;
     a.rel = x->rel;
-    a.rel_base = x->rel_base;
-    a.rel_levels = x->rel ? x->rel_levels : 0;
+    a.rel_lay = x->rel_lay;
     a.iters = x->iters;
     a.stree = x->stree;
     for (int h = 0; h < SAS_STREE_MAX_LAYERS; h++) a.stree_off[h] = x->stree_off[h];

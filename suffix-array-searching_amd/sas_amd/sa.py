@@ -115,8 +115,8 @@ class SaNaive:
         the library, an int = that p) for algo="tagged"; it replaces the SA and leaves out the
         trees, LLCP and the prefix tables (their defaults turn off).  top2_levels: depth of
         the binary-search pivots (SAS_BUILD_TOP2_LEVELS, rounded up to 4-level prefix-relative
-        blocks past the 14 LDS levels; 0 = the library default, the 26 cache-resident levels,
-        136 MiB; 30 = 2.1 GiB at n = 2^30).
+        blocks past the 15 LDS levels; 0 = the library default, 27 levels, 273 MiB; 30 -> all
+        31 levels of n = 2^30, 4.3 GiB).
         tag_lines (with tagged): the tagged entries as 128-B bucket lines + an overflow array
         (SAS_BUILD_TAG_LINES; p = ceil(log4 n) - 2 unless tagged gives it): one request gives a
         lookup its bucket and first 20 entries; algo="tagged" only, no SA array."""

@@ -65,43 +65,47 @@ def test_byte_model_splits_served_levels():
     q = bench.bytes_per_lookup("quad", st, n, m, 8.0)
     # quad at 2^30: 3 LDS layers, the 206 KB / 3.5 MB / 59 MB layers in cache, 1 GB + leaves in HBM
     assert q["lds"] == 3 * 64 and q["cache"] == 3 * 64 and q["hbm"] == 2 * 64 + m + 8
-    # PLAIN: the 14 plain levels' 16-char keys in LDS (4 B), then one 32-B prefix-relative block
-    # per 4 levels (26 levels: 3 blocks, cache-resident), then SA word + text window per probe
-    st26 = dict(st, top2_levels=26, rel_levels=26, rel_bytes=bench.rel_bytes(14, 26))
-    p = bench.bytes_per_lookup("plain", st26, n, m, 31.0)
-    assert p["lds"] == 14 * 4 and p["cache"] == 3 * 32 and p["hbm"] == 5 * (4 + m / 4) + m + 8
-    assert p["requests_model"] == {"cache": 3.0, "hbm": 5 * 2 + m / 128}
+    # PLAIN: prefix-relative blocks, levels 1-15 from LDS (3 blocks of 32 B, one of 16 B), 16-27
+    # in 3 requests (16-19 and 20-23 cache-resident, 24-27 past the cache's 256 MiB), then SA word
+    # + text window per probe
+    st27 = dict(st, top2_levels=27, rel_levels=27, rel_bytes=bench.rel_bytes(27))
+    p = bench.bytes_per_lookup("plain", st27, n, m, 31.0)
+    assert p["lds"] == 3 * 32 + 16 and p["cache"] == 2 * 32 and p["hbm"] == 32 + 4 * (4 + m / 4) + m + 8
+    assert p["requests_model"] == {"cache": 2.0, "hbm": 1 + 4 * 2 + m / 128}
     # LLCP: the same pivots (exact lcps off the keys), then one 16-B entry per probe
-    ll = bench.bytes_per_lookup("llcp", st26, n, m, 31.0)
-    assert ll["lds"] == 14 * 4 and ll["cache"] == 3 * 32 and ll["hbm"] == 5 * 16 + m + 8
-    assert ll["requests_model"] == {"cache": 3.0, "hbm": 5 + m / 128}
+    ll = bench.bytes_per_lookup("llcp", st27, n, m, 31.0)
+    assert ll["lds"] == 3 * 32 + 16 and ll["cache"] == 2 * 32 and ll["hbm"] == 32 + 4 * 16 + m + 8
+    assert ll["requests_model"] == {"cache": 2.0, "hbm": 1 + 4 + m / 128}
     h = bench.bytes_per_lookup("prefix", st, n, m, 1.0)
     assert h["hbm"] == 32 + m + 8 and h["cache"] == 0 and h["lds"] == 0
     assert bench._tree_layers(n, 4, 64, 17, 64, 8)[-1] == n // 4 * 64
 
 
 def test_byte_model_hbm_pivot_levels():
-    """Deep pivots (SAS_BUILD_TOP2_LEVELS = 30): blocks of levels 15-18, 19-22, 23-26
-    cache-resident (136 MiB), 27-30 from HBM (the 2 GiB group), level 31 an SA word + a text
-    window; requests by tier."""
-    assert bench.rel_bytes(14, 26) == 32 * ((1 << 14) + (1 << 18) + (1 << 22))
-    assert [c for _, _, c in bench.rel_groups(14, 30)] == [True, True, True, False]
-    st = {"sa_width": 4, "top_levels": 14, "top2_levels": 30, "rel_levels": 30, "rel_bytes": bench.rel_bytes(14, 30)}
+    """Deep pivots (SAS_BUILD_TOP2_LEVELS = 30, rounded up to all 31 levels of a 2^30 text):
+    levels 1-15 from LDS, blocks of 16-19 and 20-23 cache-resident, 24-27 and 28-31 from HBM;
+    the keys decide every level, then SA[r] is one read; requests by tier."""
+    assert bench.rel_bytes(27) == 74272 + 32 * ((1 << 15) + (1 << 19) + (1 << 23))
+    assert [(d, h) for d, h, _ in bench.rel_groups(27)] == [(0, 4), (4, 4), (8, 4), (12, 3), (15, 4), (19, 4), (23, 4)]
+    assert [w for _, _, w in bench.rel_groups(31)] == ["lds"] * 4 + ["cache", "cache", "hbm", "hbm"]
+    assert bench.rel_levels(31, 30) == 31 and bench.rel_levels(31, 0 or 27) == 27 and bench.rel_levels(25, 27) == 25
+    assert bench.rel_levels(31, 16) == 19 and bench.rel_levels(31, 5) == 5
+    st = {"sa_width": 4, "top_levels": 15, "top2_levels": 31, "rel_levels": 31, "rel_bytes": bench.rel_bytes(31)}
     n, m = 1 << 30, 32
-    p30 = bench.bytes_per_lookup("plain", st, n, m, 31.0)
-    assert p30["lds"] == 14 * 4 and p30["cache"] == 3 * 32
-    assert p30["hbm"] == 32 + 1 * (4 + m / 4) + m + 8
-    assert p30["requests_model"] == {"cache": 3.0, "hbm": 1 + 2 * 1 + m / 128}
+    p31 = bench.bytes_per_lookup("plain", st, n, m, 31.0)
+    assert p31["lds"] == 3 * 32 + 16 and p31["cache"] == 2 * 32
+    assert p31["hbm"] == 2 * 32 + 4 + m + 8
+    assert p31["requests_model"] == {"cache": 2.0, "hbm": 2 + 1 + m / 128}
     # fewer probes than the pivot levels (a short range): blocks entered only, SA[r] at the end
     p20 = bench.bytes_per_lookup("plain", st, n, m, 20.0)
     assert p20["hbm"] == 4 + m + 8 and p20["cache"] == 2 * 32
     assert p20["requests_model"] == {"cache": 2.0, "hbm": 1 + m / 128}
-    # INLINE: the same blocks, then level 31's fused entry
+    # INLINE: the same blocks, then its fused entry for SA[r]
     pin = bench.bytes_per_lookup("inline", st, n, m, 31.0)
-    assert pin["hbm"] == 32 + 16 + m + 8 and pin["requests_model"]["hbm"] == 1 + 1 + m / 128
-    assert pin["requests_model"]["cache"] == 3.0
+    assert pin["hbm"] == 2 * 32 + 16 + m + 8 and pin["requests_model"]["hbm"] == 2 + 1 + m / 128
+    assert pin["requests_model"]["cache"] == 2.0
     # the split: model HBM requests first, the rest of the PMC count is cache-served
-    bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23, rel_levels=23, rel_bytes=bench.rel_bytes(14, 23)),
+    bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23, rel_levels=23, rel_bytes=bench.rel_bytes(23)),
                                  n, m, 31.0)
     assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
     nq, kms = 10_000_000, 5.0
@@ -154,8 +158,8 @@ def _stats_2e30():
     u32 SA, 26 pivot levels, fused quad leaves, p = 16 two-suffix inline table)."""
     n = 1 << 30
     return {"n": n, "sa_entries": n, "text_bytes": (n // 32 + 4) * 8, "sa_bytes": 4 * n, "sa_width": 4,
-            "top_levels": 14, "top2_levels": 26, "rel_levels": 26, "rel_bytes": 32 * ((1 << 14) + (1 << 18) + (1 << 22)),
-            "top2_bytes": (16 << 14) + (4 << 14), "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
+            "top_levels": 15, "top2_levels": 27, "rel_levels": 27,
+            "rel_bytes": 74272 + 32 * ((1 << 15) + (1 << 19) + (1 << 23)), "top2_bytes": 0, "lcp_bytes": 4 * n, "llcp_bytes": 16 * n, "quad_entry_bytes": 16,
             "quad_bytes": 18_325_000_000, "sector_bytes": 19_400_000_000, "stree_bytes": 4_563_402_752,
             "prefix_bytes": (4 ** 16 + 1) * 32, "prefix_chars": 16, "index_bytes": 205_755_777_696}
 
@@ -166,12 +170,12 @@ def test_footprint_per_algorithm():
     st = _stats_2e30()
     gib = 1 << 30
     text = st["text_bytes"]
-    piv = (20 << 14) + st["rel_bytes"]  # the LDS levels' entries + keys, the 136 MiB of rel blocks
-    assert 136 << 20 < piv < 137 << 20
-    assert bench.footprint("plain", st) == 4 * gib + text + piv  # ~4.4 GiB
-    assert 4.3 * gib < bench.footprint("plain", st) < 4.5 * gib
-    st30 = dict(st, top2_levels=30, rel_levels=30, rel_bytes=bench.rel_bytes(14, 30))
-    assert bench.footprint("plain", st30) == 4 * gib + text + (20 << 14) + bench.rel_bytes(14, 30)
+    piv = st["rel_bytes"]  # the prefix-relative pivot blocks, 273 MiB
+    assert 273 << 20 < piv < 274 << 20
+    assert bench.footprint("plain", st) == 4 * gib + text + piv  # ~4.5 GiB
+    assert 4.3 * gib < bench.footprint("plain", st) < 4.6 * gib
+    st31 = dict(st, top2_levels=31, rel_levels=31, rel_bytes=bench.rel_bytes(31))
+    assert bench.footprint("plain", st31) == 4 * gib + text + bench.rel_bytes(31)
     assert bench.footprint("llcp", st) == 16 * gib + text + piv
     assert bench.footprint("quad", st) == st["quad_bytes"] + text  # ~17 GiB
     assert bench.footprint("prefix", st) == 128 * gib + 32 + 16 * gib + text  # table + fused leaves + text
@@ -233,8 +237,8 @@ def test_every_headline_algo_has_a_workload_label():
     choices = re.search(r'"--algo", default=None, choices=\[([^\]]*)\]', src).group(1)
     algos = [a.strip().strip('"') for a in choices.replace("\n", " ").split(",") if a.strip()]
     assert "plain" in algos and len(algos) >= 8
-    st = {"top_levels": 14, "rel_levels": 26, "rel_bytes": bench.rel_bytes(14, 26)}
-    assert "26" in bench.plain_label(st)
+    st = {"top_levels": 15, "rel_levels": 27, "rel_bytes": bench.rel_bytes(27)}
+    assert "1-27" in bench.plain_label(st) and "24-27 from HBM" in bench.plain_label(st)
     for a in algos:
         if a != "plain":
             assert a in bench.WORKLOADS, a

@@ -1073,8 +1073,8 @@ def test_occurrence_ranges_inline_slots(sas):
 
 
 def test_blocked_pivot_levels(sas):
-    """The pivot depth (SAS_BUILD_TOP2_LEVELS): the LDS levels' entries (16-char keys in LDS),
-    then prefix-relative blocks of 4 levels, the depth rounded up to that grid and clamped to
+    """The pivot depth (SAS_BUILD_TOP2_LEVELS): prefix-relative blocks of up to 4 levels, the
+    first 15 levels staged in LDS, the depth rounded up to the grid past them and clamped to
     the 25 iterations of an n = 3 x 2^23 text.  Every depth (blocks of 1..4 levels, none at
     all) gives PLAIN, LCP, LLCP and INLINE the positions and probe counts of the oracle's
     binary_search (sas/sa_search.rs:98-112), and sas_stats top2_bytes / rel_bytes are the
@@ -1093,14 +1093,10 @@ def test_blocked_pivot_levels(sas):
         idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False,
                                 top2_levels=L)
         st = idx.stats()
-        lv = min(26 if L == 0 else L, st["iterations"])
-        D = min(lv, 14)
-        R = min(D + -(-(lv - D) // 4) * 4, st["iterations"]) if lv > D else 0
-        assert st["top_levels"] == D and st["rel_levels"] == R, (L, st["top_levels"], st["rel_levels"])
-        assert st["top2_levels"] == (R or D), L
-        # the LDS levels' entries, and their 16-char keys again, contiguous (LDS staging)
-        assert st["top2_bytes"] == (16 << D) + (((4 << D) + 15) & ~15), L
-        assert st["rel_bytes"] == (bench.rel_bytes(D, R) if R else 0), L
+        R = bench.rel_levels(st["iterations"], 27 if L == 0 else L)
+        assert st["top_levels"] == min(R, 15) and st["rel_levels"] == R and st["top2_levels"] == R, \
+            (L, st["top_levels"], st["rel_levels"])
+        assert st["top2_bytes"] == 0 and st["rel_bytes"] == bench.rel_bytes(R), L
         if ref is None:
             sa = idx.suffix_array()
             tp = O.padded(t)
@@ -1112,9 +1108,10 @@ def test_blocked_pivot_levels(sas):
             assert np.array_equal(got, ref_all), (L, algo)
             assert np.array_equal(pr, ref_pr), (L, algo)
         idx.free()
-    # the groups: 4 levels each from the LDS levels on, the last one clamped
-    assert [(d, h) for d, h, _ in bench.rel_groups(14, 26)] == [(14, 4), (18, 4), (22, 4)]
-    assert [(d, h) for d, h, _ in bench.rel_groups(14, 25)] == [(14, 4), (18, 4), (22, 3)]
+    # the groups: 4 levels each (a 3-level one ends the LDS part at 15), the last one clamped
+    assert [(d, h) for d, h, _ in bench.rel_groups(27)] == [(0, 4), (4, 4), (8, 4), (12, 3), (15, 4), (19, 4), (23, 4)]
+    assert [(d, h) for d, h, _ in bench.rel_groups(25)][-1] == (23, 2)
+    assert [(d, h) for d, h, _ in bench.rel_groups(5)] == [(0, 4), (4, 1)]
 
 
 def test_rel_pivot_blocks(sas):
@@ -1125,6 +1122,7 @@ def test_rel_pivot_blocks(sas):
     included), one-char mutations at every offset, negatives and text-end suffixes: PLAIN,
     LCP, LLCP and INLINE equal the oracle's binary_search (sas/sa_search.rs:98-112) and PLAIN
     without the pivot levels, positions (and probe counts, where they follow it)."""
+    import bench
     from sas_amd import _lib
     rng = np.random.default_rng(21)
     base = sas.random_string(3 << 20, seed=99)
@@ -1138,7 +1136,7 @@ def test_rel_pivot_blocks(sas):
         n = len(t)
         idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False)
         st = idx.stats()
-        assert st["rel_levels"] == min(26, st["iterations"]) and st["rel_bytes"] > 0, (name, st["rel_levels"])
+        assert st["rel_levels"] == bench.rel_levels(st["iterations"], 27) and st["rel_bytes"] > 0, name
         sa = idx.suffix_array()
         qs = []
         for m in list(range(0, 41)) + [64, 100]:

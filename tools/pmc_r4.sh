@@ -3,18 +3,18 @@
 # TCC_EA0_RDREQ + 32B + hit/miss) over bench.py for each record whose traffic bench.py
 # reports, summarised into gpurun_out/pmc_r4/pmc_<key>.json stamped with the library's
 # source hash (copy them into profiles/ to have bench.py attach them).
-# usage: tools/pmc_r4.sh [keys...]   keys: prefix plain26 plain30 quad stree sector llcp c3 (bucket lines) c3tagged
+# usage: tools/pmc_r4.sh [keys...]   keys: prefix plain27 plain31 quad stree sector llcp c3 (bucket lines) c3tagged
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 out=gpurun_out/pmc_r4
 mkdir -p "$out"
-keys=${*:-prefix plain26 plain30 quad stree sector llcp c3 c3tagged}
+keys=${*:-prefix plain27 plain31 quad stree sector llcp c3 c3tagged}
 base="--no-cpu --no-c3 --no-c4 --no-e2e --no-lcp-long --variants= --c1-deep-levels 0 --steps 3 --warmup 1 --detail="
 for k in $keys; do
   case $k in
     prefix)  args="$base --algo prefix"; kern=k_sa_prefix2; nq=10000000; name=prefix16d_n1073741824_q10000000_m32 ;;
-    plain26) args="$base --algo plain"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t26 ;;
-    plain30) args="$base --algo plain --top2-levels 30"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t30 ;;
+    plain27) args="$base --algo plain"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t27 ;;
+    plain31) args="$base --algo plain --top2-levels 30"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t31 ;;
     quad)    args="$base --algo quad"; kern=k_sa_quad; nq=10000000; name=quad_n1073741824_q10000000_m32 ;;
     stree)   args="$base --algo stree"; kern=k_sa_stree; nq=10000000; name=stree_n1073741824_q10000000_m32 ;;
     sector)  args="$base --algo sector"; kern=k_sa_sector; nq=10000000; name=sector_n1073741824_q10000000_m32 ;;
