@@ -1,6 +1,7 @@
-"""Same-box A/B of the pivot-array readers: PLAIN, LLCP and INLINE kernel times at n = 2^30,
-10^7 positive queries (m = 32; LLCP also 64 / 128), on the default 23-level pivot array and
-on a 30-level one, for the library under AB_PKG (a tools/mk_variant.sh build) or the tree's:
+"""Same-box A/B of the pivot readers: PLAIN, LLCP and INLINE kernel times at n = 2^30, 10^7
+positive queries (m = 32; LLCP also 64 / 128), at the library's default pivot depth and at
+SAS_BUILD_TOP2_LEVELS(30) (keys name the depth the index reports), for the library under
+AB_PKG (a tools/mk_variant.sh build, or a git-archive build of another commit) or the tree's:
     AB_PKG=tools/_var_<name>/suffix-array-searching_amd python3 tools/ab_pivots.py"""
 import json
 import os
