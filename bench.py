@@ -102,7 +102,7 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
     hbm = cache = lds = 0.0
     sa_w = st["sa_width"]
     if algo == "prefix" and not range_flag:
-        entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)
+        entry = prefix_entry_bytes(st)
         hbm += entry  # the table entry (inline entries hold the range's first suffixes)
         leaf = 16 if st["quad_entry_bytes"] == 16 else 8 + sa_w
         hbm += max(0.0, probes - 1) * leaf
@@ -115,7 +115,7 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
     elif algo == "tagged":
         hbm += 8 + min(n / 4 ** st["tag_chars"] + 1, 8) * 8 + max(0.0, m - st["tag_chars"] - 12) / 4
     elif range_flag:  # PLAIN / LCP from the prefix table's range: table entry + SA word + window per probe
-        entry = st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1)  # (INTERP: a fused 16-B entry per probe)
+        entry = prefix_entry_bytes(st)  # (INTERP: a fused 16-B entry per probe)
         per = 16 if (algo == "interp" and st["quad_entry_bytes"] == 16) else sa_w + win
         hbm += entry + max(0.0, probes - 1) * per
     elif algo in ("plain", "lcp", "inline", "llcp"):
@@ -284,6 +284,36 @@ def rel_bytes(R: int) -> int:
 
 
 # ---------------------------------------------------------------- index footprints
+def prefix_entry_bytes(st: dict) -> int:
+    """Bytes per prefix-table entry (4, 5, 16, 32, 64): a part's table covers only its own key
+    interval (sas_stats.prefix_entries), a whole index's all 4^p + 1 keys."""
+    ents = st.get("prefix_entries") or (4 ** st["prefix_chars"] + 1)
+    return st["prefix_bytes"] // ents if ents else 0
+
+
+C4_SHARE_TARGET = 1 << 33  # SURVEY §8(e): n = 2^33 chars per GPU
+
+
+def c4_part_bytes(share: int, ws: int, p: int = 16, entry: int = 32) -> int:
+    """HBM of one configs[4] rank's part index (sas_build_part_gen, PREFIX): the whole text
+    packed (ws x share / 4), its SA range 40-bit (5 B a suffix), the fused quad leaves (16 B)
+    and inner nodes (<= 1 B a suffix), the two-suffix inline table over the part's share of
+    the 4^p keys (a whole index: all of them; + 5% for an uneven key split), the 72.5 KiB of
+    LDS pivot groups."""
+    keys = 4 ** p + 1 if ws == 1 else int(4 ** p / ws * 1.05) + 3
+    return ws * share // 4 + 5 * share + 17 * share + keys * entry + (1 << 20)
+
+
+def c4_share_for(ws: int, hbm_bytes: int, reserve: int = 12 << 30) -> int:
+    """The largest power-of-two share <= 2^33 chars per GPU whose part index fits one GPU's HBM
+    with `reserve` left for the step's buffers and the runtime (N = 1: 2^32, the whole
+    4^16-key table; N >= 2: 2^33)."""
+    share = C4_SHARE_TARGET
+    while share > (1 << 20) and c4_part_bytes(share, ws) > hbm_bytes - reserve:
+        share //= 2
+    return share
+
+
 def _quad_leaf_bytes(st: dict) -> int:
     """The quad tree's leaf layer: 64-B leaves of 4 fused {key64, SA} entries (16 B) or 8
     key-only entries (compact, 8 B)."""
@@ -879,11 +909,15 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     per rank (sas_build_part, no rank builds the whole SA), queries routed to the owner of
     their lower bound with RCCL all_to_all_single over fixed-capacity buckets, PREFIX
     queries crossing as 8-B packed words, positions back.  Weak scaling at a fixed share
-    of args.c4_share chars per GPU (BASELINE's "512 GiB" cannot hold a full SA even across
-    8 x 288 GB); each rank searches its own 10^7 len-32 positive queries.
-    N = 1 runs the same step through a world-1 RCCL group."""
+    of args.c4_share chars per GPU (default: the largest share <= 2^33 whose part fits one
+    GPU, c4_share_for: 2^33 at N >= 2, 2^32 at N = 1 where the one part holds the whole
+    4^16-key table; BASELINE's "512 GiB" cannot hold a full SA even across 8 x 288 GB,
+    DESIGN.md §6); each part's inline table covers only its own key interval (1/N of the
+    keys); each rank searches its own 10^7 len-32 positive queries.  N = 1 runs the same
+    step through a world-1 RCCL group."""
     from sas_amd.shard import ShardedSearch
-    n = args.c4_share * ws
+    share = args.c4_share or c4_share_for(ws, torch.cuda.mem_get_info(dev)[1])
+    n = share * ws
     nq, m = args.nq, args.m
     t0 = time.perf_counter()
     own = None
@@ -904,8 +938,10 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
         # text, n/4 bytes: compares need any suffix), never as n bytes; the part holds only
         # its own SA rank range (sas_build_part_gen) with the two-suffix inline table
         # (local ranks < 2^32; SA bits 32..39 in slot 1 above 2^32 chars)
+        # (the pivot blocks: the LDS levels only, 72.5 KiB -- PREFIX never reads them)
         idx = sas_amd.SaNaive.build_part_gen(n, seed=SEED + 1, part=rank, parts=ws, lcp=False, stree=False,
-                                             sector=False, quad=True, llcp=False, prefix=16, prefix_inline=2)
+                                             sector=False, quad=True, llcp=False, prefix=16, prefix_inline=2,
+                                             top2_levels=TOP_LDS_LEVELS)
         st = idx.stats()
         off = torch.from_numpy(rank_query_offsets(n, nq, m, rank).astype(np.int64)).to(dev)
         qbytes = torch.empty(nq * m, dtype=torch.uint8, device=dev)
@@ -978,7 +1014,7 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     if int(bad.item()):
         raise SystemExit(f"bench c4: {int(bad.item())} sampled sharded answers are not exact lower bounds")
     cap = engine.capacity(-(-nq // max(1, args.shard_chunks)))  # per piece
-    rec = {"workload": f"configs[4]-shaped: text of {ws} x {args.c4_share} chars sharded by SA rank ranges over "
+    rec = {"workload": f"configs[4]-shaped: text of {ws} x {share} chars sharded by SA rank ranges over "
                        f"{ws} GPU(s) (sas_build_part), {nq} len-{m} queries per GPU routed with RCCL "
                        f"all_to_all_single (fixed-capacity buckets, 8-B packed PREFIX queries, per-bucket counts "
                        f"exchanged so only filled slots are searched), positions back"
@@ -986,7 +1022,9 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
                           "(rccl_world1 times them through RCCL)" if ws == 1 else ""),
            "n": n, "parts": ws, "lookups_per_s": ws * nq * args.c4_steps / el, "ms_per_step": el / args.c4_steps * 1e3,
            "steps": args.c4_steps, "scaling": "weak", "part_sa_entries": st["sa_entries"],
-           "prefix_entry_bytes": st["prefix_bytes"] // (4 ** st["prefix_chars"] + 1),
+           "prefix_entry_bytes": prefix_entry_bytes(st), "share": share,
+           "prefix_keys": st["prefix_entries"], "prefix_bytes": st["prefix_bytes"],
+           "prefix_key_fraction": _r(st["prefix_entries"] / (4 ** st["prefix_chars"] + 1)),
            "bucket_capacity": cap, "pieces": args.shard_chunks,
            "alt_pieces": {"pieces": alt_chunks, "ms_per_step": el2 / max(3, args.c4_steps // 2) * 1e3,
                           "lookups_per_s": ws * nq * max(3, args.c4_steps // 2) / el2, "identical": True},
@@ -1388,9 +1426,9 @@ def main():
                          "rank-ordered with a bucket table; with lines the rank-ordered index runs as the cross-check")
     ap.add_argument("--proof-sample", type=int, default=3000, help="queries per batch proven exact lower bounds")
     ap.add_argument("--no-c4", action="store_true", help="skip the configs[4] (sharded text) sub-record")
-    ap.add_argument("--c4-share", type=int, default=1 << 31,
-                    help="configs[4]: text chars per GPU (2^31: at N = 8 the 2^34-char text exceeds what one GPU's "
-                         "replicated index of this shape holds)")
+    ap.add_argument("--c4-share", type=int, default=0,
+                    help="configs[4]: text chars per GPU (0: the largest power of two <= 2^33 whose part index fits "
+                         "one GPU, bench.c4_share_for: 2^33 at N >= 2, 2^32 at N = 1)")
     ap.add_argument("--shard-chunks", type=int, default=1,
                     help="sharded step in this many pieces, exchanges overlapped with the other pieces' work")
     ap.add_argument("--c4-steps", type=int, default=10)
@@ -1664,7 +1702,7 @@ def main():
         del lo_d, hi_d, lo_b, hi_b, cnt_d
         log(f"ranges: {rms:.3f} ms (bisection {bms:.3f} ms)")
 
-    pe = stats["prefix_bytes"] // (4 ** stats["prefix_chars"] + 1) if stats["prefix_chars"] else 0
+    pe = prefix_entry_bytes(stats) if stats["prefix_chars"] else 0
     pkey = str(stats["prefix_chars"]) + {16: "i", 32: "d", 64: "q"}.get(pe, "")
     hpmc = load_pmc(f"{args.algo}{pkey if args.algo == 'prefix' else ''}_n{n}_q{nq}_m{m}")
     hbpl = bytes_per_lookup(args.algo, stats, n, m, mean_probes)

@@ -241,6 +241,12 @@ typedef struct sas_stats {
     uint64_t rel_bytes;      /* their array: one 32-B block {lcp of the block's bounds, the
                                 8 chars after it of each of 15 pivots} per 4-level subtree
                                 (16 B for a shorter one), the LDS levels' first    */
+    uint64_t prefix_key_lo;  /* SAS_BUILD_PREFIX: the first p-char key the table holds an entry
+                                for: 0 for a whole index; for a part / shard (a contiguous SA
+                                rank range) the key of its first suffix                */
+    uint64_t prefix_entries; /* its entries: 4^p + 1 for a whole index; for a part, its first
+                                suffix's key .. its last one's + 2 (1/8 of the keys each at 8
+                                parts of a random text); prefix_bytes = entries x entry bytes */
 } sas_stats;
 
 const char* sas_last_error(void);

@@ -138,11 +138,14 @@ struct sas_index {
     uint8_t* sa = nullptr;        // sa_w bytes per entry (SaView<4> / SaView<5>)
     uint32_t sa_w = 4;
     uint32_t* lcp = nullptr;
-    uint8_t* prefix = nullptr;    // SAS_BUILD_PREFIX: [4^prefix_chars + 1] first rank per p-char key,
-    uint32_t prefix_chars = 0;    // prefix_w bytes per entry (4: u32; 5: packed 40-bit, for a 40-bit SA)
-    uint32_t prefix_w = 4;
+    uint8_t* prefix = nullptr;    // SAS_BUILD_PREFIX: first rank per p-char key, entry j for key
+    uint32_t prefix_chars = 0;    // prefix_key_lo + j; prefix_w bytes per entry (4: u32; 5: packed
+    uint32_t prefix_w = 4;        // 40-bit, for a 40-bit SA; 16 G: G inline slots)
+    uint64_t prefix_key_lo = 0;   // whole index: 0 and 4^p + 1 entries; a part (a rank range of the
+    uint64_t prefix_entries = 0;  // SA): its first key .. its last key + 2 (pt_slot, sas_search.hip)
     bool prefix_hi40 = false;     // inline slots of a text >= 2^32 chars: bits 32..39 of each slot's SA
-                                  // value in slot 1's rank word (only slot 0's rank is read)
+                                  // value in slot 1's rank word (only slot 0's rank is read); with two
+                                  // slots also bits 32..39 of slot 0's rank (a part of >= 2^32 suffixes)
     uint4* llcp = nullptr;        // SAS_BUILD_LLCP: {SA[m], Llcp, Rlcp, 2 x 16 chars} per rank m (sas_build.hip)
     uint32_t* stree = nullptr;   // all nodes, 16 u32 each
     uint64_t stree_nodes = 0;

@@ -948,6 +948,8 @@ __device__ __forceinline__ void pt_fill_range(uint8_t* t, uint64_t lo, uint64_t 
 #pragma unroll
             for (int j = 0; j < G; j++)
                 if (r + j < sa_n) hb |= (leaves[r + j].w & 0xFFu) << (8 * j);
+            // two slots: bits 32..39 of slot 0's rank too (a part of >= 2^32 suffixes)
+            if (G == 2) hb |= (uint32_t)((r < sa_n ? r : sa_n) >> 32 & 0xFFu) << 16;
             ev[G >= 2 ? 1 : 0].z = hb;
         }
         for (uint64_t x = lo; x <= hi; x += step) {
@@ -959,14 +961,18 @@ __device__ __forceinline__ void pt_fill_range(uint8_t* t, uint64_t lo, uint64_t 
     }
 }
 
+// Keys base .. base + entries - 1 (local entries 0 .. entries - 1): the whole key space (base 0,
+// 4^p + 1 entries), or a part's key interval (its first key .. its last key + 2, so the two
+// entries past its last key hold rank sa_n)
 template <bool KO, int TW>
-__global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint32_t p, uint8_t* __restrict__ table,
-                          uint64_t* __restrict__ big, unsigned long long* __restrict__ nbig, uint64_t big_cap) {
+__global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint32_t p, uint64_t base,
+                          uint64_t entries, uint8_t* __restrict__ table, uint64_t* __restrict__ big,
+                          unsigned long long* __restrict__ nbig, uint64_t big_cap) {
     const uint32_t sh = 64 - 2 * p;
-    const uint64_t top = 1ull << (2 * p);
+    const uint64_t top = entries - 1;
     GRID_STRIDE(r, sa_n + 1) {
-        const uint64_t kr = r < sa_n ? pt_key64<KO>(leaves, r) >> sh : top;
-        const uint64_t lo = r > 0 ? (pt_key64<KO>(leaves, r - 1) >> sh) + 1 : 0;
+        const uint64_t kr = r < sa_n ? (pt_key64<KO>(leaves, r) >> sh) - base : top;
+        const uint64_t lo = r > 0 ? (pt_key64<KO>(leaves, r - 1) >> sh) - base + 1 : 0;
         if (lo > kr) continue;  // same key as rank r - 1
         if (kr - lo < PT_SMALL) {
             pt_fill_range<TW>(table, lo, kr, 1, r, leaves, sa_n);
@@ -983,8 +989,10 @@ __global__ void k_pt_fill(const uint4* __restrict__ leaves, uint64_t sa_n, uint3
 
 template <int TW>
 __global__ void k_pt_big(const uint64_t* __restrict__ big, const unsigned long long* __restrict__ nbig,
-                         uint8_t* __restrict__ table, const uint4* __restrict__ leaves, uint64_t sa_n) {
-    for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x)
+                         uint64_t big_cap, uint8_t* __restrict__ table, const uint4* __restrict__ leaves,
+                         uint64_t sa_n) {
+    const uint64_t nb = *nbig < big_cap ? *nbig : big_cap;  // the host fails the build past the cap
+    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x)
         pt_fill_range<TW>(table, big[3 * b] + threadIdx.x, big[3 * b + 1], blockDim.x, big[3 * b + 2], leaves, sa_n);
 }
 
@@ -993,20 +1001,41 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     if (!x->quad_leaves) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX needs SAS_BUILD_QUAD (keys and SA values of the leaves)");
     // inline entries hold a u32 rank and the low 32 bits of each slot's SA value: fused
     // leaves and ranks below 2^32; the one-suffix table also needs positions below 2^32, the
-    // two/four-suffix ones carry bits 32..39 in slot 1 (a part index of a 2^33-char text)
-    if (inl && (x->quad_compact || sa_n >= 0xFFFFFFFFull || (inl == 1 && x->n > 0xFFFFFFFFull)))
+    // two/four-suffix ones carry bits 32..39 in slot 1 (a part index of a 2^33-char text), and
+    // the two-suffix one there also bits 32..39 of the rank (a part of >= 2^32 suffixes)
+    const bool hi40 = inl >= 2 && x->n > 0xFFFFFFFFull;
+    if (inl && (x->quad_compact || (sa_n >= 0xFFFFFFFFull && !(inl == 2 && hi40)) ||
+                (inl == 1 && x->n > 0xFFFFFFFFull)))
         SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX_INLINE / _INLINE2 / _INLINE4 need fused quad leaves and fewer than "
-                          "2^32 - 1 SA entries (SAS_BUILD_PREFIX_INLINE also n < 2^32)");
+                          "2^32 - 1 SA entries (SAS_BUILD_PREFIX_INLINE2 on a text of n >= 2^32: any count; "
+                          "SAS_BUILD_PREFIX_INLINE also n < 2^32)");
     // u32 entries for a u32 SA, packed 40-bit ones beside a 40-bit SA, 16-B inline ones
     const uint32_t tw = inl ? 16 * inl : (x->sa_w == 5 ? 5 : 4);
-    if (tw != 5 && sa_n >= 0xFFFFFFFFull) SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
+    if (tw != 5 && !(tw == 32 && hi40) && sa_n >= 0xFFFFFFFFull)
+        SAS_FAIL(ENOTSUP, "SAS_BUILD_PREFIX: u32 ranks need fewer than 2^32 - 1 SA entries");
     if (p == 0) {
         uint32_t l4 = 0;  // ceil(log4(sa_n))
         while (l4 < 32 && (1ull << (2 * l4)) < sa_n) l4++;
         p = l4 + 1 < 16 ? l4 + 1 : 16;
     }
     if (p > 17) SAS_FAIL(EINVAL, "SAS_BUILD_PREFIX_P: p must be 1..17");
-    const uint64_t entries = (1ull << (2 * p)) + 1;
+    // the keys the table covers: every p-char key for a whole index; for a part (a contiguous
+    // SA rank range) the interval from its first suffix's key to its last one's,
+    // plus two entries of rank sa_n.  Keys are monotone over the ranks (zero padding), so a
+    // part's suffixes are exactly that interval's, and a query outside it clamps to a
+    // neighbouring entry whose suffixes are all > q (below) or to rank sa_n (above)
+    // (pt_slot, sas_search.hip).  At 8 parts of a random text: 1/8 of the 4^p keys each
+    uint64_t base = 0, entries = (1ull << (2 * p)) + 1;
+    if (sa_n < x->n) {
+        const uint32_t sh = 64 - 2 * p;
+        uint64_t k0 = 0, k1 = 0;
+        const uint8_t* lv = reinterpret_cast<const uint8_t*>(x->quad_leaves);
+        const uint64_t eb = x->quad_compact ? 8 : 16;
+        HIP_TRY(hipMemcpy(&k0, lv, 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&k1, lv + (sa_n - 1) * eb, 8, hipMemcpyDeviceToHost));
+        base = k0 >> sh;
+        entries = (k1 >> sh) - base + 3;
+    }
     const uint64_t cap = entries / (PT_SMALL + 1) + 2;
     DevBuf t, big, nbig;
     TRY(t.alloc_flags(entries * tw + 8, "prefix table", SAS_PREFIX_ALLOC_FLAGS));
@@ -1018,24 +1047,24 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     uint64_t* bl = big.as<uint64_t>();
     unsigned long long* nb_d = nbig.as<unsigned long long>();
     if (tw == 64)
-        hipLaunchKernelGGL((k_pt_fill<false, 64>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+        hipLaunchKernelGGL((k_pt_fill<false, 64>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
     else if (tw == 32)
-        hipLaunchKernelGGL((k_pt_fill<false, 32>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+        hipLaunchKernelGGL((k_pt_fill<false, 32>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
     else if (tw == 16)
-        hipLaunchKernelGGL((k_pt_fill<false, 16>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+        hipLaunchKernelGGL((k_pt_fill<false, 16>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
     else if (x->quad_compact && tw == 5)
-        hipLaunchKernelGGL((k_pt_fill<true, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+        hipLaunchKernelGGL((k_pt_fill<true, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
     else if (x->quad_compact)
-        hipLaunchKernelGGL((k_pt_fill<true, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+        hipLaunchKernelGGL((k_pt_fill<true, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
     else if (tw == 5)
-        hipLaunchKernelGGL((k_pt_fill<false, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
+        hipLaunchKernelGGL((k_pt_fill<false, 5>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
     else
-        hipLaunchKernelGGL((k_pt_fill<false, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, tb, bl, nb_d, cap);
-    if (tw == 64) hipLaunchKernelGGL(k_pt_big<64>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
-    else if (tw == 32) hipLaunchKernelGGL(k_pt_big<32>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
-    else if (tw == 16) hipLaunchKernelGGL(k_pt_big<16>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
-    else if (tw == 5) hipLaunchKernelGGL(k_pt_big<5>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
-    else hipLaunchKernelGGL(k_pt_big<4>, dim3(4096), dim3(256), 0, 0, bl, nb_d, tb, x->quad_leaves, sa_n);
+        hipLaunchKernelGGL((k_pt_fill<false, 4>), g, b, 0, 0, x->quad_leaves, sa_n, p, base, entries, tb, bl, nb_d, cap);
+    if (tw == 64) hipLaunchKernelGGL(k_pt_big<64>, dim3(4096), dim3(256), 0, 0, bl, nb_d, cap, tb, x->quad_leaves, sa_n);
+    else if (tw == 32) hipLaunchKernelGGL(k_pt_big<32>, dim3(4096), dim3(256), 0, 0, bl, nb_d, cap, tb, x->quad_leaves, sa_n);
+    else if (tw == 16) hipLaunchKernelGGL(k_pt_big<16>, dim3(4096), dim3(256), 0, 0, bl, nb_d, cap, tb, x->quad_leaves, sa_n);
+    else if (tw == 5) hipLaunchKernelGGL(k_pt_big<5>, dim3(4096), dim3(256), 0, 0, bl, nb_d, cap, tb, x->quad_leaves, sa_n);
+    else hipLaunchKernelGGL(k_pt_big<4>, dim3(4096), dim3(256), 0, 0, bl, nb_d, cap, tb, x->quad_leaves, sa_n);
     HIP_TRY(hipGetLastError());
     uint64_t nb = 0;
     HIP_TRY(hipMemcpy(&nb, nbig.p, 8, hipMemcpyDeviceToHost));
@@ -1044,7 +1073,9 @@ static int build_prefix(sas_index* x, uint32_t p, uint32_t inl) {
     t.release();
     x->prefix_chars = p;
     x->prefix_w = tw;
-    x->prefix_hi40 = inl >= 2 && x->n > 0xFFFFFFFFull;
+    x->prefix_key_lo = base;
+    x->prefix_entries = entries;
+    x->prefix_hi40 = hi40;
     return 0;
 }
 
@@ -1095,8 +1126,9 @@ __global__ void k_tt_fill(const uint64_t* __restrict__ tw, S ent, uint64_t sa_n,
 }
 
 __global__ void k_tt_big(const uint64_t* __restrict__ big, const unsigned long long* __restrict__ nbig,
-                         uint64_t* __restrict__ table) {
-    for (uint64_t b = blockIdx.x; b < *nbig; b += gridDim.x)
+                         uint64_t big_cap, uint64_t* __restrict__ table) {
+    const uint64_t nb = *nbig < big_cap ? *nbig : big_cap;  // the host fails the build past the cap
+    for (uint64_t b = blockIdx.x; b < nb; b += gridDim.x)
         for (uint64_t x = big[3 * b] + threadIdx.x; x <= big[3 * b + 1]; x += blockDim.x) table[x] = big[3 * b + 2];
 }
 
@@ -1145,7 +1177,7 @@ static int build_tagged(sas_index* x, uint32_t p) {
     HIP_TRY(hipMemset(nbig.p, 0, 8));
     hipLaunchKernelGGL(k_tt_fill<SaView<8>>, dim3(grid_for(sa_n + 1)), b, 0, 0, x->text_w, SaView<8>{x->sa}, sa_n, p,
                        t.as<uint64_t>(), big.as<uint64_t>(), nbig.as<unsigned long long>(), cap);
-    hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(),
+    hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(), cap,
                        t.as<uint64_t>());
     hipLaunchKernelGGL(k_tt_count, dim3(grid_for(keys)), b, 0, 0, t.as<uint64_t>(), keys);
     HIP_TRY(hipGetLastError());
@@ -1360,8 +1392,8 @@ template <int W>
 __global__ void k_tl_ovf_big(const uint64_t* __restrict__ tw, SaView<W> sa, uint64_t sa_n, uint32_t p, uint32_t sb,
                              const uint64_t* __restrict__ t, const uint64_t* __restrict__ lines,
                              uint64_t* __restrict__ ovf, const uint64_t* __restrict__ big,
-                             const unsigned long long* __restrict__ nbig) {
-    const uint64_t nb = *nbig;
+                             const unsigned long long* __restrict__ nbig, uint64_t big_cap) {
+    const uint64_t nb = *nbig < big_cap ? *nbig : big_cap;  // the host fails the build past the cap
     for (uint64_t k = blockIdx.x; k < nb; k += gridDim.x) {
         const uint64_t b = big[k];
         const uint64_t first = t[b], c = t[b + 1] - first;
@@ -1389,7 +1421,7 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
     HIP_TRY(hipMemset(nbig.p, 0, 8));
     hipLaunchKernelGGL(k_tt_fill<SaView<W>>, dim3(grid_for(sa_n + 1)), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p,
                        t.as<uint64_t>(), big.as<uint64_t>(), nbig.as<unsigned long long>(), cap);
-    hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(),
+    hipLaunchKernelGGL(k_tt_big, dim3(4096), b, 0, 0, big.as<uint64_t>(), nbig.as<unsigned long long>(), cap,
                        t.as<uint64_t>());
     HIP_TRY(hipGetLastError());
     uint64_t nb = 0;
@@ -1440,7 +1472,7 @@ static int build_tag_lines_w(sas_index* x, uint32_t p) {
                            nbl.as<unsigned long long>(), bcap);
         hipLaunchKernelGGL(k_tl_ovf_big<W>, dim3(4096), b, 0, 0, x->text_w, SaView<W>{x->sa}, sa_n, p, sb,
                            t.as<uint64_t>(), lines.as<uint64_t>(), ovf.as<uint64_t>(), bl.as<uint64_t>(),
-                           nbl.as<unsigned long long>());
+                           nbl.as<unsigned long long>(), bcap);
         HIP_TRY(hipGetLastError());
         uint64_t nb = 0;
         HIP_TRY(hipMemcpy(&nb, nbl.p, 8, hipMemcpyDeviceToHost));
@@ -1636,7 +1668,8 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     } else {
     // global suffix array (caller's or built here), then this index's rank range
     DevBuf sa;
-    const uint64_t sa_bytes_full = n * W + (W == 5 ? SAS_SA40_PAD : 0);
+    // 40-bit: the pair loads' pad; u32: PLAIN's SA run loads the 16-B chunks covering its ranks
+    const uint64_t sa_bytes_full = n * W + (W == 5 ? SAS_SA40_PAD : 16);
     TRY(sa.alloc(sa_bytes_full, "suffix array"));
     if (sa_or_null) {
         TRY(load_sa(sa_or_null, n, sa_width, dev, sa.as<uint8_t>(), W));
@@ -1666,7 +1699,7 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
         x->sa = static_cast<uint8_t*>(sa.release());
     } else {
         DevBuf part;
-        const uint64_t pb = x->sa_n * W + (W == 5 ? SAS_SA40_PAD : 0);
+        const uint64_t pb = x->sa_n * W + (W == 5 ? SAS_SA40_PAD : 16);
         TRY(part.alloc(pb, "suffix array shard"));
         HIP_TRY(hipMemset(part.p, 0, pb));
         HIP_TRY(hipMemcpy(part.p, sa.as<uint8_t>() + rank_lo * W, x->sa_n * W, hipMemcpyDeviceToDevice));
@@ -1753,8 +1786,10 @@ static int build_impl(const uint8_t* text, uint64_t n, const void* sa_or_null, i
     st.sa_width = x->sa_w;
     st.lcp_bytes = x->lcp ? sa_n * 4 : 0;
     st.llcp_bytes = x->llcp ? sa_n * 16 : 0;
-    st.prefix_bytes = x->prefix ? ((1ull << (2 * x->prefix_chars)) + 1) * x->prefix_w : 0;
+    st.prefix_bytes = x->prefix ? x->prefix_entries * x->prefix_w : 0;
     st.prefix_chars = x->prefix_chars;
+    st.prefix_key_lo = x->prefix ? x->prefix_key_lo : 0;
+    st.prefix_entries = x->prefix ? x->prefix_entries : 0;
     st.stree_bytes = x->stree_nodes * 64;
     st.stree_layers = x->stree_height;
     st.stree_lds_layers = x->stree_lds_layers;

@@ -63,23 +63,29 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* s_w) {
     return t;
 }
 
-// Block b owns positions [b*CHUNK, (b+1)*CHUNK): count those whose bin is in [lo, hi).
+// Chunk k owns positions [k*CHUNK, (k+1)*CHUNK): count those whose bin is in [lo, hi).  The
+// workgroups stride over the chunks (a dispatch holds < 2^32 work-items: n = 2^36 is 2^22
+// chunks of 1024 threads)
+#define COLLECT_GRID (1u << 16)
 __global__ __launch_bounds__(COLLECT_BLOCK) void k_bucket_count(const uint64_t* __restrict__ tw, uint64_t n,
                                                                 uint32_t lo, uint32_t hi,
                                                                 uint64_t* __restrict__ block_cnt) {
     __shared__ uint32_t s_w[COLLECT_BLOCK / 64];
-    uint64_t base = (uint64_t)blockIdx.x * COLLECT_CHUNK;
-    uint32_t c = 0;
+    const uint64_t nblk = (n + COLLECT_CHUNK - 1) / COLLECT_CHUNK;
+    for (uint64_t k = blockIdx.x; k < nblk; k += gridDim.x) {
+        const uint64_t base = k * COLLECT_CHUNK;
+        uint32_t c = 0;
 #pragma unroll 4
-    for (int it = 0; it < COLLECT_ITEMS; it++) {
-        uint64_t p = base + (uint64_t)it * COLLECT_BLOCK + threadIdx.x;
-        if (p < n) {
-            uint32_t b = bin_of(text_chars32(tw, p));
-            c += (b >= lo && b < hi);
+        for (int it = 0; it < COLLECT_ITEMS; it++) {
+            uint64_t p = base + (uint64_t)it * COLLECT_BLOCK + threadIdx.x;
+            if (p < n) {
+                uint32_t b = bin_of(text_chars32(tw, p));
+                c += (b >= lo && b < hi);
+            }
         }
+        uint32_t t = block_sum(c, s_w);
+        if (threadIdx.x == 0) block_cnt[k] = t;
     }
-    uint32_t t = block_sum(c, s_w);
-    if (threadIdx.x == 0) block_cnt[blockIdx.x] = t;
 }
 
 // Same walk; matches are stored at block_off[b] + (rank among the block's
@@ -92,8 +98,10 @@ __global__ __launch_bounds__(COLLECT_BLOCK) void k_bucket_collect(const uint64_t
     __shared__ uint32_t s_w[COLLECT_BLOCK / 64];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-    uint64_t run = block_off[blockIdx.x];
-    uint64_t base = (uint64_t)blockIdx.x * COLLECT_CHUNK;
+    const uint64_t nblk = (n + COLLECT_CHUNK - 1) / COLLECT_CHUNK;
+    for (uint64_t k = blockIdx.x; k < nblk; k += gridDim.x) {
+    uint64_t run = block_off[k];
+    const uint64_t base = k * COLLECT_CHUNK;
     for (int it = 0; it < COLLECT_ITEMS; it++) {
         uint64_t p = base + (uint64_t)it * COLLECT_BLOCK + threadIdx.x;
         uint64_t key = 0;
@@ -120,6 +128,7 @@ __global__ __launch_bounds__(COLLECT_BLOCK) void k_bucket_collect(const uint64_t
         run += total;
         __syncthreads();
     }
+    }  // chunks
 }
 
 __global__ void k_b_heads(const uint64_t* __restrict__ keys, uint64_t c, uint64_t off,
@@ -272,13 +281,14 @@ static int sort_bins_into(const uint64_t* tw, uint64_t n, const std::vector<uint
         uint64_t c = 0;
         for (uint32_t i = blo; i < bhi; i++) c += h[i];
         if (c == 0) continue;
-        hipLaunchKernelGGL(k_bucket_count, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
+        const dim3 cg((unsigned)(nblk < COLLECT_GRID ? nblk : COLLECT_GRID));
+        hipLaunchKernelGGL(k_bucket_count, cg, dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
                            bcnt.as<uint64_t>());
         TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {
             return rocprim::exclusive_scan(t, sz, bcnt.as<uint64_t>(), bcnt.as<uint64_t>(), (uint64_t)0,
                                            (size_t)nblk, rocprim::plus<uint64_t>(), st);
         }));
-        hipLaunchKernelGGL(k_bucket_collect, dim3((unsigned)nblk), dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
+        hipLaunchKernelGGL(k_bucket_collect, cg, dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
                            bcnt.as<uint64_t>(), ka.as<uint64_t>(), va.as<uint64_t>());
         rocprim::double_buffer<uint64_t> kdb(ka.as<uint64_t>(), kb.as<uint64_t>());
         rocprim::double_buffer<uint64_t> vdb(va.as<uint64_t>(), vb.as<uint64_t>());

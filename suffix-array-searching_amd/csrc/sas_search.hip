@@ -39,6 +39,17 @@
 #define SEARCH_BLOCK 1024
 #define TRY_RC(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
 #define BLOCKS_PER_CU 2
+// the binary searches (k_sa_binary: PLAIN, LCP, LLCP): workgroup size and workgroups per CU.
+// The launch bound follows them (waves per SIMD = block x blocks / 256), which caps the VGPRs:
+// 1024 x 2 -> 8 waves, 64 VGPRs; 768 x 2 -> 6 waves, 80 VGPRs (the LDS pivot groups, 72.5 KiB
+// a workgroup, allow two workgroups a CU either way)
+#ifndef SAS_BIN_BLOCK
+#define SAS_BIN_BLOCK 768
+#endif
+#ifndef SAS_BIN_BPC
+#define SAS_BIN_BPC 2
+#endif
+#define SAS_BIN_WAVES (SAS_BIN_BLOCK * SAS_BIN_BPC / 256)
 
 struct SearchArgs {
     const uint64_t* tw;
@@ -52,6 +63,8 @@ struct SearchArgs {
     uint32_t prefix_chars;
     uint32_t prefix_w;       // bytes per table entry (4 or 5)
     uint32_t prefix_hi40;    // inline slots: SA bits 32..39 in slot 1's rank word
+    uint64_t pt_base;        // the table's first key (0, or a part's first suffix's key)
+    uint64_t pt_jmax;        // its last entry a lookup may start at (entries - 2)
     const uint8_t* rel;      // the prefix-relative pivot blocks (common.hpp RelLayout)
     RelLayout rel_lay;
     uint32_t iters;
@@ -142,14 +155,37 @@ __device__ __forceinline__ bool llcp_tie_less(const uint64_t* __restrict__ tw, u
     return lenS < (uint64_t)q.m;
 }
 
+// The table entry of p-char key K: K - pt_base, clamped to the table.  A whole index's table
+// holds every key (pt_base 0, pt_jmax 4^p - 1: the identity).  A part's holds its first
+// suffix's key .. its last one's and two entries of rank sa_n: a key below the interval
+// clamps to entry 0, whose suffixes (like every suffix of the part) are > q, so the lower
+// bound is rank 0 from either; a key above it to entry jmax, the empty range at sa_n
+__device__ __forceinline__ uint64_t pt_slot(const SearchArgs& a, uint64_t K) {
+    K = K > a.pt_base ? K - a.pt_base : 0;
+    return K < a.pt_jmax ? K : a.pt_jmax;
+}
+// Rank of inline entry j (16 G bytes): slot 0's rank word, and for two slots beside a text of
+// >= 2^32 chars bits 32..39 from slot 1's (a part of >= 2^32 suffixes)
+template <int G, bool HI40>
+__device__ __forceinline__ uint64_t pt_rank(const uint4* t, uint64_t j) {
+    const uint64_t r = t[G * j].z;
+    if (!(HI40 && G == 2)) return r;
+    return r | ((uint64_t)((t[G * j + 1].z >> 16) & 0xFFu) << 32);
+}
 // prefix_range (sas/sa_search.rs:86-95): the SA ranks [lo, hi) whose p-char key is K,
 // from the prefix table in any of its entry formats
 __device__ __forceinline__ void prefix_range(const SearchArgs& a, uint64_t K, uint64_t* lo, uint64_t* hi) {
+    K = pt_slot(a, K);
     if (a.prefix_w >= 16) {  // inline entries: rank in the first slot's .z
         const uint4* t = reinterpret_cast<const uint4*>(a.prefix);
-        const uint64_t st = a.prefix_w / 16;
-        *lo = t[st * K].z;
-        *hi = t[st * (K + 1)].z;
+        if (a.prefix_w == 32 && a.prefix_hi40) {
+            *lo = pt_rank<2, true>(t, K);
+            *hi = pt_rank<2, true>(t, K + 1);
+        } else {
+            const uint64_t st = a.prefix_w / 16;
+            *lo = t[st * K].z;
+            *hi = t[st * (K + 1)].z;
+        }
     } else if (a.prefix_w == 5) {
         const SaView<5> v{a.prefix};
         *lo = v[K];
@@ -202,7 +238,7 @@ __device__ __forceinline__ uint32_t rel_slot(const uint4& b0, const uint4& b1, u
     return ((j & 1u) ? (wv >> 16) : wv) & 0xFFFFu;
 }
 template <int QW, int MODE, bool TOP, int W, bool RANGE = false>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_binary(SearchArgs a) {
+__global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_binary(SearchArgs a) {
     // the prefix-relative pivot blocks, the first 15 levels' from LDS (common.hpp RelLayout)
     __shared__ uint4 s_rel[TOP ? SAS_REL_LDS_BYTES / 16 : 1];
     const SaView<W> sa{a.sa};
@@ -1370,7 +1406,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
             q.load(qb, m, &bad);
         }
         const uint64_t K64 = q.w[0];
-        const uint64_t K = K64 >> sh;
+        const uint64_t K = pt_slot(a, K64 >> sh);
         uint64_t lo, hi = 0, pos = QUAD_NO_SA;
         const uint32_t* pt = reinterpret_cast<const uint32_t*>(a.prefix);
         const uint4* pt16 = reinterpret_cast<const uint4*>(a.prefix);
@@ -1510,11 +1546,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
             q.load(qb, m, &bad);  // every lane of the group: the same addresses, one request
         }
         const uint64_t K64 = q.w[0];
-        const uint64_t K = K64 >> sh;
+        const uint64_t K = pt_slot(a, K64 >> sh);
         const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + G * K + sub) : pt[G * K + sub];
-        const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
-        const uint64_t rank = r0 + sub;
         const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
+        // two slots beside a >= 2^32-char text: bits 32..39 of the rank in slot 1's rank word
+        const uint64_t r0 = (uint64_t)(uint32_t)__shfl((int)e.z, lane0, 64) |
+                            (HI40 && G == 2 ? (uint64_t)((hb >> 16) & 0xFFu) << 32 : 0ull);
+        const uint64_t rank = r0 + sub;
         const uint64_t pe = HI40 ? ((uint64_t)e.w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32)) : (uint64_t)e.w;
         // rank sa_n stands for "past every suffix": it is the answer if reached
         const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), pe, K64, a, q);
@@ -1526,7 +1564,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
             ans = r0 + j;
             pos = ans >= sa_n ? a.next_pos : (HI40 ? ((uint64_t)pw | ((uint64_t)((hb >> (8 * j)) & 0xFFu) << 32)) : pw);
         } else {
-            uint64_t lo = r0 + G, hi = pt[G * (K + 1)].z, pr = QUAD_NO_SA;
+            uint64_t lo = r0 + G, hi = pt_rank<G, HI40>(pt, K + 1), pr = QUAD_NO_SA;
             while (lo < hi) {
                 const uint64_t mid = (lo + hi) >> 1;
                 const uint4 f = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
@@ -1548,7 +1586,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
             else a.out_pos[i] = pos;
             if (a.out_probes) {  // the reference's cnt over [table[K], table[K+1])
                 uint32_t probes = 1;
-                for (uint64_t l2 = r0, h2 = pt[G * (K + 1)].z; l2 < h2; probes++) {
+                for (uint64_t l2 = r0, h2 = pt_rank<G, HI40>(pt, K + 1); l2 < h2; probes++) {
                     const uint64_t mid = (l2 + h2) >> 1;
                     if (mid < ans) l2 = mid + 1;
                     else h2 = mid;
@@ -1640,12 +1678,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2_range(SearchArgs
         q.load(qb, m, &bad);  // every lane of the group: the same addresses, one request
         const uint64_t K64 = q.w[0];
         const uint64_t Q3 = m >= 32 ? K64 : (K64 | (~0ull >> (2 * m)));
-        const uint64_t K = K64 >> sh;
+        const uint64_t K = pt_slot(a, K64 >> sh);
         const uint4 e = pt[G * K + sub];
-        const uint64_t r0 = (uint32_t)__shfl((int)e.z, lane0, 64);
+        const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
+        const uint64_t r0 = (uint64_t)(uint32_t)__shfl((int)e.z, lane0, 64) |
+                            (HI40 && G == 2 ? (uint64_t)((hb >> 16) & 0xFFu) << 32 : 0ull);
         const uint64_t rank = r0 + sub;
         const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
-        const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
         const uint64_t pe = HI40 ? ((uint64_t)e.w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32)) : (uint64_t)e.w;
         // rank sa_n stands for "past every suffix": both bounds are reached there
         const bool past = rank >= sa_n;
@@ -1660,14 +1699,14 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2_range(SearchArgs
             lo = l1 = r0 + (uint32_t)__builtin_ctz(gge);
         } else {
             lo = r0 + G;
-            l1 = pt[G * (K + 1)].z;
+            l1 = pt_rank<G, HI40>(pt, K + 1);
         }
         if (whole) {
             if (ggt) {
                 hi = h1 = r0 + (uint32_t)__builtin_ctz(ggt);
             } else {
                 hi = r0 + G;
-                h1 = gge ? pt[G * (K + 1)].z : l1;
+                h1 = gge ? pt_rank<G, HI40>(pt, K + 1) : l1;
             }
         } else {
             prefix_range(a, Q3 >> sh, &hi, &h1);
@@ -2580,11 +2619,14 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
     const uint64_t lanes = a.nq * (coop ? QUAD_G : g);
-    uint64_t blocks = (lanes + SEARCH_BLOCK - 1) / SEARCH_BLOCK;
-    uint64_t cap = (uint64_t)x->num_cus * BLOCKS_PER_CU;
+    // k_sa_binary (PLAIN / LCP / LLCP, any SA width) has its own workgroup shape
+    const bool bin = algo == SAS_ALGO_PLAIN || algo == SAS_ALGO_LCP || algo == SAS_ALGO_LLCP;
+    const uint64_t bs = bin ? SAS_BIN_BLOCK : SEARCH_BLOCK;
+    uint64_t blocks = (lanes + bs - 1) / bs;
+    uint64_t cap = (uint64_t)x->num_cus * (bin ? SAS_BIN_BPC : BLOCKS_PER_CU);
     if (blocks > cap) blocks = cap;
     if (blocks == 0) return 0;
-    dim3 grid((unsigned)blocks), block(SEARCH_BLOCK);
+    dim3 grid((unsigned)blocks), block((unsigned)bs);
     bool top = !(flags & SAS_NO_LDS_TOP);
     const bool range = (flags & SAS_PREFIX_RANGE) != 0;
     if (algo == SAS_ALGO_TAGGED) {
@@ -2654,6 +2696,8 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
     a.prefix_chars = x->prefix_chars;
     a.prefix_w = x->prefix_w;
     a.prefix_hi40 = x->prefix_hi40;
+    a.pt_base = x->prefix_key_lo;
+    a.pt_jmax = x->prefix_entries >= 2 ? x->prefix_entries - 2 : 0;
     a.rel = x->rel;
     a.rel_lay = x->rel_lay;
     a.iters = x->iters;

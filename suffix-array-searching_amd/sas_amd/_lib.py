@@ -83,6 +83,7 @@ class SasStats(C.Structure):
         ("tag_line_slots", C.c_uint32), ("tag_line_tag_bits", C.c_uint32), ("tag_overflow_entries", C.c_uint64),
         ("text2_bytes", C.c_uint64), ("top2_bytes", C.c_uint64),
         ("rel_levels", C.c_uint32), ("rel_pad", C.c_uint32), ("rel_bytes", C.c_uint64),
+        ("prefix_key_lo", C.c_uint64), ("prefix_entries", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -288,6 +288,111 @@ def test_sharded_parts_loopback(sas, W):
         assert raised, r
 
 
+def _key(t, pos, p):
+    """p-char zero-padded key of suffix pos as an integer (the prefix table's key)."""
+    k = 0
+    for j in range(p):
+        k = 4 * k + (int(t[pos + j]) if pos + j < len(t) else 0)
+    return k
+
+
+@pytest.mark.parametrize("inl,p", [(0, 10), (1, 9), (2, 10), (2, 12), (4, 10)])
+def test_part_prefix_table_key_interval(sas, inl, p):
+    """A part's prefix table covers only its own key interval (its first suffix's p-char key
+    .. its last one's, + two entries of rank sa_n): stats name the interval, the table is
+    that many entries, and PREFIX on the part equals PLAIN on the part for queries inside,
+    below and above the interval (clamped lookups), at m below, at and above p; occurrence
+    ranges equal the whole index's clipped to the part's ranks, inline slots or not."""
+    import torch
+    from sas_amd import _lib
+    n, W = 2_000_003, 4
+    t = sas.random_string(n, seed=91)
+    dt = torch.from_numpy(t).cuda()
+    whole = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, prefix=p, prefix_inline=2)
+    rng = np.random.default_rng(inl * 31 + p)
+    for g in range(W):
+        part = sas.SaNaive.build_part(dt, g, W, lcp=False, stree=False, sector=False, llcp=False, prefix=p,
+                                      prefix_inline=inl)
+        st = part.stats()
+        sa = part.suffix_array()
+        k0, k1 = _key(t, int(sa[0]), p), _key(t, int(sa[-1]), p)
+        assert st["prefix_key_lo"] == k0 and st["prefix_entries"] == k1 - k0 + 3, (g, st)
+        w = 16 * inl if inl else 5
+        assert st["prefix_bytes"] == st["prefix_entries"] * w
+        assert st["prefix_entries"] < (4 ** p) // 2, g  # an interval, not the key space
+        for m in (p - 3, p, 32):
+            offs = rng.integers(0, n - m, 6000)
+            qs = np.stack([t[o:o + m] for o in offs])
+            qs[:1000] = rng.integers(0, 4, (1000, m))  # misses, most outside this part's keys
+            qs[1000] = 0
+            qs[1001] = 3
+            # just below / at / above the part's first and last keys
+            for j, pos in enumerate((int(sa[0]), int(sa[-1]))):
+                base = np.array([t[pos + c] if pos + c < n else 0 for c in range(m)], np.uint8)
+                qs[1002 + 4 * j] = base
+                lo = base.copy()
+                lo[min(p, m) - 1] = max(int(lo[min(p, m) - 1]) - 1, 0)
+                qs[1003 + 4 * j] = lo
+                hi = base.copy()
+                hi[min(p, m) - 1] = min(int(hi[min(p, m) - 1]) + 1, 3)
+                qs[1004 + 4 * j] = hi
+                qs[1005 + 4 * j] = np.where(np.arange(m) < min(p, m), base, 3)
+            qb = qs.reshape(-1).copy()
+            plain = part.search_fixed(qb, m, algo="plain")
+            assert np.array_equal(part.search_fixed(qb, m, algo="prefix"), plain), (g, m)
+            if inl == 2 and m <= 32:
+                words = sas.SaNaive.pack_queries(torch.from_numpy(qb).cuda(), m)
+                got = part.search_packed(words, m)
+                torch.cuda.synchronize()
+                assert np.array_equal(got.cpu().numpy().astype(np.uint64), plain), (g, m)
+            dq = torch.from_numpy(qb).cuda()
+            lo, hi = part.search_range_fixed(dq, m)
+            wl, wh = whole.search_range_fixed(dq, m)
+            r0, r1 = part.rank_lo, part.rank_lo + part.sa_n
+            torch.cuda.synchronize()
+            assert np.array_equal(lo.cpu().numpy(), np.clip(wl.cpu().numpy(), r0, r1)), (g, m)
+            assert np.array_equal(hi.cpu().numpy(), np.clip(wh.cpu().numpy(), r0, r1)), (g, m)
+            if inl >= 2:
+                lo2, hi2 = part.search_range_fixed(dq, m, flags=_lib.SAS_RANGE_NO_INLINE)
+                torch.cuda.synchronize()
+                assert torch.equal(lo, lo2) and torch.equal(hi, hi2), (g, m)
+        part.free()
+
+
+@pytest.mark.timeout(600)
+def test_two_slot_table_ranks_above_2e32(sas):
+    """A one-part index (sas_build_part_gen, parts = 1: the whole table) of a 1.125 x 2^32-char
+    text holds more than 2^32 suffixes: the two-suffix inline table carries bits 32..39 of
+    each entry's rank in slot 1's rank word, so PREFIX (bytes and packed words) equals PLAIN
+    and the inline-slot ranges equal the bisection's, with lower bounds past rank 2^32."""
+    import torch
+    from sas_amd import _lib
+    n, m, seed = 9 << 29, 32, 57
+    part = sas.SaNaive.build_part_gen(n, seed=seed, part=0, parts=1, lcp=False, stree=False, sector=False,
+                                      llcp=False, quad=True, prefix=15, prefix_inline=2, top2_levels=15)
+    st = part.stats()
+    assert st["sa_entries"] == n and st["prefix_entries"] == 4 ** 15 + 1 and st["prefix_key_lo"] == 0
+    rng = np.random.default_rng(5)
+    nq = 400_000
+    off = torch.from_numpy(rng.integers(0, n - m, nq).astype(np.int64)).cuda()
+    q = torch.empty(nq * m, dtype=torch.uint8, device="cuda")
+    part.extract(off, torch.full((nq,), m, dtype=torch.int32, device="cuda"),
+                 torch.arange(nq, device="cuda", dtype=torch.int64) * m, q)
+    q[: 20_000 * m] = torch.from_numpy(rng.integers(0, 4, 20_000 * m, dtype=np.uint8)).cuda()  # misses
+    # the last ~1/9 of the ranks lie past 2^32: queries starting with 3s land there
+    q[20_000 * m: 60_000 * m].view(40_000, m)[:, :3] = 3
+    plain = part.search_fixed(q, m, algo="plain")
+    pre = part.search_fixed(q, m, algo="prefix")
+    pk = part.search_packed(sas.SaNaive.pack_queries(q, m), m)
+    lo, hi = part.search_range_fixed(q, m)
+    lo2, hi2 = part.search_range_fixed(q, m, flags=_lib.SAS_RANGE_NO_INLINE)
+    torch.cuda.synchronize()
+    assert torch.equal(plain, pre) and torch.equal(plain, pk)
+    assert torch.equal(lo, lo2) and torch.equal(hi, hi2)
+    assert int((lo >= (1 << 32)).sum().item()) > nq // 20
+    part.free()
+
+
 def test_inline_tables_on_40bit_sa(sas):
     """The one/two/four-suffix inline prefix tables beside a packed 40-bit SA (allowed while
     n < 2^32: ranks and positions fit the entries' 32-bit fields) give the u32 index's
@@ -456,10 +561,11 @@ def test_build_gen_equals_byte_build(sas):
 def test_c4_shape_w8_loopback_past_2e32(sas):
     """configs[4]'s step at W = 8 on one GPU (loopback exchange, one thread per rank) over a
     2^32-char text: each rank's part from sas_build_part_gen (generated packed text, 40-bit
-    SA, fused quad leaves, two-suffix inline table; p = 13 instead of the bench's 16 so that
-    eight parts fit one GPU), PREFIX queries crossing as 8-B words into fixed-capacity
-    buckets (max_nq, check=False + assert_no_overflow), positions equal to the whole index's
-    PLAIN search, and the bench's per-rank lower-bound proof (bench.c4_proof) on every rank."""
+    SA, fused quad leaves, two-suffix inline table at the bench's p = 16, each part's table
+    sized to its own key interval: about 1/8 of the 4^16 keys, so eight parts fit one GPU),
+    PREFIX queries crossing as 8-B words into fixed-capacity buckets (max_nq, check=False +
+    assert_no_overflow), positions equal to the whole index's PLAIN search, and the bench's
+    per-rank lower-bound proof (bench.c4_proof) on every rank."""
     import torch
     import bench
     from sas_amd.shard import ShardedSearch
@@ -479,8 +585,13 @@ def test_c4_shape_w8_loopback_past_2e32(sas):
     whole.free()
     torch.cuda.empty_cache()
     parts = [sas.SaNaive.build_part_gen(n, seed=seed, part=g, parts=W, lcp=False, stree=False, sector=False,
-                                        quad=True, llcp=False, prefix=13, prefix_inline=2) for g in range(W)]
+                                        quad=True, llcp=False, prefix=16, prefix_inline=2, top2_levels=15)
+             for g in range(W)]
     assert sum(p.sa_n for p in parts) == n
+    ents = [p.stats()["prefix_entries"] for p in parts]
+    # contiguous key intervals: every key once, plus the 2 sentinel entries and the shared
+    # boundary keys of adjacent parts
+    assert 0.99 * 4 ** 16 <= sum(ents) <= 4 ** 16 + 2 * W and max(ents) < 1.1 * 4 ** 16 / W, ents
     assert max(p.next_pos for p in parts) == n or parts[-1].next_pos == n
     lb = Loopback(W)
     res, errs = {}, []

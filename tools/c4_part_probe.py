@@ -1,8 +1,9 @@
 """Rehearse one rank of the driver's 8-GPU configs[4] record on one GPU: a text of W x share
-chars (the bench's default share 2^31: n = 2^34 at W = 8), this rank's part built as the
-bench builds it (sas_build_part_gen: the text generated straight into the packed words; the
-two-suffix inline table at p = 16), setup time, index bytes, the device memory left, and the
-local PREFIX lookup of 10^7 packed len-32 queries (the part's share of a step).
+chars, this rank's part built as the bench builds it (sas_build_part_gen: the text generated
+straight into the packed words; the two-suffix inline table at p = 16 over the part's own key
+interval; the LDS pivot levels only), setup time, index bytes, the device memory left, and the
+local PREFIX lookup of 10^7 packed len-32 queries (the part's share of a step).  share_log2
+defaults to the bench's choice for W ranks (bench.c4_share_for).
 usage: c4_part_probe.py [parts] [part] [share_log2]   (GPU box)"""
 import json
 import os
@@ -19,12 +20,13 @@ import sas_amd  # noqa: E402
 
 W = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 g = int(sys.argv[2]) if len(sys.argv) > 2 else W - 1
-share = 1 << (int(sys.argv[3]) if len(sys.argv) > 3 else 31)
-n, nq, m = share * W, 10_000_000, 32
 torch.cuda.init()
+share = (1 << int(sys.argv[3])) if len(sys.argv) > 3 else bench.c4_share_for(W, torch.cuda.mem_get_info()[1])
+n, nq, m = share * W, 10_000_000, 32
 t0 = time.perf_counter()
 idx = sas_amd.SaNaive.build_part_gen(n, seed=bench.SEED + 1, part=g, parts=W, lcp=False, stree=False, sector=False,
-                                     quad=True, llcp=False, prefix=16, prefix_inline=2)
+                                     quad=True, llcp=False, prefix=16, prefix_inline=2,
+                                     top2_levels=bench.TOP_LDS_LEVELS)
 torch.cuda.synchronize()
 t1 = time.perf_counter()
 free, total = torch.cuda.mem_get_info()
@@ -39,6 +41,9 @@ t = bench.launch_times(torch, lambda: idx.search_packed(w, m, out=out), 10, 3, t
 print(json.dumps({"parts": W, "part": g, "n": n, "build_part_gen_s": round(t1 - t0, 2),
                   "sa_entries": st["sa_entries"], "rank_lo": st["rank_lo"], "sa_width": st["sa_width"],
                   "prefix_chars": st["prefix_chars"], "prefix_bytes": st["prefix_bytes"],
+                  "prefix_key_lo": st["prefix_key_lo"], "prefix_entries": st["prefix_entries"],
+                  "prefix_key_fraction": round(st["prefix_entries"] / (4 ** st["prefix_chars"] + 1), 4),
+                  "estimate_bytes": bench.c4_part_bytes(share, W), "share": share,
                   "index_bytes": st["index_bytes"], "free_GiB_after_build": round(free / 2**30, 1),
                   "total_GiB": round(total / 2**30, 1),
                   "local_prefix_packed_ms": round(t["mean_ms"], 4),
