@@ -58,7 +58,7 @@ SEED = 31415  # sas/main.rs:38
 TOP_LDS_LEVELS = 15  # common.hpp SAS_REL_LDS_LEVELS
 C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: rounded up to all 31 levels, 28-31 from HBM
 
-KERNELS = {"stree": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
+KERNELS = {"stree": "k_sa_stree", "stree_llcp": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
            "tagged": "k_sa_tagged"}
 
@@ -144,11 +144,11 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         reqs = {"cache": rc, "hbm": rh + max(0.0, probes - R) * rq + fin + (8.0 if packed else m) / 128}
     elif algo == "interp":
         hbm += probes * 16
-    elif algo in ("stree", "quad", "sector"):
-        if algo == "stree":
+    elif algo in ("stree", "stree_llcp", "quad", "sector"):
+        if algo in ("stree", "stree_llcp"):
             H, node, lds_l = st["stree_layers"], 64, st["stree_lds_layers"]
             sizes = _tree_layers(n, 16, 64, 17, 64, H)
-            tail = sa_w + win
+            tail = sa_w + win if algo == "stree" else 16  # STREE_LLCP: one 16-B LLCP entry a probe
         elif algo == "sector":
             H, node, lds_l = st["sector_layers"], 32, st["sector_lds_layers"]
             sizes = _tree_layers(n, 2, 32, 9, 32, H)
@@ -159,7 +159,8 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             sizes = _tree_layers(n, leaf_entries, 64, st["quad_fan"], 64, H)
             tail = 64
         h, c, l = _classify(sizes, node, lds_l)
-        hbm, cache, lds = h + max(0.0, probes - H) * tail + (max(0.0, m - 32) / 4 if algo != "stree" else 0), c, l
+        hbm, cache, lds = h + max(0.0, probes - H) * tail + (max(0.0, m - 32) / 4 if not algo.startswith("stree")
+                                                             else 0), c, l
         # one request per DRAM-level node (a 64-B node is one cooperative request; a 32-B one
         # too), per extra probe past the leaf, and the query stream
         reqs = {"cache": c / node, "hbm": h / node + max(0.0, probes - H) + (8.0 if packed else m) / 128}
@@ -170,13 +171,13 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
     # binary-search family P (4 + m) + m + 8; trees H node bytes + what the tail reads
     if algo in ("plain", "lcp", "llcp", "inline") and not range_flag:
         out["section_8d"] = P * (4 + m) + m + 8
-    elif algo in ("stree", "quad", "sector"):
+    elif algo in ("stree", "stree_llcp", "quad", "sector"):
         node = 32 if algo == "sector" else 64
-        tail = {"stree": 4 + m, "quad": 64, "sector": 12}[algo]
+        tail = {"stree": 4 + m, "stree_llcp": 4 + m, "quad": 64, "sector": 12}[algo]
         out["section_8d"] = H * node + max(0.0, probes - H) * tail + m + 8
     else:
         out["section_8d"] = hbm
-    if algo in ("plain", "lcp", "inline", "llcp", "stree", "quad", "sector") and not range_flag:
+    if algo in ("plain", "lcp", "inline", "llcp", "stree", "stree_llcp", "quad", "sector") and not range_flag:
         out["requests_model"] = reqs
     return out
 
@@ -327,7 +328,8 @@ def footprint(algo: str, st: dict) -> int:
     PLAIN / LCP = SA + packed text + the pivot levels it reads (+ nothing else: mlr
     skipping keeps its lcps in registers); LLCP = its 16-B entries + pivots + text; INLINE =
     the fused quad leaves + pivots + text; QUAD = the quad tree (+ SA with compact leaves) +
-    text; SECTOR = the sector tree + text; STREE = the S-tree + SA + text; PREFIX = the prefix
+    text; SECTOR = the sector tree + text; STREE = the S-tree + SA + text; STREE_LLCP = the
+    S-tree + the LLCP entries + text; PREFIX = the prefix
     table + the quad leaves (+ SA with compact leaves) + text; *_range = + the prefix table;
     TAGGED = the tagged index (it holds nothing else)."""
     base = algo[:-6] if algo.endswith("_range") else ("prefix" if algo == "prefix_packed" else algo)
@@ -350,6 +352,8 @@ def footprint(algo: str, st: dict) -> int:
         b = st["sector_bytes"] + text
     elif base == "stree":
         b = st["stree_bytes"] + sa + text
+    elif base == "stree_llcp":  # the S-tree + the LLCP entries (SA values included) + text
+        b = st["stree_bytes"] + st["llcp_bytes"] + text
     elif base == "prefix":
         b = st["prefix_bytes"] + _quad_leaf_bytes(st) + compact_sa + text
     elif base == "interp":
@@ -621,7 +625,7 @@ def c0_record(torch, sas_amd, dev, seconds: float):
 
 # ---------------------------------------------------------------- LCP skipping on long queries
 LCP_LONG_MS = (64, 128, 256)
-LCP_LONG_ALGOS = ("plain", "lcp", "llcp")
+LCP_LONG_ALGOS = ("plain", "lcp", "llcp", "stree_llcp", "quad")
 
 
 def cut_queries(torch, text, off_t, m: int):
@@ -692,8 +696,8 @@ def lcp_long_runs(torch, idx, text, nq: int, steps: int, warmup: int, stream, la
 
 
 def lcp_long_summary(rec: dict) -> dict:
-    """{text_m: [plain, lcp, llcp] kernel ms} and which skipping beats PLAIN where."""
-    s, wins = {}, []
+    """{text_m: kernel ms in LCP_LONG_ALGOS order} and which skipping beats PLAIN where."""
+    s, wins = {"algos": list(LCP_LONG_ALGOS)}, []
     for tk, rows in rec.items():
         if not isinstance(rows, dict) or tk in ("what", "summary"):
             continue
@@ -702,10 +706,10 @@ def lcp_long_summary(rec: dict) -> dict:
                 continue
             ms = [_r(row[a]["kernel_ms"]) for a in LCP_LONG_ALGOS]
             s[f"{tk}_{mk}"] = ms
-            for a in ("lcp", "llcp"):
+            for a in ("lcp", "llcp", "stree_llcp"):
                 if row[a]["kernel_ms"] < row["plain"]["kernel_ms"]:
                     wins.append(f"{a}@{tk}_{mk}:{row['plain']['kernel_ms'] / row[a]['kernel_ms']:.2f}x")
-    return {"ms_plain_lcp_llcp": s, "skipping_beats_plain": wins}
+    return {"ms": s, "skipping_beats_plain": wins}
 
 
 # ---------------------------------------------------------------- configs[3]
@@ -1056,96 +1060,181 @@ def run_c3(args, torch, sas_amd, dev, ws, rank):
 
 
 # ---------------------------------------------------------------- u32 path
-def run_sst(args, torch, sas_amd, dev, ws, rank):
-    """The u32 path (static-search-tree crate): the reference's bench sweeps sizes up to
-    2^30 bytes (sst/bin/bench.rs:455-472); this runs the largest, 2^28 keys (gen_vals:
-    uniform < i32::MAX, vals[0] = MAX, sorted; sst/util.rs:31-42) and 10^7 uniform
-    queries (gen_queries, :16-21) on every GPU layout, all checked against each other."""
+def sst_layouts(sas_amd):
+    """Every GPU layout of the u32 path by the reference's names (sst/bin/bench.rs:487-599)."""
+    return {
+        "SortedVec": lambda v: sas_amd.SortedVec.new(v),
+        "Eytzinger": lambda v: sas_amd.Eytzinger.new(v),
+        "STree16": lambda v: sas_amd.STree16.new(v),
+        "STree16_left_max": lambda v: sas_amd.STree16.new_params(v, True, False, False),
+        "STree15": lambda v: sas_amd.STree15.new(v),
+        "PartitionedSTree16M_b16": lambda v: sas_amd.PartitionedSTree16M.new(v, 16),
+        "PartitionedSTree16M_b20": lambda v: sas_amd.PartitionedSTree16M.new(v, 20),
+        "PartitionedSTree16_b16": lambda v: sas_amd.PartitionedSTree16.new(v, 16),
+        "PartitionedSTree16C_b16": lambda v: sas_amd.PartitionedSTree16C.new(v, 16),
+        "PartitionedSTree16L_b16": lambda v: sas_amd.PartitionedSTree16L.new(v, 16),
+        "PartitionedSTree16O_b16": lambda v: sas_amd.PartitionedSTree16O.new(v, 16),
+        "DirectMap": lambda v: sas_amd.DirectMap.new(v),
+    }
+
+
+# the default line's u32 lineup: the reference's oracle (SortedVec::binary_search), its bench
+# variant (STree16 left_max, sst/bin/bench.rs:96), its best (PartitionedSTree16M, both b of
+# its differential test's large end) and the prefix map taken to its limit
+SST_LINEUP = ("SortedVec", "STree16_left_max", "PartitionedSTree16M_b16", "PartitionedSTree16M_b20", "DirectMap")
+SST_KERNELS = {"SortedVec": "k_sst_sorted", "Eytzinger": "k_sst_eytzinger", "DirectMap": "k_sst_direct",
+               "PartitionedSTree16M_b16": "k_sst_pmap4", "PartitionedSTree16M_b20": "k_sst_pmap4"}
+
+
+def sst_bytes_per_lookup(name: str, layers: int, keys: int) -> float:
+    """SURVEY §8(d)-style algorithmic bytes of one u32 lookup: the query word, the answer word,
+    and per level what the layout reads (a 64-B node per S-tree layer, a 4-B key per binary /
+    Eytzinger probe, one 16-B entry for DirectMap's table)."""
+    if name.startswith("SortedVec") or name.startswith("Eytzinger"):
+        return 4 * (keys.bit_length()) + 8
+    if name == "DirectMap":
+        return 16 + 8
+    return 64 * layers + 8
+
+
+def sst_workload(nk: int, nq: int, positive: bool = False):
+    """gen_vals (uniform < i32::MAX, vals[0] = MAX, sorted; sst/util.rs:31-42) and 10^7
+    gen_queries (:16-21) or gen_positive_queries (:23-28)."""
     from oracle import pyoracle as O
-    nk = args.n if args.n != 1 << 30 else 1 << 28
-    nq = args.nq
     rng = np.random.default_rng(SEED)
     vals = rng.integers(0, O.MAX, nk, dtype=np.uint64).astype(np.uint32)
     vals[0] = O.MAX
     vals.sort()
-    if args.positive:  # gen_positive_queries (sst/util.rs:23-28)
-        qs = vals[rng.integers(0, nk, nq)]
-    else:  # gen_queries (sst/util.rs:16-21)
-        qs = rng.integers(0, O.MAX, nq, dtype=np.uint64).astype(np.uint32)
+    qs = vals[rng.integers(0, nk, nq)] if positive else rng.integers(0, O.MAX, nq, dtype=np.uint64).astype(np.uint32)
+    return vals, qs
+
+
+def sst_record(args, torch, sas_amd, dev, names=SST_LINEUP, nk: int = 1 << 28, cpu: bool = True) -> dict:
+    """The u32 static-search-tree path (sst/bin/bench.rs:548-599, "40x faster binary search",
+    readme.org:8) at the reference's largest size: 2^28 keys (1 GiB) and 10^7 uniform queries.
+    Every layout is timed like the headline (the driver's steps and warmup, one HIP event pair
+    per launch) and must return SortedVec::binary_search's value (the oracle) on every query.
+    Roofline: these kernels are bound by random 64-B node requests, so `frac` is the measured
+    L2->fabric request rate (same-hash PMC summary, profiles/pmc_sst_*.json) over the
+    calibrated random-request ceiling; `frac_hbm` the PMC bytes over 8 TB/s.  CPU: the
+    oracle's STree16 left_max batch_final::<128> restatement (the reference's bench variant)
+    on the allotted threads."""
+    from oracle import pyoracle as O
+    nq = args.nq
+    vals, qs = sst_workload(nk, nq, getattr(args, "positive", False))
+    expect = O.SortedVec(vals).query(qs)
     dq = torch.from_numpy(qs.view(np.int32)).to(dev)
     dout = torch.empty(nq, dtype=torch.int32, device=dev)
-    layouts = {
-        "SortedVec": lambda: sas_amd.SortedVec.new(vals),
-        "Eytzinger": lambda: sas_amd.Eytzinger.new(vals),
-        "STree16": lambda: sas_amd.STree16.new(vals),
-        "STree16_left_max": lambda: sas_amd.STree16.new_params(vals, True, False, False),
-        "STree15": lambda: sas_amd.STree15.new(vals),
-        "PartitionedSTree16M_b16": lambda: sas_amd.PartitionedSTree16M.new(vals, 16),
-        "PartitionedSTree16M_b20": lambda: sas_amd.PartitionedSTree16M.new(vals, 20),
-        "PartitionedSTree16_b16": lambda: sas_amd.PartitionedSTree16.new(vals, 16),
-        "PartitionedSTree16C_b16": lambda: sas_amd.PartitionedSTree16C.new(vals, 16),
-        "PartitionedSTree16L_b16": lambda: sas_amd.PartitionedSTree16L.new(vals, 16),
-        "PartitionedSTree16O_b16": lambda: sas_amd.PartitionedSTree16O.new(vals, 16),
-        "DirectMap": lambda: sas_amd.DirectMap.new(vals),
-    }
-    res, ref = {}, None
-    for name, mk in layouts.items():
-        idx = mk()
-        for _ in range(args.warmup):
-            idx.query(dq)
-        kns = idx.time_query(dq, dout, reps=args.steps, stream=torch.cuda.current_stream(dev).cuda_stream)
-        got = dout.cpu().numpy().view(np.uint32).copy()
-        if ref is None:
-            ref = got
-        res[name] = {"lookups_per_s": nq / (kns * 1e-9), "kernel_ms": kns * 1e-6, "ns_per_lookup": kns / nq,
-                     "layers": idx.layers(), "index_bytes": idx.size(), "agrees": bool(np.array_equal(got, ref))}
+    stream = torch.cuda.current_stream(dev)
+    mk = sst_layouts(sas_amd)
+    res = {}
+    for name in names:
+        idx = mk[name](vals)
+        t = launch_times(torch, lambda: idx.query(dq, stream=stream.cuda_stream, out=dout), args.steps, args.warmup,
+                         stream)
+        got = dout.cpu().numpy().view(np.uint32)
+        if not np.array_equal(got, expect):
+            raise SystemExit(f"bench sst: {name} differs from SortedVec::binary_search")
+        layers, size = idx.layers(), idx.size()
         idx.free()
-    if not all(r["agrees"] for r in res.values()):
-        raise SystemExit("bench sst: layouts disagree")
-    # --range mode (sst/bin/bench.rs:84-109): the interleaved [q, q+1] stream through
-    # STree16 left_max; rank(q+1) - rank(q) = number of keys equal to q (checked)
-    rq = np.stack([qs, np.minimum(qs.astype(np.uint64) + 1, O.MAX).astype(np.uint32)], 1).reshape(-1)
-    drq = torch.from_numpy(rq.view(np.int32)).to(dev)
-    drout = torch.empty(2 * nq, dtype=torch.int32, device=dev)
-    st16 = sas_amd.STree16.new_params(vals, True, False, False)
-    for _ in range(args.warmup):
-        st16.query(drq)
-    rkns = st16.time_query(drq, drout, reps=args.steps, stream=torch.cuda.current_stream(dev).cuda_stream)
-    sample = rq[: 2 * min(nq, 100_000)]
-    _, rk = st16.query(sample, want_rank=True)
-    cnt = rk[1::2].astype(np.int64) - rk[0::2].astype(np.int64)
-    expect = np.searchsorted(vals, sample[1::2], "left") - np.searchsorted(vals, sample[0::2], "left")
-    range_res = {"queries": 2 * nq, "lookups_per_s": 2 * nq / (rkns * 1e-9), "kernel_ms": rkns * 1e-6,
-                 "ranges_per_s": nq / (rkns * 1e-9), "counts_verified": bool(np.array_equal(cnt, expect))}
-    st16.free()
-    # CPU: the oracle's restatement of the reference's bench variant, STree16 left_max
-    # + batch_final::<128> (sst/bin/bench.rs:96; sst/s_tree.rs:303-326), contiguous
-    # per-thread chunks (sst/bin/bench.rs:558-573); all cores and 1 thread
-    tree = O.STree(vals, left_max=True)
-    threads = host_threads()
-    sample = nq
-    t0 = time.perf_counter()
-    cpu_out = tree.query_batch(qs[:sample], threads)
-    dt = time.perf_counter() - t0
-    s1 = min(nq, 2_000_000)
-    t1 = time.perf_counter()
-    tree.query_batch(qs[:s1], 1)
-    one = s1 / (time.perf_counter() - t1)
-    cpu_ok = bool(np.array_equal(cpu_out, ref[:sample]))
+        ks = t["mean_ms"] * 1e-3
+        bpl = sst_bytes_per_lookup(name, layers, nk)
+        r = {"lookups_per_s": nq / ks, "kernel_ms": t["mean_ms"], "kernel_ms_median": t["median_ms"],
+             "ns_per_lookup": ks * 1e9 / nq, "layers": layers, "index_bytes": size,
+             "bytes_per_lookup_model": bpl, "frac_8d_model": bpl * nq / ks / 1e9 / HBM_PEAK_GBPS,
+             "equals_sortedvec": True, "kernel": SST_KERNELS.get(name, "k_sst_stree4")}
+        pmc = load_pmc(f"sst_{name}_k{nk}_q{nq}")
+        if pmc and not pmc.get("stale") and pmc.get("rdreq_per_launch"):
+            r["requests_per_lookup"] = pmc["rdreq_per_launch"] / nq
+            r["traffic"] = pmc["hbm_bytes_per_launch"] / nq
+            r["req_frac"] = pmc["rdreq_per_launch"] / ks / CACHE_REQ_CEILING
+            r["frac_hbm"] = pmc["hbm_bytes_per_launch"] / ks / 1e9 / HBM_PEAK_GBPS
+            r["pmc_source"] = pmc["source"]
+        elif pmc:
+            r["pmc"] = pmc
+        res[name] = r
     best = max(res, key=lambda k: res[k]["lookups_per_s"])
+    rec = {"workload": f"u32 static-search-tree path: {nk} keys (gen_vals, {nk * 4 >> 20} MiB), {nq} uniform queries "
+                       f"(gen_queries), value of the first key >= q; every layout equal to SortedVec::binary_search",
+           "keys": nk, "queries": nq, "best": best, "layouts": res,
+           "frac_basis": "frac = PMC L2->fabric read requests / kernel time / the measured random-request ceiling "
+                         f"({CACHE_REQ_CEILING:.3g}/s); frac_hbm = PMC bytes (requests x 128 B + writes) / time / 8 TB/s"}
+    if cpu:
+        tree = O.STree(vals, left_max=True)
+        threads = host_threads()
+        t0 = time.perf_counter()
+        cpu_out = tree.query_batch(qs, threads)
+        dt = time.perf_counter() - t0
+        s1 = min(nq, 2_000_000)
+        t1 = time.perf_counter()
+        tree.query_batch(qs[:s1], 1)
+        one = s1 / (time.perf_counter() - t1)
+        rec["cpu_baseline"] = {"value": nq / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
+                               "single_thread_value": one, "agrees": bool(np.array_equal(cpu_out, expect)),
+                               "sample": f"oracle STree16 left_max + batch_final::<128> restatement "
+                                         f"(sst/s_tree.rs:303-326) on all {nq} queries, {threads} threads"}
+        if not rec["cpu_baseline"]["agrees"]:
+            raise SystemExit("bench sst: the CPU restatement differs from SortedVec")
+    return rec
+
+
+def sst_summary(rec: dict) -> dict:
+    """configs.sst of the line: the best layout, the reference's bench variant and oracle."""
+    b = rec["best"]
+    lay = rec["layouts"]
+    L = lay[b]
+    out = {"best": b, "lookups_per_s": _r(L["lookups_per_s"]), "kernel_ms": _r(L["kernel_ms"]),
+           "kernel_ms_median": _r(L["kernel_ms_median"]),
+           "frac": _r(L.get("req_frac"), 3), "frac_hbm": _r(L.get("frac_hbm"), 3), "traffic": _r(L.get("traffic")),
+           "index_bytes": L["index_bytes"],
+           "ms": {k.replace("PartitionedSTree16M_", "PSTree16M_"): _r(v["kernel_ms"]) for k, v in lay.items()},
+           "stree16_left_max_frac": _r(lay.get("STree16_left_max", {}).get("req_frac"), 3),
+           "equal_to_sortedvec": all(v["equals_sortedvec"] for v in lay.values())}
+    cpu = rec.get("cpu_baseline")
+    if cpu:
+        out["cpu"] = _r(cpu["value"])
+        out["cpu_cores"] = cpu["cores"]
+    return out
+
+
+def run_sst(args, torch, sas_amd, dev, ws, rank):
+    """--workload sst: the u32 path on its own line (every layout, or --sst-layouts), with the
+    --range mode (sst/bin/bench.rs:84-109) through STree16 left_max."""
+    from oracle import pyoracle as O
+    nk = args.n if args.n != 1 << 30 else 1 << 28
+    names = tuple(args.sst_layouts.split(",")) if args.sst_layouts else tuple(sst_layouts(sas_amd))
+    rec = sst_record(args, torch, sas_amd, dev, names, nk=nk, cpu=not args.no_cpu)
+    nq = args.nq
+    vals, qs = sst_workload(nk, nq, args.positive)
+    range_res = None
+    if not args.sst_layouts:
+        # --range mode: the interleaved [q, q+1] stream through STree16 left_max;
+        # rank(q+1) - rank(q) = number of keys equal to q (checked)
+        rq = np.stack([qs, np.minimum(qs.astype(np.uint64) + 1, O.MAX).astype(np.uint32)], 1).reshape(-1)
+        drq = torch.from_numpy(rq.view(np.int32)).to(dev)
+        drout = torch.empty(2 * nq, dtype=torch.int32, device=dev)
+        st16 = sas_amd.STree16.new_params(vals, True, False, False)
+        for _ in range(args.warmup):
+            st16.query(drq)
+        rkns = st16.time_query(drq, drout, reps=args.steps, stream=torch.cuda.current_stream(dev).cuda_stream)
+        sample = rq[: 2 * min(nq, 100_000)]
+        _, rk = st16.query(sample, want_rank=True)
+        cnt = rk[1::2].astype(np.int64) - rk[0::2].astype(np.int64)
+        expect = np.searchsorted(vals, sample[1::2], "left") - np.searchsorted(vals, sample[0::2], "left")
+        range_res = {"queries": 2 * nq, "lookups_per_s": 2 * nq / (rkns * 1e-9), "kernel_ms": rkns * 1e-6,
+                     "ranges_per_s": nq / (rkns * 1e-9), "counts_verified": bool(np.array_equal(cnt, expect))}
+        st16.free()
+    best = rec["best"]
     emit({
         "metric": "u32 static-search-tree lookups/s (2^28 keys = 1 GiB, 10^7 uniform queries)",
-        "value": res[best]["lookups_per_s"], "unit": "lookups/s", "n_gpus": 1, "steps": args.steps,
+        "value": rec["layouts"][best]["lookups_per_s"], "unit": "lookups/s", "n_gpus": 1, "steps": args.steps,
         "warmup": args.warmup, "higher_is_better": True, "dtype": "u32", "vs_baseline": None,
         "data": "synthetic: gen_vals / gen_queries shapes (sst/util.rs:16-42)",
         "config": {"workload": "sst u32 path", "keys": nk, "queries": nq, "best": best},
-        "layouts": res,
+        "layouts": rec["layouts"],
         "range_mode": range_res,
         "queries_kind": "positive" if args.positive else "uniform",
-        "cpu_baseline": {"value": sample / dt, "unit": "lookups/s", "cores": threads, "kind": "port",
-                         "single_thread_value": one, "host_cpu": host_cpu(), "host_nproc": os.cpu_count(),
-                         "sample": f"oracle STree16 left_max + batch_final::<128> restatement (sst/s_tree.rs:303-326) "
-                                   f"on all {sample} queries, {threads} threads, {dt:.2f} s", "agrees": cpu_ok}})
+        "cpu_baseline": rec.get("cpu_baseline")})
 
 
 def ref_sizes(frm: int = 5, to: int = 30, dense: bool = False):
@@ -1252,18 +1341,24 @@ def _r(x, d: int = 4):
 
 def config_summary(rec: dict) -> dict:
     """One flat per-config entry of the line from a full record(): throughput, kernel time
-    (event mean and median), roofline fraction of the algorithmic HBM bytes, the PMC traffic
-    per lookup when a same-hash pass exists, and the algorithm's own index footprint."""
+    (event mean and median), the roofline fraction, the PMC traffic per lookup when a
+    same-hash pass exists, and the algorithm's own index footprint.
+    frac is a physical fraction (<= 1): the PMC request floor over the kernel time (req_frac:
+    these random-access kernels are bound by L2->fabric requests) when a same-hash PMC pass
+    exists, else the HBM-served algorithmic bytes over the time and 8 TB/s (frac_hbm).
+    SURVEY §8(d)'s worst-case byte model (every level at P(4 + m) bytes, wherever it is
+    served: LDS, the Infinity Cache or HBM) is kept as frac_8d_model; it passes 1 where
+    pivot levels never reach HBM, so it is not a roofline."""
     pmc = rec.get("pmc") or {}
+    req = _r((pmc.get("requests_split") or {}).get("frac"), 3)
+    hbm = _r((rec.get("achieved_hbm_GBps") or 0.0) / HBM_PEAK_GBPS, 3)
     return {"algo": rec.get("algo"), "lookups_per_s": _r(rec.get("kernel_lookups_per_s", rec.get("lookups_per_s"))),
             "kernel_ms": _r(rec.get("kernel_ms")), "kernel_ms_median": _r(rec.get("kernel_ms_median")),
-            # SURVEY §8(d)'s algorithmic bytes per lookup (all levels); frac_hbm: the HBM-served share only
-            "frac": _r((rec.get("bytes_per_lookup") or {}).get("section_8d", 0.0) * rec["kernel_lookups_per_s"] / 1e9
-                       / HBM_PEAK_GBPS, 3) if rec.get("kernel_lookups_per_s") else None,
-            "frac_hbm": _r((rec.get("achieved_hbm_GBps") or 0.0) / HBM_PEAK_GBPS, 3),
-            # the request-rate floor over the kernel time (PMC requests; <= 1): the bound these
-            # random-access kernels run at
-            "req_frac": _r((pmc.get("requests_split") or {}).get("frac"), 3),
+            "frac": req if req is not None else hbm, "frac_basis": "req" if req is not None else "hbm",
+            "frac_hbm": hbm, "req_frac": req,
+            "frac_8d_model": _r((rec.get("bytes_per_lookup") or {}).get("section_8d", 0.0) *
+                                rec["kernel_lookups_per_s"] / 1e9 / HBM_PEAK_GBPS, 3)
+            if rec.get("kernel_lookups_per_s") else None,
             "traffic": _r(pmc.get("fabric_bytes_per_lookup")), "index_bytes": rec.get("index_bytes")}
 
 
@@ -1294,7 +1389,7 @@ def compact_line(full: dict) -> dict:
     line["cpu_baseline"] = None if not cpu else {
         "value": _r(cpu["value"]), "unit": cpu["unit"], "cores": cpu["cores"], "kind": cpu["kind"],
         "single_thread_value": _r(cpu.get("single_thread_value")), "agrees_with_gpu": cpu.get("agrees_with_gpu"),
-        "sample": cpu["sample"][:240]}
+        "sample": cpu["sample"][:160]}
     confs = full.get("configs") or {}
     out = {}
     if "c0" in confs:
@@ -1305,6 +1400,9 @@ def compact_line(full: dict) -> dict:
     for k in ("c1", "c2"):
         if k in confs:
             out[k] = config_summary(confs[k])
+    if "c2" in confs and confs["c2"].get("lcp_stree"):
+        out["c2"]["lcp_stree"] = {kk: vv for kk, vv in config_summary(confs["c2"]["lcp_stree"]).items()
+                                  if kk in ("algo", "kernel_ms", "frac", "frac_basis", "traffic")}
     if "c1" in confs and confs["c1"].get("deep_pivots"):
         out["c1_deep_pivots"] = dict(config_summary(confs["c1"]["deep_pivots"]),
                                      pivot_levels=confs["c1"]["deep_pivots"].get("pivot_levels"))
@@ -1319,11 +1417,13 @@ def compact_line(full: dict) -> dict:
         c4 = confs["c4"]
         out["c4"] = {"skipped": c4["skipped"]} if c4.get("skipped") else {
             "lookups_per_s": _r(c4["lookups_per_s"]), "ms_per_step": _r(c4["ms_per_step"]), "n": c4["n"],
-            "parts": c4["parts"], "index_bytes": c4["index_bytes"], "proven": c4.get("proven")}
+            "share": c4.get("share"), "parts": c4["parts"], "index_bytes": c4["index_bytes"],
+            "prefix_key_fraction": c4.get("prefix_key_fraction"), "proven": c4.get("proven")}
+    if "sst" in confs:
+        out["sst"] = sst_summary(confs["sst"])
     line["configs"] = out
-    line["configs_frac_basis"] = ("frac: SURVEY 8(d) algorithmic bytes per lookup (every level, wherever served) / "
-                                  "kernel time / 8 TB/s, above 1 where pivot levels come from LDS / cache-resident "
-                                  "blocks; frac_hbm: the HBM-served bytes only; req_frac: PMC request floor / time")
+    line["configs_frac_basis"] = ("frac <= 1: req = PMC request floor / kernel time, hbm = HBM-served algorithmic "
+                                  "bytes / time / 8 TB/s; frac_8d_model: SURVEY 8(d) bytes wherever served")
     if full.get("variants"):
         line["variants_kernel_ms"] = {k: _r(v["kernel_ms"]) for k, v in full["variants"].items()}
     if full.get("lcp_long"):
@@ -1364,12 +1464,14 @@ WORKLOADS = {
               "of the bucket; 2^30 text in HBM, 10^7 len-32 queries",
     "plain_rel": "configs[1]: PLAIN binary search over the SA (sas/sa_search.rs:98-112): the pivots of levels "
                  "1-{R} from {rb} of prefix-relative blocks (4 levels per 32-B block: the 8 chars after the block "
-                 "bounds' common prefix), levels 1-{t1} staged in LDS, {t1p}-{R} {where}; the rest read SA[mid] "
-                 "and a text window",
+                 "bounds' common prefix), levels 1-{t1} staged in LDS{where}; the rest read SA[mid] and a text window",
     "lcp": "configs[1] + mlr LCP skipping",
     "llcp": "configs[1] probe sequence + Manber-Myers Llcp/Rlcp skipping (16-B {SA, Llcp, Rlcp, chars} entries)",
     "inline": "configs[1] probe sequence over fused {32-char key, SA} entries",
     "stree": "configs[2]: S-tree of 16-char SA keys (17-ary 64-B nodes, top layers LDS-staged) + LCP-skipping tail",
+    "stree_llcp": "configs[2] as named: LCP-accelerated search on the static-search-tree layout, LDS-staged: the "
+                  "S-tree of 16-char SA keys (17-ary 64-B nodes, top layers in LDS) gives the run of suffixes sharing "
+                  "q's key, Manber-Myers LLCP skipping (16-B {SA, Llcp, Rlcp, chars} entries) finishes inside it",
     "sector": "configs[2]: sector S-tree (9-ary 32-B nodes, fused 32-char key + SA leaves, top layers LDS-staged)",
     "quad": "configs[2]: quad S-tree (17-ary 64-B nodes read by 4-lane groups, 4-entry fused {32-char key, SA} "
             "leaves, top layers LDS-staged)",
@@ -1383,9 +1485,16 @@ def plain_label(st: dict) -> str:
     t1, R = st["top_levels"], st.get("rel_levels", 0)
     rb = st.get("rel_bytes", 0)
     hb = [d0 for d0, _, w in rel_groups(R) if w == "hbm"]
+    if R <= t1:
+        where = ""
+    elif not hb:
+        where = f", levels {t1 + 1}-{R} cache-resident"
+    elif hb[0] <= t1:
+        where = f", levels {t1 + 1}-{R} from HBM"
+    else:
+        where = f", levels {t1 + 1}-{hb[0]} cache-resident, {hb[0] + 1}-{R} from HBM"
     return WORKLOADS["plain_rel"].format(
-        t1=t1, t1p=t1 + 1, R=R, rb=(f"{rb / 2 ** 30:.2f} GiB" if rb >= 1 << 30 else f"{rb >> 20} MiB"),
-        where=(f"levels {t1 + 1}-{hb[0]} cache-resident, {hb[0] + 1}-{R} from HBM" if hb else "cache-resident"))
+        t1=t1, R=R, rb=(f"{rb / 2 ** 30:.2f} GiB" if rb >= 1 << 30 else f"{rb >> 20} MiB"), where=where)
 
 
 def main():
@@ -1396,10 +1505,12 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default=None, choices=["stree", "plain", "lcp", "sector", "quad", "inline", "llcp",
+    ap.add_argument("--algo", default=None, choices=["stree", "stree_llcp", "plain", "lcp", "sector", "quad", "inline",
+                                                     "llcp",
                                                      "prefix", "tagged", "interp"])
     ap.add_argument("--variants",
-                    default="plain,plain_range,llcp,stree,sector,quad,inline,interp,interp_range,prefix_packed",
+                    default="plain,plain_range,llcp,stree,stree_llcp,sector,quad,inline,interp,interp_range,"
+                            "prefix_packed",
                     help="other algos timed beside the headline one (mlr LCP skipping, 'lcp', lost to PLAIN at every "
                          "m and on both texts of the lcp_long record: it runs there and in configs[3] only)")
     ap.add_argument("--prefix-chars", type=int, default=16,
@@ -1436,6 +1547,8 @@ def main():
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric) + every config's sub-record; "
                          "c3: the configs[3] record alone; sst: the u32 static-search-tree path")
     ap.add_argument("--positive", action="store_true", help="sst workload: queries drawn from the keys")
+    ap.add_argument("--sst-layouts", default="", help="sst workload: these layouts only (comma-separated names)")
+    ap.add_argument("--no-sst", action="store_true", help="skip the u32 static-search-tree sub-record (configs.sst)")
     ap.add_argument("--sweep", action="store_true",
                     help="sst workload: the reference's size sweep (32 B .. 2^--sweep-to B) instead of one size")
     ap.add_argument("--sweep-to", type=int, default=30, help="sst sweep: largest size 2^k bytes")
@@ -1617,7 +1730,8 @@ def main():
         vbase, vfl = algo_flags(v)
         bpl = bytes_per_lookup("prefix" if v == "prefix_packed" else vbase, stats, n, m, vmean,
                                range_flag=bool(vfl), packed=v == "prefix_packed")
-        key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector", "llcp": "llcp"}.get(v)
+        key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector", "llcp": "llcp",
+               "stree_llcp": "stree_llcp"}.get(v)
         pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}" + (f"_t{stats['top2_levels']}" if key == "plain" else "")) \
             if key else None
         variants[v] = record(v, nq, vk, vel, bpl, footprint(v, stats), pmc, vmean,
@@ -1662,9 +1776,10 @@ def main():
     # freed (below); N = 1 only
     lcp_long = None
     if ws == 1 and args.mode == "replicated" and not args.no_lcp_long and stats["llcp_bytes"]:
-        lcp_long = {"what": "PLAIN vs mlr LCP vs Manber-Myers LLCP skipping, 10^7 positive len-m queries, kernel ms "
-                            "(HIP events), positions identical; random: the headline's 2^30 text; repetitive: 2^24 "
-                            "random chars x 64 copies, 1% substitutions per copy",
+        lcp_long = {"what": "PLAIN vs mlr LCP vs Manber-Myers LLCP skipping vs the S-tree + LLCP tail (configs[2]'s "
+                            "combination) vs QUAD, 10^7 positive len-m queries, kernel ms (HIP events), positions "
+                            "identical; random: the headline's 2^30 text; repetitive: 2^24 random chars x 64 copies, "
+                            "1% substitutions per copy",
                     "random": lcp_long_runs(torch, idx, text, nq, args.steps, args.warmup, stream, "random")}
 
     # occurrence ranges (Search::search_prefix / search_range, sas/util.rs:36-46): the rank
@@ -1734,6 +1849,12 @@ def main():
             configs["c2"] = dict(variants[best2], workload=WORKLOADS[best2],
                                  lds_layers={"quad": stats["quad_lds_layers"], "sector": stats["sector_lds_layers"],
                                              "stree": stats["stree_lds_layers"]}[best2])
+            # BASELINE's configs[2] names the combination: LCP-accelerated search on the static
+            # search tree layout, LDS-staged (the S-tree descent + the LLCP tail); its m > 32
+            # shapes are in lcp_long
+            if "stree_llcp" in variants:
+                configs["c2"]["lcp_stree"] = dict(variants["stree_llcp"], workload=WORKLOADS["stree_llcp"],
+                                                  lds_layers=stats["stree_lds_layers"])
     idx_stats = {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
                                        "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "rel_levels",
                                        "iterations", "prefix_chars", "prefix_bytes", "sa_bytes", "text_bytes",
@@ -1744,7 +1865,7 @@ def main():
         torch.cuda.empty_cache()
         tb = time.perf_counter()
         rt = repetitive_text(torch, n, dev)
-        ridx = sas_amd.SaNaive.build(rt, lcp=True, llcp=True, stree=False, sector=False, quad=False, prefix=False)
+        ridx = sas_amd.SaNaive.build(rt, lcp=True, llcp=True, stree=True, sector=False, quad=True, prefix=False)
         log(f"lcp_long repetitive index built in {time.perf_counter() - tb:.1f} s")
         lcp_long["repetitive"] = lcp_long_runs(torch, ridx, rt, nq, args.steps, args.warmup, stream, "repetitive")
         lc = ridx.lcp_array()
@@ -1756,6 +1877,10 @@ def main():
         torch.cuda.empty_cache()
         lcp_long["summary"] = lcp_long_summary(lcp_long)
         log("lcp_long done")
+    # the u32 static-search-tree path (the reference's other crate, sst/bin/bench.rs:548-599): N = 1
+    if ws == 1 and not args.no_sst and args.mode == "replicated":
+        configs["sst"] = sst_record(args, torch, sas_amd, dev)
+        log(f"sst done: best {configs['sst']['best']}")
     # configs[3]: free the 2^30 index first (N = 1 only: the scaling runs time the headline)
     if ws == 1 and not args.no_c3 and args.mode == "replicated":
         idx.free()

@@ -183,8 +183,13 @@ enum sas_algo {
                            else SA + text.  With SAS_PREFIX_RANGE it starts from the prefix
                            table's range.  n < 2^32 (the reference asserts r_val * r fits a
                            usize, :389-392); ENOTSUP above                                   */
-    SAS_ALGO_TAGGED = 9 /* bucket table + tagged SA entries (needs SAS_BUILD_TAGGED): the
+    SAS_ALGO_TAGGED = 9, /* bucket table + tagged SA entries (needs SAS_BUILD_TAGGED): the
                            configs[3] shape's lookup, ~4-5 memory requests for a long query  */
+    SAS_ALGO_STREE_LLCP = 10 /* configs[2]'s combination: the STREE descent over the 16-char SA keys
+                           (LDS-staged top layers) gives the run of suffixes sharing q's key,
+                           then Manber-Myers LLCP skipping finishes inside it (the LLCP entries'
+                           binary-search tree walked from its root, mids outside the run decided
+                           with no read); needs SAS_BUILD_STREE and SAS_BUILD_LLCP          */
 };
 
 typedef struct sas_stats {

@@ -72,6 +72,7 @@ enum class Algo : int {
     Prefix = SAS_ALGO_PREFIX,
     Interp = SAS_ALGO_INTERP,
     Tagged = SAS_ALGO_TAGGED,
+    StreeLlcp = SAS_ALGO_STREE_LLCP,
 };
 
 /* build flags of SaNaive::build: the LCP array, the fused quad tree and the p = 16 prefix

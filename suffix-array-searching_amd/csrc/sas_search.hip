@@ -39,7 +39,8 @@
 #define SEARCH_BLOCK 1024
 #define TRY_RC(x) do { int rc_ = (x); if (rc_) return rc_; } while (0)
 #define BLOCKS_PER_CU 2
-// the binary searches (k_sa_binary: PLAIN, LCP, LLCP): workgroup size and workgroups per CU.
+// the binary searches (k_sa_binary: PLAIN, LCP, LLCP) and the S-tree descents (k_sa_stree,
+// k_sa_stree4x: STREE, STREE_LLCP): workgroup size and workgroups per CU.
 // The launch bound follows them (waves per SIMD = block x blocks / 256), which caps the VGPRs:
 // 1024 x 2 -> 8 waves, 64 VGPRs; 768 x 2 -> 6 waves, 80 VGPRs (the LDS pivot groups, 72.5 KiB
 // a workgroup, allow two workgroups a CU either way)
@@ -433,12 +434,108 @@ __device__ __forceinline__ uint64_t stree_descend(const SearchArgs& a, const uin
     return k;
 }
 
+// The exact lower bound of q inside [r0, r1], the run of suffixes whose padded 16-char key
+// is q's (the S-tree descent's result); returns its position.
+// LT = false: binary search over [r0, r1] with mlr skipping from char 16 (SA + text reads).
+// LT = true (SAS_ALGO_STREE_LLCP): the LLCP entries (Manber-Myers Llcp / Rlcp, SAS_BUILD_LLCP)
+//   belong to the implicit binary-search tree over the whole SA, so the tail walks that tree
+//   from its root: a mid outside the run is decided by the S-tree keys with no read (below r0:
+//   < q; at or past r1: > q), a mid inside reads its 16-B entry and applies the LLCP rules of
+//   k_sa_binary.  A bound outside the run has an lcp with q below 16 that no compare measured;
+//   the first entry read after it supplies it: for a suffix a < the run (key16(a) < K) and b in
+//   the run, lcp(a, b) = lcp(a, q), and symmetrically for the right bound (up to a text-end
+//   suffix b shorter than 16 chars, where lcp(b, c) may fall below lcp(q, c)).  Taking the
+//   entry's own Llcp / Rlcp for such a side makes that side tie (Llcp = llcp), so a probe
+//   decided on it always compares (from its lcp, which b shares with q either way); a side
+//   inside the run carries an exact lcp from an earlier compare or rule.  So every rule is
+//   applied on an exact lcp and the result is binary_search's.
+template <int QW, int W, bool LT>
+__device__ __forceinline__ uint64_t stree_tail(const SearchArgs& a, const QueryRegs<QW>& q, uint32_t m, uint64_t r0,
+                                               uint64_t r1, uint32_t* probes) {
+    const SaView<W> sa{a.sa};
+    const uint64_t n = a.n, sa_n = a.sa_n;
+    if (!LT) {
+        // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
+        const uint32_t h16 = m < 16 ? m : 16;
+        uint64_t l = r0, r = r1;
+        uint32_t llcp = h16, rlcp = h16;
+        sa_val_t<W> pr = 0;
+        bool have = false;
+        while (l < r) {
+            const uint64_t mid = (l + r) >> 1;
+            const sa_val_t<W> p = (sa_val_t<W>)sa[mid];
+            uint32_t lcp;
+            const uint32_t h = llcp < rlcp ? llcp : rlcp;
+            const bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
+            (*probes)++;
+            if (lt) {
+                l = mid + 1;
+                llcp = lcp;
+            } else {
+                r = mid;
+                rlcp = lcp;
+                pr = p;
+                have = true;
+            }
+        }
+        if (l >= sa_n) return a.next_pos;
+        return have ? (uint64_t)pr : (uint64_t)sa[l];
+    }
+    uint64_t l = 0, r = sa_n, pr = 0;
+    uint32_t llcp = 0, rlcp = 0;
+    bool have = false;
+    for (;;) {
+        // the walk to the next mid inside the run, ALU only: the lanes of a wave reach their
+        // in-run mids at different depths, and one load per outer iteration keeps their
+        // reads in lockstep (a load inside the walk would serialise their latencies)
+        uint64_t mid = 0;
+        while (l < r) {
+            mid = (l + r) >> 1;
+            if (mid < r0) l = mid + 1;       // key16 < K: < q, no read
+            else if (mid >= r1) r = mid;     // key16 > K: > q, no read
+            else break;
+        }
+        if (!(l < r)) break;
+        const uint4 e = a.llcp[mid];
+        const uint64_t p = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32);
+        const uint32_t x = (e.y >> 8) & SAS_LLCP_CAP, y = e.y >> 20;
+        if (l <= r0) llcp = x;  // the left bound SA[l - 1] lies before the run (or l = 0)
+        if (r >= r1) rlcp = y;  // the right bound SA[r] lies past it (or r = sa_n)
+        (*probes)++;
+        bool lt;
+        uint32_t lcp, hh = 0, inl = 0;
+        bool decided = true;
+        if (llcp >= rlcp) {
+            if (x > llcp) { lt = true; lcp = llcp; }
+            else if (x < llcp && x < SAS_LLCP_CAP) { lt = false; lcp = x; }
+            else { decided = false; hh = x; inl = e.z; }
+        } else {
+            if (y > rlcp) { lt = false; lcp = rlcp; }
+            else if (y < rlcp && y < SAS_LLCP_CAP) { lt = true; lcp = y; }
+            else { decided = false; hh = y; inl = e.w; }
+        }
+        if (!decided) lt = llcp_tie_less<QW>(a.tw, n, p, q, hh, inl, &lcp);
+        if (lt) {
+            l = mid + 1;
+            llcp = lcp;
+        } else {
+            r = mid;
+            rlcp = lcp;
+            pr = p;
+            have = true;
+        }
+    }
+    if (r >= sa_n) return a.next_pos;
+    if (have) return pr;
+    const uint4 e = a.llcp[r];  // r moved only past the run (or is r1 itself)
+    return (uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32);
+}
+
 // One 4-lane group per query.  The S-tree descent and the leaf scans are
 // cooperative; the exact tail search in [r0, r1] (SA + text reads) runs on all
 // four lanes identically, so its loads coalesce to one request each.
 template <int QW, int W>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
-    const SaView<W> sa{a.sa};
+__global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_stree(SearchArgs a) {
     __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.stree);
@@ -447,7 +544,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
     }
     uint32_t bad = 0;
     const uint32_t sub = threadIdx.x & (QUAD_G - 1);
-    const uint64_t n = a.n;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
     const uint64_t ol = a.stree_off[a.stree_height - 1];
     const uint64_t sa_n = a.sa_n;
@@ -490,34 +586,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
         }
         if (r0 > sa_n) r0 = sa_n;
         if (r1 > sa_n) r1 = sa_n;
-
-        // exact lower bound inside [r0, r1]: chars [0, min(16, m)) match every suffix there
-        const uint32_t h16 = m < 16 ? m : 16;
-        uint64_t l = r0, r = r1;
-        uint32_t llcp = h16, rlcp = h16;
-        sa_val_t<W> pr = 0;
-        bool have = false;
-        while (l < r) {
-            uint64_t mid = (l + r) >> 1;
-            sa_val_t<W> p = (sa_val_t<W>)sa[mid];
-            uint32_t lcp;
-            uint32_t h = llcp < rlcp ? llcp : rlcp;
-            bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
-            probes++;
-            if (lt) {
-                l = mid + 1;
-                llcp = lcp;
-            } else {
-                r = mid;
-                rlcp = lcp;
-                pr = p;
-                have = true;
-            }
-        }
-        uint64_t pos;
-        if (l >= sa_n) pos = a.next_pos;
-        else if (have) pos = pr;
-        else pos = sa[l];
+        const uint64_t pos = stree_tail<QW, W, false>(a, q, m, r0, r1, &probes);
         if (sub == 0) {
             a.out_pos[i] = pos;
             if (a.out_probes) a.out_probes[i] = probes;
@@ -534,9 +603,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree(SearchArgs a) {
 // every lane runs the exact tail search of its own query in parallel: the descent
 // costs one request per node as in k_sa_stree, and the tail keeps the per-lane
 // parallelism of a one-lane-per-query search (the text compares of long queries dominate).
-template <int QW, int W>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree4x(SearchArgs a) {
-    const SaView<W> sa{a.sa};
+template <int QW, int W, bool LT = false>
+__global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_stree4x(SearchArgs a) {
     __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.stree);
@@ -546,7 +614,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree4x(SearchArgs a) {
     uint32_t bad = 0;
     const uint32_t sub = threadIdx.x & (QUAD_G - 1);
     const int lane0 = (int)((threadIdx.x & 63) & ~3u);
-    const uint64_t n = a.n;
     const uint4* g = reinterpret_cast<const uint4*>(a.stree);
     const uint64_t ol = a.stree_off[a.stree_height - 1];
     const uint64_t sa_n = a.sa_n;
@@ -606,32 +673,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_stree4x(SearchArgs a) {
         }
         if (!mine) continue;
         // exact lower bound of this lane's query inside [r0, r1] (per lane)
-        const uint32_t h16 = m < 16 ? m : 16;
-        uint64_t l = my_r0, r = my_r1;
-        uint32_t llcp = h16, rlcp = h16;
-        sa_val_t<W> pr = 0;
-        bool have = false;
-        while (l < r) {
-            const uint64_t mid = (l + r) >> 1;
-            const sa_val_t<W> p = (sa_val_t<W>)sa[mid];
-            uint32_t lcp;
-            const uint32_t h = llcp < rlcp ? llcp : rlcp;
-            const bool lt = suffix_less_from<QW>(a.tw, n, p, q, h, &lcp);
-            probes++;
-            if (lt) {
-                l = mid + 1;
-                llcp = lcp;
-            } else {
-                r = mid;
-                rlcp = lcp;
-                pr = p;
-                have = true;
-            }
-        }
-        uint64_t pos;
-        if (l >= sa_n) pos = a.next_pos;
-        else if (have) pos = pr;
-        else pos = sa[l];
+        const uint64_t pos = stree_tail<QW, W, LT>(a, q, m, my_r0, my_r1, &probes);
         a.out_pos[i] = pos;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -2517,6 +2559,7 @@ static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 blo
 #define K_LCP_RANGE(Q) (k_sa_binary<Q, BS_MLR, false, W, true>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
 #define K_STREE4X(Q) (k_sa_stree4x<Q, W>)
+#define K_STREE4X_LT(Q) (k_sa_stree4x<Q, W, true>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
     if (algo == SAS_ALGO_PLAIN && range) {
         QW_CASE(K_PLAIN_RANGE)
@@ -2532,6 +2575,11 @@ static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 blo
         // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
         if (qw == 1) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
         else { QW_CASE(K_STREE4X) }
+    } else if (algo == SAS_ALGO_STREE_LLCP) {
+        // the same descent, the LLCP tail (stree_tail) on one lane per query at every m: the
+        // tail's walk to its in-run mids diverges between queries, which a 4-lane group per
+        // query would pay 4 times over (m = 32: 1.77 ms cooperative)
+        QW_CASE(K_STREE4X_LT)
     } else {  // SAS_ALGO_SECTOR: positions come from the fused leaves, W = 4 only
         QW_CASE(K_SECTOR)
     }
@@ -2619,8 +2667,10 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
     const uint64_t lanes = a.nq * (coop ? QUAD_G : g);
-    // k_sa_binary (PLAIN / LCP / LLCP, any SA width) has its own workgroup shape
-    const bool bin = algo == SAS_ALGO_PLAIN || algo == SAS_ALGO_LCP || algo == SAS_ALGO_LLCP;
+    // k_sa_binary (PLAIN / LCP / LLCP, any SA width) and the S-tree kernels have their own
+    // workgroup shape
+    const bool bin = algo == SAS_ALGO_PLAIN || algo == SAS_ALGO_LCP || algo == SAS_ALGO_LLCP ||
+                     algo == SAS_ALGO_STREE || algo == SAS_ALGO_STREE_LLCP;
     const uint64_t bs = bin ? SAS_BIN_BLOCK : SEARCH_BLOCK;
     uint64_t blocks = (lanes + bs - 1) / bs;
     uint64_t cap = (uint64_t)x->num_cus * (bin ? SAS_BIN_BPC : BLOCKS_PER_CU);
@@ -2745,7 +2795,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
 // Algorithm / index / flag compatibility, shared by the search entry points.
 static int check_algo(const sas_index* x, int algo, uint32_t flags, const char* where) {
     const std::string w(where);
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_TAGGED) SAS_FAIL(EINVAL, w + ": unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_STREE_LLCP) SAS_FAIL(EINVAL, w + ": unknown algo");
     if ((flags & SAS_PREFIX_RANGE) &&
         (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP && algo != SAS_ALGO_INTERP)))
         SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP / INTERP on an index with SAS_BUILD_PREFIX");
@@ -2754,6 +2804,8 @@ static int check_algo(const sas_index* x, int algo, uint32_t flags, const char* 
     if ((algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE) && !x->quad_leaves)
         SAS_FAIL(EINVAL, w + ": SAS_ALGO_QUAD / SAS_ALGO_INLINE need SAS_BUILD_QUAD");
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, w + ": SAS_ALGO_STREE needs SAS_BUILD_STREE");
+    if (algo == SAS_ALGO_STREE_LLCP && (!x->stree || !x->llcp))
+        SAS_FAIL(EINVAL, w + ": SAS_ALGO_STREE_LLCP needs SAS_BUILD_STREE and SAS_BUILD_LLCP");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, w + ": SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
     if (algo == SAS_ALGO_TAGGED && !x->tag_table && !x->tag_lines)
         SAS_FAIL(EINVAL, w + ": SAS_ALGO_TAGGED needs SAS_BUILD_TAGGED");

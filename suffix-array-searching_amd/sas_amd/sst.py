@@ -67,10 +67,10 @@ class _Index:
         check(lib().sst_copy_nodes(self._h, out.ctypes.data, words))
         return out[:words]
 
-    def query(self, qs, want_rank: bool = False, stream=None, flags: int = 0):
+    def query(self, qs, want_rank: bool = False, stream=None, flags: int = 0, out=None):
         if _is_cuda(qs):
             import torch
-            out = torch.empty(qs.numel(), dtype=torch.int32, device=qs.device)
+            out = torch.empty(qs.numel(), dtype=torch.int32, device=qs.device) if out is None else out
             rank = torch.empty(qs.numel(), dtype=torch.int64, device=qs.device) if want_rank else None
             st = stream if stream is not None else torch.cuda.current_stream(qs.device).cuda_stream
             check(lib().sst_query(self._h, qs.data_ptr(), qs.numel(), out.data_ptr(),

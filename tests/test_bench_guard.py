@@ -202,10 +202,12 @@ def test_result_line_is_compact_and_complete():
     import json
     import os
     full = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_record_r3.json")))
-    full["lcp_long"] = {"summary": {"ms_plain_lcp_llcp": {f"{t}_m{m}": [4.1, 4.6, 3.1] for t in ("random", "repetitive")
-                                                          for m in (64, 128, 256)},
+    full["lcp_long"] = {"summary": {"ms": dict({f"{t}_m{m}": [4.1, 4.6, 3.1, 3.3, 2.2] for t in ("random", "repetitive")
+                                                for m in (64, 128, 256)}, algos=list(bench.LCP_LONG_ALGOS)),
                                     "skipping_beats_plain": ["llcp@random_m64:1.32x"] * 6}}
     full["detail"] = "gpurun_out/bench_detail.json"
+    full["configs"]["sst"] = _sst_record()
+    full["configs"]["c2"]["lcp_stree"] = dict(full["configs"]["c2"], algo="stree_llcp")
     line = bench.compact_line(full)
     text = json.dumps(line)
     assert len(text) <= bench.LINE_LIMIT < 8192, len(text)
@@ -221,8 +223,10 @@ def test_result_line_is_compact_and_complete():
         assert k in line["roofline"], k
     for k in ("value", "unit", "cores", "kind", "sample"):
         assert k in line["cpu_baseline"], k
-    for c in ("c0", "c1", "c2", "c3", "c4"):
+    for c in ("c0", "c1", "c2", "c3", "c4", "sst"):
         assert c in line["configs"], c
+    assert line["configs"]["c2"]["lcp_stree"]["algo"] == "stree_llcp"
+    assert set(line["configs"]["sst"]) >= {"best", "lookups_per_s", "kernel_ms", "frac", "traffic", "cpu"}
     for c in ("c1", "c2"):
         assert set(line["configs"][c]) >= {"lookups_per_s", "kernel_ms", "frac", "index_bytes"}
     assert "variants" not in line and "index" not in line
@@ -238,7 +242,60 @@ def test_every_headline_algo_has_a_workload_label():
     algos = [a.strip().strip('"') for a in choices.replace("\n", " ").split(",") if a.strip()]
     assert "plain" in algos and len(algos) >= 8
     st = {"top_levels": 15, "rel_levels": 27, "rel_bytes": bench.rel_bytes(27)}
-    assert "1-27" in bench.plain_label(st) and "24-27 from HBM" in bench.plain_label(st)
+    lab = bench.plain_label(st)
+    assert "levels 1-27 from 273 MiB" in lab and "levels 1-15 staged in LDS, levels 16-23 cache-resident, 24-27 from " \
+        "HBM; the rest" in lab, lab
+    assert "16-27 levels" not in lab
+    assert "levels 16-23 cache-resident, 24-31 from HBM" in bench.plain_label(
+        {"top_levels": 15, "rel_levels": 31, "rel_bytes": bench.rel_bytes(31)})
+    assert "levels 16-19 cache-resident;" in bench.plain_label(
+        {"top_levels": 15, "rel_levels": 19, "rel_bytes": bench.rel_bytes(19)})
+    assert "staged in LDS; the rest" in bench.plain_label({"top_levels": 15, "rel_levels": 15, "rel_bytes": 74272})
     for a in algos:
         if a != "plain":
             assert a in bench.WORKLOADS, a
+
+
+def _sst_record():
+    """A configs.sst record as bench.sst_record writes it (round 4's 2^28-key figures)."""
+    lay = {}
+    for name, ms, rq in (("SortedVec", 2.851, 13.0), ("STree16_left_max", 0.4641, 2.5),
+                         ("PartitionedSTree16M_b16", 0.4717, 2.4), ("PartitionedSTree16M_b20", 0.4983, 2.3),
+                         ("DirectMap", 0.24, 1.3)):
+        ks = ms * 1e-3
+        lay[name] = {"lookups_per_s": 1e7 / ks, "kernel_ms": ms, "kernel_ms_median": ms, "index_bytes": 1 << 30,
+                     "equals_sortedvec": True, "requests_per_lookup": rq, "traffic": rq * 128 + 4,
+                     "req_frac": rq * 1e7 / ks / bench.CACHE_REQ_CEILING,
+                     "frac_hbm": (rq * 128 + 4) * 1e7 / ks / 1e9 / bench.HBM_PEAK_GBPS}
+    return {"best": "DirectMap", "layouts": lay, "keys": 1 << 28, "queries": 10_000_000,
+            "cpu_baseline": {"value": 2.48e8, "cores": 16, "unit": "lookups/s", "kind": "port"}}
+
+
+def test_line_fractions_are_physical():
+    """Every roofline fraction the line prints is a fraction of a physical ceiling (0 < frac
+    <= 1): the headline's HBM-served bytes over 8 TB/s, each config's PMC request floor (or
+    HBM-served bytes without a same-hash PMC pass), the u32 path's request rate over the
+    measured random-request ceiling.  SURVEY 8(d)'s worst-case byte model, which passes 1 where
+    pivot levels never reach HBM, is printed only as frac_8d_model."""
+    import json
+    import os
+    full = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_record_r3.json")))
+    full["configs"]["sst"] = _sst_record()
+    # round 4's c1: 8(d) model 1.02 at 1.423 ms, request floor 1.00
+    line = bench.compact_line(full)
+    assert 0 < line["roofline"]["frac"] <= 1
+    for k, c in line["configs"].items():
+        if "frac" in c and c["frac"] is not None:
+            assert 0 < c["frac"] <= 1, (k, c["frac"])
+    for k in ("c1", "c2"):
+        c = line["configs"][k]
+        assert c["frac_basis"] in ("req", "hbm")
+        assert c["frac"] == (c["req_frac"] if c["frac_basis"] == "req" else c["frac_hbm"])
+        assert "frac_8d_model" in c
+    # a deep-pivot PLAIN whose model passes 1 keeps its model out of `frac`
+    rec = dict(full["configs"]["c1"], kernel_lookups_per_s=1e7 / 1.244e-3,
+               bytes_per_lookup=dict(full["configs"]["c1"]["bytes_per_lookup"], section_8d=1156.0))
+    cs = bench.config_summary(rec)
+    assert cs["frac_8d_model"] > 1 and cs["frac"] <= 1
+    assert line["configs"]["sst"]["frac"] <= 1 and line["configs"]["sst"]["best"] == "DirectMap"
+    assert 0 < line["configs"]["sst"]["stree16_left_max_frac"] <= 1

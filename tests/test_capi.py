@@ -108,7 +108,7 @@ def test_flag_and_algo_mirror_matches_header():
     assert len(defs) >= 15
     for name, bit in defs.items():
         assert getattr(_lib, name) == 1 << int(bit), name
-    enum = dict(re.findall(r"SAS_ALGO_([A-Z]+)\s*=\s*(\d+)", hdr))
+    enum = dict(re.findall(r"SAS_ALGO_([A-Z_]+)\s*=\s*(\d+)", hdr))
     assert {k.lower(): int(v) for k, v in enum.items()} == _lib.ALGOS
     assert _lib.SAS_BUILD_PREFIX_P(17) == 17 << 16
 

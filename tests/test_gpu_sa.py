@@ -19,7 +19,7 @@ from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix", "interp")
+ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix", "interp", "stree_llcp")
 
 
 @pytest.fixture(scope="module")
@@ -739,7 +739,7 @@ def test_sa_beyond_u32(sas):
     idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True, llcp=False)  # LLCP: the second index below
     st = idx.stats()
     assert st["sa_width"] == 5 and st["n"] == n
-    algos = [a for a in ALGOS if a not in ("llcp", "prefix", "interp")]  # prefix: u32 ranks; interp: n < 2^32
+    algos = [a for a in ALGOS if a not in ("llcp", "prefix", "interp", "stree_llcp")]  # prefix: u32 ranks; interp: n < 2^32
     ht = t.cpu().numpy()
     del t
     torch.cuda.empty_cache()
@@ -1134,7 +1134,7 @@ def test_rel_pivot_blocks(sas):
     texts = {"planted": planted, "period_9": np.tile(rng.integers(0, 4, 9, dtype=np.uint8), (1 << 17) // 9 + 5)}
     for name, t in texts.items():
         n = len(t)
-        idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False)
+        idx = sas.SaNaive.build(t, lcp=True, stree=True, sector=False, quad=True, llcp=True, prefix=False)
         st = idx.stats()
         assert st["rel_levels"] == bench.rel_levels(st["iterations"], 27) and st["rel_bytes"] > 0, name
         sa = idx.suffix_array()
@@ -1161,10 +1161,11 @@ def test_rel_pivot_blocks(sas):
         assert np.array_equal(pr, pr0), name
         # LCP / LLCP take exact lcps off the same keys (a key below q that may end in padding
         # reads the whole entry); INLINE decides on them with the sector predicate
-        for algo in ("lcp", "llcp", "inline"):
+        # STREE_LLCP: the S-tree's run of equal 16-char keys, then LLCP over it (long runs here)
+        for algo in ("lcp", "llcp", "inline", "stree_llcp"):
             ga, pa = idx.search_batch(buf, qo, ql, algo=algo, probes=True)
             bad = np.nonzero(ga != expect)[0]
             assert len(bad) == 0, (name, algo, bad[:5], [qs[i] for i in bad[:2]])
-            if algo != "inline":
+            if algo in ("lcp", "llcp"):
                 assert np.array_equal(pa, pr), (name, algo)
         idx.free()

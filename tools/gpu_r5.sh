@@ -7,6 +7,9 @@
 #   abbin    tools/ab_bin.py over the tree and the tools/_var_* builds named in AB_VARS
 #   kt       the bench under rocprofv3 --kernel-trace --stats, by grid (tools/prof_r4.sh)
 #   c4:W:g   tools/c4_part_probe.py W g (part g of W at the bench's share for W ranks)
+#   sa       tests/test_gpu_sa.py only      lcp    the c1/c2 lineup + lcp_long + sst (no c3/c4/CPU/e2e)
+#   randcal  tools/pmc_randbench.sh (random-read counter calibration)
+#   pmc:k1,k2  tools/pmc_r5.sh k1 k2 (PMC / SQ passes)
 set -o pipefail
 out=gpurun_out/$1
 shift
@@ -18,6 +21,12 @@ for s in "$@"; do
                    > "$out/gputest.log" 2>&1 || exit $? ;;
         shard) timeout -k 10 900 python -u -m pytest tests/test_gpu_shard.py -m gpu -x -v --timeout 600 \
                    --timeout-method thread > "$out/shard.log" 2>&1 || exit $? ;;
+        sa) timeout -k 10 900 python -u -m pytest tests/test_gpu_sa.py -m gpu -x -v --timeout 600 \
+                   --timeout-method thread > "$out/sa.log" 2>&1 || exit $? ;;
+        lcp) timeout -k 10 600 python -u bench.py --no-c3 --no-c4 --no-cpu --no-e2e \
+                   --detail "$out/lcp_detail.json" > "$out/lcp.json" 2> "$out/lcp.err" || exit $? ;;
+        randcal) bash tools/pmc_randbench.sh "$out/randcal" > "$out/randcal.log" 2>&1 || exit $? ;;
+        pmc:*) bash tools/pmc_r5.sh $(echo "${s#pmc:}" | tr , " ") > "$out/pmc.log" 2>&1 || exit $? ;;
         smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$out/smoke.log" 2>&1 || exit $? ;;
         bench) timeout -k 10 900 python -u bench.py --detail "$out/bench_detail.json" > "$out/bench.json" \
                    2> "$out/bench.err" || exit $? ;;
