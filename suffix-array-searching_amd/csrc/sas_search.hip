@@ -51,6 +51,10 @@
 #define SAS_BIN_BPC 2
 #endif
 #define SAS_BIN_WAVES (SAS_BIN_BLOCK * SAS_BIN_BPC / 256)
+// STREE at m <= 32: one lane per query (k_sa_stree4x) instead of a 4-lane group (A/B hook)
+#ifndef SAS_STREE_PERLANE
+#define SAS_STREE_PERLANE 0
+#endif
 
 struct SearchArgs {
     const uint64_t* tw;
@@ -2573,7 +2577,7 @@ static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 blo
         if (top) { QW_CASE(K_LLCP_TOP) } else { QW_CASE(K_LLCP) }
     } else if (algo == SAS_ALGO_STREE) {
         // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
-        if (qw == 1) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
+        if (qw == 1 && !SAS_STREE_PERLANE) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
         else { QW_CASE(K_STREE4X) }
     } else if (algo == SAS_ALGO_STREE_LLCP) {
         // the same descent, the LLCP tail (stree_tail) on one lane per query at every m: the
@@ -2663,7 +2667,7 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     // PLAIN, LLCP and INLINE read the pivot levels past the LDS ones from the prefix-relative
     // blocks, which the build makes wherever the array has such levels
-    const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_STREE) && qw == 1;
+    const bool coop = (algo == SAS_ALGO_QUAD || (algo == SAS_ALGO_STREE && !SAS_STREE_PERLANE)) && qw == 1;
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
     const uint64_t lanes = a.nq * (coop ? QUAD_G : g);

@@ -1169,3 +1169,34 @@ def test_rel_pivot_blocks(sas):
             if algo in ("lcp", "llcp"):
                 assert np.array_equal(pa, pr), (name, algo)
         idx.free()
+
+
+def test_plain_sa_run_at_array_end(sas):
+    """PLAIN over a u32 SA loads the 16-B chunks covering its last <= 8 ranks at once; with
+    sa_n % 4 != 0 the chunk of rank sa_n - 1 runs past the SA's last word, so the build pads
+    the u32 SA (whole and shard copies) to a 16-B multiple (round 5).  Queries
+    whose lower bound lies in the last ranks, or past them (sentinel n), on texts of every
+    n % 4 and on shards whose rank count is not a multiple of 4: positions equal the oracle's."""
+    rng = np.random.default_rng(77)
+    for n in (4099, 4101, 4102, 65537, 65538, 65539):
+        t = rng.integers(0, 4, n, dtype=np.uint8)
+        t[-40:] = 3  # the largest suffixes: a run of 3s at the end
+        sa = O.build_sa(t)
+        qs = [np.full(k, 3, np.uint8) for k in range(1, 45)]  # near and past the top of the SA
+        qs += [np.concatenate([np.full(k, 3, np.uint8), [j]]).astype(np.uint8) for k in (5, 20, 39) for j in range(4)]
+        qs += [t[o:o + 32] for o in rng.integers(0, n - 32, 500)]
+        buf, off, lens = pack(qs)
+        expect = oracle_positions(t, sa, buf[:-64], off, lens)
+        whole = sas.SaNaive.build(t, lcp=False, stree=False, sector=False, quad=False, llcp=False, prefix=False)
+        assert whole.stats()["sa_width"] == 4
+        assert np.array_equal(whole.search_batch(buf, off, lens, algo="plain"), expect), n
+        # a shard of the top ranks, its rank count not a multiple of 4
+        lo = n - (n // 3) - (n % 4 == 0)
+        shard = sas.SaNaive.build(t, sa=sa, rank_range=(lo, n), lcp=False, stree=False, sector=False, quad=False,
+                                  llcp=False, prefix=False)
+        got = shard.search_batch(buf, off, lens, algo="plain")
+        # queries whose global lower bound lies in the shard (rank >= lo) get the same answer
+        rank_of = {int(p): r for r, p in enumerate(sa)}
+        rk = np.array([rank_of.get(int(p), n) for p in expect])
+        sel = rk > lo
+        assert np.array_equal(got[sel], expect[sel]), n

@@ -40,8 +40,10 @@ for m in sorted({int(m) for _, m in cases}):
     src = torch.from_numpy(off.astype(np.int64)).cuda()
     qs[m] = t[(src[:, None] + torch.arange(m, device="cuda")[None, :]).reshape(-1)].contiguous()
 need_llcp = any(a == "llcp" for a, _ in cases)
-need_quad = any(a == "inline" for a, _ in cases)
-idx = {p: mods[p].SaNaive.build(t, lcp=True, stree=False, sector=False, quad=need_quad, llcp=need_llcp,
+need_llcp = need_llcp or any(a == "stree_llcp" for a, _ in cases)
+need_quad = any(a in ("inline", "quad") for a, _ in cases)
+need_stree = any(a.startswith("stree") for a, _ in cases)
+idx = {p: mods[p].SaNaive.build(t, lcp=True, stree=need_stree, sector=False, quad=need_quad, llcp=need_llcp,
                                  prefix=False) for p in pkgs}
 out = torch.empty(nq, dtype=torch.int64, device="cuda")
 res = {p: {"source_hash": mods[p].source_hash()} for p in pkgs}
