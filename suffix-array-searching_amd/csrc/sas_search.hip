@@ -215,6 +215,12 @@ static_assert(SAS_PLAIN_SA_RUN == 0 || SAS_PLAIN_SA_RUN == 4 || SAS_PLAIN_SA_RUN
 #define BS_PLAIN 0
 #define BS_MLR 1
 #define BS_LLCP 2
+// LLCP: a range of at most this many ranks (0: off, 2..4) has its 16-B entries loaded together
+// (consecutive ranks: one or two lines) for the remaining probes (A/B hook)
+#ifndef SAS_LLCP_RUN
+#define SAS_LLCP_RUN 0
+#endif
+static_assert(SAS_LLCP_RUN == 0 || (SAS_LLCP_RUN >= 2 && SAS_LLCP_RUN <= 4), "SAS_LLCP_RUN: 0 or 2..4");
 // The rel blocks' LDS groups (common.hpp RelLayout) into a workgroup's LDS: 16-B copies
 __device__ __forceinline__ void stage_rel(uint4* s, const uint8_t* __restrict__ rel, uint32_t bytes) {
     const uint4* src = reinterpret_cast<const uint4*>(rel);
@@ -336,8 +342,9 @@ __global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_binary(Sear
             }
         }
         bool run = false;  // PLAIN, u32 SA: the range's SA words are in sc0..sc2 (from rank rb)
-        uint32_t rb = 0;
-        uint4 sc0 = make_uint4(0, 0, 0, 0), sc1 = sc0, sc2 = sc0;
+        uint32_t rb = 0;   // LLCP (SAS_LLCP_RUN): the range's entries are in sc0..sc3 (from rank rl)
+        uint4 sc0 = make_uint4(0, 0, 0, 0), sc1 = sc0, sc2 = sc0, sc3 = sc0;
+        rank_t rl = 0;
         for (; it < a.iters; ++it) {
             if (l < r) {
                 const rank_t mid = (rank_t)(((uint64_t)l + r) >> 1);
@@ -352,7 +359,26 @@ __global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_binary(Sear
                     // pivot on L's side of q (< q, same lcp), Llcp < llcp on R's side
                     // (> q, lcp = Llcp); symmetric with Rlcp.  A tie (or a capped value)
                     // compares from the known lcp, first against the inlined chars.
-                    const uint4 e = a.llcp[mid];
+                    uint4 e;
+                    if (SAS_LLCP_RUN) {
+                        if (!run && r - l <= SAS_LLCP_RUN) {
+                            run = true;
+                            rl = l;
+                            const uint4* c = a.llcp + l;  // consecutive 16-B entries: one or two lines
+                            sc0 = c[0];
+                            if (r - l > 1) sc1 = c[1];
+                            if (SAS_LLCP_RUN > 2 && r - l > 2) sc2 = c[2];
+                            if (SAS_LLCP_RUN > 3 && r - l > 3) sc3 = c[3];
+                        }
+                        if (run) {
+                            const uint32_t o = (uint32_t)(mid - rl);
+                            e = o == 0 ? sc0 : o == 1 ? sc1 : (SAS_LLCP_RUN > 3 && o == 3) ? sc3 : sc2;
+                        } else {
+                            e = a.llcp[mid];
+                        }
+                    } else {
+                        e = a.llcp[mid];
+                    }
                     p = (sa_val_t<W>)((uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32));
                     const uint32_t x = (e.y >> 8) & SAS_LLCP_CAP, y = e.y >> 20;
                     uint32_t hh = 0, inl = 0;

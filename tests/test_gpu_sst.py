@@ -91,6 +91,36 @@ def test_differential(sas, size):
         assert np.array_equal(v, ref) and np.array_equal(r, ref_rank), (size, b)
 
 
+@pytest.mark.parametrize("size", [(1 << 23) * 7 // 4, 1 << 24, (1 << 25) * 5 // 4, (1 << 26) * 3 // 2, 1 << 26])
+def test_differential_to_reference_max_size(sas, size):
+    """The reference's sweep runs to 2^26 bytes (sst/test.rs:146-153); past the sizes whose
+    layouts are compared word for word with the oracle above, every GPU layout of the lineup
+    (SortedVec, Eytzinger, STree16/15 with left_max, PartitionedSTree16M at the test's largest b,
+    every other PartitionedSTree16 marker, DirectMap) returns SortedVec::binary_search's values
+    (ranks for SortedVec / DirectMap) on 1024 uniform and 1024 positive queries."""
+    rng = np.random.default_rng(size)
+    vals = gen_vals(size // 4, rng)
+    qs = np.concatenate([rng.integers(0, O.MAX, 1024, dtype=np.uint64).astype(np.uint32),
+                         vals[rng.integers(0, len(vals), 1024)]])
+    ref_rank = np.searchsorted(vals, qs, "left")
+    ref = np.where(ref_rank < len(vals), vals[np.minimum(ref_rank, len(vals) - 1)], np.uint32(O.MAX))
+    v, r = sas.SortedVec.new(vals).query(qs, want_rank=True)
+    assert np.array_equal(v, ref) and np.array_equal(r, ref_rank)
+    builders = [sas.Eytzinger.new, sas.STree16.new, sas.STree15.new,
+                lambda v_: sas.STree16.new_params(v_, True, False, False),
+                lambda v_: sas.STree15.new_params(v_, True, False, True),
+                lambda v_: sas.PartitionedSTree16M.new(v_, 20)]
+    builders += [lambda v_, c=c: c.new(v_, 16) for c in (sas.PartitionedSTree16, sas.PartitionedSTree16C,
+                                                          sas.PartitionedSTree16L, sas.PartitionedSTree16O)]
+    for mk in builders:
+        idx = mk(vals)
+        assert np.array_equal(idx.query(qs), ref), (size, idx.__class__.__name__)
+        idx.free()
+    dm = sas.DirectMap.new(vals)
+    v, r = dm.query(qs, want_rank=True)
+    assert np.array_equal(v, ref) and np.array_equal(r, ref_rank), size
+
+
 def test_direct_map_edges(sas):
     """SST_DIRECT_MAP on clustered keys (huge empty bucket runs: the gap list), runs of
     equal keys longer than the three inlined ones (the fallback search), queries above
