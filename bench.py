@@ -124,6 +124,11 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         # then per probe: SA word + text window (PLAIN / LCP, two requests) or one 16-B entry
         # (INLINE / LLCP, one request); a lookup decided by keys alone reads SA[r] at the end
         per, rq = (sa_w + win, 2) if algo in ("plain", "lcp") else (16, 1)
+        # PLAIN over a u32 SA: once the range holds <= 8 ranks (SAS_PLAIN_SA_RUN) their SA words
+        # come in one 32-B run (one request), so each later probe reads its text window only
+        run = algo == "plain" and sa_w == 4
+        if run:
+            per, rq = win, 1
         R = st.get("rel_levels") or 0
         rc = rh = 0.0
         for d0, h, where in rel_groups(R):
@@ -139,9 +144,11 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
                 hbm += bb
                 rh += 1
         hbm += max(0.0, probes - R) * per
+        srun = 1.0 if run and probes > R else 0.0  # the SA run: 32 B, one request
+        hbm += srun * 32
         fin = 1.0 if probes <= R else 0.0
         hbm += fin * (sa_w if algo in ("plain", "lcp") else 16)
-        reqs = {"cache": rc, "hbm": rh + max(0.0, probes - R) * rq + fin + (8.0 if packed else m) / 128}
+        reqs = {"cache": rc, "hbm": rh + max(0.0, probes - R) * rq + srun + fin + (8.0 if packed else m) / 128}
     elif algo == "interp":
         hbm += probes * 16
     elif algo in ("stree", "stree_llcp", "quad", "sector"):

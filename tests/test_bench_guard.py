@@ -66,12 +66,15 @@ def test_byte_model_splits_served_levels():
     # quad at 2^30: 3 LDS layers, the 206 KB / 3.5 MB / 59 MB layers in cache, 1 GB + leaves in HBM
     assert q["lds"] == 3 * 64 and q["cache"] == 3 * 64 and q["hbm"] == 2 * 64 + m + 8
     # PLAIN: prefix-relative blocks, levels 1-15 from LDS (3 blocks of 32 B, one of 16 B), 16-27
-    # in 3 requests (16-19 and 20-23 cache-resident, 24-27 past the cache's 256 MiB), then SA word
-    # + text window per probe
+    # in 3 requests (16-19 and 20-23 cache-resident, 24-27 past the cache's 256 MiB), then the
+    # SA run of the last <= 8 ranks (32 B, one request) and a text window per probe
     st27 = dict(st, top2_levels=27, rel_levels=27, rel_bytes=bench.rel_bytes(27))
     p = bench.bytes_per_lookup("plain", st27, n, m, 31.0)
-    assert p["lds"] == 3 * 32 + 16 and p["cache"] == 2 * 32 and p["hbm"] == 32 + 4 * (4 + m / 4) + m + 8
-    assert p["requests_model"] == {"cache": 2.0, "hbm": 1 + 4 * 2 + m / 128}
+    assert p["lds"] == 3 * 32 + 16 and p["cache"] == 2 * 32 and p["hbm"] == 32 + 4 * (m / 4) + 32 + m + 8
+    assert p["requests_model"] == {"cache": 2.0, "hbm": 1 + 4 + 1 + m / 128}
+    # mlr LCP has no SA run: SA word + text window per probe
+    lc = bench.bytes_per_lookup("lcp", st27, n, m, 31.0)
+    assert lc["hbm"] == 32 + 4 * (4 + m / 4) + m + 8 and lc["requests_model"]["hbm"] == 1 + 4 * 2 + m / 128
     # LLCP: the same pivots (exact lcps off the keys), then one 16-B entry per probe
     ll = bench.bytes_per_lookup("llcp", st27, n, m, 31.0)
     assert ll["lds"] == 3 * 32 + 16 and ll["cache"] == 2 * 32 and ll["hbm"] == 32 + 4 * 16 + m + 8
@@ -107,11 +110,11 @@ def test_byte_model_hbm_pivot_levels():
     # the split: model HBM requests first, the rest of the PMC count is cache-served
     bpl = bench.bytes_per_lookup("plain", dict(st, top2_levels=23, rel_levels=23, rel_bytes=bench.rel_bytes(23)),
                                  n, m, 31.0)
-    assert bpl["requests_model"]["hbm"] == 8 * 2 + m / 128
+    assert bpl["requests_model"]["hbm"] == 8 + 1 + m / 128
     nq, kms = 10_000_000, 5.0
     sp = bench.request_split(bpl, {"rdreq_per_launch": 20.0 * nq}, nq, kms)
-    assert abs(sp["hbm_per_lookup"] - 16.25) < 1e-9 and abs(sp["cache_per_lookup"] - 3.75) < 1e-9
-    floor = max(nq * 16.25 / bench.RANDOM_REQ_CEILING, nq * 20.0 / bench.CACHE_REQ_CEILING)
+    assert abs(sp["hbm_per_lookup"] - 9.25) < 1e-9 and abs(sp["cache_per_lookup"] - 10.75) < 1e-9
+    floor = max(nq * 9.25 / bench.RANDOM_REQ_CEILING, nq * 20.0 / bench.CACHE_REQ_CEILING)
     assert abs(sp["frac"] - floor / (kms * 1e-3)) < 1e-12 and sp["frac"] < 1
     # round 3's measured PLAIN (23 levels): 22.74 requests at 4.089 ms per 10^7 is under both limits
     sp = bench.request_split(bpl, {"rdreq_per_launch": 22.74 * nq}, nq, 4.089)
@@ -299,3 +302,15 @@ def test_line_fractions_are_physical():
     assert cs["frac_8d_model"] > 1 and cs["frac"] <= 1
     assert line["configs"]["sst"]["frac"] <= 1 and line["configs"]["sst"]["best"] == "DirectMap"
     assert 0 < line["configs"]["sst"]["stree16_left_max_frac"] <= 1
+
+
+def test_c1_request_floor_of_round5_plain():
+    """Round 5's PLAIN (27 pivot levels, u32 SA): 7.199 PMC requests per lookup at 1.323 ms per
+    10^7.  With its SA run in the model (one request for the last <= 8 ranks' SA words) the DRAM
+    share is 6.25 requests, under the total, and the request floor stays a fraction (the model
+    without the run counted 9.25 DRAM requests and put the floor above the measured time)."""
+    st = {"sa_width": 4, "top_levels": 15, "top2_levels": 27, "rel_levels": 27, "rel_bytes": bench.rel_bytes(27)}
+    n, m, nq = 1 << 30, 32, 10_000_000
+    bpl = bench.bytes_per_lookup("plain", st, n, m, 31.0)
+    sp = bench.request_split(bpl, {"rdreq_per_launch": 7.199 * nq}, nq, 1.323)
+    assert sp["hbm_per_lookup"] == 6.25 and 0.9 < sp["frac"] <= 1, sp

@@ -27,7 +27,7 @@ for k in $keys; do
     plain)   args="$base --algo plain"; kern=k_sa_binary; nq=10000000; name=plain_n1073741824_q10000000_m32_t27 ;;
     quad)    args="$base --algo quad"; kern=k_sa_quad; nq=10000000; name=quad_n1073741824_q10000000_m32 ;;
     stree)   args="$base --algo stree"; kern=k_sa_stree; nq=10000000; name=stree_n1073741824_q10000000_m32 ;;
-    stree_llcp) args="$base --algo stree_llcp"; kern=k_sa_stree; nq=10000000; name=stree_llcp_n1073741824_q10000000_m32 ;;
+    stree_llcp) args="$base --algo stree_llcp"; kern=k_sa_stree4x; nq=10000000; name=stree_llcp_n1073741824_q10000000_m32 ;;
     sector)  args="$base --algo sector"; kern=k_sa_sector; nq=10000000; name=sector_n1073741824_q10000000_m32 ;;
     llcp)    args="$base --algo llcp"; kern=k_sa_binary; nq=10000000; name=llcp_n1073741824_q10000000_m32 ;;
     c3)      args="--workload c3 --c3-steps 2 --warmup 1 --c3-no-cross --detail="; kern=k_sa_tagged_lines; nq=100000000; name=c3_tagged_lines_n17179869184_q100000000 ;;
