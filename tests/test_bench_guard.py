@@ -133,7 +133,8 @@ def test_pmc_attached_only_for_the_same_source_hash(tmp_path, monkeypatch):
     import sas_amd
     prof = tmp_path / "profiles"
     prof.mkdir()
-    monkeypatch.setattr(bench, "REPO", str(tmp_path))
+    import benchlib.common
+    monkeypatch.setattr(benchlib.common, "REPO", str(tmp_path))
     json.dump({"hbm_bytes_per_launch": 1e9, "TCC_EA0_RDREQ": 1e7, "source_hash": sas_amd.source_hash()},
               open(prof / "pmc_same.json", "w"))
     json.dump({"hbm_bytes_per_launch": 1e9, "TCC_EA0_RDREQ": 1e7, "source_hash": "0000000000000000"},
