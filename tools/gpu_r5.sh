@@ -35,6 +35,7 @@ for s in "$@"; do
         abbin) AB_PKGS="tree${AB_VARS:+:}${AB_VARS}" timeout -k 10 500 python3 -u tools/ab_bin.py > "$out/ab_bin.json" \
                    2> "$out/ab_bin.err" || exit $? ;;
         kt) bash tools/prof_r5.sh "$out/prof" > "$out/prof.log" 2>&1 || exit $? ;;
+        kt34) bash tools/prof_r5_c34.sh "$out/prof34" > "$out/prof34.log" 2>&1 || exit $? ;;
         c4:*) IFS=: read -r _ W g <<< "$s"
               timeout -k 10 400 python3 -u tools/c4_part_probe.py "$W" "$g" > "$out/c4probe_${W}_${g}.json" \
                   2> "$out/c4probe_${W}_${g}.err" || exit $? ;;
