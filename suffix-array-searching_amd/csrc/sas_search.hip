@@ -1670,96 +1670,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     if (bad) atomicOr(a.bad, 1u);
 }
 
-// The headline shape of k_sa_prefix2 (two-slot entries, fixed 32-char queries on 16-B
-// aligned device bytes, no probes) with U queries per lane pair in flight: each iteration
-// loads U queries (prefetched one iteration ahead), issues their U entry reads back to back,
-// then finishes them in turn.  A wave so keeps U x 32 entry requests outstanding where
-// k_sa_prefix2 keeps 32 (SAS_PREFIX_UNROLL, A/B hook).
-#ifndef SAS_PREFIX_UNROLL
-#define SAS_PREFIX_UNROLL 1
-#endif
-template <int U, bool HI40>
-__global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2u(SearchArgs a) {
-    constexpr int G = 2;
-    uint32_t bad = 0;
-    const uint32_t sh = 64 - 2 * a.prefix_chars;
-    const uint64_t sa_n = a.sa_n, nq = a.nq;
-    const uint32_t sub = threadIdx.x & 1u;
-    const int lane0 = (int)((threadIdx.x & 63) & ~1u);
-    const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
-    const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / G;
-    auto qload = [&](uint64_t k) -> uint4 {
-        const uint4* p = reinterpret_cast<const uint4*>(a.qbytes + k * 32) + sub;
-        return SAS_QUAD_NT_IO ? nt_load4(p) : *p;
-    };
-    const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
-    uint4 vn[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) vn[u] = i0 + u * stride < nq ? qload(i0 + u * stride) : make_uint4(0, 0, 0, 0);
-    for (uint64_t base = i0; base < nq; base += U * stride) {
-        uint64_t K64[U], K[U];
-        uint4 e[U];
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint4 v = vn[u];
-            const uint64_t nx = base + (U + u) * stride;
-            if (nx < nq) vn[u] = qload(nx);
-            bad |= (v.x | v.y | v.z | v.w) & 0xFCFCFCFCu;
-            const uint32_t part = (pack4(v.x) << 24) | (pack4(v.y) << 16) | (pack4(v.z) << 8) | pack4(v.w);
-            const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)part, 0xB1, 0xF, 0xF, false);
-            K64[u] = sub ? (((uint64_t)other << 32) | part) : (((uint64_t)part << 32) | other);
-            K[u] = pt_slot(a, K64[u] >> sh);
-        }
-#pragma unroll
-        for (int u = 0; u < U; u++)  // the U entry reads back to back (pair-uniform guards)
-            e[u] = base + u * stride < nq ? (SAS_PREFIX_NT ? nt_load4(pt + G * K[u] + sub) : pt[G * K[u] + sub])
-                                          : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int u = 0; u < U; u++) {
-            const uint64_t i = base + u * stride;
-            if (i >= nq) break;  // pair-uniform
-            QueryRegs<1> q;
-            q.bytes = a.qbytes + i * 32;
-            q.m = 32;
-            q.w[0] = K64[u];
-            const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e[u].z, lane0 + 1, 64) : 0u;
-            const uint64_t r0 = (uint64_t)(uint32_t)__shfl((int)e[u].z, lane0, 64) |
-                                (HI40 ? (uint64_t)((hb >> 16) & 0xFFu) << 32 : 0ull);
-            const uint64_t rank = r0 + sub;
-            const uint64_t pe = HI40 ? ((uint64_t)e[u].w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32))
-                                     : (uint64_t)e[u].w;
-            const bool ok = rank >= sa_n || sector_ge<1>((uint64_t)e[u].x | ((uint64_t)e[u].y << 32), pe, K64[u], a, q);
-            const uint32_t grp = (uint32_t)(__ballot(ok) >> lane0) & 3u;
-            const uint32_t j = grp ? (uint32_t)__builtin_ctz(grp) : 0u;
-            const uint32_t pw = (uint32_t)__shfl((int)e[u].w, lane0 + (int)j, 64);
-            uint64_t pos;
-            if (grp) {
-                const uint64_t ans = r0 + j;
-                pos = ans >= sa_n ? a.next_pos
-                                  : (HI40 ? ((uint64_t)pw | ((uint64_t)((hb >> (8 * j)) & 0xFFu) << 32)) : pw);
-            } else {
-                uint64_t lo = r0 + G, hi = pt_rank<G, HI40>(pt, K[u] + 1), pr = QUAD_NO_SA;
-                while (lo < hi) {
-                    const uint64_t mid = (lo + hi) >> 1;
-                    const uint4 f = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
-                    const uint64_t pp = (uint64_t)f.z | ((uint64_t)(f.w & 0xFFu) << 32);
-                    if (sector_ge<1>((uint64_t)f.x | ((uint64_t)f.y << 32), pp, K64[u], a, q)) {
-                        hi = mid;
-                        pr = pp;
-                    } else {
-                        lo = mid + 1;
-                    }
-                }
-                if (lo >= sa_n) pos = a.next_pos;
-                else if (pr != QUAD_NO_SA) pos = pr;
-                else pos = quad_entry_sa<false, 4>(a, lo);
-            }
-            if (sub == 0) a.out_pos[i] = pos;
-        }
-    }
-    if (bad) atomicOr(a.bad, 1u);
-}
-
 // Occurrence ranges from the prefix table (any entry format; Search::search_prefix,
 // sas/util.rs:36-46): lo = the lower bound, bisected in [table[K], table[K+1]]; hi = the
 // first suffix whose first min(m, len) chars are > q, bisected in the range of the
@@ -2734,13 +2644,6 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
     } else if (algo == SAS_ALGO_PREFIX) {
         if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) }
         else if (a.prefix_w == 16 && !KO) { QW_CASE(K_PREFIX16) }
-        else if (SAS_PREFIX_UNROLL > 1 && a.prefix_w == 32 && !KO && qw == 1 && a.qoff == nullptr &&
-                 a.qwords == nullptr && a.bcounts == nullptr && a.out_probes == nullptr && a.m_fixed == 32 &&
-                 (((uintptr_t)a.qbytes) & 15) == 0) {
-            // the headline shape, U queries per lane pair in flight
-            if (a.prefix_hi40) hipLaunchKernelGGL((k_sa_prefix2u<SAS_PREFIX_UNROLL, true>), grid, block, 0, st, a);
-            else hipLaunchKernelGGL((k_sa_prefix2u<SAS_PREFIX_UNROLL, false>), grid, block, 0, st, a);
-        }
         else if (a.prefix_w == 32 && !KO && a.prefix_hi40) { QW_CASE(K_PREFIX2H) }
         else if (a.prefix_w == 64 && !KO && a.prefix_hi40) { QW_CASE(K_PREFIX4H) }
         else if (a.prefix_w == 32 && !KO) { QW_CASE(K_PREFIX2) }
