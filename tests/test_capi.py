@@ -135,3 +135,20 @@ def test_rust_stats_mirror_matches_header():
     rs = rs[:rs.index("\n}")]
     rust_fields = re.findall(r"pub (\w+): u(32|64)", rs)
     assert [(w, f) for f, w in rust_fields] == c_fields
+
+
+def test_pmc_summaries_match_the_built_library():
+    """Every committed PMC summary the bench attaches (profiles/pmc_*.json) was collected on the
+    library this tree builds: a kernel edit after the PMC sweep would leave the line's traffic
+    and request fractions stale (the bench reports them as `stale` and drops them)."""
+    import glob
+    import json
+    root = os.path.join(os.path.dirname(_lib.LIB_PATH), "..")
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.skip("libsas_amd.so not built")
+    import sas_amd
+    h = sas_amd.source_hash()
+    files = glob.glob(os.path.join(root, "profiles", "pmc_*.json"))
+    assert files
+    stale = [os.path.basename(f) for f in files if json.load(open(f)).get("source_hash") != h]
+    assert not stale, (h, stale)
