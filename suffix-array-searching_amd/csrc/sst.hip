@@ -13,6 +13,40 @@
 #include <vector>
 
 #define SST_BLOCK 1024
+// query stream of the u32 kernels: the next query of this lane (group) is loaded while the
+// current one's nodes are in flight (SST_QPREFETCH), and the query and answer streams can
+// bypass L2 (SST_NT_IO: non-temporal loads and stores).  Same-box A/B at 2^28 keys, 10^7
+// queries (tools/ab_sst_var.py, profiles/r5/ab_sst_prefetch/): prefetch takes DirectMap from
+// 0.239 to 0.208 ms (its one entry read no longer waits behind the query's round trip) and
+// leaves the S-trees and SortedVec within 0.3%; NT I/O gains nothing beside it (0.215 ms).
+#ifndef SST_QPREFETCH
+#define SST_QPREFETCH 1
+#endif
+#ifndef SST_NT_IO
+#define SST_NT_IO 0
+#endif
+__device__ __forceinline__ uint32_t sst_qload(const uint32_t* qs, uint64_t i) {
+    return SST_NT_IO ? __builtin_nontemporal_load(qs + i) : qs[i];
+}
+__device__ __forceinline__ void sst_out(uint32_t* out, uint64_t i, uint32_t v) {
+    if (SST_NT_IO) __builtin_nontemporal_store(v, out + i);
+    else out[i] = v;
+}
+// the query stream of one lane (group): get(i) returns query i; with SST_QPREFETCH query
+// i + stride is loaded then, so the next iteration does not start with a dependent round trip
+struct SstQueries {
+    const uint32_t* qs;
+    uint64_t nq, stride;
+    uint32_t nxt;
+    __device__ SstQueries(const uint32_t* q, uint64_t n, uint64_t i0, uint64_t s)
+        : qs(q), nq(n), stride(s), nxt((SST_QPREFETCH && i0 < n) ? sst_qload(q, i0) : 0u) {}
+    __device__ __forceinline__ uint32_t get(uint64_t i) {
+        if (!SST_QPREFETCH) return sst_qload(qs, i);
+        const uint32_t q = nxt;
+        if (i + stride < nq) nxt = sst_qload(qs, i + stride);
+        return q;
+    }
+};
 #define SST_EYT_LDS 8192  // first 13 Eytzinger levels (32 KiB) in LDS
 
 
@@ -99,8 +133,10 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_stree4(SstArgs a) {
     const uint32_t B = a.B, sub = threadIdx.x & (QUAD_G - 1);
     const uint32_t lds_layers = TOP ? a.lds_layers : 0;
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
-    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
-        const int32_t q = (int32_t)a.qs[i];
+    const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G;
+    SstQueries qs(a.qs, a.nq, i0, stride);
+    for (uint64_t i = i0; i < a.nq; i += stride) {
+        const int32_t q = (int32_t)qs.get(i);
         auto cnt4 = [&](uint4 v) -> uint32_t {
             return quad_sum((q > (int32_t)v.x) + (q > (int32_t)v.y) + (q > (int32_t)v.z) + (q > (int32_t)v.w));
         };
@@ -118,7 +154,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_stree4(SstArgs a) {
         uint32_t val = (uint32_t)__shfl((int)mine, src, 64);
         if (sub == 0) {
             if (idx >= 16) val = a.nodes[(o + k + 1) * 16];
-            a.out[i] = val;
+            sst_out(a.out, i, val);
             if (a.rank) a.rank[i] = k * B + idx;
         }
     }
@@ -164,8 +200,10 @@ __global__ __launch_bounds__(SST_BLOCK) void k_sst_pmap(SstArgs a) {
 __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_pmap4(SstArgs a) {
     const uint32_t sub = threadIdx.x & (QUAD_G - 1);
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
-    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
-        const int32_t q = (int32_t)a.qs[i];
+    const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G;
+    SstQueries qs(a.qs, a.nq, i0, stride);
+    for (uint64_t i = i0; i < a.nq; i += stride) {
+        const int32_t q = (int32_t)qs.get(i);
         uint32_t p = (uint32_t)q >> a.shift;
         if (p >= a.parts) p = a.parts - 1;  // q above every key's prefix (UB in the reference)
         const uint64_t key = a.prefix_map[p];
@@ -197,7 +235,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_pmap4(SstArgs a) {
             rank = key + c0;
         }
         if (sub == 0) {
-            a.out[i] = val;
+            sst_out(a.out, i, val);
             if (a.rank) a.rank[i] = rank;
         }
     }
@@ -214,8 +252,10 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_part4(SstArgs a) {
     const uint32_t sub = threadIdx.x & (QUAD_G - 1);
     const uint64_t stride = ((uint64_t)gridDim.x * blockDim.x) / QUAD_G;
     const bool compact = a.bpp != 0;
-    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G; i < a.nq; i += stride) {
-        const int32_t q = (int32_t)a.qs[i];
+    const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / QUAD_G;
+    SstQueries qs(a.qs, a.nq, i0, stride);
+    for (uint64_t i = i0; i < a.nq; i += stride) {
+        const int32_t q = (int32_t)qs.get(i);
         uint64_t part = (uint32_t)q >> a.shift;
         if (part >= a.parts) part = a.parts - 1;  // q above every key's prefix (UB in the reference)
         auto cnt4 = [&](uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) -> uint32_t {
@@ -241,7 +281,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_part4(SstArgs a) {
         const uint32_t mine = r == 0 ? w0 : r == 1 ? w1 : r == 2 ? w2 : w3;
         uint32_t val = (uint32_t)__shfl((int)mine, (int)((threadIdx.x & 63) & ~3u) + (int)((c >> 2) & 3), 64);
         if (c >= 16) val = a.nodes[e + 16];
-        if (sub == 0) a.out[i] = val;
+        if (sub == 0) sst_out(a.out, i, val);
     }
 }
 
@@ -268,16 +308,17 @@ __global__ __launch_bounds__(SST_BLOCK) void k_sst_eytzinger(SstArgs a) {
 }
 
 __global__ __launch_bounds__(SST_BLOCK) void k_sst_sorted(SstArgs a) {
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        uint32_t q = a.qs[i];
+    const uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    SstQueries qs(a.qs, a.nq, i0, stride);
+    for (uint64_t i = i0; i < a.nq; i += stride) {
+        const uint32_t q = qs.get(i);
         uint64_t l = 0, r = a.n;
         while (l < r) {
             uint64_t m = (l + r) >> 1;
             if (a.nodes[m] < q) l = m + 1;
             else r = m;
         }
-        a.out[i] = l < a.n ? a.nodes[l] : 0xFFFFFFFFu;
+        sst_out(a.out, i, l < a.n ? a.nodes[l] : 0xFFFFFFFFu);
         if (a.rank) a.rank[i] = l;
     }
 }
@@ -328,9 +369,10 @@ __global__ void k_direct_big(const uint32_t* __restrict__ vals, uint64_t n, cons
 __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_direct(SstArgs a) {
     const uint32_t sh = 31 - a.shift;  // a.shift holds b here
     const uint64_t top = 1ull << a.shift;
-    for (uint64_t i = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; i < a.nq;
-         i += (uint64_t)gridDim.x * blockDim.x) {
-        const uint32_t q = a.qs[i];
+    const uint64_t i0 = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    SstQueries qs(a.qs, a.nq, i0, stride);
+    for (uint64_t i = i0; i < a.nq; i += stride) {
+        const uint32_t q = qs.get(i);
         uint64_t x = q >> sh;
         x = x < top ? x : top;
         const uint4 e = nt_load4(a.direct + x);
@@ -349,7 +391,7 @@ __global__ __launch_bounds__(SST_BLOCK, 8) void k_sst_direct(SstArgs a) {
             r = l;
             v = l < a.n ? a.nodes[l] : 0xFFFFFFFFu;
         }
-        a.out[i] = v;
+        sst_out(a.out, i, v);
         if (a.rank) a.rank[i] = r < a.n ? r : a.n;
     }
 }

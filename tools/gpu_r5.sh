@@ -4,6 +4,7 @@
 #   suite    pytest -m gpu                 smoke  __graft_entry__.smoke()
 #   shard    tests/test_gpu_shard.py only  bench  the default bench line
 #   quick    the c1/c2 lineup only (no c0/c3/c4/CPU/e2e/lcp_long)
+#   absst    tools/ab_sst_var.py (the u32 lineup) over the tree and AB_VARS, like abbin
 #   abbin    tools/ab_bin.py over the tree and the tools/_var_* builds named in AB_VARS
 #   kt       the bench under rocprofv3 --kernel-trace --stats, by grid (tools/prof_r4.sh)
 #   c4:W:g   tools/c4_part_probe.py W g (part g of W at the bench's share for W ranks)
@@ -34,6 +35,8 @@ for s in "$@"; do
                    --detail "$out/quick_detail.json" > "$out/quick.json" 2> "$out/quick.err" || exit $? ;;
         abbin) AB_PKGS="tree${AB_VARS:+:}${AB_VARS}" timeout -k 10 500 python3 -u tools/ab_bin.py > "$out/ab_bin.json" \
                    2> "$out/ab_bin.err" || exit $? ;;
+        absst) AB_PKGS="tree${AB_VARS:+:}${AB_VARS}" timeout -k 10 500 python3 -u tools/ab_sst_var.py > "$out/ab_sst.json" \
+                   2> "$out/ab_sst.err" || exit $? ;;
         kt) bash tools/prof_r5.sh "$out/prof" > "$out/prof.log" 2>&1 || exit $? ;;
         kt34) bash tools/prof_r5_c34.sh "$out/prof34" > "$out/prof34.log" 2>&1 || exit $? ;;
         c4:*) IFS=: read -r _ W g <<< "$s"
