@@ -12,6 +12,9 @@ import torch
 import sas_amd
 
 n, nq, m = 1 << 30, 10_000_000, 32
+# PROBE_BALLAST_GB: device memory held before the text and index (placement probe)
+_bg = float(os.environ.get("PROBE_BALLAST_GB", "0"))
+ballast = torch.empty(int(_bg * 2**30), dtype=torch.uint8, device="cuda") if _bg else None
 t = sas_amd.random_string(n, seed=31415, device="cuda")
 off, _, _ = sas_amd.random_queries(n, nq, seed=31415, word_pos=n, margin=200, len_lo=m, len_hi=m + 1)
 src = torch.from_numpy(off.astype(np.int64)).cuda()
@@ -23,7 +26,7 @@ for mode in os.environ.get("AB_MODES", "16r").split(","):
     p, inl = int(mode[:-1]), {"r": 0, "i": 1, "d": 2, "q": 4}[mode[-1]]
     idx = sas_amd.SaNaive.build(t, lcp=False, stree=False, sector=False, llcp=False, quad=True, prefix=p,
                                 prefix_inline=inl)
-    line = {"mode": mode, "p": idx.stats()["prefix_chars"]}
+    line = {"mode": mode, "p": idx.stats()["prefix_chars"], "ballast_gb": _bg}
     ref = None
     for algo in ("prefix", "quad"):
         idx.time_fixed(qb, m, nq, out, algo=algo, reps=2)
