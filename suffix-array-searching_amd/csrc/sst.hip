@@ -16,9 +16,10 @@
 // query stream of the u32 kernels: the next query of this lane (group) is loaded while the
 // current one's nodes are in flight (SST_QPREFETCH), and the query and answer streams can
 // bypass L2 (SST_NT_IO: non-temporal loads and stores).  Same-box A/B at 2^28 keys, 10^7
-// queries (tools/ab_sst_var.py, profiles/r5/ab_sst_prefetch/): prefetch takes DirectMap from
-// 0.239 to 0.208 ms (its one entry read no longer waits behind the query's round trip) and
-// leaves the S-trees and SortedVec within 0.3%; NT I/O gains nothing beside it (0.215 ms).
+// queries, one table placement (tools/ab_sst_var.py, profiles/r5/placement/): prefetch takes
+// DirectMap from 0.211 to 0.207 ms (its one entry read no longer waits behind the query's
+// round trip) and leaves the S-trees and SortedVec within 0.3%; NT I/O gains nothing beside
+// it.  Where the 8 GiB table lands moves DirectMap far more (0.235 vs 0.209 ms).
 #ifndef SST_QPREFETCH
 #define SST_QPREFETCH 1
 #endif
