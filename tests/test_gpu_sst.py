@@ -186,3 +186,23 @@ def test_build_assertions(sas):
         sas.STree16.new([])
     with pytest.raises(sas.SasError):
         sas.STree16.new_params([1, 2, 3], False, True, True)  # full + reverse
+
+
+def test_query_counts_around_the_grid(sas):
+    """Every layout at batch sizes that stop inside a group, a wave, the first grid pass and
+    a later one (each lane loads its next query one pass ahead, SST_QPREFETCH): values and
+    ranks equal SortedVec's."""
+    rng = np.random.default_rng(17)
+    vals = gen_vals(1 << 16, rng)
+    allq = rng.integers(0, O.MAX, 3_000_003, dtype=np.uint64).astype(np.uint32)
+    ref, ref_rank = O.SortedVec(vals).query(allq, want_rank=True)
+    layouts = [sas.SortedVec.new(vals), sas.Eytzinger.new(vals), sas.STree16.new(vals), sas.STree15.new(vals),
+               sas.PartitionedSTree16M.new(vals, 16), sas.PartitionedSTree16.new(vals, 8), sas.DirectMap.new(vals)]
+    for nq in (1, 2, 3, 5, 63, 65, 1023, 1025, 600_001, 3_000_003):
+        for idx in layouts:
+            v = idx.query(allq[:nq])
+            assert np.array_equal(v, ref[:nq]), (type(idx).__name__, nq)
+        v, r = layouts[-1].query(allq[:nq], want_rank=True)
+        assert np.array_equal(r, ref_rank[:nq]), nq
+    for idx in layouts:
+        idx.free()
