@@ -5,7 +5,8 @@ BASELINE.json metric: "pattern lookups/s + achieved HBM GB/s, 2^30-byte text,
 GPU (inputs already resident in HBM), through the C ABI (sas_search_fixed).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--algo prefix|plain|quad|...]
-    torchrun --nproc-per-node N bench.py --gpus N ...   (one process per GPU)
+        (N > 1: bench.py starts N rank processes itself, one per GPU, benchlib/launch.py)
+    torchrun --nproc-per-node N bench.py --gpus N ...   (the same N ranks from a launcher)
 
 One JSON line.  `value` is the headline algorithm (PREFIX: a p = 16-char bucket table with
 32-B inline entries over fused quad leaves) on the configs[1]/[2] workload; `configs` holds
@@ -50,11 +51,14 @@ from benchlib.model import _classify, _quad_leaf_bytes, _tree_layers  # noqa: E4
 from benchlib.records import *  # noqa: E402,F401,F403
 from benchlib.sst import *  # noqa: E402,F401,F403
 from benchlib.line import *  # noqa: E402,F401,F403
+from benchlib.launch import needs_spawn, probe_main, resolve_world, spawn_ranks  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (ranks) on this node: without a launcher, N > 1 starts N rank processes itself "
+                         "(benchlib/launch.py); under torchrun it must equal WORLD_SIZE (default: WORLD_SIZE, else 1)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
@@ -98,7 +102,7 @@ def main():
     ap.add_argument("--shard-chunks", type=int, default=1,
                     help="sharded step in this many pieces, exchanges overlapped with the other pieces' work")
     ap.add_argument("--c4-steps", type=int, default=10)
-    ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst"],
+    ap.add_argument("--workload", default="c1", choices=["c1", "c3", "sst", "launch_probe"],
                     help="c1: 2^30 text, 10^7 len-32 queries (BASELINE metric) + every config's sub-record; "
                          "c3: the configs[3] record alone; sst: the u32 static-search-tree path")
     ap.add_argument("--positive", action="store_true", help="sst workload: queries drawn from the keys")
@@ -114,18 +118,28 @@ def main():
     ap.add_argument("--mode", default="replicated", choices=["replicated", "shard"],
                     help="replicated index (weak scaling, no data-path collective) or sharded SA rank "
                          "ranges with RCCL all-to-all query routing (SURVEY §8e)")
+    ap.add_argument("--probe-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    # --gpus N without a launcher: N fresh rank processes, started before this process makes
+    # any HIP call; rank 0 prints the line, the job fails if any rank does
+    if needs_spawn(args.gpus):
+        return spawn_ranks(args.gpus, os.path.abspath(__file__), sys.argv[1:])
+    ws, rank, local = resolve_world(args.gpus)  # under a launcher: --gpus must equal WORLD_SIZE
     keep_stdout_for_result()
+    if args.workload == "launch_probe":
+        return probe_main(args, emit, log)
 
     import torch
     import sas_amd
 
-    ws, rank, local = dist_env()
     dist = None
     if ws > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
+        # n_gpus is the group the step ran in, not the environment's claim
+        ws = dist.get_world_size()
+        rank = dist.get_rank()
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -514,4 +528,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
