@@ -64,11 +64,11 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30, help="text length (chars)")
     ap.add_argument("--nq", type=int, default=10_000_000, help="queries per GPU")
     ap.add_argument("--m", type=int, default=32, help="query length")
-    ap.add_argument("--algo", default=None, choices=["stree", "stree_llcp", "plain", "lcp", "sector", "quad", "inline",
+    ap.add_argument("--algo", default=None, choices=["stree", "stree_llcp", "quad_llcp", "plain", "lcp", "sector", "quad", "inline",
                                                      "llcp",
                                                      "prefix", "tagged", "interp"])
     ap.add_argument("--variants",
-                    default="plain,plain_range,llcp,stree,stree_llcp,sector,quad,inline,interp,interp_range,"
+                    default="plain,plain_range,llcp,stree,stree_llcp,sector,quad,quad_llcp,inline,interp,interp_range,"
                             "prefix_packed",
                     help="other algos timed beside the headline one (mlr LCP skipping, 'lcp', lost to PLAIN at every "
                          "m and on both texts of the lcp_long record: it runs there and in configs[3] only)")
@@ -300,7 +300,7 @@ def main():
         bpl = bytes_per_lookup("prefix" if v == "prefix_packed" else vbase, stats, n, m, vmean,
                                range_flag=bool(vfl), packed=v == "prefix_packed")
         key = {"plain": "plain", "quad": "quad", "stree": "stree", "sector": "sector", "llcp": "llcp",
-               "stree_llcp": "stree_llcp"}.get(v)
+               "stree_llcp": "stree_llcp", "quad_llcp": "quad_llcp"}.get(v)
         pmc = load_pmc(f"{key}_n{n}_q{nq}_m{m}" + (f"_t{stats['top2_levels']}" if key == "plain" else "")) \
             if key else None
         variants[v] = record(v, nq, vk, vel, bpl, footprint(v, stats), pmc, vmean,
@@ -424,6 +424,11 @@ def main():
             if "stree_llcp" in variants:
                 configs["c2"]["lcp_stree"] = dict(variants["stree_llcp"], workload=WORKLOADS["stree_llcp"],
                                                   lds_layers=stats["stree_lds_layers"])
+            # the two joined: QUAD's descent + the LLCP tail where the leaf does not settle q (at
+            # m = 32 the 32-char key always does: QUAD's kernel; its long-query shapes in lcp_long)
+            if "quad_llcp" in variants:
+                configs["c2"]["lcp_quad"] = dict(variants["quad_llcp"], workload=WORKLOADS["quad_llcp"],
+                                                 lds_layers=stats["quad_lds_layers"])
     idx_stats = {k: stats[k] for k in ("stree_layers", "stree_lds_layers", "sector_layers", "sector_lds_layers",
                                        "quad_layers", "quad_lds_layers", "quad_fan", "top_levels", "top2_levels", "rel_levels",
                                        "iterations", "prefix_chars", "prefix_bytes", "sa_bytes", "text_bytes",

@@ -34,7 +34,7 @@ C1_DEEP_TOP2_LEVELS = 30  # the second configs[1] figure: rounded up to all 31 l
 
 KERNELS = {"stree": "k_sa_stree", "stree_llcp": "k_sa_stree", "sector": "k_sa_sector", "quad": "k_sa_quad", "inline": "k_sa_inline",
            "llcp": "k_sa_binary", "plain": "k_sa_binary", "lcp": "k_sa_binary", "interp": "k_sa_interp",
-           "tagged": "k_sa_tagged"}
+           "tagged": "k_sa_tagged", "quad_llcp": "k_sa_quad"}
 
 
 # ---------------------------------------------------------------- harness

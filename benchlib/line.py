@@ -76,9 +76,10 @@ def compact_line(full: dict) -> dict:
     for k in ("c1", "c2"):
         if k in confs:
             out[k] = config_summary(confs[k])
-    if "c2" in confs and confs["c2"].get("lcp_stree"):
-        out["c2"]["lcp_stree"] = {kk: vv for kk, vv in config_summary(confs["c2"]["lcp_stree"]).items()
-                                  if kk in ("algo", "kernel_ms", "frac", "frac_basis", "traffic")}
+    for sk in ("lcp_stree", "lcp_quad"):
+        if "c2" in confs and confs["c2"].get(sk):
+            out["c2"][sk] = {kk: vv for kk, vv in config_summary(confs["c2"][sk]).items()
+                             if kk in ("algo", "kernel_ms", "frac", "frac_basis", "traffic")}
     if "c1" in confs and confs["c1"].get("deep_pivots"):
         out["c1_deep_pivots"] = dict(config_summary(confs["c1"]["deep_pivots"]),
                                      pivot_levels=confs["c1"]["deep_pivots"].get("pivot_levels"))
@@ -151,6 +152,9 @@ WORKLOADS = {
     "sector": "configs[2]: sector S-tree (9-ary 32-B nodes, fused 32-char key + SA leaves, top layers LDS-staged)",
     "quad": "configs[2]: quad S-tree (17-ary 64-B nodes read by 4-lane groups, 4-entry fused {32-char key, SA} "
             "leaves, top layers LDS-staged)",
+    "quad_llcp": "configs[2] as one kernel: the quad S-tree's descent (17-ary 64-B nodes, top layers LDS-staged, "
+                 "fused {32-char key, SA} leaves); where the leaf does not settle q, Manber-Myers LLCP skipping inside "
+                 "the run of suffixes sharing q's key (m <= 32: the quad S-tree alone)",
     "interp": "interpolation_search<16> (sas/sa_search.rs:376-421) over fused {32-char key, SA} entries",
     "tagged": "tagged SA entries + bucket table",
 }

@@ -96,7 +96,7 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
         reqs = {"cache": rc, "hbm": rh + max(0.0, probes - R) * rq + srun + fin + (8.0 if packed else m) / 128}
     elif algo == "interp":
         hbm += probes * 16
-    elif algo in ("stree", "stree_llcp", "quad", "sector"):
+    elif algo in ("stree", "stree_llcp", "quad", "quad_llcp", "sector"):
         if algo in ("stree", "stree_llcp"):
             H, node, lds_l = st["stree_layers"], 64, st["stree_lds_layers"]
             sizes = _tree_layers(n, 16, 64, 17, 64, H)
@@ -109,7 +109,7 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
             H, node, lds_l = st["quad_layers"], 64, st["quad_lds_layers"]
             leaf_entries = 4 if st["quad_entry_bytes"] == 16 else 8
             sizes = _tree_layers(n, leaf_entries, 64, st["quad_fan"], 64, H)
-            tail = 64
+            tail = 64 if algo == "quad" else 16  # QUAD_LLCP: a 16-B LLCP entry (or a leaf) a probe
         h, c, l = _classify(sizes, node, lds_l)
         hbm, cache, lds = h + max(0.0, probes - H) * tail + (max(0.0, m - 32) / 4 if not algo.startswith("stree")
                                                              else 0), c, l
@@ -123,13 +123,13 @@ def bytes_per_lookup(algo: str, st: dict, n: int, m: float, probes: float, range
     # binary-search family P (4 + m) + m + 8; trees H node bytes + what the tail reads
     if algo in ("plain", "lcp", "llcp", "inline") and not range_flag:
         out["section_8d"] = P * (4 + m) + m + 8
-    elif algo in ("stree", "stree_llcp", "quad", "sector"):
+    elif algo in ("stree", "stree_llcp", "quad", "quad_llcp", "sector"):
         node = 32 if algo == "sector" else 64
-        tail = {"stree": 4 + m, "stree_llcp": 4 + m, "quad": 64, "sector": 12}[algo]
+        tail = {"stree": 4 + m, "stree_llcp": 4 + m, "quad": 64, "quad_llcp": 16, "sector": 12}[algo]
         out["section_8d"] = H * node + max(0.0, probes - H) * tail + m + 8
     else:
         out["section_8d"] = hbm
-    if algo in ("plain", "lcp", "inline", "llcp", "stree", "stree_llcp", "quad", "sector") and not range_flag:
+    if algo in ("plain", "lcp", "inline", "llcp", "stree", "stree_llcp", "quad", "quad_llcp", "sector") and not range_flag:
         out["requests_model"] = reqs
     return out
 
@@ -239,7 +239,7 @@ def footprint(algo: str, st: dict) -> int:
     skipping keeps its lcps in registers); LLCP = its 16-B entries + pivots + text; INLINE =
     the fused quad leaves + pivots + text; QUAD = the quad tree (+ SA with compact leaves) +
     text; SECTOR = the sector tree + text; STREE = the S-tree + SA + text; STREE_LLCP = the
-    S-tree + the LLCP entries + text; PREFIX = the prefix
+    S-tree + the LLCP entries + text; QUAD_LLCP = the quad tree + the LLCP entries + text; PREFIX = the prefix
     table + the quad leaves (+ SA with compact leaves) + text; *_range = + the prefix table;
     TAGGED = the tagged index (it holds nothing else)."""
     base = algo[:-6] if algo.endswith("_range") else ("prefix" if algo == "prefix_packed" else algo)
@@ -264,6 +264,8 @@ def footprint(algo: str, st: dict) -> int:
         b = st["stree_bytes"] + sa + text
     elif base == "stree_llcp":  # the S-tree + the LLCP entries (SA values included) + text
         b = st["stree_bytes"] + st["llcp_bytes"] + text
+    elif base == "quad_llcp":  # the quad tree + the LLCP entries (SA values included) + text
+        b = st["quad_bytes"] + st["llcp_bytes"] + text
     elif base == "prefix":
         b = st["prefix_bytes"] + _quad_leaf_bytes(st) + compact_sa + text
     elif base == "interp":

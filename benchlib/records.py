@@ -164,7 +164,7 @@ def c0_record(torch, sas_amd, dev, seconds: float):
 
 # ---------------------------------------------------------------- LCP skipping on long queries
 LCP_LONG_MS = (64, 128, 256)
-LCP_LONG_ALGOS = ("plain", "lcp", "llcp", "stree_llcp", "quad")
+LCP_LONG_ALGOS = ("plain", "lcp", "llcp", "stree_llcp", "quad", "quad_llcp")
 
 
 def cut_queries(torch, text, off_t, m: int):
@@ -245,10 +245,19 @@ def lcp_long_summary(rec: dict) -> dict:
                 continue
             ms = [_r(row[a]["kernel_ms"]) for a in LCP_LONG_ALGOS]
             s[f"{tk}_{mk}"] = ms
-            for a in ("lcp", "llcp", "stree_llcp"):
+            for a in ("lcp", "llcp", "stree_llcp", "quad_llcp"):
                 if row[a]["kernel_ms"] < row["plain"]["kernel_ms"]:
                     wins.append(f"{a}@{tk}_{mk}:{row['plain']['kernel_ms'] / row[a]['kernel_ms']:.2f}x")
-    return {"ms": s, "skipping_beats_plain": wins}
+    # configs[2]'s one kernel against the best of the two it joins, shape by shape
+    best = {}
+    for tk, rows in rec.items():
+        if not isinstance(rows, dict) or tk in ("what", "summary"):
+            continue
+        for mk, row in rows.items():
+            if isinstance(row, dict) and "quad_llcp" in row:
+                ref = min(row["quad"]["kernel_ms"], row["stree_llcp"]["kernel_ms"])
+                best[f"{tk}_{mk}"] = _r(row["quad_llcp"]["kernel_ms"] / ref, 3)
+    return {"ms": s, "skipping_beats_plain": wins, "quad_llcp_over_min_quad_stree_llcp": best}
 
 
 # ---------------------------------------------------------------- configs[3]
@@ -527,7 +536,20 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
     if not int(same.item()):
         raise SystemExit("bench c4: the pieced step differs from the whole step")
     del out2
-    rccl1 = None
+    rccl1 = routed1 = None
+    if ws == 1:  # the routed shape a W > 1 rank runs (route + identity exchange + gather)
+        engr = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", max_nq=nq, routed=True)
+        outr = torch.empty(nq, dtype=torch.int64, device=dev)
+        elr = timed_loop(lambda: engr.search_fixed(qbytes, m, check=False, out=outr), max(3, args.c4_steps // 2),
+                         args.warmup, torch.cuda.synchronize, dist.barrier, reduce_max)
+        engr.assert_no_overflow()
+        if not bool(torch.equal(out, outr)):
+            raise SystemExit("bench c4: the routed world-1 step differs from the identity step")
+        routed1 = {"ms_per_step": elr / max(3, args.c4_steps // 2) * 1e3,
+                   "lookups_per_s": nq * max(3, args.c4_steps // 2) / elr, "identical": True,
+                   "what": "routed=True: sas_route_pack_cap + the identity exchange + sas_shard_gather around the "
+                           "bucket lookup (the shape of each rank's step at N > 1)"}
+        del outr
     if ws == 1:  # the same step with the world-1 exchanges sent through RCCL (self copies)
         eng1 = ShardedSearch(idx, dist, ws, rank, dev, algo="prefix", max_nq=nq, exchange_self=True)
         out3 = torch.empty(nq, dtype=torch.int64, device=dev)
@@ -561,8 +583,9 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
                        f"{ws} GPU(s) (sas_build_part), {nq} len-{m} queries per GPU routed with RCCL "
                        f"all_to_all_single (fixed-capacity buckets, 8-B packed PREFIX queries, per-bucket counts "
                        f"exchanged so only filled slots are searched), positions back"
-                       + (" -- at N = 1 every query is local: the exchanges are the identity, no collective "
-                          "(rccl_world1 times them through RCCL)" if ws == 1 else ""),
+                       + (" -- at N = 1 every query is local: route, exchanges and gather are the identity, the "
+                          "step is the part's lookup (routed_world1 times the routed shape, rccl_world1 its "
+                          "exchanges through RCCL)" if ws == 1 else ""),
            "n": n, "parts": ws, "lookups_per_s": ws * nq * args.c4_steps / el, "ms_per_step": el / args.c4_steps * 1e3,
            "steps": args.c4_steps, "scaling": "weak", "part_sa_entries": st["sa_entries"],
            "prefix_entry_bytes": prefix_entry_bytes(st), "share": share,
@@ -572,7 +595,7 @@ def c4_record(args, torch, sas_amd, dev, ws, rank, dist):
            "alt_pieces": {"pieces": alt_chunks, "ms_per_step": el2 / max(3, args.c4_steps // 2) * 1e3,
                           "lookups_per_s": ws * nq * max(3, args.c4_steps // 2) / el2, "identical": True},
            "exchange_bytes_per_step_per_rank": 2 * ws * cap * 8 * args.shard_chunks if ws > 1 else 0,
-           "rccl_world1": rccl1,
+           "rccl_world1": rccl1, "routed_world1": routed1,
            "index_bytes": st["index_bytes"], "setup_s": setup, "verified": True,
            "proven": proven["checked"], "proof": "each rank: a sample of the queries it received in its last step, "
                                                   "proven exact lower bounds on its own part's SA"}

@@ -185,11 +185,19 @@ enum sas_algo {
                            usize, :389-392); ENOTSUP above                                   */
     SAS_ALGO_TAGGED = 9, /* bucket table + tagged SA entries (needs SAS_BUILD_TAGGED): the
                            configs[3] shape's lookup, ~4-5 memory requests for a long query  */
-    SAS_ALGO_STREE_LLCP = 10 /* configs[2]'s combination: the STREE descent over the 16-char SA keys
+    SAS_ALGO_STREE_LLCP = 10, /* configs[2]'s combination: the STREE descent over the 16-char SA keys
                            (LDS-staged top layers) gives the run of suffixes sharing q's key,
                            then Manber-Myers LLCP skipping finishes inside it (the LLCP entries'
                            binary-search tree walked from its root, mids outside the run decided
                            with no read); needs SAS_BUILD_STREE and SAS_BUILD_LLCP          */
+    SAS_ALGO_QUAD_LLCP = 11 /* configs[2] as one kernel: QUAD's descent over the fused 32-char
+                           keys (LDS-staged top layers); a query the routed leaf does not settle
+                           (q's 32-char key shared by several suffixes: long queries on
+                           repetitive text) continues with LLCP skipping inside the run of
+                           suffixes sharing its key, whose far end comes from where the path of
+                           the next 16-char key parts from q's.  m <= 32: QUAD itself.  Needs
+                           SAS_BUILD_QUAD with fused leaves in the absolute layout (the default
+                           below 2^31 suffixes; SAS_BUILD_QUAD_ABS) and SAS_BUILD_LLCP        */
 };
 
 typedef struct sas_stats {
@@ -391,9 +399,12 @@ int sas_extract(const sas_index* index, const uint64_t* pos, const uint32_t* len
 int sas_verify(const sas_index* index);
 
 /* Ragged batch: query k = qbytes[qoff[k] .. qoff[k] + qlen[k]).
- * out_pos[k] = SA[lower_bound(q_k)] (or n).  out_probes (optional) = number
- * of suffix comparisons / S-tree nodes touched for query k, the reference's
- * `cnt` counter (sas/sa_search.rs:104,178).  stream: hipStream_t or NULL.
+ * out_pos[k] = SA[lower_bound(q_k)] (or n).  out_probes (optional): for PLAIN, LCP,
+ * LLCP and INTERP the number of probes of query k, the reference's `cnt` counter
+ * (sas/sa_search.rs:104,178); for the tree algorithms the memory reads of the lookup
+ * (tree nodes and leaves; STREE_LLCP / QUAD_LLCP: + the LLCP entries read, QUAD_LLCP: + the
+ * text compare of the leaf's candidate), which have no reference counterpart.
+ * stream: hipStream_t or NULL.
  * With host pointers the call is synchronous; with SAS_DEVICE_PTRS it is
  * asynchronous on `stream`. */
 int sas_search_batch(const sas_index* index, const uint8_t* qbytes, const uint64_t* qoff,

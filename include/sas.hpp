@@ -73,6 +73,7 @@ enum class Algo : int {
     Interp = SAS_ALGO_INTERP,
     Tagged = SAS_ALGO_TAGGED,
     StreeLlcp = SAS_ALGO_STREE_LLCP,
+    QuadLlcp = SAS_ALGO_QUAD_LLCP,
 };
 
 /* build flags of SaNaive::build: the LCP array, the fused quad tree and the p = 16 prefix

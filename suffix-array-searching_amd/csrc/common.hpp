@@ -428,6 +428,24 @@ struct QueryRegs {
     }
 };
 
+// QueryRegs for a kernel launched only with m <= 32 QW: every word is in registers and the
+// words past them are 0, so no code repacks words from the bytes (k_sa_quad_llcp)
+template <int QW>
+struct QueryRegsExact : QueryRegs<QW> {
+    __device__ __forceinline__ uint64_t word(uint32_t j) const {
+        uint64_t r = 0;
+#pragma unroll
+        for (int k = 0; k < QW; k++) r = (j == (uint32_t)k) ? this->w[k] : r;
+        return r;
+    }
+    __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
+        const uint32_t j = off >> 5, s = (off & 31) << 1;
+        const uint64_t a = word(j);
+        if (s == 0) return a;
+        return (a << s) | (word(j + 1) >> (64 - s));
+    }
+};
+
 // Rust slice order `t[p..n] < q`, with the first h chars known equal.
 // Returns lt; *lcp = lcp(t[p..n], q) (capped at min(n-p, m)).
 template <int QW, class Q>

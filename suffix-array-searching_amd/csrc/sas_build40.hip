@@ -30,6 +30,7 @@
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <cstdlib>
 #include <vector>
 
 #define HIST_BITS 14
@@ -67,6 +68,16 @@ __device__ __forceinline__ uint32_t block_sum(uint32_t v, uint32_t* s_w) {
 // workgroups stride over the chunks (a dispatch holds < 2^32 work-items: n = 2^36 is 2^22
 // chunks of 1024 threads)
 #define COLLECT_GRID (1u << 16)
+// debug: SAS_COLLECT_GRID=g caps the grid at g workgroups, so a small text takes the stride loop
+// that n = 2^36 needs (tests/test_gpu_sa.py::test_collect_grid_stride)
+static uint32_t collect_grid(uint64_t nblk) {
+    uint64_t g = nblk < COLLECT_GRID ? nblk : COLLECT_GRID;
+    if (const char* e = getenv("SAS_COLLECT_GRID")) {
+        const long v = atol(e);
+        if (v > 0 && (uint64_t)v < g) g = (uint64_t)v;
+    }
+    return (uint32_t)g;
+}
 __global__ __launch_bounds__(COLLECT_BLOCK) void k_bucket_count(const uint64_t* __restrict__ tw, uint64_t n,
                                                                 uint32_t lo, uint32_t hi,
                                                                 uint64_t* __restrict__ block_cnt) {
@@ -281,7 +292,7 @@ static int sort_bins_into(const uint64_t* tw, uint64_t n, const std::vector<uint
         uint64_t c = 0;
         for (uint32_t i = blo; i < bhi; i++) c += h[i];
         if (c == 0) continue;
-        const dim3 cg((unsigned)(nblk < COLLECT_GRID ? nblk : COLLECT_GRID));
+        const dim3 cg(collect_grid(nblk));
         hipLaunchKernelGGL(k_bucket_count, cg, dim3(COLLECT_BLOCK), 0, st, tw, n, blo, bhi,
                            bcnt.as<uint64_t>());
         TRY(with_temp(tmp, tmp_have, [&](void* t, size_t& sz) {

@@ -107,6 +107,7 @@ struct SearchArgs {
     const uint64_t* qoff;
     const uint32_t* qlen;
     uint32_t m_fixed;
+    uint32_t m_max;          // longest query of the batch when the host knows it (0: unknown)
     uint64_t nq;
     uint64_t* out_pos;
     uint32_t* out_probes;
@@ -1192,6 +1193,57 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
 #ifndef SAS_QUAD4X_PREFETCH
 #define SAS_QUAD4X_PREFETCH false
 #endif
+// The per-lane finish of k_sa_quad4x: every entry before x0 is < q (the routed leaf's count
+// of 32-char keys below q's); key0 / p0 = entry x0's key and SA value when the leaf read
+// delivered them (known).  The predicate at x0 (a key tie: one text compare from char 32),
+// and in the rare case it fails an exponential + binary search over the following entries.
+// Returns the position.
+template <int QW, bool KO, int W>
+__device__ __forceinline__ uint64_t quad_x0_finish(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64,
+                                                   uint64_t x0, bool known, uint64_t key0, uint64_t p0,
+                                                   uint32_t* probes) {
+    const uint64_t sa_n = a.sa_n;
+    bool ok = false;
+    if (x0 < sa_n) {
+        const uint64_t key = known ? key0 : quad_entry_key<KO>(a, x0);
+        if (key != K64) {
+            ok = key > K64;
+        } else {
+            if (p0 == QUAD_NO_SA) p0 = quad_entry_sa<KO, W>(a, x0);
+            ok = sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, p0, K64, a, q);
+        }
+        if (!known) (*probes)++;
+    }
+    uint64_t x = x0;
+    if (!ok && x0 < sa_n) {  // rare: exponential + binary search over x0+1 ..
+        auto pred = [&](uint64_t y) -> bool {
+            const uint64_t key = quad_entry_key<KO>(a, y);
+            if (key != K64) return key > K64;
+            return sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
+        };
+        uint64_t lo = x0 + 1, hi = sa_n, step = 1;
+        while (lo < sa_n) {
+            hi = lo + step - 1;
+            if (hi >= sa_n) { hi = sa_n; break; }
+            (*probes)++;
+            if (pred(hi)) break;
+            lo = hi + 1;
+            step *= 2;
+            hi = sa_n;
+        }
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            (*probes)++;
+            if (pred(mid)) hi = mid;
+            else lo = mid + 1;
+        }
+        x = lo;
+        p0 = QUAD_NO_SA;
+    }
+    if (x >= sa_n) return a.next_pos;
+    return (p0 != QUAD_NO_SA) ? p0 : quad_entry_sa<KO, W>(a, x);
+}
+
 // Long queries (QW > 1), as k_sa_stree4x: one query per LANE, four per 4-lane group.
 // The group descends the quad tree and reads the routed leaf cooperatively for each
 // of its four queries in turn (one request per 64-B node), which places each query
@@ -1209,7 +1261,6 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
     uint32_t bad = 0;
     const uint32_t sub = threadIdx.x & (QUAD_G - 1);
     const int lane0 = (int)((threadIdx.x & 63) & ~3u);
-    const uint64_t sa_n = a.sa_n;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     // the loop runs while ANY query of the group is in range (group-uniform)
     for (uint64_t gi = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) - sub; gi < a.nq; gi += stride) {
@@ -1257,48 +1308,375 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
             }
         }
         if (!mine) continue;
-        const uint64_t K64 = Kmine;
-        // predicate at x0 with the values the leaf read already delivered
-        bool ok = false;
-        if (x0 < sa_n) {
-            const uint64_t key = known ? key0 : quad_entry_key<KO>(a, x0);
-            if (key != K64) {
-                ok = key > K64;
+        const uint64_t pos = quad_x0_finish<QW, KO, W>(a, q, Kmine, x0, known, key0, p0, &probes);
+        a.out_pos[i] = pos;
+        if (a.out_probes) a.out_probes[i] = probes;
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+
+// quad_x0_finish for a query of m <= 32 chars on fused leaves: the 32-char key and the
+// suffix length decide every entry (sector_ge's m <= 32 case), so no text is compared
+__device__ __forceinline__ uint64_t quad_short_finish(const SearchArgs& a, uint64_t K64, uint32_t m, uint64_t x0,
+                                                      bool known, bool eq0, uint64_t p0, uint32_t* probes) {
+    const uint64_t sa_n = a.sa_n;
+    auto pred = [&](uint64_t y, uint64_t* py) -> bool {
+        const uint4 e = a.quad_leaves[y];
+        const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+        *py = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+        if (key != K64) return key > K64;
+        return a.n - *py >= (uint64_t)m;
+    };
+    if (x0 >= sa_n) return a.next_pos;
+    bool ok;
+    if (known) {
+        ok = !eq0 || a.n - p0 >= (uint64_t)m;
+    } else {
+        ok = pred(x0, &p0);
+        (*probes)++;
+    }
+    if (ok) return p0;
+    // rare: exponential + binary search over x0+1 ..
+    uint64_t lo = x0 + 1, hi = sa_n, step = 1, py;
+    while (lo < sa_n) {
+        hi = lo + step - 1;
+        if (hi >= sa_n) { hi = sa_n; break; }
+        (*probes)++;
+        if (pred(hi, &py)) break;
+        lo = hi + 1;
+        step *= 2;
+        hi = sa_n;
+    }
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        (*probes)++;
+        if (pred(mid, &py)) hi = mid;
+        else lo = mid + 1;
+    }
+    if (lo >= sa_n) return a.next_pos;
+    (*probes)++;
+    pred(lo, &py);
+    return py;
+}
+
+// ------------------------------------------------------------------ QUAD_LLCP
+// configs[2] as one kernel (SAS_ALGO_QUAD_LLCP): QUAD's descent over the fused 32-char keys,
+// and where the routed leaf does not settle the query, Manber-Myers LLCP skipping
+// (the SAS_BUILD_LLCP entries, as stree_tail<.., true>) inside the run of suffixes that share
+// q's key.  Absolute layout (quad_fan 17: 16-char left-max separators), fused leaves.
+//
+// The descent routes on q's 16-char key K16, so leaf k holds the first suffix whose 16-char key
+// is >= K16 (s0 = 4k + count(key16 < K16)), and every suffix before it has key16 < K16.  At
+// every inner node the group also counts the separators <= K16: the first level where that
+// count exceeds the < K16 one is where the path of K16 + 1 leaves q's path (a run of equal
+// 16-char keys spans at most a few leaves, so the paths part near the leaves), and the
+// suffixes past q's 16-char run are found by descending from there -- one or two requests
+// instead of a second descent from the root.  From the leaves' 32-char keys:
+//   L0 = 4k + count(key64 < K64): every suffix before L0 is < q;
+//   U  = the first suffix whose key64 > K64 (leaf k, or the leaf of K16 + 1 when it holds a
+//        key <= K64), else the end s1 of the 16-char run: every suffix from U on is > q.
+// A query that the leaf settles (the common case on random text: U <= L0 + 1) costs QUAD's
+// reads and at most one text compare (k_sa_quad4x's).  Otherwise the LLCP walk runs from the
+// root of the entries' implicit binary-search tree: a mid below L0 goes right and one at or
+// past U goes left with no read; a mid in [L0, U) reads its 16-B entry.  A bound that no read
+// measured takes an lcp as stree_tail does -- the entry's own Llcp / Rlcp, which makes that
+// side tie (so the probe compares from there) -- except a left bound inside leaf k, whose exact
+// lcp with q the leaf's 32-char key gives (min(first differing char, suffix length)).  That
+// substitution is sound because every mid read lies in q's 16-char run [s0, s1), and in q's
+// 32-char run when both L0 and U are exact at 32 chars (kappa = 32): then a ties' compare
+// starts at char kappa (a suffix shorter than kappa in the run is a proper prefix of q).
+// Queries of <= 32 chars in a ragged batch finish as k_sa_quad4x's do (their 32-char key
+// decides every entry).  out_probes: inner levels + leaves + entries + text compares read.
+template <int QW, class Q>
+__device__ __forceinline__ bool qllcp_tie_less(const SearchArgs& a, uint64_t p, const Q& q, uint32_t hh, uint32_t inl,
+                                               uint32_t kappa, uint32_t* lcp) {
+    const uint64_t lenS = a.n - p;
+    if (lenS < kappa) {  // its padded key matched q's: a proper prefix of q (m > 32)
+        *lcp = (uint32_t)lenS;
+        return true;
+    }
+    uint32_t h = kappa;
+    if (hh + 16 > kappa) {
+        // llcp_tie_less: the entry's 16 chars after hh first (those below kappa compare equal)
+        const uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
+        if (hh < L) {
+            const uint32_t c = L - hh < 16 ? L - hh : 16;
+            const uint32_t mk = ~0u << (32 - 2 * c);
+            const uint32_t av = inl & mk, bv = (uint32_t)(q.chars32(hh) >> 32) & mk;
+            if (av != bv) {
+                *lcp = hh + (uint32_t)(__clz(av ^ bv) >> 1);
+                return av < bv;
+            }
+        }
+        h = hh + 16;
+    }
+    return suffix_less_from<QW>(a.tw, a.n, p, q, h, lcp);
+}
+
+#define QLLCP_NONE 0xFFu
+// k_sa_quad_llcp's workgroup size (two workgroups a CU): 768 -> 6 waves a SIMD, 80 VGPRs;
+// 512 -> 4 waves, 128 VGPRs
+#ifndef SAS_QLLCP_BLOCK
+#define SAS_QLLCP_BLOCK 768
+#endif
+// ... for m > 64 (4 or 8 query words in registers)
+#ifndef SAS_QLLCP_BLOCK_LONG
+#define SAS_QLLCP_BLOCK_LONG 768
+#endif
+#define QLLCP_BLOCK(QW) ((QW) <= 2 ? SAS_QLLCP_BLOCK : SAS_QLLCP_BLOCK_LONG)
+// descent on K16 recording where K16 + 1's path parts from it (level, node index one level down)
+__device__ __forceinline__ uint32_t quad_descend_split(const SearchArgs& a, const uint4* s_nodes, uint32_t K16,
+                                                       uint32_t sub, uint32_t* dlev, uint32_t* dnode) {
+    uint32_t k = 0, dl = QLLCP_NONE, dn = 0;
+    auto step = [&](uint4 v, uint32_t h) {
+        const uint32_t lt = (v.x < K16) + (v.y < K16) + (v.z < K16) + (v.w < K16);
+        const uint32_t le = (v.x <= K16) + (v.y <= K16) + (v.z <= K16) + (v.w <= K16);
+        const uint32_t cc = quad_sum(lt | (le << 8));
+        const uint32_t c = cc & 0xFFu, c2 = cc >> 8;
+        if (dl == QLLCP_NONE && c2 > c) {
+            dl = h;
+            dn = k * SAS_QUAD_FAN + c2;
+        }
+        k = k * SAS_QUAD_FAN + c;
+    };
+#pragma unroll
+    for (uint32_t h = 0; h < SAS_QUAD_MAX_LDS; h++)
+        if (h < a.quad_lds_layers) step(s_nodes[((uint32_t)a.quad_off[h] + k) * 4 + sub], h);
+#pragma unroll
+    for (uint32_t h = 0; h < SAS_QUAD_MAX_INNER; h++) {
+        if (h >= a.quad_lds_layers && h < a.quad_inner_layers) {
+            const uint4* pv = a.quad_inner + (a.quad_off[h] + k) * 4 + sub;
+            step(h >= a.quad_nt_from ? nt_load4(pv) : *pv, h);
+        }
+    }
+    *dlev = dl;
+    *dnode = dn;
+    return k;
+}
+
+// K16 + 1's descent from node k of level h0 (separators <= K16 = < K16 + 1)
+__device__ __forceinline__ uint32_t quad_descend_from(const SearchArgs& a, const uint4* s_nodes, uint32_t h0,
+                                                      uint32_t k, uint32_t K16, uint32_t sub) {
+#pragma unroll
+    for (uint32_t h = 0; h < SAS_QUAD_MAX_LDS; h++) {
+        if (h >= h0 && h < a.quad_lds_layers) {
+            const uint4 v = s_nodes[((uint32_t)a.quad_off[h] + k) * 4 + sub];
+            k = k * SAS_QUAD_FAN + quad_sum((v.x <= K16) + (v.y <= K16) + (v.z <= K16) + (v.w <= K16));
+        }
+    }
+#pragma unroll
+    for (uint32_t h = 0; h < SAS_QUAD_MAX_INNER; h++) {
+        if (h >= h0 && h >= a.quad_lds_layers && h < a.quad_inner_layers) {
+            const uint4* pv = a.quad_inner + (a.quad_off[h] + k) * 4 + sub;
+            const uint4 v = h >= a.quad_nt_from ? nt_load4(pv) : *pv;
+            k = k * SAS_QUAD_FAN + quad_sum((v.x <= K16) + (v.y <= K16) + (v.z <= K16) + (v.w <= K16));
+        }
+    }
+    return k;
+}
+
+// the per-query state a lane keeps between the group steps, packed (k_sa_quad_llcp)
+#define QL_C16(st) ((st) & 7u)           // leaf k's keys16 < K16
+#define QL_C64(st) (((st) >> 3) & 7u)    // leaf k's keys64 < K64 (4: none >= K64 in it)
+#define QL_FU(st) (((st) >> 6) & 7u)     // U = 4 kU + FU
+#define QL_KNOWN (1u << 9)               // leaf k holds a key >= K64 (L0 exact at 32 chars)
+#define QL_EQ0 (1u << 10)                // ... and it is K64
+#define QL_UK (1u << 11)                 // U known
+#define QL_X32 (1u << 12)                // U exact at 32 chars too: q's 32-char run
+#define QL_LAM0 (1u << 13)               // entry L0 compared below q: L0 + 1, its lcp in lcp0
+#define QL_END (1u << 14)                // q's 16-char run reaches the end: U = sa_n
+#define QL_DLEV(st) ((st) >> 24)         // where K16 + 1's path parts from q's (QLLCP_NONE: not)
+
+// EXACT: launched only with m <= 32 QW (QueryRegsExact: no repacking from the bytes);
+// R32: sa_n < 2^32, the walk's ranks in 32 bits
+template <int QW, bool EXACT, bool R32>
+__global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp(SearchArgs a) {
+    using QR = typename std::conditional<EXACT, QueryRegsExact<QW>, QueryRegs<QW>>::type;
+    __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
+    stage_quad_top(a, s_nodes);
+    uint32_t bad = 0;
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const int lane0 = (int)((threadIdx.x & 63) & ~3u);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t gi = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) - sub; gi < a.nq; gi += stride) {
+        const uint64_t i = gi + sub;
+        const bool mine = i < a.nq;
+        const uint8_t* qb;
+        uint32_t m = 0;
+        QR q;
+        if (mine) {
+            query_ptr(a, i, &qb, &m);
+            q.load(qb, m, &bad);
+        } else {
+            q.bytes = a.qbytes;
+            q.m = 0;
+            for (int j = 0; j < QW; j++) q.w[j] = 0;
+        }
+        const uint64_t Kmine = q.w[0];
+        uint32_t probes = a.quad_inner_layers + 1;
+        // this lane's query, from its group step: leaf k, the leaf kU of U, the packed counts and
+        // flags (QL_*), leaf k's entries' lcps with q (8 bits each), K16 + 1's node below its
+        // parting level, and the SA values at L0 and U when a leaf read delivered them
+        uint32_t kq = 0, kU = 0, st = 0, lam = 0, dnode = 0;
+        uint64_t p0 = QUAD_NO_SA;
+        for (uint32_t j = 0; j < QUAD_G; j++) {
+            if (gi + j >= a.nq) break;  // group-uniform
+            const uint64_t K64 = __shfl((unsigned long long)Kmine, lane0 + (int)j, 64);
+            const uint32_t K16 = (uint32_t)(K64 >> 32);
+            uint32_t dl, dn;
+            const uint32_t k = quad_descend_split(a, s_nodes, K16, sub, &dl, &dn);
+            const uint4 e = quad_leaf_load(a, a.quad_leaves + 4 * (uint64_t)k + sub);
+            const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+            const uint32_t cc = quad_sum((uint32_t)(e.y < K16) | ((uint32_t)(key < K64) << 8) |
+                                         ((uint32_t)(key <= K64) << 16));
+            const uint32_t c16 = cc & 0xFFu, c64 = (cc >> 8) & 0xFFu, le64 = cc >> 16;
+            // this entry's lcp with q: min(first differing char of the 32-char keys, length)
+            uint32_t d = key == K64 ? 32u : (uint32_t)__clzll(key ^ K64) >> 1;
+            if (4 * (uint64_t)k + sub < a.sa_n) {
+                const uint64_t len = a.n - ((uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32));
+                if ((uint64_t)d > len) d = (uint32_t)len;
+            }
+            const uint32_t lamj = quad_sum(d << (8 * sub));  // disjoint bytes: the sum is the OR
+            const uint32_t eq0 = (uint32_t)__shfl((int)(e.x == (uint32_t)K64 && e.y == K16), lane0 + (int)(c64 & 3), 64);
+            const uint32_t z0 = (uint32_t)__shfl((int)e.z, lane0 + (int)(c64 & 3), 64);
+            const uint32_t w0 = (uint32_t)__shfl((int)e.w, lane0 + (int)(c64 & 3), 64);
+            if (sub == j) {
+                kq = k;
+                kU = k;
+                lam = lamj;
+                dnode = dn;
+                st = c16 | (c64 << 3) | (dl << 24);
+                if (c64 < 4) {
+                    st |= QL_KNOWN | QL_X32 | (eq0 ? QL_EQ0 : 0u);
+                    p0 = (uint64_t)z0 | ((uint64_t)(w0 & 0xFFu) << 32);
+                }
+                if (le64 < 4) {  // leaf k holds the first key > K64
+                    st |= QL_UK | (le64 << 6);
+                } else if (K16 == 0xFFFFFFFFu) {  // q's 16-char run reaches the end
+                    st = (st & ~QL_X32) | QL_UK | QL_END;
+                }
+            }
+        }
+        uint64_t pos = 0;
+        bool done = !mine;
+        uint32_t lcp0 = 0;
+        if (mine && m <= 32) {
+            // the 32-char key decides every entry: k_sa_quad4x's finish
+#ifdef QLLCP_NO_FINISH
+            pos = p0;
+#else
+            pos = quad_short_finish(a, Kmine, m, 4 * (uint64_t)kq + QL_C64(st), (st & QL_KNOWN) != 0,
+                                    (st & QL_EQ0) != 0, p0, &probes);
+#endif
+            done = true;
+        } else if (mine && 4 * (uint64_t)kq + QL_C64(st) >= a.sa_n) {
+            pos = a.next_pos;
+            done = true;
+        } else if (mine && (st & QL_KNOWN)) {
+            // the first suffix not below q's 32-char key: > it, or one compare from char 32
+            // (k_sa_quad4x's common case); below q, it is the walk's exact left bound
+            if (!(st & QL_EQ0) || (probes++, !suffix_less_from<QW>(a.tw, a.n, p0, q, 32, &lcp0))) {
+                pos = p0;
+                done = true;
             } else {
-                if (p0 == QUAD_NO_SA) p0 = quad_entry_sa<KO, W>(a, x0);
-                ok = sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, p0, K64, a, q);
+                st |= QL_LAM0;
             }
-            if (!known) probes++;
         }
-        uint64_t x = x0;
-        if (!ok && x0 < sa_n) {  // rare: exponential + binary search over x0+1 ..
-            auto pred = [&](uint64_t y) -> bool {
-                const uint64_t key = quad_entry_key<KO>(a, y);
-                if (key != K64) return key > K64;
-                return sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
-            };
-            uint64_t lo = x0 + 1, hi = sa_n, step = 1;
-            while (lo < sa_n) {
-                hi = lo + step - 1;
-                if (hi >= sa_n) { hi = sa_n; break; }
-                probes++;
-                if (pred(hi)) break;
-                lo = hi + 1;
-                step *= 2;
-                hi = sa_n;
+        // U for the queries whose 32-char run leaves leaf k: the leaf of K16 + 1, from where its
+        // path parts from q's (near the leaves: one or two requests)
+#ifdef QLLCP_NO_NEEDU
+        const bool needU = false;
+#else
+        const bool needU = !done && !(st & QL_UK);
+#endif
+        for (uint32_t j = 0; j < QUAD_G; j++) {
+            if (!(quad_mask(needU) & (1u << j))) continue;  // group-uniform
+            const uint64_t K64 = __shfl((unsigned long long)Kmine, lane0 + (int)j, 64);
+            const uint32_t K16 = (uint32_t)(K64 >> 32);
+            const uint32_t dl = (uint32_t)__shfl((int)st, lane0 + (int)j, 64) >> 24;
+            uint32_t ku = (uint32_t)__shfl((int)kq, lane0 + (int)j, 64);
+            if (dl != QLLCP_NONE) {
+                ku = quad_descend_from(a, s_nodes, dl + 1, (uint32_t)__shfl((int)dnode, lane0 + (int)j, 64), K16, sub);
+                if (sub == j) probes += a.quad_inner_layers - dl;
             }
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                probes++;
-                if (pred(mid)) hi = mid;
-                else lo = mid + 1;
+            const uint4 eU = quad_leaf_load(a, a.quad_leaves + 4 * (uint64_t)ku + sub);
+            const uint64_t keyU = (uint64_t)eU.x | ((uint64_t)eU.y << 32);
+            const uint32_t cu = quad_sum((uint32_t)(keyU <= K64) | ((uint32_t)(eU.y <= K16) << 8));
+            const uint32_t le64U = cu & 0xFFu, le16U = cu >> 8;
+            // a key <= K64 in the leaf: everything before it is too, and the next one is the
+            // first key > K64; none: the 16-char run's end, exact at 16 chars
+            const uint32_t f = le64U ? le64U : le16U;
+            if (sub == j) {
+                kU = ku;
+                st = (st & ~(7u << 6)) | (f << 6) | QL_UK;
+                if (!le64U) st &= ~QL_X32;
             }
-            x = lo;
-            p0 = QUAD_NO_SA;
         }
-        uint64_t pos;
-        if (x >= sa_n) pos = a.next_pos;
-        else pos = (p0 != QUAD_NO_SA) ? p0 : quad_entry_sa<KO, W>(a, x);
+        if (!mine) continue;
+        if (!done) {
+            using rk_t = typename std::conditional<R32, uint32_t, uint64_t>::type;
+            const rk_t sa_n = (rk_t)a.sa_n;
+            const rk_t kb = 4 * (rk_t)kq;
+            const rk_t s0 = kb + QL_C16(st);
+            const rk_t L0 = kb + QL_C64(st) + ((st & QL_LAM0) ? 1 : 0);
+            rk_t U = (st & QL_END) ? sa_n : 4 * (rk_t)kU + QL_FU(st);
+            if (U >= sa_n) U = sa_n;
+            const uint32_t kappa = (st & QL_X32) ? 32u : 16u;
+            rk_t l = 0, r = sa_n;
+            uint64_t pr = QUAD_NO_SA;
+            uint32_t llcp = 0, rlcp = 0;
+            for (;;) {
+                rk_t mid = 0;
+                while (l < r) {  // ALU only, as stree_tail
+                    mid = (l + r) >> 1;
+                    if (mid < L0) l = mid + 1;
+                    else if (mid >= U) r = mid;
+                    else break;
+                }
+                if (!(l < r)) break;
+                const uint4 e = a.llcp[mid];
+                const uint32_t x = (e.y >> 8) & SAS_LLCP_CAP, y = e.y >> 20;
+                if (l <= s0) llcp = x;  // SA[l - 1] before q's 16-char run (or l = 0)
+                else if (l <= L0)       // in leaf k, below q: exact
+                    llcp = ((st & QL_LAM0) && l == L0) ? lcp0 : (lam >> (8 * (uint32_t)(l - 1 - kb))) & 0xFFu;
+                if (r >= U) rlcp = y;   // SA[r] past q's run (or r = sa_n)
+                probes++;
+                bool lt;
+                uint32_t lcp, hh = 0, inl = 0;
+                bool decided = true;
+                if (llcp >= rlcp) {
+                    if (x > llcp) { lt = true; lcp = llcp; }
+                    else if (x < llcp && x < SAS_LLCP_CAP) { lt = false; lcp = x; }
+                    else { decided = false; hh = x; inl = e.z; }
+                } else {
+                    if (y > rlcp) { lt = false; lcp = rlcp; }
+                    else if (y < rlcp && y < SAS_LLCP_CAP) { lt = true; lcp = y; }
+                    else { decided = false; hh = y; inl = e.w; }
+                }
+                const uint64_t p = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32);
+#ifdef QLLCP_NO_TIE
+                if (!decided) { lt = p & 1; lcp = hh + inl; }
+#else
+                if (!decided) lt = qllcp_tie_less<QW, QR>(a, p, q, hh, inl, kappa, &lcp);
+#endif
+                if (lt) {
+                    l = mid + 1;
+                    llcp = lcp;
+                } else {
+                    r = mid;
+                    rlcp = lcp;
+                    pr = p;
+                }
+            }
+            if (r >= sa_n) pos = a.next_pos;
+            else if (pr != QUAD_NO_SA) pos = pr;
+            else {
+                const uint4 eu = a.llcp[r];
+                pos = (uint64_t)eu.x | ((uint64_t)(eu.y & 0xFFu) << 32);
+                probes++;
+            }
+        }
         a.out_pos[i] = pos;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -2693,15 +3071,18 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
     // PLAIN, LLCP and INLINE read the pivot levels past the LDS ones from the prefix-relative
     // blocks, which the build makes wherever the array has such levels
-    const bool coop = (algo == SAS_ALGO_QUAD || (algo == SAS_ALGO_STREE && !SAS_STREE_PERLANE)) && qw == 1;
+    const bool coop = (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_QUAD_LLCP ||
+                       (algo == SAS_ALGO_STREE && !SAS_STREE_PERLANE)) && qw == 1;
     // inline prefix tables with G slots: G lanes per query
     const uint64_t g = (algo == SAS_ALGO_PREFIX && x->prefix_w >= 32) ? x->prefix_w / 16 : 1;
     const uint64_t lanes = a.nq * (coop ? QUAD_G : g);
     // k_sa_binary (PLAIN / LCP / LLCP, any SA width) and the S-tree kernels have their own
     // workgroup shape
     const bool bin = algo == SAS_ALGO_PLAIN || algo == SAS_ALGO_LCP || algo == SAS_ALGO_LLCP ||
-                     algo == SAS_ALGO_STREE || algo == SAS_ALGO_STREE_LLCP;
-    const uint64_t bs = bin ? SAS_BIN_BLOCK : SEARCH_BLOCK;
+                     algo == SAS_ALGO_STREE || algo == SAS_ALGO_STREE_LLCP || (algo == SAS_ALGO_QUAD_LLCP && qw > 1);
+    const bool qx = algo == SAS_ALGO_QUAD_LLCP && qw > 1;  // k_sa_quad_llcp: exact QW, or two words (QLLCP_BLOCK(2))
+    const bool qx_exact = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
+    const uint64_t bs = qx ? (qx_exact ? QLLCP_BLOCK(qw) : QLLCP_BLOCK(2)) : bin ? SAS_BIN_BLOCK : SEARCH_BLOCK;
     uint64_t blocks = (lanes + bs - 1) / bs;
     uint64_t cap = (uint64_t)x->num_cus * (bin ? SAS_BIN_BPC : BLOCKS_PER_CU);
     if (blocks > cap) blocks = cap;
@@ -2744,6 +3125,30 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
         else launch_interp<4, false>(qw, grid, block, st, a, range);
     } else if (x->sa_w == 8) {
         launch_w8(algo, top, qw, grid, block, st, a);
+    } else if (algo == SAS_ALGO_QUAD_LLCP) {
+        // m <= 32: QUAD (the 32-char key decides); longer: k_sa_quad_llcp (fused leaves, any SA width:
+        // the leaves and the LLCP entries carry 40-bit positions), with every query word in
+        // registers when the batch's longest query is known to fit them, else two words and the
+        // rest repacked from the bytes
+        const bool exact = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
+        if (qw > 1 && !exact) {
+            if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<2, false, true>), grid, block, 0, st, a);
+            else hipLaunchKernelGGL((k_sa_quad_llcp<2, false, false>), grid, block, 0, st, a);
+        } else switch (qw) {
+            case 1: hipLaunchKernelGGL((k_sa_quad<1, false, 4>), grid, block, 0, st, a); break;
+            case 2:
+                if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<2, true, true>), grid, block, 0, st, a);
+                else hipLaunchKernelGGL((k_sa_quad_llcp<2, true, false>), grid, block, 0, st, a);
+                break;
+            case 4:
+                if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<4, true, true>), grid, block, 0, st, a);
+                else hipLaunchKernelGGL((k_sa_quad_llcp<4, true, false>), grid, block, 0, st, a);
+                break;
+            default:
+                if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<8, true, true>), grid, block, 0, st, a);
+                else hipLaunchKernelGGL((k_sa_quad_llcp<8, true, false>), grid, block, 0, st, a);
+                break;
+        }
     } else if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
         if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
         else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);
@@ -2825,7 +3230,7 @@ static void fill_args(const sas_index* x, SearchArgs& a) {
 // Algorithm / index / flag compatibility, shared by the search entry points.
 static int check_algo(const sas_index* x, int algo, uint32_t flags, const char* where) {
     const std::string w(where);
-    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_STREE_LLCP) SAS_FAIL(EINVAL, w + ": unknown algo");
+    if (algo < SAS_ALGO_PLAIN || algo > SAS_ALGO_QUAD_LLCP) SAS_FAIL(EINVAL, w + ": unknown algo");
     if ((flags & SAS_PREFIX_RANGE) &&
         (!x->prefix || (algo != SAS_ALGO_PLAIN && algo != SAS_ALGO_LCP && algo != SAS_ALGO_INTERP)))
         SAS_FAIL(EINVAL, "SAS_PREFIX_RANGE: PLAIN / LCP / INTERP on an index with SAS_BUILD_PREFIX");
@@ -2836,6 +3241,10 @@ static int check_algo(const sas_index* x, int algo, uint32_t flags, const char* 
     if (algo == SAS_ALGO_STREE && !x->stree) SAS_FAIL(EINVAL, w + ": SAS_ALGO_STREE needs SAS_BUILD_STREE");
     if (algo == SAS_ALGO_STREE_LLCP && (!x->stree || !x->llcp))
         SAS_FAIL(EINVAL, w + ": SAS_ALGO_STREE_LLCP needs SAS_BUILD_STREE and SAS_BUILD_LLCP");
+    if (algo == SAS_ALGO_QUAD_LLCP &&
+        (!x->quad_leaves || x->quad_compact || x->quad_fan != SAS_QUAD_FAN || !x->llcp || x->sa_w == 8))
+        SAS_FAIL(EINVAL, w + ": SAS_ALGO_QUAD_LLCP needs SAS_BUILD_LLCP and SAS_BUILD_QUAD with fused leaves in the "
+                             "absolute layout (SAS_BUILD_QUAD_ABS)");
     if (algo == SAS_ALGO_SECTOR && !x->sec_leaves) SAS_FAIL(EINVAL, w + ": SAS_ALGO_SECTOR needs SAS_BUILD_SECTOR");
     if (algo == SAS_ALGO_TAGGED && !x->tag_table && !x->tag_lines)
         SAS_FAIL(EINVAL, w + ": SAS_ALGO_TAGGED needs SAS_BUILD_TAGGED");
@@ -2942,6 +3351,7 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
                 memcpy(sl.h_in + b, src + b, std::min(piece, in_bytes - b));
             };
             if (mode == HM_FIXED) qw = qw_for(m);
+            a.m_max = mode == HM_FIXED ? m : 0;
         } else if (mode == HM_PACK) {
             // smaller chunks than the byte modes: the host packing is the longest stage, and
             // the pipeline fills and drains faster
@@ -2975,6 +3385,7 @@ static int host_pipeline(const sas_index* x, int mode, const uint8_t* qbytes, co
                 for (uint64_t j = b; j < ee; j++) memcpy(sl.h_in + sl.h_off[j], qbytes + qoff[s0 + j], sl.h_len[j]);
             };
             qw = qw_for(maxlen);
+            a.m_max = maxlen ? maxlen : 1;
         }
         // h_out of this slot is read by the copy-out pieces before the new chunk's D2H is
         // queued below, so both can run in one job
@@ -3145,6 +3556,7 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
         a.out_pos = out_pos;
         a.out_probes = out_probes;
         if (!ragged) qw = qw_for(m_fixed);
+        a.m_max = ragged ? 0 : m_fixed;
     } else {
         uint64_t span;
         uint64_t maxlen = m_fixed;
@@ -3160,6 +3572,7 @@ static int search_impl(const sas_index* x, const uint8_t* qbytes, const uint64_t
             span = nq * (uint64_t)m_fixed;
         }
         qw = qw_for(maxlen);
+        a.m_max = maxlen ? (uint32_t)maxlen : 1;
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMalloc(&bqb.p, span + 64));
         if (span) HIP_TRY(hipMemcpy(bqb.p, qbytes, span, hipMemcpyHostToDevice));
@@ -3298,6 +3711,7 @@ extern "C" int sas_search_buckets(const sas_index* x, const void* queries, uint3
     fill_args(x, a);
     a.nq = nq;
     a.m_fixed = m;
+    a.m_max = m;
     a.bad = x->scratch;  // device pointers: codes unchecked, as sas_search_fixed without SAS_VALIDATE
     if (packed) a.qwords = static_cast<const uint64_t*>(queries);
     else a.qbytes = static_cast<const uint8_t*>(queries);
@@ -3318,6 +3732,7 @@ extern "C" int sas_time_fixed(const sas_index* x, const uint8_t* d_qbytes, uint3
     fill_args(x, a);
     a.nq = nq;
     a.m_fixed = m;
+    a.m_max = m;
     a.qbytes = d_qbytes;
     a.out_pos = d_out_pos;
     a.bad = x->scratch;
@@ -3905,6 +4320,7 @@ static int range_impl(const sas_index* x, const uint8_t* qbytes, uint32_t m_fixe
             }
         }
         qw = qw_for(maxlen);
+        a.m_max = maxlen ? (uint32_t)maxlen : 1;
         HIP_TRY(hipStreamSynchronize(st));
         HIP_TRY(hipMalloc(&bqb.p, span + 64));
         if (span) HIP_TRY(hipMemcpy(bqb.p, qbytes, span, hipMemcpyHostToDevice));

@@ -56,7 +56,7 @@ def SAS_BUILD_PREFIX_P(p: int) -> int:
 
 SAS_MULTI_REPLICATE, SAS_MULTI_SHARD = 0, 1
 ALGOS = {"plain": 0, "lcp": 1, "stree": 2, "sector": 3, "quad": 4, "inline": 5, "llcp": 6, "prefix": 7,
-         "interp": 8, "tagged": 9, "stree_llcp": 10}
+         "interp": 8, "tagged": 9, "stree_llcp": 10, "quad_llcp": 11}
 
 SST_SORTED, SST_EYTZINGER, SST_STREE16, SST_STREE15, SST_PARTITIONED_MAP, SST_DIRECT_MAP = 0, 1, 2, 3, 4, 5
 SST_PARTITIONED, SST_PARTITIONED_COMPACT, SST_PARTITIONED_L1, SST_PARTITIONED_OVERLAP = 6, 7, 8, 9

@@ -29,9 +29,12 @@ The capacity is agreed by a collective that every rank runs: once, in the constr
 a declared `max_nq` (steps of at most that many queries then run no extra collective), or
 at the start of every step otherwise.  Ranks may pass different batch sizes either way.
 
-At world size 1 every query is the rank's own: the exchanges are the identity, so the step
-routes, searches and gathers with no collective (`exchange_self=True` sends them through the
-process group anyway, which is how the world-1 RCCL test exercises the exchange path).
+At world size 1 every query is the rank's own: the exchanges are the identity, and so are the
+route (one bucket) and the gather (slot = query index), so the step is the local lookup of the
+query batch itself (round 6: 0.49 -> ~0.31 ms per 10^7 at n = 2^32).  `routed=True` keeps the
+route + identity exchange + gather shape (what each rank of a W > 1 step runs), and
+`exchange_self=True` also sends the exchanges through the process group, which is how the
+world-1 RCCL test exercises the exchange path.
 """
 from __future__ import annotations
 
@@ -53,7 +56,7 @@ class ShardedSearch:
 
     def __init__(self, index, dist, world: int, rank: int, device, algo: str = "stree", group=None,
                  slack: float | None = None, min_cap: int = 256, chunks: int = 1, max_nq: int | None = None,
-                 exchange_self: bool = False):
+                 exchange_self: bool = False, routed: bool = False):
         """chunks > 1: a step cuts its batch into that many pieces and overlaps one piece's
         exchanges (all_to_all_single with async_op, on the collective's own stream) with
         another's routing, lookup and gather.  Every rank must use the same value.
@@ -67,6 +70,8 @@ class ShardedSearch:
         self.slack = self.SLACK if slack is None else slack
         self.min_cap = min_cap
         self.exchange = world > 1 or exchange_self
+        # world 1 without exchange: route and gather are the identity too (routed=False)
+        self.identity = not self.exchange and not routed
         self._sa_width = index.stats().get("sa_width", 4) if hasattr(index, "stats") else 4
         first = torch.tensor([int(index.suffix_array(1)[0])], dtype=torch.int64, device=device)
         firsts = [torch.empty_like(first) for _ in range(world)]
@@ -171,6 +176,8 @@ class ShardedSearch:
     def search_fixed(self, qbytes, m: int, check: bool = True, out=None):
         """qbytes: uint8 tensor [nq*m] of this rank's queries -> int64 positions (written
         into `out` when given)."""
+        if self.identity:
+            return self._search_identity(qbytes, m, out)
         if not hasattr(self.index, "route_pack"):
             return self.search_fixed_exact(qbytes, m)
         if self.chunks > 1 and hasattr(self.index, "shard_gather"):
@@ -203,6 +210,21 @@ class ShardedSearch:
             if int(flag.item()):
                 exact = self.search_fixed_exact(qbytes, m)
                 return out.copy_(exact) if out is not None else exact
+        return out
+
+    def _search_identity(self, qbytes, m: int, out):
+        """World 1: every query is this rank's and lands in bucket 0 at its own index, so the
+        lookup runs on the batch as given and its positions are the answer (no route, no
+        gather; one piece whatever `chunks` says: there is no exchange to overlap)."""
+        import torch
+        nq = qbytes.numel() // m
+        out = self.index.search_fixed(qbytes, m, algo=self.algo, out=out)
+        key = ("identity", nq)
+        if key not in self._bufs:
+            self._bufs[key] = torch.full((1,), nq, dtype=torch.int64, device=self.device)
+        # the one bucket this rank "received" (c4_proof samples it)
+        self.last = {"recv": qbytes, "rcounts": self._bufs[key], "local": out, "cap": max(nq, 1), "m": m,
+                     "packed": False}
         return out
 
     def _search_pipelined(self, qbytes, m: int, check: bool, out):

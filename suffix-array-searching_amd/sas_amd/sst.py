@@ -17,7 +17,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import check, lib
+from ._lib import SasError, check, lib
 
 MAX = 0x7FFFFFFF  # sst/node.rs:5
 
@@ -68,14 +68,23 @@ class _Index:
         return out[:words]
 
     def query(self, qs, want_rank: bool = False, stream=None, flags: int = 0, out=None):
+        """out: (device queries only) a caller-owned 4-byte result tensor of at least qs.numel()
+        elements, contiguous, on qs's device; host queries refuse it (they return a new array)."""
         if _is_cuda(qs):
             import torch
-            out = torch.empty(qs.numel(), dtype=torch.int32, device=qs.device) if out is None else out
+            if out is None:
+                out = torch.empty(qs.numel(), dtype=torch.int32, device=qs.device)
+            elif not (_is_cuda(out) and out.device == qs.device and out.element_size() == 4 and
+                      out.is_contiguous() and out.numel() >= qs.numel()):
+                raise SasError(22, "sst query: out must be a contiguous 4-byte tensor on the queries' device "
+                                   f"with >= {qs.numel()} elements")
             rank = torch.empty(qs.numel(), dtype=torch.int64, device=qs.device) if want_rank else None
             st = stream if stream is not None else torch.cuda.current_stream(qs.device).cuda_stream
             check(lib().sst_query(self._h, qs.data_ptr(), qs.numel(), out.data_ptr(),
                                   rank.data_ptr() if want_rank else None, st, flags | _lib.SST_DEVICE_PTRS))
             return (out, rank) if want_rank else out
+        if out is not None:
+            raise SasError(22, "sst query: out= is for device queries; host queries return a new array")
         qs = np.ascontiguousarray(qs, np.uint32)
         out = np.zeros(max(len(qs), 1), np.uint32)
         rank = np.zeros(max(len(qs), 1), np.uint64) if want_rank else None

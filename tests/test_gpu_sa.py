@@ -19,7 +19,7 @@ from oracle import pyoracle as O
 
 pytestmark = pytest.mark.gpu
 
-ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix", "interp", "stree_llcp")
+ALGOS = ("plain", "lcp", "stree", "sector", "quad", "inline", "llcp", "prefix", "interp", "stree_llcp", "quad_llcp")
 
 
 @pytest.fixture(scope="module")
@@ -169,7 +169,7 @@ def test_llcp_capped_lcps(sas):
     }
     for name, t in texts.items():
         n = len(t)
-        idx = sas.SaNaive.build(t, verify=True, stree=False, sector=False, quad=False)
+        idx = sas.SaNaive.build(t, verify=True, stree=False, sector=False, quad=True, prefix=False)
         assert idx.stats()["llcp_bytes"] == 16 * n
         sa = O.build_sa(t)
         qs = []
@@ -188,7 +188,7 @@ def test_llcp_capped_lcps(sas):
         buf, qo, ql = pack(qs)
         expect = oracle_positions(t, sa, buf[:-64], qo, ql)
         for flags in (0, _lib.SAS_NO_LDS_TOP):
-            for algo in ("plain", "llcp"):
+            for algo in ("plain", "llcp", "quad_llcp"):
                 got, probes = idx.search_batch(buf, qo, ql, algo=algo, probes=True, flags=flags)
                 assert np.array_equal(got, expect), (name, algo, flags, np.nonzero(got != expect)[0][:5])
 
@@ -739,7 +739,7 @@ def test_sa_beyond_u32(sas):
     idx = sas.SaNaive.build(t, lcp=False, stree=True, verify=True, llcp=False)  # LLCP: the second index below
     st = idx.stats()
     assert st["sa_width"] == 5 and st["n"] == n
-    algos = [a for a in ALGOS if a not in ("llcp", "prefix", "interp", "stree_llcp")]  # prefix: u32 ranks; interp: n < 2^32
+    algos = [a for a in ALGOS if a not in ("llcp", "prefix", "interp", "stree_llcp", "quad_llcp")]  # prefix: u32 ranks; interp: n < 2^32
     ht = t.cpu().numpy()
     del t
     torch.cuda.empty_cache()
@@ -1161,8 +1161,9 @@ def test_rel_pivot_blocks(sas):
         assert np.array_equal(pr, pr0), name
         # LCP / LLCP take exact lcps off the same keys (a key below q that may end in padding
         # reads the whole entry); INLINE decides on them with the sector predicate
-        # STREE_LLCP: the S-tree's run of equal 16-char keys, then LLCP over it (long runs here)
-        for algo in ("lcp", "llcp", "inline", "stree_llcp"):
+        # STREE_LLCP: the S-tree's run of equal 16-char keys, then LLCP over it (long runs here);
+        # QUAD_LLCP: the same inside the run of q's 32-char key (or its 16-char run)
+        for algo in ("lcp", "llcp", "inline", "stree_llcp", "quad_llcp"):
             ga, pa = idx.search_batch(buf, qo, ql, algo=algo, probes=True)
             bad = np.nonzero(ga != expect)[0]
             assert len(bad) == 0, (name, algo, bad[:5], [qs[i] for i in bad[:2]])
@@ -1195,8 +1196,150 @@ def test_plain_sa_run_at_array_end(sas):
         shard = sas.SaNaive.build(t, sa=sa, rank_range=(lo, n), lcp=False, stree=False, sector=False, quad=False,
                                   llcp=False, prefix=False)
         got = shard.search_batch(buf, off, lens, algo="plain")
-        # queries whose global lower bound lies in the shard (rank >= lo) get the same answer
+        # queries whose global lower bound lies in the shard (rank >= lo, the boundary rank
+        # included) get the same answer; those below it get the shard's clamped lower bound,
+        # rank 0 of the shard = SA[lo]
         rank_of = {int(p): r for r, p in enumerate(sa)}
         rk = np.array([rank_of.get(int(p), n) for p in expect])
-        sel = rk > lo
+        sel = rk >= lo
         assert np.array_equal(got[sel], expect[sel]), n
+        below = rk < lo
+        assert below.any(), n
+        assert (got[below] == sa[lo]).all(), n
+
+
+def test_quad_llcp_runs(sas):
+    """SAS_ALGO_QUAD_LLCP (k_sa_quad_llcp): QUAD's descent, then LLCP skipping inside the run of
+    q's 32-char key where the routed leaf does not settle it.  A text of 64 copies of a random
+    block with 1% substitutions per copy (the bench's lcp_long repetitive shape, small): runs of
+    equal 32-char keys span many leaves, q's key run and 16-char run differ, and the path of the
+    next 16-char key parts from q's at various levels.  Positive queries of 33..300 chars,
+    one-char mutations past char 16 and past char 32, text-end suffixes shorter than 32 chars
+    inside runs, and a ragged mix with queries of <= 32 chars: positions equal the oracle's
+    binary_search (sas/sa_search.rs:98-112) and PLAIN's.  A relative-layout quad tree is
+    refused (EINVAL)."""
+    from sas_amd import _lib
+    rng = np.random.default_rng(5)
+    blk = sas.random_string(1 << 14, seed=7)
+    copies = []
+    for _ in range(64):
+        c = blk.copy()
+        k = rng.integers(0, len(c), len(c) // 100)
+        c[k] = rng.integers(0, 4, len(k), dtype=np.uint8)
+        copies.append(c)
+    t = np.concatenate(copies)
+    n = len(t)
+    idx = sas.SaNaive.build(t, lcp=True, stree=False, sector=False, quad=True, llcp=True, prefix=False)
+    assert idx.stats()["quad_fan"] == 17
+    sa = idx.suffix_array()
+    qs = []
+    for m in (33, 40, 48, 63, 64, 65, 100, 128, 129, 200, 256, 300):
+        for o in rng.integers(0, n - m - 1, 400):
+            q = t[o:o + m].copy()
+            qs.append(q)
+            for k in (int(rng.integers(16, 32)), int(rng.integers(32, m))):
+                mq = q.copy()
+                mq[k] = (mq[k] + 1 + rng.integers(0, 3)) % 4
+                qs.append(mq)
+    for k in (1, 5, 17, 31, 32, 33, 40):
+        tail = t[n - k:]
+        qs += [np.concatenate([tail, np.zeros(j, np.uint8)]) for j in (0, 1, 40) if k + j > 32]
+        qs += [np.concatenate([tail, np.full(40, 3, np.uint8)])]
+    qs += [t[o:o + m] for o, m in zip(rng.integers(0, n - 40, 2000), rng.integers(0, 33, 2000))]  # <= 32
+    order = rng.permutation(len(qs))
+    qs = [qs[i] for i in order]
+    buf, qo, ql = pack(qs)
+    expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+    got = idx.search_batch(buf, qo, ql, algo="quad_llcp")
+    bad = np.nonzero(got != expect)[0]
+    assert len(bad) == 0, (bad[:5], [qs[i][:40] for i in bad[:2]])
+    assert np.array_equal(got, idx.search_batch(buf, qo, ql, algo="plain"))
+    # fixed-length batches (the lcp_long shape) through the device path
+    import torch
+    for m in (64, 256):
+        off = rng.integers(0, n - m - 1, 5000)
+        qb = np.concatenate([t[o:o + m] for o in off])
+        exp_m = oracle_positions(t, sa, qb, np.arange(len(off), dtype=np.uint64) * m, np.full(len(off), m, np.uint32))
+        dq = torch.from_numpy(qb).cuda()
+        assert np.array_equal(idx.search_fixed(dq, m, algo="quad_llcp").cpu().numpy().astype(np.uint64), exp_m), m
+    idx.free()
+    rel = sas.SaNaive.build(t[: 1 << 16], lcp=True, stree=False, sector=False, llcp=True, prefix=False,
+                            flags=_lib.SAS_BUILD_QUAD_REL)
+    assert rel.stats()["quad_fan"] == 31
+    rb, ro, rl = pack([t[:40]])
+    with pytest.raises(sas.SasError):
+        rel.search_batch(rb, ro, rl, algo="quad_llcp")
+    rel.free()
+
+
+def test_collect_grid_stride(sas):
+    """k_bucket_count / k_bucket_collect stride over their chunks (a dispatch holds < 2^32
+    work-items: the n = 2^36 part build of round 5 failed with "invalid configuration"
+    before).  SAS_COLLECT_GRID caps the grid so that a 2^22-char text takes the same stride
+    loop: the 40-bit whole and part builds through the capped grid equal the uncapped ones."""
+    n = (1 << 22) + 12345
+    t = sas.random_string(n, seed=4)
+    kw = dict(lcp=False, stree=False, sector=False, quad=False, llcp=False, prefix=False)
+    ref = sas.SaNaive.build(t, sa40=True, **kw)
+    sa_ref = ref.suffix_array()
+    ref.free()
+    refp = sas.SaNaive.build_part(t, 1, 3, **kw)
+    part_ref = refp.suffix_array()
+    refp.free()
+    old = os.environ.get("SAS_COLLECT_GRID")
+    try:
+        for g in ("1", "3", "7"):
+            os.environ["SAS_COLLECT_GRID"] = g
+            idx = sas.SaNaive.build(t, sa40=True, verify=True, **kw)
+            assert np.array_equal(idx.suffix_array(), sa_ref), g
+            idx.free()
+            part = sas.SaNaive.build_part(t, 1, 3, **kw)
+            assert np.array_equal(part.suffix_array(), part_ref), g
+            part.free()
+    finally:
+        if old is None:
+            os.environ.pop("SAS_COLLECT_GRID", None)
+        else:
+            os.environ["SAS_COLLECT_GRID"] = old
+    assert O.check_sa(t, sa_ref) == 0
+
+
+def test_llcp_tails_short_suffixes_and_probes(sas):
+    """The two LLCP tails (STREE_LLCP: runs of equal 16-char keys; QUAD_LLCP: of equal 32-char
+    keys, or 16-char ones) substitute an entry's own Llcp / Rlcp for a run bound no compare
+    measured; a text-end suffix shorter than the key inside or beside a run is the case where
+    that substitute falls below the true lcp.  A periodic text ending in a short
+    aperiodic tail and a run of As (text-end suffixes of 1..40 chars whose zero-padded keys
+    equal their neighbours'), queries that are those suffixes (zero-padded and not), queries of
+    m < 16, and mutations: positions equal the oracle's binary_search.  out_probes of the tree
+    algorithms counts memory reads, not the reference's cnt (include/sas.h): every lookup
+    reads at least its descent and leaf, and at most the descent(s), the leaf extension and
+    one LLCP entry per binary-search level."""
+    rng = np.random.default_rng(12)
+    per = rng.integers(0, 4, 23, dtype=np.uint8)
+    t = np.concatenate([np.tile(per, 4000), rng.integers(0, 4, 7, dtype=np.uint8), per[:9],
+                        np.zeros(20, np.uint8), per[:5], np.zeros(3, np.uint8)])
+    n = len(t)
+    idx = sas.SaNaive.build(t, lcp=True, stree=True, sector=False, quad=True, llcp=True, prefix=False)
+    st = idx.stats()
+    sa = idx.suffix_array()
+    qs = []
+    for k in range(1, 41):
+        tail = t[n - k:]
+        qs += [tail, np.concatenate([tail, np.zeros(3, np.uint8)]), np.concatenate([tail, [1]]).astype(np.uint8)]
+    qs += [t[o:o + m] for o, m in zip(rng.integers(0, n - 70, 1500), rng.integers(1, 16, 1500))]
+    qs += [t[o:o + m] for o, m in zip(rng.integers(0, n - 70, 1500), rng.integers(16, 70, 1500))]
+    for q in list(qs[-400:]):
+        mq = q.copy()
+        mq[int(rng.integers(0, len(mq)))] ^= 1
+        qs.append(mq)
+    buf, qo, ql = pack(qs)
+    expect = oracle_positions(t, sa, buf[:-64], qo, ql)
+    lvl = int(np.ceil(np.log2(n))) + 2
+    for algo, layers in (("stree_llcp", st["stree_layers"]), ("quad_llcp", st["quad_layers"])):
+        got, pr = idx.search_batch(buf, qo, ql, algo=algo, probes=True)
+        bad = np.nonzero(got != expect)[0]
+        assert len(bad) == 0, (algo, bad[:5], [qs[i] for i in bad[:2]])
+        assert (pr >= layers).all(), (algo, int(pr.min()))
+        assert (pr <= 2 * layers + 4 + lvl + 2).all(), (algo, int(pr.max()))
+    idx.free()

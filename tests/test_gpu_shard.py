@@ -54,12 +54,17 @@ def test_sharded_nccl_world1(sas):
         qb = queries(t, nq, m, 1)
         expect = full.search_fixed(qb, m, algo="plain")
         dq = torch.from_numpy(qb).cuda()
-        for algo, chunks, xself in (("plain", 1, True), ("quad", 1, True), ("prefix", 1, True), ("prefix", 3, True),
-                                    ("plain", 2, True), ("prefix", 1, False), ("prefix", 2, False)):
+        for algo, chunks, xself, routed in (("plain", 1, True, False), ("quad", 1, True, False),
+                                            ("prefix", 1, True, False), ("prefix", 3, True, False),
+                                            ("plain", 2, True, False), ("prefix", 1, False, True),
+                                            ("prefix", 2, False, True), ("prefix", 1, False, False),
+                                            ("plain", 2, False, False)):
             # prefix: 8-B packed words cross the exchange; chunks > 1: async RCCL pieces;
-            # exchange_self: the world-1 exchanges still go through RCCL (default: identity)
+            # exchange_self: the world-1 exchanges still go through RCCL; routed: route + identity
+            # exchange + gather; neither: the world-1 identity step (the lookup alone)
             eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo=algo, chunks=chunks,
-                                exchange_self=xself, max_nq=nq if chunks == 1 else None)
+                                exchange_self=xself, routed=routed, max_nq=nq if chunks == 1 else None)
+            assert eng.identity == (not xself and not routed)
             assert eng.packed(m) == (algo == "prefix")
             got = eng.search_fixed(dq, m)
             got2 = eng.search_fixed(dq, m, check=False)
@@ -148,16 +153,16 @@ def test_c4_record_shape_world1(sas):
     s.close()
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
     try:
-        for xself in (True, False):
+        for xself, routed in ((True, False), (False, True), (False, False)):
             eng = ShardedSearch(part, dist, 1, 0, torch.device("cuda"), algo="prefix", max_nq=nq,
-                                exchange_self=xself)
+                                exchange_self=xself, routed=routed)
             assert eng.packed(m)
             out = torch.empty(nq, dtype=torch.int64, device="cuda")
             for _ in range(2):
                 eng.search_fixed(qb, m, check=False, out=out)
             eng.assert_no_overflow()
             torch.cuda.synchronize()
-            assert torch.equal(out, expect), xself
+            assert torch.equal(out, expect), (xself, routed)
     finally:
         dist.destroy_process_group()
         part.free()

@@ -206,3 +206,27 @@ def test_query_counts_around_the_grid(sas):
         assert np.array_equal(r, ref_rank[:nq]), nq
     for idx in layouts:
         idx.free()
+
+
+def test_query_out_tensor_checked(sas):
+    """sst query(out=...): a caller-owned result tensor must hold >= nq 4-byte elements,
+    contiguously, on the queries' device (the kernel writes out.data_ptr() directly); host
+    queries refuse out=."""
+    import torch
+    rng = np.random.default_rng(3)
+    vals = gen_vals(1 << 12, rng)
+    idx = sas.STree16.new(vals)
+    qs = torch.from_numpy(rng.integers(0, O.MAX, 1000, dtype=np.uint64).astype(np.uint32).view(np.int32)).cuda()
+    ok = torch.empty(1000, dtype=torch.int32, device="cuda")
+    ref = idx.query(qs.cpu().numpy().view(np.uint32))
+    assert np.array_equal(idx.query(qs, out=ok).cpu().numpy().view(np.uint32), ref)
+    bad = [torch.empty(999, dtype=torch.int32, device="cuda"),            # short
+           torch.empty(1000, dtype=torch.int64, device="cuda"),           # 8-byte elements
+           torch.empty(2000, dtype=torch.int32, device="cuda")[::2],      # not contiguous
+           torch.empty(1000, dtype=torch.int32)]                          # host
+    for o in bad:
+        with pytest.raises(sas.SasError):
+            idx.query(qs, out=o)
+    with pytest.raises(sas.SasError):
+        idx.query(qs.cpu().numpy().view(np.uint32), out=ok)
+    idx.free()

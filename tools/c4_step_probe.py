@@ -1,7 +1,10 @@
 """Where configs[4]'s N = 1 step spends its time: the step as the bench times it (event pair
-around K steps), the host's enqueue time for K steps (no sync inside), each piece alone (route,
-lookup, gather), and the step replayed from a HIP graph (torch.cuda.CUDAGraph; the identity
-exchange at world 1 has no collective).  One JSON line.
+around K steps; round 6: the world-1 identity step, the part's lookup alone), the routed shape
+each rank of a W > 1 step runs (routed=True: route + identity exchange + gather), the host's
+enqueue time for K steps (no sync inside), each piece alone (route, lookup, gather), the route
+and gather at the W = 8 shape on this one part (7 splitters = the SA values at ranks j n / 8,
+8 buckets of 1.125 nq / 8 + 256 slots: what an 8-GPU rank's send and receive sides cost), and
+the routed step replayed from a HIP graph (torch.cuda.CUDAGraph).  One JSON line.
 usage: c4_step_probe.py [share_log2=30]   (GPU box)"""
 import json
 import os
@@ -35,8 +38,10 @@ q = torch.empty(nq * m, dtype=torch.uint8, device=dev)
 idx.extract(off, torch.full((nq,), m, dtype=torch.int32, device=dev),
             torch.arange(nq, device=dev, dtype=torch.int64) * m, q)
 eng = ShardedSearch(idx, dist, 1, 0, dev, algo="prefix", chunks=1, max_nq=nq)
+assert eng.identity
+engr = ShardedSearch(idx, dist, 1, 0, dev, algo="prefix", chunks=1, max_nq=nq, routed=True)
 out = torch.empty(nq, dtype=torch.int64, device=dev)
-res = {"n": n, "nq": nq}
+res = {"n": n, "nq": nq, "source_hash": sas_amd.source_hash()}
 
 
 def ev_time(fn, k=K):
@@ -54,9 +59,15 @@ def ev_time(fn, k=K):
     return a.elapsed_time(b) / k, (h1 - h0) * 1e3 / k
 
 
-step = lambda: eng.search_fixed(q, m, check=False, out=out)  # noqa: E731
-res["step_ms"], res["step_host_enqueue_ms"] = ev_time(step)
+res["step_ms"], res["step_host_enqueue_ms"] = ev_time(lambda: eng.search_fixed(q, m, check=False, out=out))
 ref = out.clone()
+# the replicated headline's kernel on the same batch (the identity step's target)
+res["replicated_lookup_ms"], _ = ev_time(lambda: idx.search_fixed(q, m, algo="prefix", out=out))
+assert torch.equal(out, ref)
+step = lambda: engr.search_fixed(q, m, check=False, out=out)  # noqa: E731
+res["routed_step_ms"], res["routed_step_host_enqueue_ms"] = ev_time(step)
+assert torch.equal(out, ref)
+eng = engr
 cap = eng.capacity(nq)
 buf = eng._buffers(m, cap)
 counts, send, slot = idx.route_pack(eng.splitters, q, m, cap=cap, send=buf["send"], packed=True)
@@ -66,7 +77,22 @@ res["lookup_ms"], res["lookup_host_ms"] = ev_time(lambda: eng._lookup(buf, send,
 local = eng._lookup(buf, send, counts, m, cap)
 res["gather_ms"], res["gather_host_ms"] = ev_time(
     lambda: idx.shard_gather(local, slot, out=out, counts=counts, cap=cap, overflow=eng.overflow))
-# the step captured once and replayed
+# the W = 8 shape on this part: 7 splitters, 8 fixed-capacity buckets (packed words)
+W8 = 8
+sa_n = idx.stats()["sa_entries"]
+sp8 = torch.tensor([int(idx.suffix_array(count=1, start=(j * sa_n) // W8)[0]) for j in range(1, W8)],
+                   dtype=torch.int64, device=dev)
+cap8 = int(nq * ShardedSearch.SLACK / W8) + 256
+send8 = torch.zeros(W8 * cap8, dtype=torch.int64, device=dev)
+res["w8_route_ms"], res["w8_route_host_ms"] = ev_time(
+    lambda: idx.route_pack(sp8, q, m, cap=cap8, send=send8, packed=True))
+c8, s8, slot8 = idx.route_pack(sp8, q, m, cap=cap8, send=send8, packed=True)
+res["w8_counts"] = c8.cpu().tolist()
+back8 = torch.zeros(W8 * cap8, dtype=torch.int64, device=dev)
+flag8 = torch.zeros(1, dtype=torch.int32, device=dev)
+res["w8_gather_ms"], _ = ev_time(lambda: idx.shard_gather(back8, slot8, out=out, counts=c8, cap=cap8, overflow=flag8))
+res["w8_overflow"] = int(flag8.item())
+# the routed step captured once and replayed
 s = torch.cuda.Stream()
 s.wait_stream(torch.cuda.current_stream())
 with torch.cuda.stream(s):
