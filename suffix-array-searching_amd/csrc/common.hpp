@@ -408,7 +408,11 @@ struct QueryRegs {
 #pragma unroll
         for (int j = 0; j < QW; j++) w[j] = pack_query_word(q, len, j, bad);
     }
-    // aligned word j (static select over the register copy; beyond QW, repack from bytes)
+    // aligned word j (static select over the register copy; beyond QW, repack from bytes).
+    // An instance with QW <= 2 only ever runs batches whose queries fit its words (qw_for:
+    // 1 for m <= 32, 2 for m <= 64; an unknown longest query gives 4), so past them it is 0
+    // and no repacking code is compiled (the register spills it cost, round 6); the two
+    // kernels that run longer queries on two register words use QueryRegsRepack
     __device__ __forceinline__ uint64_t word(uint32_t j) const {
         if (j < (uint32_t)QW) {
             uint64_t r = w[0];
@@ -416,6 +420,7 @@ struct QueryRegs {
             for (int k = 1; k < QW; k++) r = (j == (uint32_t)k) ? w[k] : r;
             return r;
         }
+        if (QW <= 2) return 0;
         uint32_t dummy = 0;
         return pack_query_word(bytes, m, j, &dummy);
     }
@@ -437,6 +442,23 @@ struct QueryRegsExact : QueryRegs<QW> {
 #pragma unroll
         for (int k = 0; k < QW; k++) r = (j == (uint32_t)k) ? this->w[k] : r;
         return r;
+    }
+    __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
+        const uint32_t j = off >> 5, s = (off & 31) << 1;
+        const uint64_t a = word(j);
+        if (s == 0) return a;
+        return (a << s) | (word(j + 1) >> (64 - s));
+    }
+};
+
+// QueryRegs whose words past the registers are repacked from the bytes at any QW (k_sa_quad4x
+// and k_sa_quad_llcp hold two register words for queries of any length)
+template <int QW>
+struct QueryRegsRepack : QueryRegs<QW> {
+    __device__ __forceinline__ uint64_t word(uint32_t j) const {
+        if (j < (uint32_t)QW) return QueryRegs<QW>::word(j);
+        uint32_t dummy = 0;
+        return pack_query_word(this->bytes, this->m, j, &dummy);
     }
     __device__ __forceinline__ uint64_t chars32(uint32_t off) const {
         const uint32_t j = off >> 5, s = (off & 31) << 1;

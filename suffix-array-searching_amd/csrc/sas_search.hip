@@ -51,6 +51,12 @@
 #define SAS_BIN_BPC 2
 #endif
 #define SAS_BIN_WAVES (SAS_BIN_BLOCK * SAS_BIN_BPC / 256)
+// ... for queries past 64 chars (4 or 8 query words in registers): an A/B hook
+#ifndef SAS_BIN_BLOCK_LONG
+#define SAS_BIN_BLOCK_LONG SAS_BIN_BLOCK
+#endif
+#define BIN_BLOCK(QW) ((QW) <= 2 ? SAS_BIN_BLOCK : SAS_BIN_BLOCK_LONG)
+#define BIN_WAVES(QW) (BIN_BLOCK(QW) * SAS_BIN_BPC / 256)
 // STREE at m <= 32: one lane per query (k_sa_stree4x) instead of a 4-lane group (A/B hook)
 #ifndef SAS_STREE_PERLANE
 #define SAS_STREE_PERLANE 0
@@ -112,6 +118,8 @@ struct SearchArgs {
     uint64_t* out_pos;
     uint32_t* out_probes;
     uint32_t* bad;
+    uint4* defer;            // k_sa_quad_llcp_a -> _b: 32-B entries of the unsettled queries
+    uint32_t* defer_n;       // and their count
     const uint64_t* bcounts; // sas_search_buckets: queries per bucket (null: every slot is a query)
     uint32_t bcap;           // slots per bucket
 };
@@ -142,9 +150,9 @@ using sa_val_t = typename std::conditional<W == 4, uint32_t, uint64_t>::type;
 // LLCP tie: the first h chars of suffix p are known equal to q's; inl = the suffix's
 // chars [h, h + 16) from its LLCP entry.  Same result as suffix_less_from(.., h, ..),
 // which only runs when those 16 chars match and both strings go on.
-template <int QW>
+template <int QW, class Q>
 __device__ __forceinline__ bool llcp_tie_less(const uint64_t* __restrict__ tw, uint64_t n, uint64_t p,
-                                              const QueryRegs<QW>& q, uint32_t h, uint32_t inl, uint32_t* lcp) {
+                                              const Q& q, uint32_t h, uint32_t inl, uint32_t* lcp) {
     const uint64_t lenS = n - p;
     const uint32_t L = lenS < (uint64_t)q.m ? (uint32_t)lenS : q.m;
     if (h < L) {
@@ -249,8 +257,11 @@ __device__ __forceinline__ uint32_t rel_slot(const uint4& b0, const uint4& b1, u
     const uint32_t wv = cw == 0 ? v.x : cw == 1 ? v.y : cw == 2 ? v.z : v.w;
     return ((j & 1u) ? (wv >> 16) : wv) & 0xFFFFu;
 }
-template <int QW, int MODE, bool TOP, int W, bool RANGE = false>
-__global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_binary(SearchArgs a) {
+// EXQ (QW >= 4): launched only with m <= 32 QW, the query words all in registers (QueryRegsExact:
+// no repacking code, fewer registers; the plain form repacks words past them from the bytes)
+template <int QW, int MODE, bool TOP, int W, bool RANGE = false, bool EXQ = false>
+__global__ __launch_bounds__(BIN_BLOCK(QW), BIN_WAVES(QW)) void k_sa_binary(SearchArgs a) {
+    using QR = typename std::conditional<EXQ && (QW > 2), QueryRegsExact<QW>, QueryRegs<QW>>::type;
     // the prefix-relative pivot blocks, the first 15 levels' from LDS (common.hpp RelLayout)
     __shared__ uint4 s_rel[TOP ? SAS_REL_LDS_BYTES / 16 : 1];
     const SaView<W> sa{a.sa};
@@ -266,7 +277,7 @@ __global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_binary(Sear
         const uint8_t* qb;
         uint32_t m;
         query_ptr(a, i, &qb, &m);
-        QueryRegs<QW> q;
+        QR q;
         q.load(qb, m, &bad);
 
         // ranks fit 32 bits beside a u32 SA (sa_n < 2^32): fewer registers for l, r, mid
@@ -480,8 +491,8 @@ __device__ __forceinline__ uint64_t stree_descend(const SearchArgs& a, const uin
 //   decided on it always compares (from its lcp, which b shares with q either way); a side
 //   inside the run carries an exact lcp from an earlier compare or rule.  So every rule is
 //   applied on an exact lcp and the result is binary_search's.
-template <int QW, int W, bool LT>
-__device__ __forceinline__ uint64_t stree_tail(const SearchArgs& a, const QueryRegs<QW>& q, uint32_t m, uint64_t r0,
+template <int QW, int W, bool LT, class Q>
+__device__ __forceinline__ uint64_t stree_tail(const SearchArgs& a, const Q& q, uint32_t m, uint64_t r0,
                                                uint64_t r1, uint32_t* probes) {
     const SaView<W> sa{a.sa};
     const uint64_t n = a.n, sa_n = a.sa_n;
@@ -634,8 +645,9 @@ __global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_stree(Searc
 // every lane runs the exact tail search of its own query in parallel: the descent
 // costs one request per node as in k_sa_stree, and the tail keeps the per-lane
 // parallelism of a one-lane-per-query search (the text compares of long queries dominate).
-template <int QW, int W, bool LT = false>
-__global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_stree4x(SearchArgs a) {
+template <int QW, int W, bool LT = false, bool EXQ = false>
+__global__ __launch_bounds__(BIN_BLOCK(QW), BIN_WAVES(QW)) void k_sa_stree4x(SearchArgs a) {
+    using QR = typename std::conditional<EXQ && (QW > 2), QueryRegsExact<QW>, QueryRegs<QW>>::type;
     __shared__ uint4 s_nodes[SAS_STREE_LDS_NODES * 4];
     {
         const uint4* g = reinterpret_cast<const uint4*>(a.stree);
@@ -656,7 +668,7 @@ __global__ __launch_bounds__(SAS_BIN_BLOCK, SAS_BIN_WAVES) void k_sa_stree4x(Sea
         const bool mine = i < a.nq;
         const uint8_t* qb;
         uint32_t m = 0;
-        QueryRegs<QW> q;
+        QR q;
         if (mine) {
             query_ptr(a, i, &qb, &m);
             q.load(qb, m, &bad);
@@ -751,9 +763,9 @@ __device__ __forceinline__ bool tail_less32(const uint64_t* __restrict__ tw, uin
 // the per-lane sector kernel, slower for the 4-lane quad kernel (register spills).
 // SHORT1: QW == 1 means m <= 32 (qw_for), so the text compare is dead code there;
 // false for kernels that hold fewer query words in registers than the query has.
-template <int QW, bool PREFETCH = false, bool SHORT1 = true>
+template <int QW, bool PREFETCH = false, bool SHORT1 = true, class Q = QueryRegs<QW>>
 __device__ __forceinline__ bool sector_ge(uint64_t key, uint64_t p, uint64_t K64, const SearchArgs& a,
-                                          const QueryRegs<QW>& q) {
+                                          const Q& q) {
     if (key != K64) return key > K64;
     if ((SHORT1 && QW == 1) || q.m <= 32) return (a.n - p) >= (uint64_t)q.m;
     if (PREFETCH) return !tail_less32<QW>(a.tw, a.n, p, q);
@@ -1198,8 +1210,8 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad(SearchArgs a) {
 // delivered them (known).  The predicate at x0 (a key tie: one text compare from char 32),
 // and in the rare case it fails an exponential + binary search over the following entries.
 // Returns the position.
-template <int QW, bool KO, int W>
-__device__ __forceinline__ uint64_t quad_x0_finish(const SearchArgs& a, const QueryRegs<QW>& q, uint64_t K64,
+template <int QW, bool KO, int W, class Q>
+__device__ __forceinline__ uint64_t quad_x0_finish(const SearchArgs& a, const Q& q, uint64_t K64,
                                                    uint64_t x0, bool known, uint64_t key0, uint64_t p0,
                                                    uint32_t* probes) {
     const uint64_t sa_n = a.sa_n;
@@ -1210,7 +1222,7 @@ __device__ __forceinline__ uint64_t quad_x0_finish(const SearchArgs& a, const Qu
             ok = key > K64;
         } else {
             if (p0 == QUAD_NO_SA) p0 = quad_entry_sa<KO, W>(a, x0);
-            ok = sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, p0, K64, a, q);
+            ok = sector_ge<QW, SAS_QUAD4X_PREFETCH, false, Q>(key, p0, K64, a, q);
         }
         if (!known) (*probes)++;
     }
@@ -1219,7 +1231,7 @@ __device__ __forceinline__ uint64_t quad_x0_finish(const SearchArgs& a, const Qu
         auto pred = [&](uint64_t y) -> bool {
             const uint64_t key = quad_entry_key<KO>(a, y);
             if (key != K64) return key > K64;
-            return sector_ge<QW, SAS_QUAD4X_PREFETCH, false>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
+            return sector_ge<QW, SAS_QUAD4X_PREFETCH, false, Q>(key, quad_entry_sa<KO, W>(a, y), K64, a, q);
         };
         uint64_t lo = x0 + 1, hi = sa_n, step = 1;
         while (lo < sa_n) {
@@ -1253,8 +1265,10 @@ __device__ __forceinline__ uint64_t quad_x0_finish(const SearchArgs& a, const Qu
 // (typically a key tie -> one text compare from char 32, the part that dominates for
 // long queries), and in the rare case it fails an exponential + binary search over
 // the following entries.
-template <int QW, bool KO, int W>
+// RP: queries longer than QW register words (their later words repacked from the bytes)
+template <int QW, bool KO, int W, bool RP>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
+    using QR = typename std::conditional<RP, QueryRegsRepack<QW>, QueryRegs<QW>>::type;
     constexpr uint32_t EPL = KO ? 8 : 4;
     __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
     stage_quad_top(a, s_nodes);
@@ -1268,7 +1282,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
         const bool mine = i < a.nq;
         const uint8_t* qb;
         uint32_t m = 0;
-        QueryRegs<QW> q;
+        QR q;
         if (mine) {
             query_ptr(a, i, &qb, &m);
             q.load(qb, m, &bad);
@@ -1308,7 +1322,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_quad4x(SearchArgs a) {
             }
         }
         if (!mine) continue;
-        const uint64_t pos = quad_x0_finish<QW, KO, W>(a, q, Kmine, x0, known, key0, p0, &probes);
+        const uint64_t pos = quad_x0_finish<QW, KO, W, QR>(a, q, Kmine, x0, known, key0, p0, &probes);
         a.out_pos[i] = pos;
         if (a.out_probes) a.out_probes[i] = probes;
     }
@@ -1488,11 +1502,14 @@ __device__ __forceinline__ uint32_t quad_descend_from(const SearchArgs& a, const
 #define QL_END (1u << 14)                // q's 16-char run reaches the end: U = sa_n
 #define QL_DLEV(st) ((st) >> 24)         // where K16 + 1's path parts from q's (QLLCP_NONE: not)
 
-// EXACT: launched only with m <= 32 QW (QueryRegsExact: no repacking from the bytes);
-// R32: sa_n < 2^32, the walk's ranks in 32 bits
-template <int QW, bool EXACT, bool R32>
-__global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp(SearchArgs a) {
-    using QR = typename std::conditional<EXACT, QueryRegsExact<QW>, QueryRegs<QW>>::type;
+// k_sa_quad_llcp_a: the group step (descent, leaf, counts) and the settle (k_sa_quad4x's reads:
+// the first entry not below q's 32-char key and at most one compare), 1024-thread workgroups
+// like k_sa_quad4x; what it does not settle it defers.
+// EXACT: launched only with m <= 32 QW (QueryRegsExact: no repacking from the bytes)
+#define QLLCP_A_BLOCK(QW) ((QW) <= 2 ? SEARCH_BLOCK : SAS_BIN_BLOCK)  // 4 or 8 query words: 80 VGPRs
+template <int QW, bool EXACT>
+__global__ __launch_bounds__(QLLCP_A_BLOCK(QW), QLLCP_A_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp_a(SearchArgs a) {
+    using QR = typename std::conditional<EXACT, QueryRegsExact<QW>, QueryRegsRepack<QW>>::type;
     __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
     stage_quad_top(a, s_nodes);
     uint32_t bad = 0;
@@ -1518,7 +1535,7 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
         // this lane's query, from its group step: leaf k, the leaf kU of U, the packed counts and
         // flags (QL_*), leaf k's entries' lcps with q (8 bits each), K16 + 1's node below its
         // parting level, and the SA values at L0 and U when a leaf read delivered them
-        uint32_t kq = 0, kU = 0, st = 0, lam = 0, dnode = 0;
+        uint32_t kq = 0, st = 0, lam = 0, dnode = 0;
         uint64_t p0 = QUAD_NO_SA;
         for (uint32_t j = 0; j < QUAD_G; j++) {
             if (gi + j >= a.nq) break;  // group-uniform
@@ -1543,7 +1560,6 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
             const uint32_t w0 = (uint32_t)__shfl((int)e.w, lane0 + (int)(c64 & 3), 64);
             if (sub == j) {
                 kq = k;
-                kU = k;
                 lam = lamj;
                 dnode = dn;
                 st = c16 | (c64 << 3) | (dl << 24);
@@ -1563,35 +1579,109 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
         uint32_t lcp0 = 0;
         if (mine && m <= 32) {
             // the 32-char key decides every entry: k_sa_quad4x's finish
-#ifdef QLLCP_NO_FINISH
-            pos = p0;
-#else
             pos = quad_short_finish(a, Kmine, m, 4 * (uint64_t)kq + QL_C64(st), (st & QL_KNOWN) != 0,
                                     (st & QL_EQ0) != 0, p0, &probes);
-#endif
             done = true;
         } else if (mine && 4 * (uint64_t)kq + QL_C64(st) >= a.sa_n) {
             pos = a.next_pos;
             done = true;
-        } else if (mine && (st & QL_KNOWN)) {
-            // the first suffix not below q's 32-char key: > it, or one compare from char 32
-            // (k_sa_quad4x's common case); below q, it is the walk's exact left bound
-            if (!(st & QL_EQ0) || (probes++, !suffix_less_from<QW>(a.tw, a.n, p0, q, 32, &lcp0))) {
-                pos = p0;
-                done = true;
-            } else {
-                st |= QL_LAM0;
+        } else if (mine) {
+            if (!(st & QL_KNOWN)) {
+                // leaf k's keys are all below q's: the next entry, as k_sa_quad4x reads it (a
+                // key still below q's leaves L0 inexact at 32 chars, the walk's kappa 16)
+                const uint4 e = a.quad_leaves[4 * (uint64_t)kq + 4];
+                const uint64_t key = (uint64_t)e.x | ((uint64_t)e.y << 32);
+                probes++;
+                if (key >= Kmine) {
+                    st |= QL_KNOWN | ((st & QL_END) ? 0u : QL_X32) | (key == Kmine ? QL_EQ0 : 0u);
+                    p0 = (uint64_t)e.z | ((uint64_t)(e.w & 0xFFu) << 32);
+                }
+            }
+            if (st & QL_KNOWN) {
+                // the first suffix not below q's 32-char key: > it, or one compare from char 32
+                // (k_sa_quad4x's common case); below q, it is the walk's exact left bound
+                if (!(st & QL_EQ0) || (probes++, !suffix_less_from<QW>(a.tw, a.n, p0, q, 32, &lcp0))) {
+                    pos = p0;
+                    done = true;
+                } else {
+                    st |= QL_LAM0;
+                }
             }
         }
+        // settled: the answer; else the state goes to k_sa_quad_llcp_b (one 32-B entry, claimed
+        // by one atomic per wave)
+        const bool dfr = mine && !done;
+        const uint64_t bal = __ballot(dfr);
+        if (bal) {
+            const int lane = (int)(threadIdx.x & 63), leader = __ffsll((unsigned long long)bal) - 1;
+            uint32_t base = 0;
+            if (lane == leader) base = atomicAdd(a.defer_n, (uint32_t)__popcll(bal));
+            base = (uint32_t)__shfl((int)base, leader, 64);
+            if (dfr) {
+                const uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
+                if (lcp0 > 0xFFFFFFu) st &= ~QL_LAM0;  // not kept: the walk reads entry L0 again
+                const uint32_t pk = probes < 511u ? probes : 511u;
+                a.defer[2 * (uint64_t)slot] = make_uint4((uint32_t)i, (uint32_t)(i >> 32), kq, st | (pk << 15));
+                a.defer[2 * (uint64_t)slot + 1] =
+                    make_uint4(lam, dnode, (uint32_t)p0, (uint32_t)((p0 >> 32) & 0xFFu) | (lcp0 << 8));
+            }
+        }
+        if (mine && done) {
+            a.out_pos[i] = pos;
+            if (a.out_probes) a.out_probes[i] = probes;
+        }
+    }
+    if (bad) atomicOr(a.bad, 1u);
+}
+
+// k_sa_quad_llcp_b: the queries k_sa_quad_llcp_a did not settle, one per lane from its 32-B
+// deferred entry (the lane's packed state, k_sa_quad_llcp_a's variables): U where the run
+// leaves leaf k (cooperative, as the first step), then the LLCP walk.
+// R32: sa_n < 2^32, the walk's ranks in 32 bits
+template <int QW, bool EXACT, bool R32>
+__global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp_b(SearchArgs a) {
+    using QR = typename std::conditional<EXACT, QueryRegsExact<QW>, QueryRegsRepack<QW>>::type;
+    __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
+    stage_quad_top(a, s_nodes);
+    uint32_t bad = 0;
+    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
+    const int lane0 = (int)((threadIdx.x & 63) & ~3u);
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t cnt = *a.defer_n;  // stream-ordered after k_sa_quad_llcp_a
+    for (uint64_t gs = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) - sub; gs < cnt; gs += stride) {
+        const uint64_t slot = gs + sub;
+        const bool mine = slot < cnt;
+        uint64_t i = 0, p0 = QUAD_NO_SA;
+        uint32_t kq = 0, st = 0, lam = 0, dnode = 0, lcp0 = 0, probes = 0, m = 0;
+        const uint8_t* qb;
+        QR q;
+        if (mine) {
+            const uint4 d0 = a.defer[2 * slot], d1 = a.defer[2 * slot + 1];
+            i = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
+            kq = d0.z;
+            st = d0.w & ~(511u << 15);
+            probes = (d0.w >> 15) & 511u;
+            lam = d1.x;
+            dnode = d1.y;
+            p0 = (uint64_t)d1.z | ((uint64_t)(d1.w & 0xFFu) << 32);
+            lcp0 = d1.w >> 8;
+            query_ptr(a, i, &qb, &m);
+            q.load(qb, m, &bad);
+        } else {
+            q.bytes = a.qbytes;
+            q.m = 0;
+            for (int j = 0; j < QW; j++) q.w[j] = 0;
+        }
+        (void)p0;
+        const uint64_t Kmine = q.w[0];
+        uint32_t kU = kq;
+        const bool done = !mine;
         // U for the queries whose 32-char run leaves leaf k: the leaf of K16 + 1, from where its
         // path parts from q's (near the leaves: one or two requests)
-#ifdef QLLCP_NO_NEEDU
-        const bool needU = false;
-#else
         const bool needU = !done && !(st & QL_UK);
-#endif
-        for (uint32_t j = 0; j < QUAD_G; j++) {
-            if (!(quad_mask(needU) & (1u << j))) continue;  // group-uniform
+        const uint32_t nu = quad_mask(needU);  // group-uniform
+        for (uint32_t j = 0; nu && j < QUAD_G; j++) {
+            if (!(nu & (1u << j))) continue;
             const uint64_t K64 = __shfl((unsigned long long)Kmine, lane0 + (int)j, 64);
             const uint32_t K16 = (uint32_t)(K64 >> 32);
             const uint32_t dl = (uint32_t)__shfl((int)st, lane0 + (int)j, 64) >> 24;
@@ -1614,7 +1704,8 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
             }
         }
         if (!mine) continue;
-        if (!done) {
+        uint64_t pos;
+        {
             using rk_t = typename std::conditional<R32, uint32_t, uint64_t>::type;
             const rk_t sa_n = (rk_t)a.sa_n;
             const rk_t kb = 4 * (rk_t)kq;
@@ -1655,11 +1746,7 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
                     else { decided = false; hh = y; inl = e.w; }
                 }
                 const uint64_t p = (uint64_t)e.x | ((uint64_t)(e.y & 0xFFu) << 32);
-#ifdef QLLCP_NO_TIE
-                if (!decided) { lt = p & 1; lcp = hh + inl; }
-#else
                 if (!decided) lt = qllcp_tie_less<QW, QR>(a, p, q, hh, inl, kappa, &lcp);
-#endif
                 if (lt) {
                     l = mid + 1;
                     llcp = lcp;
@@ -1739,14 +1826,13 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
         const uint64_t K64 = q.w[0];
         uint64_t l = 0, r = a.sa_n, pr = QUAD_NO_SA;
         uint32_t k = 1, probes = 0;
+        // selects, not a branch on ge: the branch form made the compiler store l or pr through a
+        // selected pointer into scratch (24 B a lane, round 5's make resource)
         auto take = [&](uint64_t mid, bool ge, uint64_t p) {
             probes++;
-            if (ge) {
-                r = mid;
-                pr = p;
-            } else {
-                l = mid + 1;
-            }
+            r = ge ? mid : r;
+            pr = ge ? p : pr;
+            l = ge ? l : mid + 1;
         };
         uint32_t it = 0;
         if (TOP) {
@@ -2957,41 +3043,57 @@ static void launch_w(int algo, bool top, bool range, int qw, dim3 grid, dim3 blo
         case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
         default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
     }
-#define K_PLAIN_TOP(Q) (k_sa_binary<Q, BS_PLAIN, true, W>)
-#define K_PLAIN(Q) (k_sa_binary<Q, BS_PLAIN, false, W>)
-#define K_LCP_TOP(Q) (k_sa_binary<Q, BS_MLR, true, W>)
-#define K_LCP(Q) (k_sa_binary<Q, BS_MLR, false, W>)
-#define K_LLCP_TOP(Q) (k_sa_binary<Q, BS_LLCP, true, W>)
-#define K_LLCP(Q) (k_sa_binary<Q, BS_LLCP, false, W>)
+    // the query words all in registers when the batch's longest query is known to fit them
+    const bool exq = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
+#define QWX_CASE(KERNEL_T)                                                                      \
+    switch (qw) {                                                                               \
+        case 1: hipLaunchKernelGGL(KERNEL_T(1, false), grid, block, 0, st, a); break;           \
+        case 2: hipLaunchKernelGGL(KERNEL_T(2, false), grid, block, 0, st, a); break;           \
+        case 4:                                                                                 \
+            if (exq) hipLaunchKernelGGL(KERNEL_T(4, true), grid, block, 0, st, a);              \
+            else hipLaunchKernelGGL(KERNEL_T(4, false), grid, block, 0, st, a);                 \
+            break;                                                                              \
+        default:                                                                                \
+            if (exq) hipLaunchKernelGGL(KERNEL_T(8, true), grid, block, 0, st, a);              \
+            else hipLaunchKernelGGL(KERNEL_T(8, false), grid, block, 0, st, a);                 \
+            break;                                                                              \
+    }
+#define K_PLAIN_TOP(Q, X) (k_sa_binary<Q, BS_PLAIN, true, W, false, X>)
+#define K_PLAIN(Q, X) (k_sa_binary<Q, BS_PLAIN, false, W, false, X>)
+#define K_LCP_TOP(Q, X) (k_sa_binary<Q, BS_MLR, true, W, false, X>)
+#define K_LCP(Q, X) (k_sa_binary<Q, BS_MLR, false, W, false, X>)
+#define K_LLCP_TOP(Q, X) (k_sa_binary<Q, BS_LLCP, true, W, false, X>)
+#define K_LLCP(Q, X) (k_sa_binary<Q, BS_LLCP, false, W, false, X>)
 #define K_PLAIN_RANGE(Q) (k_sa_binary<Q, BS_PLAIN, false, W, true>)
 #define K_LCP_RANGE(Q) (k_sa_binary<Q, BS_MLR, false, W, true>)
 #define K_STREE(Q) (k_sa_stree<Q, W>)
-#define K_STREE4X(Q) (k_sa_stree4x<Q, W>)
-#define K_STREE4X_LT(Q) (k_sa_stree4x<Q, W, true>)
+#define K_STREE4X(Q, X) (k_sa_stree4x<Q, W, false, X>)
+#define K_STREE4X_LT(Q, X) (k_sa_stree4x<Q, W, true, X>)
 #define K_SECTOR(Q) (k_sa_sector<Q>)
     if (algo == SAS_ALGO_PLAIN && range) {
         QW_CASE(K_PLAIN_RANGE)
     } else if (algo == SAS_ALGO_LCP && range) {
         QW_CASE(K_LCP_RANGE)
     } else if (algo == SAS_ALGO_PLAIN) {
-        if (top) { QW_CASE(K_PLAIN_TOP) } else { QW_CASE(K_PLAIN) }
+        if (top) { QWX_CASE(K_PLAIN_TOP) } else { QWX_CASE(K_PLAIN) }
     } else if (algo == SAS_ALGO_LCP) {
-        if (top) { QW_CASE(K_LCP_TOP) } else { QW_CASE(K_LCP) }
+        if (top) { QWX_CASE(K_LCP_TOP) } else { QWX_CASE(K_LCP) }
     } else if (algo == SAS_ALGO_LLCP) {
-        if (top) { QW_CASE(K_LLCP_TOP) } else { QW_CASE(K_LLCP) }
+        if (top) { QWX_CASE(K_LLCP_TOP) } else { QWX_CASE(K_LLCP) }
     } else if (algo == SAS_ALGO_STREE) {
         // m <= 32: the cooperative kernel (descent dominates); longer: one lane per query
         if (qw == 1 && !SAS_STREE_PERLANE) hipLaunchKernelGGL(K_STREE(1), grid, block, 0, st, a);
-        else { QW_CASE(K_STREE4X) }
+        else { QWX_CASE(K_STREE4X) }
     } else if (algo == SAS_ALGO_STREE_LLCP) {
         // the same descent, the LLCP tail (stree_tail) on one lane per query at every m: the
         // tail's walk to its in-run mids diverges between queries, which a 4-lane group per
         // query would pay 4 times over (m = 32: 1.77 ms cooperative)
-        QW_CASE(K_STREE4X_LT)
+        QWX_CASE(K_STREE4X_LT)
     } else {  // SAS_ALGO_SECTOR: positions come from the fused leaves, W = 4 only
         QW_CASE(K_SECTOR)
     }
 #undef QW_CASE
+#undef QWX_CASE
 }
 
 // QUAD / INLINE: fused leaves read no SA (W = 4 instantiation only); KO leaves read
@@ -3005,7 +3107,6 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
         case 4: hipLaunchKernelGGL(KERNEL_T(4), grid, block, 0, st, a); break;      \
         default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
     }
-#define K_QUAD4X(Q) (k_sa_quad4x<(Q < SAS_QUAD4X_MAXREGS ? Q : SAS_QUAD4X_MAXREGS), KO, W>)
 #define K_INLINE_TOP(Q) (k_sa_inline<Q, true, KO, W>)
 #define K_INLINE(Q) (k_sa_inline<Q, false, KO, W>)
 #define K_PREFIX(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 4>)
@@ -3016,9 +3117,11 @@ static void launch_quad(int algo, bool top, int qw, dim3 grid, dim3 block, hipSt
 #define K_PREFIX4H(Q) (k_sa_prefix2<Q, 4, true>)
 #define K_PREFIX16(Q) (k_sa_prefix<(Q < SAS_PREFIX_QWMAX ? Q : SAS_PREFIX_QWMAX), KO, W, 16>)
     if (algo == SAS_ALGO_QUAD) {
-        // m <= 32: the cooperative kernel; longer: one lane per query (as STREE)
+        // m <= 32: the cooperative kernel; longer: one lane per query (as STREE), two query
+        // words in registers (m <= 64), later ones repacked from the bytes
         if (qw == 1) hipLaunchKernelGGL((k_sa_quad<1, KO, W>), grid, block, 0, st, a);
-        else { QW_CASE(K_QUAD4X) }
+        else if (qw == 2) hipLaunchKernelGGL((k_sa_quad4x<2, KO, W, false>), grid, block, 0, st, a);
+        else hipLaunchKernelGGL((k_sa_quad4x<SAS_QUAD4X_MAXREGS, KO, W, true>), grid, block, 0, st, a);
     } else if (algo == SAS_ALGO_PREFIX) {
         if (a.prefix_w == 5) { QW_CASE(K_PREFIX5) }
         else if (a.prefix_w == 16 && !KO) { QW_CASE(K_PREFIX16) }
@@ -3054,18 +3157,33 @@ static void launch_w8(int algo, bool top, int qw, dim3 grid, dim3 block, hipStre
         default: hipLaunchKernelGGL(KERNEL_T(8), grid, block, 0, st, a); break;     \
     }
 #define K_TAGGED(Q) (k_sa_tagged<Q>)
-#define K8_PLAIN_TOP(Q) (k_sa_binary<Q, BS_PLAIN, true, 8>)
-#define K8_PLAIN(Q) (k_sa_binary<Q, BS_PLAIN, false, 8>)
-#define K8_LCP_TOP(Q) (k_sa_binary<Q, BS_MLR, true, 8>)
-#define K8_LCP(Q) (k_sa_binary<Q, BS_MLR, false, 8>)
+    const bool exq = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
+#define QWX_CASE(KERNEL_T)                                                                      \
+    switch (qw) {                                                                               \
+        case 1: hipLaunchKernelGGL(KERNEL_T(1, false), grid, block, 0, st, a); break;           \
+        case 2: hipLaunchKernelGGL(KERNEL_T(2, false), grid, block, 0, st, a); break;           \
+        case 4:                                                                                 \
+            if (exq) hipLaunchKernelGGL(KERNEL_T(4, true), grid, block, 0, st, a);              \
+            else hipLaunchKernelGGL(KERNEL_T(4, false), grid, block, 0, st, a);                 \
+            break;                                                                              \
+        default:                                                                                \
+            if (exq) hipLaunchKernelGGL(KERNEL_T(8, true), grid, block, 0, st, a);              \
+            else hipLaunchKernelGGL(KERNEL_T(8, false), grid, block, 0, st, a);                 \
+            break;                                                                              \
+    }
+#define K8_PLAIN_TOP(Q, X) (k_sa_binary<Q, BS_PLAIN, true, 8, false, X>)
+#define K8_PLAIN(Q, X) (k_sa_binary<Q, BS_PLAIN, false, 8, false, X>)
+#define K8_LCP_TOP(Q, X) (k_sa_binary<Q, BS_MLR, true, 8, false, X>)
+#define K8_LCP(Q, X) (k_sa_binary<Q, BS_MLR, false, 8, false, X>)
     if (algo == SAS_ALGO_TAGGED) {
         QW_CASE(K_TAGGED)
     } else if (algo == SAS_ALGO_PLAIN) {
-        if (top) { QW_CASE(K8_PLAIN_TOP) } else { QW_CASE(K8_PLAIN) }
+        if (top) { QWX_CASE(K8_PLAIN_TOP) } else { QWX_CASE(K8_PLAIN) }
     } else {
-        if (top) { QW_CASE(K8_LCP_TOP) } else { QW_CASE(K8_LCP) }
+        if (top) { QWX_CASE(K8_LCP_TOP) } else { QWX_CASE(K8_LCP) }
     }
 #undef QW_CASE
+#undef QWX_CASE
 }
 
 static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, uint32_t flags, hipStream_t st) {
@@ -3079,10 +3197,10 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
     // k_sa_binary (PLAIN / LCP / LLCP, any SA width) and the S-tree kernels have their own
     // workgroup shape
     const bool bin = algo == SAS_ALGO_PLAIN || algo == SAS_ALGO_LCP || algo == SAS_ALGO_LLCP ||
-                     algo == SAS_ALGO_STREE || algo == SAS_ALGO_STREE_LLCP || (algo == SAS_ALGO_QUAD_LLCP && qw > 1);
-    const bool qx = algo == SAS_ALGO_QUAD_LLCP && qw > 1;  // k_sa_quad_llcp: exact QW, or two words (QLLCP_BLOCK(2))
-    const bool qx_exact = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
-    const uint64_t bs = qx ? (qx_exact ? QLLCP_BLOCK(qw) : QLLCP_BLOCK(2)) : bin ? SAS_BIN_BLOCK : SEARCH_BLOCK;
+                     algo == SAS_ALGO_STREE || algo == SAS_ALGO_STREE_LLCP;
+    // k_sa_binary / k_sa_stree4x instances: QW = qw (1, 2, 4, and 8 for anything longer);
+    // QUAD_LLCP past 32 chars sizes its two kernels itself
+    const uint64_t bs = bin ? (coop ? SAS_BIN_BLOCK : BIN_BLOCK(qw)) : SEARCH_BLOCK;
     uint64_t blocks = (lanes + bs - 1) / bs;
     uint64_t cap = (uint64_t)x->num_cus * (bin ? SAS_BIN_BPC : BLOCKS_PER_CU);
     if (blocks > cap) blocks = cap;
@@ -3125,30 +3243,40 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
         else launch_interp<4, false>(qw, grid, block, st, a, range);
     } else if (x->sa_w == 8) {
         launch_w8(algo, top, qw, grid, block, st, a);
+    } else if (algo == SAS_ALGO_QUAD_LLCP && qw == 1) {
+        // m <= 32: QUAD (the 32-char key decides every entry)
+        hipLaunchKernelGGL((k_sa_quad<1, false, 4>), grid, block, 0, st, a);
     } else if (algo == SAS_ALGO_QUAD_LLCP) {
-        // m <= 32: QUAD (the 32-char key decides); longer: k_sa_quad_llcp (fused leaves, any SA width:
-        // the leaves and the LLCP entries carry 40-bit positions), with every query word in
-        // registers when the batch's longest query is known to fit them, else two words and the
-        // rest repacked from the bytes
+        // longer: k_sa_quad_llcp_a settles what QUAD's reads settle and defers the rest to
+        // k_sa_quad_llcp_b (U + the LLCP walk), each kernel in its own workgroup shape; fused
+        // leaves, any SA width (the leaves and the LLCP entries carry 40-bit positions); every
+        // query word in registers when the batch's longest query is known to fit them, else
+        // two words and the rest repacked from the bytes
+        if (a.nq >= (1ull << 32)) SAS_FAIL(EINVAL, "SAS_ALGO_QUAD_LLCP: batches of < 2^32 queries");
         const bool exact = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
-        if (qw > 1 && !exact) {
-            if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<2, false, true>), grid, block, 0, st, a);
-            else hipLaunchKernelGGL((k_sa_quad_llcp<2, false, false>), grid, block, 0, st, a);
-        } else switch (qw) {
-            case 1: hipLaunchKernelGGL((k_sa_quad<1, false, 4>), grid, block, 0, st, a); break;
-            case 2:
-                if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<2, true, true>), grid, block, 0, st, a);
-                else hipLaunchKernelGGL((k_sa_quad_llcp<2, true, false>), grid, block, 0, st, a);
-                break;
-            case 4:
-                if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<4, true, true>), grid, block, 0, st, a);
-                else hipLaunchKernelGGL((k_sa_quad_llcp<4, true, false>), grid, block, 0, st, a);
-                break;
-            default:
-                if (a.sa_n < (1ull << 32)) hipLaunchKernelGGL((k_sa_quad_llcp<8, true, true>), grid, block, 0, st, a);
-                else hipLaunchKernelGGL((k_sa_quad_llcp<8, true, false>), grid, block, 0, st, a);
-                break;
-        }
+        void* dbuf = nullptr;
+        HIP_TRY(hipMallocAsync(&dbuf, a.nq * 32 + 256, st));
+        SearchArgs b = a;
+        b.defer_n = static_cast<uint32_t*>(dbuf);
+        b.defer = reinterpret_cast<uint4*>(static_cast<uint8_t*>(dbuf) + 256);
+        HIP_TRY(hipMemsetAsync(dbuf, 0, 4, st));
+        const uint32_t ba = exact ? QLLCP_A_BLOCK(qw) : QLLCP_A_BLOCK(2);
+        uint64_t ga = (a.nq + ba - 1) / ba;
+        if (ga > (uint64_t)x->num_cus * 2) ga = (uint64_t)x->num_cus * 2;
+        const dim3 gA((unsigned)ga), bA(ba);
+        const dim3 gB((unsigned)(x->num_cus * 2)), bB((unsigned)(exact ? QLLCP_BLOCK(qw) : QLLCP_BLOCK(2)));
+        const bool r32 = a.sa_n < (1ull << 32);
+#define QLLCP_AB(Q, X)                                                                            \
+    hipLaunchKernelGGL((k_sa_quad_llcp_a<Q, X>), gA, bA, 0, st, b);                               \
+    if (r32) hipLaunchKernelGGL((k_sa_quad_llcp_b<Q, X, true>), gB, bB, 0, st, b);                \
+    else hipLaunchKernelGGL((k_sa_quad_llcp_b<Q, X, false>), gB, bB, 0, st, b)
+        if (!exact) { QLLCP_AB(2, false); }
+        else if (qw == 2) { QLLCP_AB(2, true); }
+        else if (qw == 4) { QLLCP_AB(4, true); }
+        else { QLLCP_AB(8, true); }
+#undef QLLCP_AB
+        HIP_TRY(hipGetLastError());
+        HIP_TRY(hipFreeAsync(dbuf, st));
     } else if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
         if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
         else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);

@@ -57,11 +57,13 @@ def model(t, sa, lcpa, q, stats):
         ln = n - int(sa[x]) if x < sa_n else 0
         return min(d, ln)
     x32 = c64 < 4
+    x32_u = True
     if le64 < 4:
         U = kb + le64
     elif K16 == 0xFFFFFFFF:
         U = sa_n
         x32 = False
+        x32_u = False
     else:
         firstgt = next((r for r in range(sa_n) if (keys[r] >> 32) > K16), sa_n)
         kU = min(firstgt // 4, nl - 1)
@@ -70,6 +72,7 @@ def model(t, sa, lcpa, q, stats):
         le16U = sum((x >> 32) <= K16 for x in lf)
         f = le64U if le64U else le16U
         x32 = x32 and le64U > 0
+        x32_u = le64U > 0
         U = 4 * kU + f
         stats["kU_descents"] += kU != k
     U = min(U, sa_n)
@@ -83,6 +86,11 @@ def model(t, sa, lcpa, q, stats):
     if L0 >= sa_n:
         return n, 0
     lam0 = None
+    if c64 == 4 and keys[L0] >= K64:
+        # the kernel reads the next entry: its key >= q's makes L0 exact at 32 chars
+        c64 = 3  # (as if leaf k had held it)
+        x32 = x32_u
+        kappa = 32 if x32 else 16
     if c64 < 4:
         # the first suffix not below q's 32-char key: > it, or one compare from char 32
         S0 = suf(int(sa[L0]))
