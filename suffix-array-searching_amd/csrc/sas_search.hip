@@ -118,8 +118,6 @@ struct SearchArgs {
     uint64_t* out_pos;
     uint32_t* out_probes;
     uint32_t* bad;
-    uint4* defer;            // k_sa_quad_llcp_a -> _b: 32-B entries of the unsettled queries
-    uint32_t* defer_n;       // and their count
     const uint64_t* bcounts; // sas_search_buckets: queries per bucket (null: every slot is a query)
     uint32_t bcap;           // slots per bucket
 };
@@ -1429,6 +1427,7 @@ __device__ __forceinline__ bool qllcp_tie_less(const SearchArgs& a, uint64_t p, 
 }
 
 #define QLLCP_NONE 0xFFu
+
 // k_sa_quad_llcp's workgroup size (two workgroups a CU): 768 -> 6 waves a SIMD, 80 VGPRs;
 // 512 -> 4 waves, 128 VGPRs
 #ifndef SAS_QLLCP_BLOCK
@@ -1502,13 +1501,15 @@ __device__ __forceinline__ uint32_t quad_descend_from(const SearchArgs& a, const
 #define QL_END (1u << 14)                // q's 16-char run reaches the end: U = sa_n
 #define QL_DLEV(st) ((st) >> 24)         // where K16 + 1's path parts from q's (QLLCP_NONE: not)
 
-// k_sa_quad_llcp_a: the group step (descent, leaf, counts) and the settle (k_sa_quad4x's reads:
-// the first entry not below q's 32-char key and at most one compare), 1024-thread workgroups
-// like k_sa_quad4x; what it does not settle it defers.
-// EXACT: launched only with m <= 32 QW (QueryRegsExact: no repacking from the bytes)
-#define QLLCP_A_BLOCK(QW) ((QW) <= 2 ? SEARCH_BLOCK : SAS_BIN_BLOCK)  // 4 or 8 query words: 80 VGPRs
-template <int QW, bool EXACT>
-__global__ __launch_bounds__(QLLCP_A_BLOCK(QW), QLLCP_A_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp_a(SearchArgs a) {
+// k_sa_quad_llcp: the group step (descent, leaf, counts), the settle (k_sa_quad4x's reads: the
+// first entry not below q's 32-char key and at most one compare), then for what that does not
+// settle U (where the run leaves leaf k; cooperative) and the LLCP walk.  (Round 6 also
+// measured it split in two kernels, the unsettled queries' state handed over in a list: the
+// list's scattered query and result accesses cost more than the split saved)
+// EXACT: launched only with m <= 32 QW (QueryRegsExact: no repacking from the bytes);
+// R32: sa_n < 2^32, the walk's ranks in 32 bits
+template <int QW, bool EXACT, bool R32>
+__global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp(SearchArgs a) {
     using QR = typename std::conditional<EXACT, QueryRegsExact<QW>, QueryRegsRepack<QW>>::type;
     __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
     stage_quad_top(a, s_nodes);
@@ -1608,74 +1609,7 @@ __global__ __launch_bounds__(QLLCP_A_BLOCK(QW), QLLCP_A_BLOCK(QW) * 2 / 256) voi
                 }
             }
         }
-        // settled: the answer; else the state goes to k_sa_quad_llcp_b (one 32-B entry, claimed
-        // by one atomic per wave)
-        const bool dfr = mine && !done;
-        const uint64_t bal = __ballot(dfr);
-        if (bal) {
-            const int lane = (int)(threadIdx.x & 63), leader = __ffsll((unsigned long long)bal) - 1;
-            uint32_t base = 0;
-            if (lane == leader) base = atomicAdd(a.defer_n, (uint32_t)__popcll(bal));
-            base = (uint32_t)__shfl((int)base, leader, 64);
-            if (dfr) {
-                const uint32_t slot = base + (uint32_t)__popcll(bal & ((1ull << lane) - 1ull));
-                if (lcp0 > 0xFFFFFFu) st &= ~QL_LAM0;  // not kept: the walk reads entry L0 again
-                const uint32_t pk = probes < 511u ? probes : 511u;
-                a.defer[2 * (uint64_t)slot] = make_uint4((uint32_t)i, (uint32_t)(i >> 32), kq, st | (pk << 15));
-                a.defer[2 * (uint64_t)slot + 1] =
-                    make_uint4(lam, dnode, (uint32_t)p0, (uint32_t)((p0 >> 32) & 0xFFu) | (lcp0 << 8));
-            }
-        }
-        if (mine && done) {
-            a.out_pos[i] = pos;
-            if (a.out_probes) a.out_probes[i] = probes;
-        }
-    }
-    if (bad) atomicOr(a.bad, 1u);
-}
-
-// k_sa_quad_llcp_b: the queries k_sa_quad_llcp_a did not settle, one per lane from its 32-B
-// deferred entry (the lane's packed state, k_sa_quad_llcp_a's variables): U where the run
-// leaves leaf k (cooperative, as the first step), then the LLCP walk.
-// R32: sa_n < 2^32, the walk's ranks in 32 bits
-template <int QW, bool EXACT, bool R32>
-__global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_sa_quad_llcp_b(SearchArgs a) {
-    using QR = typename std::conditional<EXACT, QueryRegsExact<QW>, QueryRegsRepack<QW>>::type;
-    __shared__ uint4 s_nodes[SAS_QUAD_LDS_NODES * 4];
-    stage_quad_top(a, s_nodes);
-    uint32_t bad = 0;
-    const uint32_t sub = threadIdx.x & (QUAD_G - 1);
-    const int lane0 = (int)((threadIdx.x & 63) & ~3u);
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t cnt = *a.defer_n;  // stream-ordered after k_sa_quad_llcp_a
-    for (uint64_t gs = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) - sub; gs < cnt; gs += stride) {
-        const uint64_t slot = gs + sub;
-        const bool mine = slot < cnt;
-        uint64_t i = 0, p0 = QUAD_NO_SA;
-        uint32_t kq = 0, st = 0, lam = 0, dnode = 0, lcp0 = 0, probes = 0, m = 0;
-        const uint8_t* qb;
-        QR q;
-        if (mine) {
-            const uint4 d0 = a.defer[2 * slot], d1 = a.defer[2 * slot + 1];
-            i = (uint64_t)d0.x | ((uint64_t)d0.y << 32);
-            kq = d0.z;
-            st = d0.w & ~(511u << 15);
-            probes = (d0.w >> 15) & 511u;
-            lam = d1.x;
-            dnode = d1.y;
-            p0 = (uint64_t)d1.z | ((uint64_t)(d1.w & 0xFFu) << 32);
-            lcp0 = d1.w >> 8;
-            query_ptr(a, i, &qb, &m);
-            q.load(qb, m, &bad);
-        } else {
-            q.bytes = a.qbytes;
-            q.m = 0;
-            for (int j = 0; j < QW; j++) q.w[j] = 0;
-        }
-        (void)p0;
-        const uint64_t Kmine = q.w[0];
         uint32_t kU = kq;
-        const bool done = !mine;
         // U for the queries whose 32-char run leaves leaf k: the leaf of K16 + 1, from where its
         // path parts from q's (near the leaves: one or two requests)
         const bool needU = !done && !(st & QL_UK);
@@ -1704,8 +1638,7 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
             }
         }
         if (!mine) continue;
-        uint64_t pos;
-        {
+        if (!done) {
             using rk_t = typename std::conditional<R32, uint32_t, uint64_t>::type;
             const rk_t sa_n = (rk_t)a.sa_n;
             const rk_t kb = 4 * (rk_t)kq;
@@ -3247,36 +3180,22 @@ static int launch_search(const sas_index* x, SearchArgs& a, int algo, int qw, ui
         // m <= 32: QUAD (the 32-char key decides every entry)
         hipLaunchKernelGGL((k_sa_quad<1, false, 4>), grid, block, 0, st, a);
     } else if (algo == SAS_ALGO_QUAD_LLCP) {
-        // longer: k_sa_quad_llcp_a settles what QUAD's reads settle and defers the rest to
-        // k_sa_quad_llcp_b (U + the LLCP walk), each kernel in its own workgroup shape; fused
-        // leaves, any SA width (the leaves and the LLCP entries carry 40-bit positions); every
-        // query word in registers when the batch's longest query is known to fit them, else
-        // two words and the rest repacked from the bytes
-        if (a.nq >= (1ull << 32)) SAS_FAIL(EINVAL, "SAS_ALGO_QUAD_LLCP: batches of < 2^32 queries");
+        // longer: k_sa_quad_llcp (fused leaves, any SA width: the leaves and the LLCP entries carry
+        // 40-bit positions), with every query word in registers when the batch's longest query
+        // is known to fit them, else two words and the rest repacked from the bytes
         const bool exact = a.m_max && a.m_max <= 32u * (uint32_t)qw && qw <= 8;
-        void* dbuf = nullptr;
-        HIP_TRY(hipMallocAsync(&dbuf, a.nq * 32 + 256, st));
-        SearchArgs b = a;
-        b.defer_n = static_cast<uint32_t*>(dbuf);
-        b.defer = reinterpret_cast<uint4*>(static_cast<uint8_t*>(dbuf) + 256);
-        HIP_TRY(hipMemsetAsync(dbuf, 0, 4, st));
-        const uint32_t ba = exact ? QLLCP_A_BLOCK(qw) : QLLCP_A_BLOCK(2);
-        uint64_t ga = (a.nq + ba - 1) / ba;
-        if (ga > (uint64_t)x->num_cus * 2) ga = (uint64_t)x->num_cus * 2;
-        const dim3 gA((unsigned)ga), bA(ba);
-        const dim3 gB((unsigned)(x->num_cus * 2)), bB((unsigned)(exact ? QLLCP_BLOCK(qw) : QLLCP_BLOCK(2)));
         const bool r32 = a.sa_n < (1ull << 32);
-#define QLLCP_AB(Q, X)                                                                            \
-    hipLaunchKernelGGL((k_sa_quad_llcp_a<Q, X>), gA, bA, 0, st, b);                               \
-    if (r32) hipLaunchKernelGGL((k_sa_quad_llcp_b<Q, X, true>), gB, bB, 0, st, b);                \
-    else hipLaunchKernelGGL((k_sa_quad_llcp_b<Q, X, false>), gB, bB, 0, st, b)
-        if (!exact) { QLLCP_AB(2, false); }
-        else if (qw == 2) { QLLCP_AB(2, true); }
-        else if (qw == 4) { QLLCP_AB(4, true); }
-        else { QLLCP_AB(8, true); }
-#undef QLLCP_AB
-        HIP_TRY(hipGetLastError());
-        HIP_TRY(hipFreeAsync(dbuf, st));
+        uint64_t gq = (a.nq + QLLCP_BLOCK(2) - 1) / QLLCP_BLOCK(2);
+        if (gq > (uint64_t)x->num_cus * 2) gq = (uint64_t)x->num_cus * 2;
+        const dim3 g1((unsigned)gq), b1((unsigned)(exact ? QLLCP_BLOCK(qw) : QLLCP_BLOCK(2)));
+#define QLLCP_GO(Q, X)                                                                            \
+    if (r32) hipLaunchKernelGGL((k_sa_quad_llcp<Q, X, true>), g1, b1, 0, st, a);                  \
+    else hipLaunchKernelGGL((k_sa_quad_llcp<Q, X, false>), g1, b1, 0, st, a)
+        if (!exact) { QLLCP_GO(2, false); }
+        else if (qw == 2) { QLLCP_GO(2, true); }
+        else if (qw == 4) { QLLCP_GO(4, true); }
+        else { QLLCP_GO(8, true); }
+#undef QLLCP_GO
     } else if (algo == SAS_ALGO_QUAD || algo == SAS_ALGO_INLINE || algo == SAS_ALGO_PREFIX) {
         if (!x->quad_compact) launch_quad<false, 4>(algo, top, qw, grid, block, st, a);
         else if (x->sa_w == 5) launch_quad<true, 5>(algo, top, qw, grid, block, st, a);
