@@ -80,6 +80,11 @@ def compact_line(full: dict) -> dict:
         if "c2" in confs and confs["c2"].get(sk):
             out["c2"][sk] = {kk: vv for kk, vv in config_summary(confs["c2"][sk]).items()
                              if kk in ("algo", "kernel_ms", "frac", "frac_basis", "traffic")}
+    # configs[2]'s one kernel on the long-query shapes: QUAD_LLCP's time over the better of
+    # QUAD and STREE_LLCP, text_m -> ratio (<= 1: at or below both; lcp_long in the detail file)
+    qo = ((full.get("lcp_long") or {}).get("summary") or {}).get("quad_llcp_over_min_quad_stree_llcp")
+    if "c2" in out and qo:
+        out["c2"]["lcp_quad_long_vs_min"] = qo
     if "c1" in confs and confs["c1"].get("deep_pivots"):
         out["c1_deep_pivots"] = dict(config_summary(confs["c1"]["deep_pivots"]),
                                      pivot_levels=confs["c1"]["deep_pivots"].get("pivot_levels"))

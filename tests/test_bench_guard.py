@@ -208,10 +208,13 @@ def test_result_line_is_compact_and_complete():
     full = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "bench_record_r3.json")))
     full["lcp_long"] = {"summary": {"ms": dict({f"{t}_m{m}": [4.1, 4.6, 3.1, 3.3, 2.2] for t in ("random", "repetitive")
                                                 for m in (64, 128, 256)}, algos=list(bench.LCP_LONG_ALGOS)),
-                                    "skipping_beats_plain": ["llcp@random_m64:1.32x"] * 6}}
+                                    "skipping_beats_plain": ["llcp@random_m64:1.32x"] * 6,
+                                    "quad_llcp_over_min_quad_stree_llcp": {f"{t}_m{m}": 0.987 for t in (
+                                        "random", "repetitive") for m in (64, 128, 256)}}}
     full["detail"] = "gpurun_out/bench_detail.json"
     full["configs"]["sst"] = _sst_record()
     full["configs"]["c2"]["lcp_stree"] = dict(full["configs"]["c2"], algo="stree_llcp")
+    full["configs"]["c2"]["lcp_quad"] = dict(full["configs"]["c2"], algo="quad_llcp")
     line = bench.compact_line(full)
     text = json.dumps(line)
     assert len(text) <= bench.LINE_LIMIT < 8192, len(text)
@@ -230,6 +233,8 @@ def test_result_line_is_compact_and_complete():
     for c in ("c0", "c1", "c2", "c3", "c4", "sst"):
         assert c in line["configs"], c
     assert line["configs"]["c2"]["lcp_stree"]["algo"] == "stree_llcp"
+    assert line["configs"]["c2"]["lcp_quad"]["algo"] == "quad_llcp"
+    assert len(line["configs"]["c2"]["lcp_quad_long_vs_min"]) == 6
     assert set(line["configs"]["sst"]) >= {"best", "lookups_per_s", "kernel_ms", "frac", "traffic", "cpu"}
     for c in ("c1", "c2"):
         assert set(line["configs"][c]) >= {"lookups_per_s", "kernel_ms", "frac", "index_bytes"}
