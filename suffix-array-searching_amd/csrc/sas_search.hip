@@ -1852,6 +1852,11 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_inline(SearchArgs a) {
 #ifndef SAS_PREFIX_QWMAX
 #define SAS_PREFIX_QWMAX 8  // register-resident query words (later ones repacked from the bytes)
 #endif
+// k_sa_prefix2 on the headline shape (fixed 32-char queries, lane pairs): queries in flight
+// per lane pair (round 6 A/B hook; 1 = one lookup at a time)
+#ifndef SAS_PREFIX_ILP
+#define SAS_PREFIX_ILP 1
+#endif
 #ifndef SAS_PREFIX_PAIR
 #define SAS_PREFIX_PAIR 0  // table[K], table[K+1] as one dword-aligned 8-B load
 #endif
@@ -1965,11 +1970,65 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix(SearchArgs a) {
 // first that is >= q; only if all are < q does the search go on in [r + G, table[K+1]).
 // HI40 (a part index of a text >= 2^32 chars): slot 1's rank word holds bits 32..39 of
 // every slot's SA value, one byte per slot.
+// k_sa_prefix2's lookup of query i once its table entry e (entry K) is in: the pair's slots
+// tested, the rare bisection past them, the position (and the reference's cnt) stored
+template <int QW, int G, bool HI40>
+__device__ __forceinline__ void prefix2_finish(const SearchArgs& a, const uint4* pt, uint64_t i, uint64_t K,
+                                               const uint4& e, const QueryRegs<QW>& q, uint64_t K64, uint32_t sub,
+                                               int lane0) {
+    const uint64_t sa_n = a.sa_n;
+    const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
+    // two slots beside a >= 2^32-char text: bits 32..39 of the rank in slot 1's rank word
+    const uint64_t r0 = (uint64_t)(uint32_t)__shfl((int)e.z, lane0, 64) |
+                        (HI40 && G == 2 ? (uint64_t)((hb >> 16) & 0xFFu) << 32 : 0ull);
+    const uint64_t rank = r0 + sub;
+    const uint64_t pe = HI40 ? ((uint64_t)e.w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32)) : (uint64_t)e.w;
+    // rank sa_n stands for "past every suffix": it is the answer if reached
+    const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), pe, K64, a, q);
+    const uint32_t grp = (uint32_t)(__ballot(ok) >> lane0) & ((1u << G) - 1u);
+    const uint32_t j = grp ? (uint32_t)__builtin_ctz(grp) : 0u;
+    const uint32_t pw = (uint32_t)__shfl((int)e.w, lane0 + (int)j, 64);
+    uint64_t ans, pos;
+    if (grp) {
+        ans = r0 + j;
+        pos = ans >= sa_n ? a.next_pos : (HI40 ? ((uint64_t)pw | ((uint64_t)((hb >> (8 * j)) & 0xFFu) << 32)) : pw);
+    } else {
+        uint64_t lo = r0 + G, hi = pt_rank<G, HI40>(pt, K + 1), pr = QUAD_NO_SA;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            const uint4 f = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
+            const uint64_t pp = (uint64_t)f.z | ((uint64_t)(f.w & 0xFFu) << 32);
+            if (sector_ge<QW>((uint64_t)f.x | ((uint64_t)f.y << 32), pp, K64, a, q)) {
+                hi = mid;
+                pr = pp;
+            } else {
+                lo = mid + 1;
+            }
+        }
+        ans = lo;
+        if (lo >= sa_n) pos = a.next_pos;
+        else if (pr != QUAD_NO_SA) pos = pr;
+        else pos = quad_entry_sa<false, 4>(a, lo);
+    }
+    if (sub == 0) {
+        if (SAS_PREFIX_NT_OUT) __builtin_nontemporal_store(pos, a.out_pos + i);
+        else a.out_pos[i] = pos;
+        if (a.out_probes) {  // the reference's cnt over [table[K], table[K+1])
+            uint32_t probes = 1;
+            for (uint64_t l2 = r0, h2 = pt_rank<G, HI40>(pt, K + 1); l2 < h2; probes++) {
+                const uint64_t mid = (l2 + h2) >> 1;
+                if (mid < ans) l2 = mid + 1;
+                else h2 = mid;
+            }
+            a.out_probes[i] = probes;
+        }
+    }
+}
+
 template <int QW, int G, bool HI40 = false>
 __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
     uint32_t bad = 0;
     const uint32_t sh = 64 - 2 * a.prefix_chars;
-    const uint64_t sa_n = a.sa_n;
     const uint32_t sub = threadIdx.x & (G - 1);
     const int lane0 = (int)((threadIdx.x & 63) & ~(uint32_t)(G - 1));
     const uint4* pt = reinterpret_cast<const uint4*>(a.prefix);
@@ -1983,6 +2042,38 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
         return SAS_QUAD_NT_IO ? nt_load4(p) : *p;
     };
     const uint64_t i0 = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) / G;
+    if (SAS_PREFIX_ILP > 1 && split) {
+        // two queries per lane pair in flight: i and i + stride, both table entries requested
+        // before either is tested (the next two queries' loads overlap the lookups)
+        auto pack_q = [&](const uint4& v, uint64_t k, QueryRegs<QW>& q) {
+            bad |= (v.x | v.y | v.z | v.w) & 0xFCFCFCFCu;
+            const uint32_t part = (pack4(v.x) << 24) | (pack4(v.y) << 16) | (pack4(v.z) << 8) | pack4(v.w);
+            const uint32_t other = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)part, 0xB1, 0xF, 0xF, false);
+            q.bytes = a.qbytes + k * 32;
+            q.m = 32;
+            q.w[0] = sub ? (((uint64_t)other << 32) | part) : (((uint64_t)part << 32) | other);
+        };
+        const uint4 z = make_uint4(0, 0, 0, 0);
+        uint4 va = i0 < a.nq ? qload(i0) : z, vb = i0 + stride < a.nq ? qload(i0 + stride) : z;
+        for (uint64_t i = i0; i < a.nq; i += 2 * stride) {
+            const uint64_t i2 = i + stride;
+            const bool two = i2 < a.nq;  // group-uniform
+            const uint4 ua = va, ub = vb;
+            if (i + 2 * stride < a.nq) va = qload(i + 2 * stride);
+            if (i2 + 2 * stride < a.nq) vb = qload(i2 + 2 * stride);
+            QueryRegs<QW> qa, qb2;
+            pack_q(ua, i, qa);
+            pack_q(ub, i2, qb2);
+            const uint64_t Ka = pt_slot(a, qa.w[0] >> sh), Kb = pt_slot(a, qb2.w[0] >> sh);
+            const uint4 ea = SAS_PREFIX_NT ? nt_load4(pt + G * Ka + sub) : pt[G * Ka + sub];
+            uint4 eb = z;
+            if (two) eb = SAS_PREFIX_NT ? nt_load4(pt + G * Kb + sub) : pt[G * Kb + sub];
+            prefix2_finish<QW, G, HI40>(a, pt, i, Ka, ea, qa, qa.w[0], sub, lane0);
+            if (two) prefix2_finish<QW, G, HI40>(a, pt, i2, Kb, eb, qb2, qb2.w[0], sub, lane0);
+        }
+        if (bad) atomicOr(a.bad, 1u);
+        return;
+    }
     uint4 vnext = make_uint4(0, 0, 0, 0);
     if (SAS_PREFIX_QPREFETCH && split && i0 < a.nq) vnext = qload(i0);
     for (uint64_t i = i0; i < a.nq; i += stride) {
@@ -2017,52 +2108,7 @@ __global__ __launch_bounds__(SEARCH_BLOCK, 8) void k_sa_prefix2(SearchArgs a) {
         const uint64_t K64 = q.w[0];
         const uint64_t K = pt_slot(a, K64 >> sh);
         const uint4 e = SAS_PREFIX_NT ? nt_load4(pt + G * K + sub) : pt[G * K + sub];
-        const uint32_t hb = HI40 ? (uint32_t)__shfl((int)e.z, lane0 + 1, 64) : 0u;
-        // two slots beside a >= 2^32-char text: bits 32..39 of the rank in slot 1's rank word
-        const uint64_t r0 = (uint64_t)(uint32_t)__shfl((int)e.z, lane0, 64) |
-                            (HI40 && G == 2 ? (uint64_t)((hb >> 16) & 0xFFu) << 32 : 0ull);
-        const uint64_t rank = r0 + sub;
-        const uint64_t pe = HI40 ? ((uint64_t)e.w | ((uint64_t)((hb >> (8 * sub)) & 0xFFu) << 32)) : (uint64_t)e.w;
-        // rank sa_n stands for "past every suffix": it is the answer if reached
-        const bool ok = rank >= sa_n || sector_ge<QW>((uint64_t)e.x | ((uint64_t)e.y << 32), pe, K64, a, q);
-        const uint32_t grp = (uint32_t)(__ballot(ok) >> lane0) & ((1u << G) - 1u);
-        const uint32_t j = grp ? (uint32_t)__builtin_ctz(grp) : 0u;
-        const uint32_t pw = (uint32_t)__shfl((int)e.w, lane0 + (int)j, 64);
-        uint64_t ans, pos;
-        if (grp) {
-            ans = r0 + j;
-            pos = ans >= sa_n ? a.next_pos : (HI40 ? ((uint64_t)pw | ((uint64_t)((hb >> (8 * j)) & 0xFFu) << 32)) : pw);
-        } else {
-            uint64_t lo = r0 + G, hi = pt_rank<G, HI40>(pt, K + 1), pr = QUAD_NO_SA;
-            while (lo < hi) {
-                const uint64_t mid = (lo + hi) >> 1;
-                const uint4 f = SAS_PREFIX_NT ? nt_load4(a.quad_leaves + mid) : a.quad_leaves[mid];
-                const uint64_t pp = (uint64_t)f.z | ((uint64_t)(f.w & 0xFFu) << 32);
-                if (sector_ge<QW>((uint64_t)f.x | ((uint64_t)f.y << 32), pp, K64, a, q)) {
-                    hi = mid;
-                    pr = pp;
-                } else {
-                    lo = mid + 1;
-                }
-            }
-            ans = lo;
-            if (lo >= sa_n) pos = a.next_pos;
-            else if (pr != QUAD_NO_SA) pos = pr;
-            else pos = quad_entry_sa<false, 4>(a, lo);
-        }
-        if (sub == 0) {
-            if (SAS_PREFIX_NT_OUT) __builtin_nontemporal_store(pos, a.out_pos + i);
-            else a.out_pos[i] = pos;
-            if (a.out_probes) {  // the reference's cnt over [table[K], table[K+1])
-                uint32_t probes = 1;
-                for (uint64_t l2 = r0, h2 = pt_rank<G, HI40>(pt, K + 1); l2 < h2; probes++) {
-                    const uint64_t mid = (l2 + h2) >> 1;
-                    if (mid < ans) l2 = mid + 1;
-                    else h2 = mid;
-                }
-                a.out_probes[i] = probes;
-            }
-        }
+        prefix2_finish<QW, G, HI40>(a, pt, i, K, e, q, K64, sub, lane0);
     }
     if (bad) atomicOr(a.bad, 1u);
 }

@@ -46,7 +46,7 @@ for k in $keys; do
   mkdir -p "$d"
   if [ $sq = 2 ]; then
     echo "[pmc_r6] ta $k: $args"
-    timeout -s KILL 420 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY TA_BUSY_avr TA_BUSY_max --output-format csv -d "$d/ta/sq_ta" -o run -- python3 bench.py $args > "$d/ta.log" 2>&1 || exit $?
+    timeout -s KILL 420 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_BUSY_CYCLES SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_WAIT_ANY TA_BUSY_avr TA_BUSY_max TA_ADDR_STALLED_BY_TC_CYCLES_sum --output-format csv -d "$d/ta/sq_ta" -o run -- python3 bench.py $args > "$d/ta.log" 2>&1 || exit $?
     python3 tools/sq_to_json.py "$d/ta" "$kern" > "$out/ta_$k.json" || exit $?
     find "$d/ta" -name "*.csv" -delete
     continue
