@@ -5,7 +5,7 @@
 # kernels (tools/kt_by_grid.py) and rocprofv3's own kernel_stats.csv.
 # usage: tools/prof_r5.sh [outdir]
 set -o pipefail
-out=${1:-gpurun_out/prof5}
+out=${1:-gpurun_out/prof6}
 mkdir -p "$out"
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- python3 bench.py \
