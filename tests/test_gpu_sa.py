@@ -800,6 +800,66 @@ def test_sa_beyond_u32(sas):
             assert int(lidx.suffix_array(count=1, start=r)[0]) == int(got["plain"][k]), k
 
 
+def test_llcp_tails_beyond_u32(sas):
+    """The LCP-skipping tails with 64-bit ranks (n > 2^32: k_sa_quad_llcp<.., R32 = false>, the
+    40-bit LLCP entries of STREE_LLCP and LLCP): 64 copies of a 400-char block that starts with
+    20 'T's are planted in a 2^32 + 12345-char random text, so the copies' first suffixes sort
+    at ranks above 2^32 in runs of 64 equal 32-char keys, each copy followed by different random
+    text.  Queries of 33..256 chars from the copies' first 9 offsets (with one char changed past
+    char 32 too), from positions above 2^32 and the text's last suffixes: QUAD_LLCP (on
+    the absolute quad layout, which it needs), STREE_LLCP and LLCP equal PLAIN, and every PLAIN
+    answer is proven the exact lower bound on the host text (sas/sa_search.rs:98-112)."""
+    import torch
+    n = (1 << 32) + 12345
+    t = sas.random_string(n, seed=987, device="cuda")
+    rng = np.random.default_rng(8)
+    blk = torch.from_numpy(np.concatenate([np.full(20, 3, np.uint8), rng.integers(0, 4, 380, dtype=np.uint8)])).cuda()
+    starts = np.sort(rng.choice(np.arange(1 << 20, n - 1000, 4096, dtype=np.int64), 64, replace=False))
+    for s in starts:
+        t[int(s):int(s) + 400] = blk
+    ht = t.cpu().numpy()
+    idx = sas.SaNaive.build(t, lcp=False, stree=True, sector=False, quad="abs", llcp=True, prefix=False)
+    del t
+    torch.cuda.empty_cache()
+    st = idx.stats()
+    assert st["sa_width"] == 5 and st["quad_fan"] == 17 and st["llcp_bytes"] == 16 * n
+    qs = []
+    for s in starts[:48]:
+        for m in (33, 48, 64, 100, 200, 256):
+            # >= 12 leading 'T's: among the text's top ~10^3 suffixes, ranks above 2^32
+            o = int(s) + int(rng.integers(0, 9))
+            q = ht[o:o + m].copy()
+            qs.append(q)
+            mq = q.copy()
+            k = int(rng.integers(32, m))
+            mq[k] = (mq[k] + 1 + rng.integers(0, 3)) % 4
+            qs.append(mq)
+    hi_offs = rng.integers((1 << 32) - 100, n - 300, 200)
+    qs += [ht[o:o + m] for o, m in zip(hi_offs, rng.integers(33, 257, 200))]
+    qs += [np.concatenate([ht[n - k:], np.zeros(j, np.uint8)]) for k in (20, 40, 300) for j in (0, 30)]
+    buf, off, lens = pack(qs)
+    plain = idx.search_batch(buf, off, lens, algo="plain")
+    for algo in ("quad_llcp", "stree_llcp", "llcp"):
+        got = idx.search_batch(buf, off, lens, algo=algo)
+        bad = np.nonzero(got != plain)[0]
+        assert len(bad) == 0, (algo, bad[:5])
+    lo, _ = idx.search_range(buf, off, lens)
+    above = 0
+    for k, q in enumerate(qs):
+        qb = bytes(q)
+        r = int(lo[k])
+        pair = idx.suffix_array(count=2 if r > 0 else 1, start=r - 1 if r > 0 else 0)
+        cur = int(pair[-1]) if r < n else n
+        assert int(plain[k]) == cur, k
+        if r < n:
+            assert bytes(ht[cur:cur + len(q)]) >= qb, k
+        if r > 0:
+            assert bytes(ht[int(pair[0]):int(pair[0]) + len(q)]) < qb, k
+        above += r >= (1 << 32)
+    assert above >= 48 * 12  # the planted copies' queries were answered at ranks above 2^32
+    idx.free()
+
+
 def test_fasta_genome_like_end_to_end(sas, tmp_path):
     """read_fasta_file (sas/util.rs:144-169) -> GPU SA -> every algorithm vs the oracle,
     on a genome-shaped FASTA: several records, soft-masked (lowercase) runs, long N
