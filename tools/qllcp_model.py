@@ -4,6 +4,7 @@ quad tree's routing invariants (leaf k = the leaf of the first suffix whose 16-c
 LLCP walk with its substituted lcps.  Every tie compare asserts that the chars it skips are
 really equal to q's, and every answer is checked against the oracle's binary_search.  A
 design check run before the kernel meets the GPU (python tools/qllcp_model.py)."""
+import bisect
 import os
 import sys
 
@@ -32,18 +33,25 @@ def lcp_str(a, b):
     return k
 
 
-def model(t, sa, lcpa, q, stats):
+def leaf_keys(t, sa):
+    """the fused leaves' 32-char keys in SA order, the last leaf padded with all ones"""
+    sa_n = len(sa)
+    nl = (sa_n + 3) // 4
+    return [key_of(t, int(sa[r]), 32) for r in range(sa_n)] + [(1 << 64) - 1] * (4 * nl - sa_n)
+
+
+def model(t, sa, lcpa, q, stats, keys=None):
     n = len(t)
     sa_n = n
     m = len(q)
     assert m > 32
     K64 = key_of(q, 0, 32)
     K16 = K64 >> 32
-    k64 = [key_of(t, int(sa[r]), 32) for r in range(sa_n)]
-    # padding entries of the last leaf: all ones
+    if keys is None:
+        keys = leaf_keys(t, sa)
     nl = (sa_n + 3) // 4
-    keys = k64 + [(1 << 64) - 1] * (4 * nl - sa_n)
-    first16 = next((r for r in range(sa_n) if (keys[r] >> 32) >= K16), sa_n)
+    k16s = [x >> 32 for x in keys[:sa_n]] if "k16s" not in stats else stats["k16s"]
+    first16 = bisect.bisect_left(k16s, K16)
     k = min(first16 // 4, nl - 1)
     leaf = keys[4 * k:4 * k + 4]
     c16 = sum((x >> 32) < K16 for x in leaf)
@@ -65,7 +73,7 @@ def model(t, sa, lcpa, q, stats):
         x32 = False
         x32_u = False
     else:
-        firstgt = next((r for r in range(sa_n) if (keys[r] >> 32) > K16), sa_n)
+        firstgt = bisect.bisect_right(k16s, K16)
         kU = min(firstgt // 4, nl - 1)
         lf = keys[4 * kU:4 * kU + 4]
         le64U = sum(x <= K64 for x in lf)
@@ -181,6 +189,8 @@ def run(name, t, nq=400, seed=1):
     qs += [np.concatenate([t[n - k:], np.zeros(j, np.uint8)]) for k in (33, 40, 70) for j in (0, 5)]
     qs += [np.concatenate([t[n - k:], np.full(40, 3, np.uint8)]) for k in (5, 20)]
     st = {"settled": 0, "one": 0, "walk": 0, "reads": 0, "kU_descents": 0}
+    keys = leaf_keys(t, sa)
+    aux = dict(st, k16s=[x >> 32 for x in keys[:n]])
     tp = O.padded(t)
     for q in qs:
         if len(q) <= 32:
@@ -188,9 +198,11 @@ def run(name, t, nq=400, seed=1):
         qb = np.concatenate([q, np.zeros(64, np.uint8)])
         exp, _ = O.search_many(tp, n, sa, qb, np.zeros(1, np.uint64), np.array([len(q)], np.uint32),
                                "binary_search", 1)
-        got, _ = model(t, sa, lcpa, q, st)
+        got, _ = model(t, sa, lcpa, q, aux, keys)
         assert got == int(exp[0]), (name, got, int(exp[0]), q[:40])
+    st = {k: aux[k] for k in st}
     print(name, st)
+    return st
 
 
 if __name__ == "__main__":
