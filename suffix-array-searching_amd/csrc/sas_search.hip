@@ -1500,6 +1500,15 @@ __device__ __forceinline__ uint32_t quad_descend_from(const SearchArgs& a, const
 #define QL_LAM0 (1u << 13)               // entry L0 compared below q: L0 + 1, its lcp in lcp0
 #define QL_END (1u << 14)                // q's 16-char run reaches the end: U = sa_n
 #define QL_DLEV(st) ((st) >> 24)         // where K16 + 1's path parts from q's (QLLCP_NONE: not)
+// leaf k's keys all below q's (L0 past it): read the next entry to settle q as k_sa_quad4x
+// would (1), or go to the walk from L0 = 4k + 4 with kappa 16 (0), or read it only when just
+// leaf k's last entry shares q's 16-char key (2).  On random text that is the usual shape of
+// the case (one other suffix with q's 16-char key below q, a leaf boundary between them) and
+// the next entry is q's; on repetitive text a 16-char run fills more of the leaf and the
+// next entry is rarely L0 itself, so the read would mostly be wasted
+#ifndef SAS_QLLCP_NEXT
+#define SAS_QLLCP_NEXT 2
+#endif
 
 // k_sa_quad_llcp: the group step (descent, leaf, counts), the settle (k_sa_quad4x's reads: the
 // first entry not below q's 32-char key and at most one compare), then for what that does not
@@ -1587,7 +1596,7 @@ __global__ __launch_bounds__(QLLCP_BLOCK(QW), QLLCP_BLOCK(QW) * 2 / 256) void k_
             pos = a.next_pos;
             done = true;
         } else if (mine) {
-            if (!(st & QL_KNOWN)) {
+            if (!(st & QL_KNOWN) && (SAS_QLLCP_NEXT == 1 || (SAS_QLLCP_NEXT == 2 && QL_C16(st) == 3))) {
                 // leaf k's keys are all below q's: the next entry, as k_sa_quad4x reads it (a
                 // key still below q's leaves L0 inexact at 32 chars, the walk's kappa 16)
                 const uint4 e = a.quad_leaves[4 * (uint64_t)kq + 4];

@@ -14,6 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from oracle import pyoracle as O  # noqa: E402
 
 CAP = 4095
+NEXT_MODE = int(os.environ.get("QLLCP_NEXT", "2"))  # the kernel's SAS_QLLCP_NEXT
 
 
 def key_of(t, p, c):
@@ -94,7 +95,8 @@ def model(t, sa, lcpa, q, stats, keys=None):
     if L0 >= sa_n:
         return n, 0
     lam0 = None
-    if c64 == 4 and keys[L0] >= K64:
+    next_read = NEXT_MODE == 1 or (NEXT_MODE == 2 and c16 == 3)
+    if next_read and c64 == 4 and keys[L0] >= K64:
         # the kernel reads the next entry: its key >= q's makes L0 exact at 32 chars
         c64 = 3  # (as if leaf k had held it)
         x32 = x32_u
