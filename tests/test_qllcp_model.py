@@ -8,6 +8,7 @@ import importlib.util
 import os
 
 import numpy as np
+import pytest
 
 
 def _model():
@@ -18,8 +19,12 @@ def _model():
     return mod
 
 
-def test_quad_llcp_model_matches_oracle():
+@pytest.mark.parametrize("next_mode", [0, 1, 2])
+def test_quad_llcp_model_matches_oracle(next_mode):
+    """next_mode: the kernel's SAS_QLLCP_NEXT (the entry after leaf k never read / always /
+    only when just leaf k's last entry shares K16, the shipped policy)."""
     M = _model()
+    M.NEXT_MODE = next_mode
     rng = np.random.default_rng(3)
     blk = rng.integers(0, 4, 700, dtype=np.uint8)
     st = M.run("random", rng.integers(0, 4, 3000, dtype=np.uint8))
