@@ -133,7 +133,10 @@ def main():
     import sas_amd
 
     dist = None
-    if ws > 1:
+    # under a launcher (torchrun, or this script's own children) the group comes from its
+    # environment, at world size 1 too: torchrun's agent hosts the store, and a group of our
+    # own over tcp:// would wait as a client of a store nobody serves (the configs[4] record)
+    if ws > 1 or "WORLD_SIZE" in os.environ:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("nccl")
